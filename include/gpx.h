@@ -1,0 +1,139 @@
+/*
+ * gpx.h — C ABI of the MI355X exact-GP regression engine (libgpx.so, gfx950).
+ *
+ * This is the drop-in boundary for the reference's GP hot path. The reference has no FFI of
+ * its own: its seam is the duck-typed GPflow model it calls from Python
+ * (SURVEY.md §8b). Each entry point below replaces one piece of GPflow 2.9.1 arithmetic at a
+ * reference call site:
+ *
+ *   gpx_batch_lml_grad  <- model.training_loss + its gradient inside
+ *                          gpflow.optimizers.Scipy().minimize(...)   GPR/model_trainer.py:18-19
+ *                          (also Multi-Input_GPR/models/model_trainer.py:20-21, 36-37)
+ *   gpx_batch_predict   <- model.predict_f(X, full_cov=False)        GPR/model_trainer.py:20,
+ *                          GPR/predictor.py:6;  model.predict_y(X)   GPR/predictor.py:7
+ *   gpx_kernel_spec     <- the kernel objects of GPR/main.py:105-114 and the composite
+ *                          Exponential*Exponential of Multi-Input_GPR/main.py:118-135
+ *
+ * Conventions
+ *  - All arithmetic is fp64. X, Y, Xnew and the predict outputs are caller-owned DEVICE
+ *    pointers (e.g. torch tensors' data_ptr()); the library never frees them.
+ *  - theta / lml / grad / info of gpx_batch_lml_grad are HOST arrays; the call returns when
+ *    they are filled (the L-BFGS-B driver on the host needs them immediately).
+ *  - theta is in constrained space (θ > 0), row stride GPX_THETA_STRIDE per problem:
+ *    theta[b*GPX_THETA_STRIDE + p] for the kernel parameters p < spec.n_params, followed by the
+ *    Gaussian noise variance σn² at p = spec.n_params. grad has the same layout and holds
+ *    ∂logML/∂θ (the chain rule to the unconstrained variables is the caller's job).
+ *  - Per-term parameter order follows GPflow's tf.Module flattening (sorted attribute names):
+ *      SE/Matern12/Matern32/Matern52/Exponential : [lengthscales, variance]
+ *      RationalQuadratic                         : [alpha, lengthscales, variance]
+ *      Periodic(SquaredExponential)              : [base.lengthscales, base.variance, period]
+ *      Linear                                    : [variance]
+ *  - Return codes: GPX_OK, GPX_NOT_PD (some problem's K+σn²I is not positive definite; its
+ *    info[b] holds the 1-based index of the first failing pivot, like LAPACK potrf),
+ *    GPX_BAD_ARG, GPX_HIP_ERROR. No C++ exception crosses this boundary.
+ *  - A context is bound to one device and is NOT thread-safe.
+ */
+#ifndef GPX_H_
+#define GPX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPX_OK 0
+#define GPX_NOT_PD 1
+#define GPX_BAD_ARG 2
+#define GPX_HIP_ERROR 3
+
+#define GPX_MAX_TERMS 4
+#define GPX_THETA_STRIDE 16 /* kernel params + 1 noise slot, per problem */
+#define GPX_MAX_DIM 16      /* input dimension D limit */
+
+typedef enum {
+  GPX_SE = 1,          /* σ² exp(-r²/2)                         gpflow.kernels.SquaredExponential */
+  GPX_MATERN12 = 2,    /* σ² exp(-r)                            gpflow.kernels.Matern12 */
+  GPX_MATERN32 = 3,    /* σ² (1+√3r) exp(-√3r)                  gpflow.kernels.Matern32 */
+  GPX_MATERN52 = 4,    /* σ² (1+√5r+5r²/3) exp(-√5r)            gpflow.kernels.Matern52 */
+  GPX_EXPONENTIAL = 5, /* σ² exp(-r/2)                          gpflow.kernels.Exponential */
+  GPX_RQ = 6,          /* σ² (1+r²/(2α))^(-α)                   gpflow.kernels.RationalQuadratic */
+  GPX_PERIODIC_SE = 7, /* σ² exp(-½Σ(sin(πΔ/p)/ℓ)²)             gpflow.kernels.Periodic(SE) */
+  GPX_LINEAR = 8       /* σ² x·x'                               gpflow.kernels.Linear */
+} gpx_term_kind;
+
+typedef enum { GPX_SUM = 0, GPX_PRODUCT = 1 } gpx_combine;
+
+typedef struct {
+  int32_t kind;         /* gpx_term_kind */
+  int32_t dim_start;    /* active_dims = slice(dim_start, dim_start + dim_count) */
+  int32_t dim_count;
+  int32_t param_offset; /* index of this term's first parameter in the theta row */
+} gpx_term;
+
+typedef struct {
+  int32_t n_terms;      /* 1..GPX_MAX_TERMS */
+  int32_t combine;      /* gpx_combine (ignored when n_terms == 1) */
+  int32_t n_params;     /* kernel parameters; the noise variance sits at theta[n_params] */
+  int32_t reserved;
+  gpx_term terms[GPX_MAX_TERMS];
+} gpx_kernel_spec;
+
+typedef struct gpx_ctx gpx_ctx;
+typedef struct gpx_batch gpx_batch;
+
+const char* gpx_version(void);
+
+/* One context per device. */
+int gpx_create(int device, gpx_ctx** out);
+int gpx_destroy(gpx_ctx* ctx);
+const char* gpx_last_error(const gpx_ctx* ctx);
+
+/*
+ * A batch of B independent GPR problems (the per-asset / per-kernel fits of
+ * GPR/main.py:23-37 x GPR/model_trainer.py:14). Problem b has n[b] <= N_max points.
+ *   X : device fp64 [B, N_max, D] row-major;  Y : device fp64 [B, N_max].
+ *   n : host int32 [B];  specs : host [B].
+ * The batch keeps pointers to X and Y (they must outlive it) and owns its HBM workspace
+ * (about 4 * B * Np^2 * 8 bytes, Np = N_max rounded up to 64).
+ */
+int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, const double* Y,
+                     const int32_t* n, const gpx_kernel_spec* specs, gpx_batch** out);
+int gpx_batch_destroy(gpx_batch* batch);
+
+/*
+ * logML and ∂logML/∂θ at theta for the n_active problems listed in active (host int32).
+ * Outputs are written at each active problem's row: lml[b], grad[b*GPX_THETA_STRIDE + p],
+ * info[b]. stream may be NULL (library stream). Returns after the outputs are on the host.
+ */
+int gpx_batch_lml_grad(gpx_batch* batch, int n_active, const int32_t* active, const double* theta,
+                       double* lml, double* grad, int32_t* info, void* stream);
+
+/*
+ * Posterior marginals at Xnew for the active problems: GPflow GPR.predict_f(full_cov=False)
+ * (add_noise = 0) or predict_y (add_noise = 1: variance + σn²).
+ *   Xnew : device fp64 [B, M, D];  mean, var : device fp64 [B, M] (caller-owned).
+ * theta/info are host arrays as above. Re-factorises K+σn²I at theta like GPflow (no caching
+ * across calls unless theta is bit-identical to the last factorisation of that problem).
+ */
+int gpx_batch_predict(gpx_batch* batch, int n_active, const int32_t* active, const double* theta,
+                      const double* Xnew, int M, int add_noise, double* mean, double* var,
+                      int32_t* info, void* stream);
+
+/* Timing hooks for bench.py: total device time (ms) of the last call's kernels, measured with
+ * HIP events on the stream they ran on, split by phase. */
+typedef struct {
+  double factor_ms;   /* K build + recursive Cholesky-and-inverse */
+  double alpha_ms;    /* the two triangular matrix-vector products */
+  double grad_ms;     /* fused K^-1 = W^T W formation + gradient contraction + reduce */
+  double predict_ms;  /* predict-only kernels */
+  double total_ms;
+  double gemm_flops;  /* MFMA flops issued by the GEMM kernels of the last call */
+} gpx_timing;
+int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
+int gpx_set_profiling(gpx_ctx* ctx, int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPX_H_ */

@@ -1,0 +1,133 @@
+"""ctypes binding of the C ABI in ``include/gpx.h`` (libgpx.so, built for gfx950).
+
+There is no CPU fallback: importing the engine without the shared library, or evaluating
+without a HIP device, raises. The oracle under ``oracle/`` is test infrastructure and is never
+imported from here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+GPX_OK, GPX_NOT_PD, GPX_BAD_ARG, GPX_HIP_ERROR = 0, 1, 2, 3
+GPX_MAX_TERMS = 4
+GPX_THETA_STRIDE = 16
+GPX_MAX_DIM = 16
+
+(GPX_SE, GPX_MATERN12, GPX_MATERN32, GPX_MATERN52, GPX_EXPONENTIAL, GPX_RQ, GPX_PERIODIC_SE,
+ GPX_LINEAR) = range(1, 9)
+GPX_SUM, GPX_PRODUCT = 0, 1
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgpx.so")
+
+# every symbol include/gpx.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = (
+    "gpx_version", "gpx_create", "gpx_destroy", "gpx_last_error", "gpx_batch_create",
+    "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_predict", "gpx_batch_last_timing",
+    "gpx_set_profiling",
+)
+
+
+class GpxTerm(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("dim_start", ctypes.c_int32),
+                ("dim_count", ctypes.c_int32), ("param_offset", ctypes.c_int32)]
+
+
+class GpxKernelSpec(ctypes.Structure):
+    _fields_ = [("n_terms", ctypes.c_int32), ("combine", ctypes.c_int32),
+                ("n_params", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("terms", GpxTerm * GPX_MAX_TERMS)]
+
+
+class GpxTiming(ctypes.Structure):
+    _fields_ = [("factor_ms", ctypes.c_double), ("alpha_ms", ctypes.c_double),
+                ("grad_ms", ctypes.c_double), ("predict_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double), ("gemm_flops", ctypes.c_double)]
+
+
+class GPXError(RuntimeError):
+    pass
+
+
+class NotPositiveDefiniteError(GPXError):
+    """K + σn²I is not positive definite (GPflow raises tf.errors.InvalidArgumentError from
+    tf.linalg.cholesky in the same situation)."""
+
+    def __init__(self, msg, info=None):
+        super().__init__(msg)
+        self.info = info
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load libgpx.so and declare its signatures. Raises if the library is missing."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise GPXError(
+                f"libgpx.so not found at {p}: build it with `make` (or __graft_entry__.build()). "
+                "portfoliooptgp_amd has no CPU fallback.")
+        lib = ctypes.CDLL(p)
+        c_int, c_void_p, c_double_p = ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)
+        c_int_p = ctypes.POINTER(ctypes.c_int32)
+        lib.gpx_version.restype = ctypes.c_char_p
+        lib.gpx_version.argtypes = []
+        lib.gpx_create.restype = c_int
+        lib.gpx_create.argtypes = [c_int, ctypes.POINTER(c_void_p)]
+        lib.gpx_destroy.restype = c_int
+        lib.gpx_destroy.argtypes = [c_void_p]
+        lib.gpx_last_error.restype = ctypes.c_char_p
+        lib.gpx_last_error.argtypes = [c_void_p]
+        lib.gpx_set_profiling.restype = c_int
+        lib.gpx_set_profiling.argtypes = [c_void_p, c_int]
+        lib.gpx_batch_create.restype = c_int
+        lib.gpx_batch_create.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int_p,
+                                         ctypes.POINTER(GpxKernelSpec), ctypes.POINTER(c_void_p)]
+        lib.gpx_batch_destroy.restype = c_int
+        lib.gpx_batch_destroy.argtypes = [c_void_p]
+        lib.gpx_batch_lml_grad.restype = c_int
+        lib.gpx_batch_lml_grad.argtypes = [c_void_p, c_int, c_int_p, c_double_p, c_double_p,
+                                           c_double_p, c_int_p, c_void_p]
+        lib.gpx_batch_predict.restype = c_int
+        lib.gpx_batch_predict.argtypes = [c_void_p, c_int, c_int_p, c_double_p, c_void_p, c_int,
+                                          c_int, c_void_p, c_void_p, c_int_p, c_void_p]
+        lib.gpx_batch_last_timing.restype = c_int
+        lib.gpx_batch_last_timing.argtypes = [c_void_p, ctypes.POINTER(GpxTiming)]
+        if path is None:
+            _lib = lib
+        return lib
+
+
+class Context:
+    """One gpx context per HIP device (process-wide cache)."""
+
+    _cache = {}
+
+    def __init__(self, device: int):
+        self.lib = load_library()
+        self.device = device
+        h = ctypes.c_void_p()
+        rc = self.lib.gpx_create(device, ctypes.byref(h))
+        if rc != GPX_OK:
+            raise GPXError(f"gpx_create(device={device}) failed with code {rc}: no usable HIP device?")
+        self.handle = h
+
+    @classmethod
+    def get(cls, device: int) -> "Context":
+        if device not in cls._cache:
+            cls._cache[device] = Context(device)
+        return cls._cache[device]
+
+    def last_error(self) -> str:
+        return self.lib.gpx_last_error(self.handle).decode()
+
+    def set_profiling(self, on: bool) -> None:
+        self.lib.gpx_set_profiling(self.handle, 1 if on else 0)

@@ -1,0 +1,520 @@
+// gpx_api.hip — C ABI (include/gpx.h) and host orchestration of the exact-GP engine.
+//
+// One evaluation of logML and ∂logML/∂θ for B problems (the closure gpflow.optimizers.Scipy
+// calls from GPR/model_trainer.py:19) runs, all on one stream:
+//   1. K = k(X,X) + σn²I                                      build_kernel
+//   2. (L, W = L⁻¹) by recursive blocked Cholesky-and-inverse  leaf + MFMA TRMM/SYRK GEMMs
+//        chol_inv(A):  (L11,W11) = chol_inv(A11);  L21 = A21 W11ᵀ;  A22 -= L21 L21ᵀ;
+//                      (L22,W22) = chol_inv(A22);  W21 = −W22 (L21 W11)
+//   3. z = W y, α = Wᵀ z                                      trmv kernels
+//   4. K⁻¹ = WᵀW formed tile by tile and contracted on the fly with (ααᵀ − K⁻¹)∘∂K/∂θ
+//   5. logML = −½‖z‖² − Σ log L_ii − (n/2) log 2π;  ∂logML/∂θ = ½ Σ (ααᵀ − K⁻¹)∘∂K/∂θ
+// Algorithmic flops per problem: N³/3 (potrf) + N³/3 (trtri) + N³/3 (WᵀW) ≈ N³.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "gpx_internal.h"
+
+using namespace gpx;
+
+struct gpx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int profiling = 0;
+};
+
+struct gpx_batch {
+  gpx_ctx* ctx = nullptr;
+  int B = 0, Nmax = 0, D = 0, Np = 0;
+  const double* X = nullptr;
+  const double* Y = nullptr;
+  std::vector<int> n;
+  std::vector<gpx_kernel_spec> specs;
+  int* d_n = nullptr;
+  DevSpec* d_specs = nullptr;
+  double* d_theta = nullptr;
+  int* d_active = nullptr;
+  int* d_info = nullptr;
+  double *K = nullptr, *L = nullptr, *W = nullptr;     // [B][Np][Np]
+  double *z = nullptr, *alpha = nullptr, *ldiag = nullptr;  // [B][Np]
+  double* partial = nullptr;       // [B][ntiles64][16]
+  long long partial_stride = 0;
+  double* results = nullptr;       // [B][kResStride]
+  // predict workspace
+  double* kxs = nullptr; size_t kxs_cap = 0;
+  double* pvp = nullptr; size_t pvp_cap = 0;
+  // factor cache: theta row of the last factorisation per problem
+  std::vector<double> fac_theta;
+  std::vector<char> fac_valid;
+  std::vector<double> h_results;
+  std::vector<int> h_info;
+  gpx_timing timing{};
+  double flops_acc = 0.0;
+};
+
+namespace {
+
+const char* kVersion = "gpx 0.1.0 (gfx950, fp64 MFMA)";
+
+int fail(gpx_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+#define HIPX(ctx, expr)                                                               \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(ctx, GPX_HIP_ERROR, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+inline long long mat_stride(const gpx_batch* bt) { return (long long)bt->Np * bt->Np; }
+
+// MFMA flops the GEMM launcher will issue for these args (bench / roofline bookkeeping)
+double gemm_issued_flops(const GemmArgs& a) {
+  const int bm = gemm_tile(a);
+  const int ti = a.M / bm, tj = a.N / bm;
+  double f = 0.0;
+  for (int x = 0; x < ti; ++x)
+    for (int y = 0; y < tj; ++y) {
+      if (a.lower_only && y > x) continue;
+      const int i0 = x * bm, j0 = y * bm;
+      int kmin = 0, kmax = a.K;
+      if (a.tri & TRI_KMAX_I) kmax = std::min(kmax, i0 + bm);
+      if (a.tri & TRI_KMAX_J) kmax = std::min(kmax, j0 + bm);
+      if (a.tri & TRI_KMIN_J) kmin = std::max(kmin, j0);
+      if (a.tri & TRI_KMIN_I) kmin = std::max(kmin, i0);
+      if (kmax > kmin) f += 2.0 * bm * bm * (kmax - kmin);
+    }
+  return f;
+}
+
+void gemm(gpx_batch* bt, GemmArgs a, int epi, bool ta, bool tb, int na, hipStream_t s) {
+  a.active = bt->d_active;
+  launch_gemm(a, epi, ta, tb, na, s);
+  if (bt->ctx->profiling) bt->flops_acc += na * gemm_issued_flops(a);
+}
+
+GemmArgs gemm_args(const double* A, int lda, const double* B, int ldb, double* C, int ldc,
+                   long long stride, int M, int N, int K, int tri, int lower, double alpha,
+                   double beta) {
+  GemmArgs g{};
+  g.A = A; g.sA = stride; g.lda = lda;
+  g.Bm = B; g.sB = stride; g.ldb = ldb;
+  g.C = C; g.sC = stride; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K; g.tri = tri; g.lower_only = lower;
+  g.alpha = alpha; g.beta = beta;
+  return g;
+}
+
+// Recursive Cholesky-and-inverse on the diagonal block [off, off+n) of every active problem.
+void chol_inv(gpx_batch* bt, int off, int n, int na, hipStream_t s) {
+  const int Np = bt->Np;
+  const long long st = mat_stride(bt);
+  if (n == kLeaf) {
+    LeafArgs la{};
+    la.active = bt->d_active; la.K = bt->K; la.W = bt->W; la.sMat = st; la.ld = Np; la.off = off;
+    la.ldiag = bt->ldiag; la.sVec = Np; la.info = bt->d_info;
+    launch_leaf(la, na, s);
+    return;
+  }
+  int n1 = ((n / 2 + kLeaf - 1) / kLeaf) * kLeaf;
+  if (n1 >= n) n1 = n - kLeaf;
+  const int n2 = n - n1;
+  chol_inv(bt, off, n1, na, s);
+  const long long o11 = (long long)off * Np + off;
+  const long long o21 = (long long)(off + n1) * Np + off;
+  const long long o22 = (long long)(off + n1) * Np + off + n1;
+  // L21 = A21 · W11ᵀ          (opB(k,j) = W11[j][k], nonzero for k <= j)
+  gemm(bt, gemm_args(bt->K + o21, Np, bt->W + o11, Np, bt->L + o21, Np, st, n2, n1, n1,
+                     TRI_KMAX_J, 0, 1.0, 0.0), EPI_STORE, false, true, na, s);
+  // A22 -= L21 · L21ᵀ         (lower tiles only)
+  gemm(bt, gemm_args(bt->L + o21, Np, bt->L + o21, Np, bt->K + o22, Np, st, n2, n2, n1, 0, 1,
+                     -1.0, 1.0), EPI_STORE, false, true, na, s);
+  chol_inv(bt, off + n1, n2, na, s);
+  // T = L21 · W11 → the dead A21 region of K   (opB(k,j) = W11[k][j], nonzero for k >= j)
+  gemm(bt, gemm_args(bt->L + o21, Np, bt->W + o11, Np, bt->K + o21, Np, st, n2, n1, n1,
+                     TRI_KMIN_J, 0, 1.0, 0.0), EPI_STORE, false, false, na, s);
+  // W21 = −W22 · T             (opA(i,k) = W22[i][k], nonzero for k <= i)
+  gemm(bt, gemm_args(bt->W + o22, Np, bt->K + o21, Np, bt->W + o21, Np, st, n2, n1, n2,
+                     TRI_KMAX_I, 0, -1.0, 0.0), EPI_STORE, false, false, na, s);
+}
+
+// K build + factor + α for the active problems (device active list already uploaded).
+void factor_and_alpha(gpx_batch* bt, int na, hipStream_t s) {
+  const long long st = mat_stride(bt);
+  BuildArgs ba{};
+  ba.active = bt->d_active; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
+  ba.X = bt->X; ba.sX = (long long)bt->Nmax * bt->D; ba.X2 = bt->X; ba.sX2 = ba.sX; ba.D = bt->D;
+  ba.m2 = 0; ba.out = bt->K; ba.sOut = st; ba.ldo = bt->Np; ba.rows = ba.cols = bt->Np;
+  ba.symmetric = 1;
+  launch_build(ba, na, s);
+  chol_inv(bt, 0, bt->Np, na, s);
+}
+
+void alpha_solve(gpx_batch* bt, int na, hipStream_t s) {
+  const long long st = mat_stride(bt);
+  TrmvArgs t{};
+  t.active = bt->d_active; t.Wm = bt->W; t.sW = st; t.ld = bt->Np;
+  t.x = bt->Y; t.sx = bt->Nmax; t.nvalid = bt->d_n; t.y = bt->z; t.sy = bt->Np;
+  t.rows = t.cols = bt->Np; t.lower = 1;
+  launch_trmv_n(t, na, s);
+  TrmvArgs u{};
+  u.active = bt->d_active; u.Wm = bt->W; u.sW = st; u.ld = bt->Np;
+  u.x = bt->z; u.sx = bt->Np; u.nvalid = nullptr; u.y = bt->alpha; u.sy = bt->Np;
+  u.rows = u.cols = bt->Np; u.lower = 1;
+  launch_trmv_t(u, na, s);
+}
+
+struct PhaseTimer {
+  bool on;
+  hipStream_t s;
+  std::vector<hipEvent_t> ev;
+  PhaseTimer(bool enabled, hipStream_t st) : on(enabled), s(st) {}
+  void mark() {
+    if (!on) return;
+    hipEvent_t e;
+    hipEventCreate(&e);
+    hipEventRecord(e, s);
+    ev.push_back(e);
+  }
+  double ms(int i, int j) {
+    float t = 0.f;
+    hipEventElapsedTime(&t, ev[i], ev[j]);
+    return t;
+  }
+  ~PhaseTimer() {
+    for (auto e : ev) hipEventDestroy(e);
+  }
+};
+
+int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                  hipStream_t s) {
+  gpx_ctx* ctx = bt->ctx;
+  if (n_active <= 0 || n_active > bt->B || !active || !theta)
+    return fail(ctx, GPX_BAD_ARG, "bad active set / theta");
+  for (int i = 0; i < n_active; ++i)
+    if (active[i] < 0 || active[i] >= bt->B) return fail(ctx, GPX_BAD_ARG, "active index out of range");
+  for (int i = 0; i < n_active; ++i) {
+    const int b = active[i];
+    const int np = bt->specs[b].n_params;
+    for (int p = 0; p <= np; ++p) {
+      const double v = theta[(size_t)b * GPX_THETA_STRIDE + p];
+      if (!(v > 0.0) || !std::isfinite(v))
+        return fail(ctx, GPX_BAD_ARG, "theta must be finite and > 0 (constrained space)");
+    }
+  }
+  HIPX(ctx, hipMemcpyAsync(bt->d_active, active, sizeof(int) * n_active, hipMemcpyHostToDevice, s));
+  HIPX(ctx, hipMemcpyAsync(bt->d_theta, theta, sizeof(double) * GPX_THETA_STRIDE * bt->B,
+                           hipMemcpyHostToDevice, s));
+  HIPX(ctx, hipMemsetAsync(bt->d_info, 0, sizeof(int) * bt->B, s));
+  return GPX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gpx_version(void) { return kVersion; }
+
+int gpx_create(int device, gpx_ctx** out) {
+  if (!out) return GPX_BAD_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return GPX_HIP_ERROR;
+  if (device < 0 || device >= ndev) return GPX_BAD_ARG;
+  if (hipSetDevice(device) != hipSuccess) return GPX_HIP_ERROR;
+  gpx_ctx* c = new gpx_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return GPX_HIP_ERROR;
+  }
+  *out = c;
+  return GPX_OK;
+}
+
+int gpx_destroy(gpx_ctx* ctx) {
+  if (!ctx) return GPX_BAD_ARG;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return GPX_OK;
+}
+
+const char* gpx_last_error(const gpx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int gpx_set_profiling(gpx_ctx* ctx, int enabled) {
+  if (!ctx) return GPX_BAD_ARG;
+  ctx->profiling = enabled;
+  return GPX_OK;
+}
+
+int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, const double* Y,
+                     const int32_t* n, const gpx_kernel_spec* specs, gpx_batch** out) {
+  if (!ctx || !out) return GPX_BAD_ARG;
+  *out = nullptr;
+  if (B <= 0 || N_max <= 0 || D <= 0 || D > GPX_MAX_DIM || !X || !Y || !n || !specs)
+    return fail(ctx, GPX_BAD_ARG, "bad batch dimensions or null pointer");
+  for (int b = 0; b < B; ++b) {
+    if (n[b] < 1 || n[b] > N_max) return fail(ctx, GPX_BAD_ARG, "n[b] must be in [1, N_max]");
+    const gpx_kernel_spec& sp = specs[b];
+    if (sp.n_terms < 1 || sp.n_terms > GPX_MAX_TERMS || sp.n_params < 1 ||
+        sp.n_params >= GPX_THETA_STRIDE)
+      return fail(ctx, GPX_BAD_ARG, "bad kernel spec");
+    for (int t = 0; t < sp.n_terms; ++t) {
+      const gpx_term& tm = sp.terms[t];
+      const int np = (tm.kind == GPX_RQ || tm.kind == GPX_PERIODIC_SE) ? 3 : (tm.kind == GPX_LINEAR ? 1 : 2);
+      if (tm.kind < GPX_SE || tm.kind > GPX_LINEAR || tm.dim_start < 0 || tm.dim_count < 1 ||
+          tm.dim_start + tm.dim_count > D || tm.param_offset < 0 || tm.param_offset + np > sp.n_params)
+        return fail(ctx, GPX_BAD_ARG, "bad kernel term");
+    }
+  }
+  HIPX(ctx, hipSetDevice(ctx->device));
+  gpx_batch* bt = new gpx_batch();
+  bt->ctx = ctx; bt->B = B; bt->Nmax = N_max; bt->D = D;
+  bt->Np = ((N_max + kLeaf - 1) / kLeaf) * kLeaf;
+  bt->X = X; bt->Y = Y;
+  bt->n.assign(n, n + B);
+  bt->specs.assign(specs, specs + B);
+  const size_t mat = (size_t)B * bt->Np * bt->Np * sizeof(double);
+  const size_t vec = (size_t)B * bt->Np * sizeof(double);
+  const int t64 = bt->Np / 64;
+  bt->partial_stride = (long long)t64 * (t64 + 1) / 2 * GPX_THETA_STRIDE;
+  auto cleanup = [&](const std::string& m) {
+    gpx_batch_destroy(bt);
+    return fail(ctx, GPX_HIP_ERROR, m);
+  };
+  if (hipMalloc(&bt->K, mat) != hipSuccess || hipMalloc(&bt->L, mat) != hipSuccess ||
+      hipMalloc(&bt->W, mat) != hipSuccess)
+    return cleanup("out of device memory for K/L/W workspace");
+  if (hipMalloc(&bt->z, vec) != hipSuccess || hipMalloc(&bt->alpha, vec) != hipSuccess ||
+      hipMalloc(&bt->ldiag, vec) != hipSuccess ||
+      hipMalloc(&bt->partial, (size_t)B * bt->partial_stride * sizeof(double)) != hipSuccess ||
+      hipMalloc(&bt->results, (size_t)B * kResStride * sizeof(double)) != hipSuccess ||
+      hipMalloc(&bt->d_n, sizeof(int) * B) != hipSuccess ||
+      hipMalloc(&bt->d_specs, sizeof(DevSpec) * B) != hipSuccess ||
+      hipMalloc(&bt->d_theta, sizeof(double) * GPX_THETA_STRIDE * B) != hipSuccess ||
+      hipMalloc(&bt->d_active, sizeof(int) * B) != hipSuccess ||
+      hipMalloc(&bt->d_info, sizeof(int) * B) != hipSuccess)
+    return cleanup("out of device memory for batch vectors");
+  // W and L upper triangles must read as exact zeros (never written afterwards)
+  if (hipMemset(bt->W, 0, mat) != hipSuccess || hipMemset(bt->L, 0, mat) != hipSuccess ||
+      hipMemset(bt->K, 0, mat) != hipSuccess)
+    return cleanup("memset failed");
+  std::vector<DevSpec> ds(B);
+  for (int b = 0; b < B; ++b) std::memcpy(&ds[b], &specs[b], sizeof(DevSpec));
+  static_assert(sizeof(DevSpec) == sizeof(gpx_kernel_spec), "spec layout");
+  if (hipMemcpy(bt->d_specs, ds.data(), sizeof(DevSpec) * B, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(bt->d_n, n, sizeof(int) * B, hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup("upload failed");
+  bt->fac_theta.assign((size_t)B * GPX_THETA_STRIDE, 0.0);
+  bt->fac_valid.assign(B, 0);
+  bt->h_results.assign((size_t)B * kResStride, 0.0);
+  bt->h_info.assign(B, 0);
+  *out = bt;
+  return GPX_OK;
+}
+
+int gpx_batch_destroy(gpx_batch* bt) {
+  if (!bt) return GPX_BAD_ARG;
+  hipSetDevice(bt->ctx->device);
+  for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
+                  (void*)bt->ldiag, (void*)bt->partial, (void*)bt->results, (void*)bt->d_n,
+                  (void*)bt->d_specs, (void*)bt->d_theta, (void*)bt->d_active, (void*)bt->d_info,
+                  (void*)bt->kxs, (void*)bt->pvp})
+    if (p) hipFree(p);
+  delete bt;
+  return GPX_OK;
+}
+
+int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                       double* lml, double* grad, int32_t* info, void* stream) {
+  if (!bt) return GPX_BAD_ARG;
+  gpx_ctx* ctx = bt->ctx;
+  if (!lml || !grad || !info) return fail(ctx, GPX_BAD_ARG, "null output");
+  HIPX(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  int rc = upload_common(bt, n_active, active, theta, s);
+  if (rc != GPX_OK) return rc;
+  const int na = n_active;
+  PhaseTimer pt(ctx->profiling != 0, s);
+  bt->flops_acc = 0.0;
+  pt.mark();
+  factor_and_alpha(bt, na, s);
+  pt.mark();
+  alpha_solve(bt, na, s);
+  pt.mark();
+  // fused K⁻¹ = WᵀW + gradient contraction over lower tiles
+  GemmArgs g = gemm_args(bt->W, bt->Np, bt->W, bt->Np, nullptr, 0, mat_stride(bt), bt->Np, bt->Np,
+                         bt->Np, TRI_KMIN_I, 1, 1.0, 0.0);
+  g.vec = bt->alpha; g.sVec = bt->Np; g.X = bt->X; g.sX = (long long)bt->Nmax * bt->D; g.D = bt->D;
+  g.specs = bt->d_specs; g.theta = bt->d_theta; g.nvalid = bt->d_n;
+  g.partial = bt->partial; g.sPartial = bt->partial_stride;
+  gemm(bt, g, EPI_CONTRACT, true, false, na, s);
+  const int bm = gemm_tile(g), tt = bt->Np / bm;
+  ReduceArgs r{};
+  r.active = bt->d_active; r.partial = bt->partial; r.sPartial = bt->partial_stride;
+  r.ntiles = tt * (tt + 1) / 2; r.z = bt->z; r.sVec = bt->Np; r.ldiag = bt->ldiag;
+  r.nvalid = bt->d_n; r.specs = bt->d_specs; r.results = bt->results; r.Np = bt->Np;
+  launch_reduce(r, na, s);
+  pt.mark();
+  HIPX(ctx, hipGetLastError());
+  HIPX(ctx, hipMemcpyAsync(bt->h_results.data(), bt->results, sizeof(double) * kResStride * bt->B,
+                           hipMemcpyDeviceToHost, s));
+  HIPX(ctx, hipMemcpyAsync(bt->h_info.data(), bt->d_info, sizeof(int) * bt->B, hipMemcpyDeviceToHost, s));
+  HIPX(ctx, hipStreamSynchronize(s));
+  if (pt.on) {
+    bt->timing.factor_ms = pt.ms(0, 1);
+    bt->timing.alpha_ms = pt.ms(1, 2);
+    bt->timing.grad_ms = pt.ms(2, 3);
+    bt->timing.predict_ms = 0.0;
+    bt->timing.total_ms = pt.ms(0, 3);
+    bt->timing.gemm_flops = bt->flops_acc;
+  }
+  int status = GPX_OK;
+  for (int i = 0; i < na; ++i) {
+    const int b = active[i];
+    const double* res = bt->h_results.data() + (size_t)b * kResStride;
+    info[b] = bt->h_info[b];
+    const int np = bt->specs[b].n_params;
+    if (info[b] != 0) {
+      status = GPX_NOT_PD;
+      lml[b] = NAN;
+      for (int p = 0; p <= np; ++p) grad[(size_t)b * GPX_THETA_STRIDE + p] = NAN;
+      bt->fac_valid[b] = 0;
+      continue;
+    }
+    lml[b] = res[0];
+    for (int p = 0; p <= np; ++p) grad[(size_t)b * GPX_THETA_STRIDE + p] = res[1 + p];
+    std::memcpy(&bt->fac_theta[(size_t)b * GPX_THETA_STRIDE], theta + (size_t)b * GPX_THETA_STRIDE,
+                sizeof(double) * GPX_THETA_STRIDE);
+    bt->fac_valid[b] = 1;
+  }
+  if (status == GPX_NOT_PD) ctx->err = "K + noise*I is not positive definite for some problem";
+  return status;
+}
+
+int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                      const double* Xnew, int M, int add_noise, double* mean, double* var,
+                      int32_t* info, void* stream) {
+  if (!bt) return GPX_BAD_ARG;
+  gpx_ctx* ctx = bt->ctx;
+  if (!Xnew || M <= 0 || !mean || !var || !info) return fail(ctx, GPX_BAD_ARG, "bad predict args");
+  HIPX(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  int rc = upload_common(bt, n_active, active, theta, s);
+  if (rc != GPX_OK) return rc;
+  PhaseTimer pt(ctx->profiling != 0, s);
+  bt->flops_acc = 0.0;
+  pt.mark();
+  // re-factorise the problems whose cached factor is not at exactly this theta
+  std::vector<int> refac;
+  for (int i = 0; i < n_active; ++i) {
+    const int b = active[i];
+    const bool same = bt->fac_valid[b] &&
+                      std::memcmp(&bt->fac_theta[(size_t)b * GPX_THETA_STRIDE],
+                                  theta + (size_t)b * GPX_THETA_STRIDE,
+                                  sizeof(double) * GPX_THETA_STRIDE) == 0;
+    if (!same) refac.push_back(b);
+  }
+  if (!refac.empty()) {
+    HIPX(ctx, hipMemcpyAsync(bt->d_active, refac.data(), sizeof(int) * refac.size(),
+                             hipMemcpyHostToDevice, s));
+    factor_and_alpha(bt, (int)refac.size(), s);
+    alpha_solve(bt, (int)refac.size(), s);
+    HIPX(ctx, hipMemcpyAsync(bt->d_active, active, sizeof(int) * n_active, hipMemcpyHostToDevice, s));
+  }
+  pt.mark();
+  const int Np = bt->Np;
+  const int Mp = ((M + 63) / 64) * 64;
+  // cross-covariance workspace [B][Np][Mp]
+  const size_t need = (size_t)bt->B * Np * Mp;
+  double* kxs;
+  if ((size_t)Mp <= (size_t)Np) {
+    kxs = bt->L;  // L is dead once W is formed
+    for (int b : refac) (void)b;
+  } else {
+    if (bt->kxs_cap < need) {
+      if (bt->kxs) hipFree(bt->kxs);
+      bt->kxs = nullptr; bt->kxs_cap = 0;
+      HIPX(ctx, hipMalloc(&bt->kxs, need * sizeof(double)));
+      bt->kxs_cap = need;
+    }
+    kxs = bt->kxs;
+  }
+  const long long skx = (long long)Np * Mp;
+  BuildArgs ba{};
+  ba.active = bt->d_active; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
+  ba.X = bt->X; ba.sX = (long long)bt->Nmax * bt->D; ba.X2 = Xnew; ba.sX2 = (long long)M * bt->D;
+  ba.D = bt->D; ba.m2 = M; ba.out = kxs; ba.sOut = skx; ba.ldo = Mp; ba.rows = Np; ba.cols = Mp;
+  ba.symmetric = 0;
+  launch_build(ba, n_active, s);
+  // mean = Kxsᵀ α
+  TrmvArgs t{};
+  t.active = bt->d_active; t.Wm = kxs; t.sW = skx; t.ld = Mp; t.x = bt->alpha; t.sx = Np;
+  t.nvalid = nullptr; t.y = mean; t.sy = M; t.rows = Np; t.cols = M; t.lower = 0;
+  launch_trmv_t(t, n_active, s);
+  // A = W · Kxs with fused column sum of squares
+  GemmArgs g = gemm_args(bt->W, Np, kxs, Mp, nullptr, Mp, 0, Np, Mp, Np, TRI_KMAX_I, 0, 1.0, 0.0);
+  g.sA = mat_stride(bt); g.sB = skx; g.sC = 0;
+  const int bm = gemm_tile(g);
+  const int nrt = Np / bm;
+  const size_t pneed = (size_t)bt->B * nrt * Mp;
+  if (bt->pvp_cap < pneed) {
+    if (bt->pvp) hipFree(bt->pvp);
+    bt->pvp = nullptr; bt->pvp_cap = 0;
+    HIPX(ctx, hipMalloc(&bt->pvp, pneed * sizeof(double)));
+    bt->pvp_cap = pneed;
+  }
+  g.partial = bt->pvp; g.sPartial = (long long)nrt * Mp;
+  gemm(bt, g, EPI_COLSUMSQ, false, false, n_active, s);
+  PredVarArgs pv{};
+  pv.active = bt->d_active; pv.partial = bt->pvp; pv.sPartial = (long long)nrt * Mp;
+  pv.nrowtiles = nrt; pv.ldp = Mp; pv.Xnew = Xnew; pv.sXnew = (long long)M * bt->D; pv.D = bt->D;
+  pv.specs = bt->d_specs; pv.theta = bt->d_theta; pv.M = M; pv.add_noise = add_noise;
+  pv.var = var; pv.sVar = M;
+  launch_predvar(pv, n_active, s);
+  pt.mark();
+  HIPX(ctx, hipGetLastError());
+  HIPX(ctx, hipMemcpyAsync(bt->h_info.data(), bt->d_info, sizeof(int) * bt->B, hipMemcpyDeviceToHost, s));
+  HIPX(ctx, hipStreamSynchronize(s));
+  if (pt.on) {
+    bt->timing.factor_ms = pt.ms(0, 1);
+    bt->timing.alpha_ms = 0.0;
+    bt->timing.grad_ms = 0.0;
+    bt->timing.predict_ms = pt.ms(1, 2);
+    bt->timing.total_ms = pt.ms(0, 2);
+    bt->timing.gemm_flops = bt->flops_acc;
+  }
+  int status = GPX_OK;
+  for (int i = 0; i < n_active; ++i) {
+    const int b = active[i];
+    // info is only (re)computed for re-factorised problems; cached ones were OK
+    const bool was_refac = std::find(refac.begin(), refac.end(), b) != refac.end();
+    info[b] = was_refac ? bt->h_info[b] : 0;
+    if (info[b] != 0) {
+      status = GPX_NOT_PD;
+      bt->fac_valid[b] = 0;
+    } else if (was_refac) {
+      std::memcpy(&bt->fac_theta[(size_t)b * GPX_THETA_STRIDE], theta + (size_t)b * GPX_THETA_STRIDE,
+                  sizeof(double) * GPX_THETA_STRIDE);
+      bt->fac_valid[b] = 1;
+    }
+  }
+  if (status == GPX_NOT_PD) ctx->err = "K + noise*I is not positive definite for some problem";
+  return status;
+}
+
+int gpx_batch_last_timing(const gpx_batch* bt, gpx_timing* out) {
+  if (!bt || !out) return GPX_BAD_ARG;
+  *out = bt->timing;
+  return GPX_OK;
+}
+
+}  // extern "C"

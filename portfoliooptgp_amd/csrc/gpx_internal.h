@@ -1,0 +1,96 @@
+// gpx_internal.h — launch arguments and launcher entry points shared by gpx_api.hip and
+// gpx_kernels.hip. Not part of the public ABI (include/gpx.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "gpx_kfun.h"
+
+namespace gpx {
+
+constexpr int kLeaf = 64;      // diagonal-block size of the recursive Cholesky-and-inverse
+constexpr int kResStride = 32; // results row: [0]=lml, [1..16]=grad, [17]=yᵀK⁻¹y, [18]=Σlog L_ii
+
+// ---- K / cross-covariance build -------------------------------------------------------
+struct BuildArgs {
+  const int* active;
+  const DevSpec* specs;
+  const double* theta;     // [B][16] device
+  const int* nvalid;       // [B] valid rows (training points)
+  const double* X; long long sX;   // row points: X + b*sX, [rows][D]
+  const double* X2; long long sX2; // column points (cross mode)
+  int D;
+  int m2;                  // valid columns in cross mode
+  double* out; long long sOut; int ldo;
+  int rows, cols;          // padded, multiples of 64
+  int symmetric;           // 1: lower tiles of K(X,X)+σn²I with identity padding
+};
+
+// ---- leaf: 64x64 Cholesky + triangular inverse in LDS --------------------------------
+struct LeafArgs {
+  const int* active;
+  const double* K; double* W; long long sMat; int ld; int off;
+  double* ldiag; long long sVec;   // log L_ii, [B][Np]
+  int* info;                       // [B], first failing pivot (1-based), 0 = ok
+};
+
+// ---- batched fp64 MFMA GEMM -----------------------------------------------------------
+enum : int { TRI_KMAX_I = 1, TRI_KMAX_J = 2, TRI_KMIN_J = 4, TRI_KMIN_I = 8 };
+enum : int { EPI_STORE = 0, EPI_CONTRACT = 1, EPI_COLSUMSQ = 2 };
+
+struct GemmArgs {
+  const int* active;
+  const double* A; long long sA; int lda;   // opA(i,k) = A[i*lda+k] (N) or A[k*lda+i] (T)
+  const double* Bm; long long sB; int ldb;  // opB(k,j) = B[k*ldb+j] (N) or B[j*ldb+k] (T)
+  double* C; long long sC; int ldc;
+  int M, N, K;
+  int tri;            // TRI_* flags restricting the k range per tile
+  int lower_only;     // only tiles with ti >= tj
+  double alpha, beta;
+  // EPI_CONTRACT
+  const double* vec; long long sVec;        // α vectors [B][Np]
+  const double* X; long long sX; int D;
+  const DevSpec* specs; const double* theta; const int* nvalid;
+  double* partial; long long sPartial;      // [B][ntiles][16] / [B][rowtiles][ldc]
+};
+
+// ---- vectors --------------------------------------------------------------------------
+struct TrmvArgs {
+  const int* active;
+  const double* Wm; long long sW; int ld;
+  const double* x; long long sx;   // input vector
+  const int* nvalid;               // mask input x beyond n (for y); may be null
+  double* y; long long sy;         // output
+  int rows, cols;                  // operator dims
+  int lower;                       // 1: triangular (skip known zeros)
+};
+
+struct ReduceArgs {
+  const int* active;
+  const double* partial; long long sPartial; int ntiles;
+  const double* z; long long sVec;
+  const double* ldiag;
+  const int* nvalid;
+  const DevSpec* specs;
+  double* results;   // [B][kResStride]
+  int Np;
+};
+
+struct PredVarArgs {
+  const int* active;
+  const double* partial; long long sPartial; int nrowtiles; int ldp;
+  const double* Xnew; long long sXnew; int D;
+  const DevSpec* specs; const double* theta;
+  int M; int add_noise;
+  double* var; long long sVar;
+};
+
+void launch_build(const BuildArgs& a, int n_active, hipStream_t s);
+void launch_leaf(const LeafArgs& a, int n_active, hipStream_t s);
+void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hipStream_t s);
+void launch_trmv_n(const TrmvArgs& a, int n_active, hipStream_t s);   // y = M x   (row dots)
+void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s);   // y = Mᵀ x  (column sums)
+void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s);
+void launch_predvar(const PredVarArgs& a, int n_active, hipStream_t s);
+int gemm_tile(const GemmArgs& a);  // tile edge the launcher will use (64 or 128)
+
+}  // namespace gpx

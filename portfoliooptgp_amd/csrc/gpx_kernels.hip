@@ -1,0 +1,553 @@
+// gpx_kernels.hip — CDNA4 (gfx950) kernels of the exact-GP engine, all fp64.
+//
+// Per loss+gradient evaluation (one L-BFGS-B function call of gpflow.optimizers.Scipy,
+// GPR/model_trainer.py:18-19) the host drives, for a batch of independent problems:
+//   build_kernel        K = k(X,X) + σn² I, lower 64x64 tiles, identity padding to Np
+//   leaf_kernel         64x64 diagonal block: Cholesky + triangular inverse, in LDS
+//   gemm_kernel<...>    fp64 MFMA (v_mfma_f64_16x16x4_f64) tile GEMM, batched over problems:
+//                       the TRMM/SYRK steps of the recursive Cholesky-and-inverse and the
+//                       fused K⁻¹ = WᵀW formation + gradient contraction (EPI_CONTRACT)
+//   trmv_n/trmv_t       z = W y, α = Wᵀ z  (W = L⁻¹)
+//   reduce_kernel       logML and ½Σ(αα−K⁻¹)∘∂K/∂θ from per-tile partials (deterministic)
+// and for predict_f: the cross-covariance build, mean = Kxsᵀα, and W·Kxs with a fused
+// column-sum-of-squares epilogue (EPI_COLSUMSQ) for the variance.
+#include "gpx_internal.h"
+
+namespace gpx {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+// linear index -> (ti, tj) of the lower-triangular tile enumeration (ti >= tj)
+__device__ __forceinline__ void lower_tile(int idx, int& ti, int& tj) {
+  int t = (int)((sqrt(8.0 * (double)idx + 1.0) - 1.0) * 0.5);
+  while ((t + 1) * (t + 2) / 2 <= idx) ++t;
+  while (t * (t + 1) / 2 > idx) --t;
+  ti = t;
+  tj = idx - t * (t + 1) / 2;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ======================================================================================
+// K build (and cross-covariance Kxs for predict)
+// ======================================================================================
+__global__ __launch_bounds__(256) void build_kernel(BuildArgs a) {
+  const int b = a.active[blockIdx.y];
+  int ti, tj;
+  if (a.symmetric) {
+    lower_tile(blockIdx.x, ti, tj);
+  } else {
+    const int ntj = a.cols / 64;
+    ti = blockIdx.x / ntj;
+    tj = blockIdx.x - ti * ntj;
+  }
+  __shared__ double sxi[64 * GPX_MAX_DIM];
+  __shared__ double sxj[64 * GPX_MAX_DIM];
+  __shared__ double sth[GPX_THETA_STRIDE];
+  const int D = a.D, tid = threadIdx.x;
+  const int n = a.nvalid[b];
+  const int ncol = a.symmetric ? n : a.m2;
+  const double* X = a.X + (long long)b * a.sX;
+  const double* X2 = a.symmetric ? X : a.X2 + (long long)b * a.sX2;
+  for (int e = tid; e < 64 * D; e += 256) {
+    const int r = e / D, d = e - (e / D) * D;
+    const int gi = ti * 64 + r, gj = tj * 64 + r;
+    sxi[e] = gi < n ? X[(long long)gi * D + d] : 0.0;
+    sxj[e] = gj < ncol ? X2[(long long)gj * D + d] : 0.0;
+  }
+  if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
+  __syncthreads();
+  const DevSpec spec = a.specs[b];
+  const double noise = sth[spec.n_params];
+  double* out = a.out + (long long)b * a.sOut;
+  const int c = tid & 63;
+  const int gj = tj * 64 + c;
+#pragma unroll 4
+  for (int q = 0; q < 16; ++q) {
+    const int r = (tid >> 6) + 4 * q;
+    const int gi = ti * 64 + r;
+    double v;
+    if (a.symmetric) {
+      if (gi < n && gj < n) {
+        v = eval_k(spec, sth, sxi + r * D, sxj + c * D);
+        if (gi == gj) v += noise;
+      } else {
+        v = (gi == gj) ? 1.0 : 0.0;
+      }
+    } else {
+      v = (gi < n && gj < ncol) ? eval_k(spec, sth, sxi + r * D, sxj + c * D) : 0.0;
+    }
+    out[(long long)gi * a.ldo + gj] = v;
+  }
+}
+
+void launch_build(const BuildArgs& a, int n_active, hipStream_t s) {
+  const int ti = a.rows / 64, tj = a.cols / 64;
+  const int ntiles = a.symmetric ? ti * (ti + 1) / 2 : ti * tj;
+  hipLaunchKernelGGL(build_kernel, dim3(ntiles, n_active), dim3(256), 0, s, a);
+}
+
+// ======================================================================================
+// Leaf: Cholesky of the 64x64 diagonal block at (off, off) of the (already updated) K,
+// then W11 = L11⁻¹. Writes W11 (zeros above the diagonal) and log L_ii. One WG per problem.
+// ======================================================================================
+__global__ __launch_bounds__(256) void leaf_kernel(LeafArgs a) {
+  const int b = a.active[blockIdx.x];
+  __shared__ double sL[64][65];
+  __shared__ double sW[64][65];
+  __shared__ double sd[64];
+  const double* K = a.K + (long long)b * a.sMat;
+  double* W = a.W + (long long)b * a.sMat;
+  const int ld = a.ld, off = a.off, tid = threadIdx.x;
+  for (int e = tid; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    sL[r][c] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
+  }
+  __syncthreads();
+  int fail = -1;
+  for (int j = 0; j < 64; ++j) {
+    const double d = sL[j][j];
+    if (!(d > 0.0) && fail < 0) fail = j;
+    const double ljj = sqrt(d);
+    if (tid > j && tid < 64) sL[tid][j] = sL[tid][j] / ljj;
+    if (tid == 0) sd[j] = ljj;
+    __syncthreads();
+    for (int e = tid; e < 4096; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      if (c > j && c <= r) sL[r][c] = fma(-sL[r][j], sL[c][j], sL[r][c]);
+    }
+    __syncthreads();
+  }
+  if (tid < 64) sL[tid][tid] = sd[tid];
+  __syncthreads();
+  // W = L⁻¹ by forward substitution; thread j owns column j (W[k][j] = 0 for k < j).
+  if (tid < 64) {
+    const int j = tid;
+    for (int i = 0; i < 64; ++i) {
+      double s = 0.0;
+      for (int k = 0; k < i; ++k) s = fma(sL[i][k], sW[k][j], s);
+      const double v = (i < j) ? 0.0 : (i == j ? 1.0 / sL[i][i] : -s / sL[i][i]);
+      sW[i][j] = v;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    W[(long long)(off + r) * ld + off + c] = sW[r][c];
+  }
+  if (tid < 64) a.ldiag[(long long)b * a.sVec + off + tid] = log(sd[tid]);
+  if (tid == 0 && fail >= 0 && a.info[b] == 0) a.info[b] = off + fail + 1;
+}
+
+void launch_leaf(const LeafArgs& a, int n_active, hipStream_t s) {
+  hipLaunchKernelGGL(leaf_kernel, dim3(n_active), dim3(256), 0, s, a);
+}
+
+// ======================================================================================
+// Batched fp64 MFMA GEMM: C(tile) = alpha * Σ_k opA(i,k) opB(k,j) + beta * C, with
+// per-tile k-range restriction for triangular operands and three epilogues.
+// 256 threads = 4 waves in a 2x2 arrangement, each wave (BM/2)x(BM/2) of 16x16 MFMA tiles.
+// Operands are staged global -> registers -> LDS (double-buffered, one barrier per K-tile)
+// into [k][row] images whose row stride S ≡ 16 (mod 32) doubles makes the fragment reads
+// (lanes 0-15 consecutive rows, lanes 16-31 next k) bank-conflict free for ds_read_b64.
+// v_mfma_f64_16x16x4_f64: lane l holds A[l&15][l>>4], B[l>>4][l&15]; result register r of
+// lane l is C[(l>>4) + 4r][l&15] (verified on gfx950, tools/probe_f64.hip).
+// ======================================================================================
+template <int BM, bool TA, bool TB, int EPI>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
+  constexpr int BN = BM, BK = 16, S = BM + 16;
+  constexpr int WT = BM / 2;
+  constexpr int MT = WT / 16;
+  constexpr int NLD = BM * BK / 2 / 256;  // double2 chunks per thread per operand
+  __shared__ __attribute__((aligned(16))) double smem[2 * 2 * BK * S];
+
+  const int b = a.active[blockIdx.y];
+  int ti, tj;
+  if (a.lower_only) {
+    lower_tile(blockIdx.x, ti, tj);
+  } else {
+    const int ntj = a.N / BN;
+    ti = blockIdx.x / ntj;
+    tj = blockIdx.x - ti * ntj;
+  }
+  const int i0 = ti * BM, j0 = tj * BN;
+  int kmin = 0, kmax = a.K;
+  if (a.tri & TRI_KMAX_I) kmax = min(kmax, i0 + BM);
+  if (a.tri & TRI_KMAX_J) kmax = min(kmax, j0 + BN);
+  if (a.tri & TRI_KMIN_J) kmin = max(kmin, j0);
+  if (a.tri & TRI_KMIN_I) kmin = max(kmin, i0);
+
+  const double* __restrict__ A = a.A + (long long)b * a.sA;
+  const double* __restrict__ B = a.Bm + (long long)b * a.sB;
+  const long long lda = a.lda, ldb = a.ldb;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+
+  d4 acc[MT][MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < MT; ++n) acc[m][n] = (d4){0.0, 0.0, 0.0, 0.0};
+
+  d2 ra[NLD], rb[NLD];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int c = tid + 256 * q;
+      if (!TA) {
+        const int row = c >> 3, kc = (c & 7) * 2;
+        ra[q] = *reinterpret_cast<const d2*>(A + (long long)(i0 + row) * lda + k0 + kc);
+      } else {
+        const int krow = c / (BM / 2), ic = (c % (BM / 2)) * 2;
+        ra[q] = *reinterpret_cast<const d2*>(A + (long long)(k0 + krow) * lda + i0 + ic);
+      }
+      if (TB) {
+        const int row = c >> 3, kc = (c & 7) * 2;
+        rb[q] = *reinterpret_cast<const d2*>(B + (long long)(j0 + row) * ldb + k0 + kc);
+      } else {
+        const int krow = c / (BN / 2), jc = (c % (BN / 2)) * 2;
+        rb[q] = *reinterpret_cast<const d2*>(B + (long long)(k0 + krow) * ldb + j0 + jc);
+      }
+    }
+  };
+  auto swrite = [&](int buf) {
+    double* sA = smem + (buf * 2 + 0) * BK * S;
+    double* sB = smem + (buf * 2 + 1) * BK * S;
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int c = tid + 256 * q;
+      if (!TA) {
+        const int row = c >> 3, kc = (c & 7) * 2;
+        sA[kc * S + row] = ra[q].x;
+        sA[(kc + 1) * S + row] = ra[q].y;
+      } else {
+        const int krow = c / (BM / 2), ic = (c % (BM / 2)) * 2;
+        *reinterpret_cast<d2*>(sA + krow * S + ic) = ra[q];
+      }
+      if (TB) {
+        const int row = c >> 3, kc = (c & 7) * 2;
+        sB[kc * S + row] = rb[q].x;
+        sB[(kc + 1) * S + row] = rb[q].y;
+      } else {
+        const int krow = c / (BN / 2), jc = (c % (BN / 2)) * 2;
+        *reinterpret_cast<d2*>(sB + krow * S + jc) = rb[q];
+      }
+    }
+  };
+
+  const int nk = (kmax - kmin) / BK;
+  if (nk > 0) {
+    gload(kmin);
+    swrite(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) gload(kmin + (kt + 1) * BK);
+      const double* sA = smem + (cur * 2 + 0) * BK * S;
+      const double* sB = smem + (cur * 2 + 1) * BK * S;
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        const int kr = (kk * 4 + (lane >> 4)) * S + (lane & 15);
+        double af[MT], bf[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) af[m] = sA[kr + wr * WT + m * 16];
+#pragma unroll
+        for (int n = 0; n < MT; ++n) bf[n] = sB[kr + wc * WT + n * 16];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int n = 0; n < MT; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
+      }
+      if (kt + 1 < nk) swrite(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  if constexpr (EPI == EPI_STORE) {
+    double* C = a.C + (long long)b * a.sC;
+    const long long ldc = a.ldc;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < MT; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + wr * WT + m * 16 + (lane >> 4) + 4 * r;
+          const int j = j0 + wc * WT + n * 16 + (lane & 15);
+          double v = a.alpha * acc[m][n][r];
+          if (a.beta != 0.0) v = fma(a.beta, C[i * ldc + j], v);
+          C[i * ldc + j] = v;
+        }
+  } else if constexpr (EPI == EPI_CONTRACT) {
+    // Gradient contraction over this lower tile of K⁻¹ = WᵀW (acc = K⁻¹_ij):
+    //   g_θ += w_ij (α_i α_j − K⁻¹_ij) ∂K_ij/∂θ,  w = 2 below the diagonal, 1 on it.
+    const int D = a.D;
+    double* sxi = smem;                   // [BM][D]
+    double* sxj = sxi + BM * D;           // [BN][D]
+    double* sai = sxj + BN * D;           // [BM]
+    double* saj = sai + BM;               // [BN]
+    double* sth = saj + BN;               // [16]
+    double* sred = sth + GPX_THETA_STRIDE;  // [4 waves][16]
+    __syncthreads();
+    const int n = a.nvalid[b];
+    const double* X = a.X + (long long)b * a.sX;
+    const double* al = a.vec + (long long)b * a.sVec;
+    for (int e = tid; e < BM * D; e += 256) {
+      const int r = e / D, d = e - (e / D) * D;
+      sxi[e] = (i0 + r < n) ? X[(long long)(i0 + r) * D + d] : 0.0;
+      sxj[e] = (j0 + r < n) ? X[(long long)(j0 + r) * D + d] : 0.0;
+    }
+    if (tid < BM) { sai[tid] = al[i0 + tid]; saj[tid] = al[j0 + tid]; }
+    if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
+    __syncthreads();
+    const DevSpec spec = a.specs[b];
+    double sums[GPX_MAX_TERMS][3];
+#pragma unroll
+    for (int t = 0; t < GPX_MAX_TERMS; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
+    double snoise = 0.0;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int nn = 0; nn < MT; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int il = wr * WT + m * 16 + (lane >> 4) + 4 * r;
+          const int jl = wc * WT + nn * 16 + (lane & 15);
+          const int i = i0 + il, j = j0 + jl;
+          if (i >= j && i < n) {
+            const double w = (i == j) ? 1.0 : 2.0;
+            const double v = w * fma(sai[il], saj[jl], -acc[m][nn][r]);
+            double dk[GPX_MAX_TERMS][3];
+            eval_k_grad(spec, sth, sxi + il * D, sxj + jl * D, dk);
+#pragma unroll
+            for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+              sums[t][0] = fma(v, dk[t][0], sums[t][0]);
+              sums[t][1] = fma(v, dk[t][1], sums[t][1]);
+              sums[t][2] = fma(v, dk[t][2], sums[t][2]);
+            }
+            if (i == j) snoise += v;
+          }
+        }
+    // block reduction of the 13 sums, then scatter to θ positions
+    double vals[GPX_MAX_TERMS * 3 + 1];
+#pragma unroll
+    for (int t = 0; t < GPX_MAX_TERMS; ++t)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) vals[t * 3 + q] = wave_sum(sums[t][q]);
+    vals[GPX_MAX_TERMS * 3] = wave_sum(snoise);
+    if (lane == 0) {
+#pragma unroll
+      for (int v = 0; v < GPX_MAX_TERMS * 3 + 1; ++v) sred[wave * 16 + v] = vals[v];
+    }
+    __syncthreads();
+    if (tid < GPX_THETA_STRIDE) {
+      double* out = a.partial + (long long)b * a.sPartial + (long long)blockIdx.x * GPX_THETA_STRIDE;
+      // map slot tid -> θ index
+      double s = 0.0;
+      int slot = -1;
+      if (tid == spec.n_params) {
+        slot = GPX_MAX_TERMS * 3;
+      } else {
+        for (int t = 0; t < spec.n_terms; ++t) {
+          const int o = spec.terms[t].param_offset;
+          const int np = (spec.terms[t].kind == GPX_RQ || spec.terms[t].kind == GPX_PERIODIC_SE) ? 3
+                         : (spec.terms[t].kind == GPX_LINEAR ? 1 : 2);
+          if (tid >= o && tid < o + np) slot = t * 3 + (tid - o);
+        }
+      }
+      if (slot >= 0) s = sred[slot] + sred[16 + slot] + sred[32 + slot] + sred[48 + slot];
+      out[tid] = s;
+    }
+  } else {  // EPI_COLSUMSQ
+    double* scol = smem;  // [2][BN]
+    __syncthreads();
+#pragma unroll
+    for (int nn = 0; nn < MT; ++nn) {
+      double s = 0.0;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s = fma(acc[m][nn][r], acc[m][nn][r], s);
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 16) scol[wr * BN + wc * WT + nn * 16 + lane] = s;
+    }
+    __syncthreads();
+    if (tid < BN) {
+      double* out = a.partial + (long long)b * a.sPartial + (long long)ti * a.ldc;
+      out[j0 + tid] = scol[tid] + scol[BN + tid];
+    }
+  }
+}
+
+int gemm_tile(const GemmArgs& a) {
+  return (a.M % 128 == 0 && a.N % 128 == 0) ? 128 : 64;
+}
+
+template <int BM, int EPI>
+static void launch_gemm_t(const GemmArgs& a, bool ta, bool tb, int n_active, hipStream_t s) {
+  const int ti = a.M / BM, tj = a.N / BM;
+  const int ntiles = a.lower_only ? ti * (ti + 1) / 2 : ti * tj;
+  dim3 grid(ntiles, n_active);
+  if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<BM, false, false, EPI>), grid, dim3(256), 0, s, a);
+  else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<BM, false, true, EPI>), grid, dim3(256), 0, s, a);
+  else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<BM, true, false, EPI>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((gemm_kernel<BM, true, true, EPI>), grid, dim3(256), 0, s, a);
+}
+
+void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hipStream_t s) {
+  const int bm = gemm_tile(a);
+  if (bm == 128) {
+    if (epi == EPI_STORE) launch_gemm_t<128, EPI_STORE>(a, ta, tb, n_active, s);
+    else if (epi == EPI_CONTRACT) launch_gemm_t<128, EPI_CONTRACT>(a, ta, tb, n_active, s);
+    else launch_gemm_t<128, EPI_COLSUMSQ>(a, ta, tb, n_active, s);
+  } else {
+    if (epi == EPI_STORE) launch_gemm_t<64, EPI_STORE>(a, ta, tb, n_active, s);
+    else if (epi == EPI_CONTRACT) launch_gemm_t<64, EPI_CONTRACT>(a, ta, tb, n_active, s);
+    else launch_gemm_t<64, EPI_COLSUMSQ>(a, ta, tb, n_active, s);
+  }
+}
+
+// ======================================================================================
+// y = M x (row dot products; lower: k <= i). 64 rows per WG, 16 rows per wave.
+// ======================================================================================
+__global__ __launch_bounds__(256) void trmv_n_kernel(TrmvArgs a) {
+  const int b = a.active[blockIdx.y];
+  const double* M = a.Wm + (long long)b * a.sW;
+  const double* x = a.x + (long long)b * a.sx;
+  const int nx = a.nvalid ? a.nvalid[b] : a.cols;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int rr = 0; rr < 16; ++rr) {
+    const int i = blockIdx.x * 64 + wave * 16 + rr;
+    if (i >= a.rows) break;
+    const int kend = a.lower ? min(i + 1, a.cols) : a.cols;
+    double s = 0.0;
+    for (int k = lane; k < kend; k += 64) {
+      const double xv = (k < nx) ? x[k] : 0.0;
+      s = fma(M[(long long)i * a.ld + k], xv, s);
+    }
+    s = wave_sum(s);
+    if (lane == 0) a.y[(long long)b * a.sy + i] = s;
+  }
+}
+
+void launch_trmv_n(const TrmvArgs& a, int n_active, hipStream_t s) {
+  hipLaunchKernelGGL(trmv_n_kernel, dim3((a.rows + 63) / 64, n_active), dim3(256), 0, s, a);
+}
+
+// y = Mᵀ x (column sums; lower: i >= j). 64 columns per WG, rows split over 4 waves.
+__global__ __launch_bounds__(256) void trmv_t_kernel(TrmvArgs a) {
+  const int b = a.active[blockIdx.y];
+  const double* M = a.Wm + (long long)b * a.sW;
+  const double* x = a.x + (long long)b * a.sx;
+  __shared__ double sred[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j0 = blockIdx.x * 64, j = j0 + lane;
+  const int istart = a.lower ? j0 : 0;
+  double s = 0.0;
+  if (j < a.cols) {
+    for (int i = istart + wave; i < a.rows; i += 4) s = fma(M[(long long)i * a.ld + j], x[i], s);
+  }
+  sred[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && j < a.cols)
+    a.y[(long long)b * a.sy + j] = sred[0][lane] + sred[1][lane] + sred[2][lane] + sred[3][lane];
+}
+
+void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s) {
+  hipLaunchKernelGGL(trmv_t_kernel, dim3((a.cols + 63) / 64, n_active), dim3(256), 0, s, a);
+}
+
+// ======================================================================================
+// logML and gradient from the per-tile partials: one WG per problem, fixed order.
+// ======================================================================================
+__global__ __launch_bounds__(256) void reduce_kernel(ReduceArgs a) {
+  const int b = a.active[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ double sred[4][GPX_THETA_STRIDE + 2];
+  double ps[GPX_THETA_STRIDE];
+#pragma unroll
+  for (int p = 0; p < GPX_THETA_STRIDE; ++p) ps[p] = 0.0;
+  const double* part = a.partial + (long long)b * a.sPartial;
+  for (int t = tid; t < a.ntiles; t += 256) {
+#pragma unroll
+    for (int p = 0; p < GPX_THETA_STRIDE; ++p) ps[p] += part[(long long)t * GPX_THETA_STRIDE + p];
+  }
+  double zz = 0.0, sl = 0.0;
+  const double* z = a.z + (long long)b * a.sVec;
+  const double* ld = a.ldiag + (long long)b * a.sVec;
+  for (int i = tid; i < a.Np; i += 256) {
+    zz = fma(z[i], z[i], zz);
+    sl += ld[i];
+  }
+#pragma unroll
+  for (int p = 0; p < GPX_THETA_STRIDE; ++p) ps[p] = wave_sum(ps[p]);
+  zz = wave_sum(zz);
+  sl = wave_sum(sl);
+  if (lane == 0) {
+#pragma unroll
+    for (int p = 0; p < GPX_THETA_STRIDE; ++p) sred[wave][p] = ps[p];
+    sred[wave][GPX_THETA_STRIDE] = zz;
+    sred[wave][GPX_THETA_STRIDE + 1] = sl;
+  }
+  __syncthreads();
+  if (tid < GPX_THETA_STRIDE + 2) {
+    const double v = sred[0][tid] + sred[1][tid] + sred[2][tid] + sred[3][tid];
+    double* res = a.results + (long long)b * kResStride;
+    if (tid < GPX_THETA_STRIDE) {
+      res[1 + tid] = 0.5 * v;
+    } else if (tid == GPX_THETA_STRIDE) {
+      res[17] = v;
+    } else {
+      res[18] = v;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double* res = a.results + (long long)b * kResStride;
+    const double zz2 = sred[0][GPX_THETA_STRIDE] + sred[1][GPX_THETA_STRIDE] +
+                       sred[2][GPX_THETA_STRIDE] + sred[3][GPX_THETA_STRIDE];
+    const double sl2 = sred[0][GPX_THETA_STRIDE + 1] + sred[1][GPX_THETA_STRIDE + 1] +
+                       sred[2][GPX_THETA_STRIDE + 1] + sred[3][GPX_THETA_STRIDE + 1];
+    const int n = a.nvalid[b];
+    res[0] = -0.5 * zz2 - sl2 - 0.5 * (double)n * 1.8378770664093453;  // log(2π)
+  }
+}
+
+void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(n_active), dim3(256), 0, s, a);
+}
+
+// var_j = k(x*_j, x*_j) − Σ_rowtiles colsum partials (+ σn² for predict_y)
+__global__ __launch_bounds__(256) void predvar_kernel(PredVarArgs a) {
+  const int b = a.active[blockIdx.y];
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.M) return;
+  const DevSpec spec = a.specs[b];
+  const double* th = a.theta + b * GPX_THETA_STRIDE;
+  double thr[GPX_THETA_STRIDE];
+#pragma unroll
+  for (int p = 0; p < GPX_THETA_STRIDE; ++p) thr[p] = th[p];
+  const double* x = a.Xnew + (long long)b * a.sXnew + (long long)j * a.D;
+  double xl[GPX_MAX_DIM];
+  for (int d = 0; d < a.D; ++d) xl[d] = x[d];
+  double kss = eval_kdiag(spec, thr, xl);
+  const double* part = a.partial + (long long)b * a.sPartial;
+  double s = 0.0;
+  for (int t = 0; t < a.nrowtiles; ++t) s += part[(long long)t * a.ldp + j];
+  double v = kss - s;
+  if (a.add_noise) v += thr[spec.n_params];
+  a.var[(long long)b * a.sVar + j] = v;
+}
+
+void launch_predvar(const PredVarArgs& a, int n_active, hipStream_t s) {
+  hipLaunchKernelGGL(predvar_kernel, dim3((a.M + 255) / 256, n_active), dim3(256), 0, s, a);
+}
+
+}  // namespace gpx

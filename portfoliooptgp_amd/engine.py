@@ -1,0 +1,159 @@
+"""Device engine: a ``gpx_batch`` (include/gpx.h) over a list of GPR problems.
+
+One engine holds the problems' X/Y resident in HBM ([B, N_max, D] / [B, N_max] fp64, ragged
+problems padded, the padding handled exactly inside the kernels) plus the library's
+factorisation workspace. Evaluations run on the caller's current torch stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+
+def default_device() -> int:
+    """The HIP device this process uses: GPX_DEVICE, else LOCAL_RANK (one process per GPU),
+    else 0."""
+    for var in ("GPX_DEVICE", "LOCAL_RANK"):
+        v = os.environ.get(var)
+        if v is not None:
+            return int(v)
+    return 0
+
+
+def require_gpu(device: Optional[int] = None) -> int:
+    device = default_device() if device is None else int(device)
+    if not torch.cuda.is_available():
+        raise N.GPXError("portfoliooptgp_amd needs a HIP device (MI355X / gfx950); none is visible. "
+                         "There is no CPU fallback.")
+    return device
+
+
+def to_device_f64(a, device: int) -> torch.Tensor:
+    if isinstance(a, torch.Tensor):
+        t = a.detach()
+    else:
+        t = torch.as_tensor(np.asarray(a, dtype=np.float64))
+    return t.to(device=f"cuda:{device}", dtype=torch.float64).contiguous()
+
+
+class Engine:
+    def __init__(self, Xs: Sequence, Ys: Sequence, specs: Sequence[N.GpxKernelSpec],
+                 device: Optional[int] = None):
+        self.device = require_gpu(device)
+        self.ctx = N.Context.get(self.device)
+        self.lib = self.ctx.lib
+        B = len(Xs)
+        if B == 0 or len(Ys) != B or len(specs) != B:
+            raise ValueError("Engine needs matching non-empty lists of X, Y and specs")
+        xs = [to_device_f64(x, self.device) for x in Xs]
+        xs = [x.reshape(x.shape[0], -1) for x in xs]
+        ys = [to_device_f64(y, self.device).reshape(-1) for y in Ys]
+        D = xs[0].shape[1]
+        if any(x.shape[1] != D for x in xs):
+            raise ValueError("all problems in one engine must have the same input dimension")
+        if D > N.GPX_MAX_DIM:
+            raise NotImplementedError(f"input dimension {D} > {N.GPX_MAX_DIM}")
+        ns = [x.shape[0] for x in xs]
+        if any(y.shape[0] != n for y, n in zip(ys, ns)):
+            raise ValueError("X and Y must have the same number of rows")
+        self.B, self.D, self.Nmax = B, D, max(ns)
+        self.n = np.asarray(ns, dtype=np.int32)
+        dev = f"cuda:{self.device}"
+        self.X = torch.zeros(B, self.Nmax, D, dtype=torch.float64, device=dev)
+        self.Y = torch.zeros(B, self.Nmax, dtype=torch.float64, device=dev)
+        for b in range(B):
+            self.X[b, : ns[b]] = xs[b]
+            self.Y[b, : ns[b]] = ys[b]
+        self.specs = (N.GpxKernelSpec * B)(*specs)
+        torch.cuda.synchronize(self.device)
+        h = ctypes.c_void_p()
+        rc = self.lib.gpx_batch_create(
+            self.ctx.handle, B, self.Nmax, D, ctypes.c_void_p(self.X.data_ptr()),
+            ctypes.c_void_p(self.Y.data_ptr()),
+            self.n.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), self.specs, ctypes.byref(h))
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_batch_create failed ({rc}): {self.ctx.last_error()}")
+        self.handle = h
+        self.n_params = np.asarray([s.n_params for s in specs], dtype=np.int64)
+        self.eval_count = 0
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.lib.gpx_batch_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @staticmethod
+    def _active(active) -> np.ndarray:
+        return np.ascontiguousarray(np.asarray(active, dtype=np.int32))
+
+    def lml_grad(self, active: Sequence[int], theta: np.ndarray):
+        """logML [B], ∂logML/∂θ [B, 16], info [B] for the active rows (others untouched)."""
+        act = self._active(active)
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        assert theta.shape == (self.B, N.GPX_THETA_STRIDE)
+        lml = np.full(self.B, np.nan)
+        grad = np.full((self.B, N.GPX_THETA_STRIDE), np.nan)
+        info = np.zeros(self.B, dtype=np.int32)
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        rc = self.lib.gpx_batch_lml_grad(self.handle, len(act), act.ctypes.data_as(ip),
+                                         theta.ctypes.data_as(dp), lml.ctypes.data_as(dp),
+                                         grad.ctypes.data_as(dp), info.ctypes.data_as(ip),
+                                         self._stream())
+        if rc not in (N.GPX_OK, N.GPX_NOT_PD):
+            raise N.GPXError(f"gpx_batch_lml_grad failed ({rc}): {self.ctx.last_error()}")
+        self.eval_count += len(act)
+        return lml, grad, info
+
+    def predict(self, active: Sequence[int], theta: np.ndarray, Xnew: Sequence, add_noise: bool):
+        """Marginal posterior mean/var at Xnew[i] (for problem active[i]); returns lists of
+        device tensors [M_i] and info."""
+        act = self._active(active)
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        xs = [to_device_f64(x, self.device) for x in Xnew]
+        xs = [x.reshape(x.shape[0], -1) for x in xs]
+        if any(x.shape[1] != self.D for x in xs):
+            raise ValueError(f"Xnew must have {self.D} columns")
+        M = max(x.shape[0] for x in xs)
+        dev = f"cuda:{self.device}"
+        Xn = torch.zeros(self.B, M, self.D, dtype=torch.float64, device=dev)
+        for b, x in zip(act, xs):
+            Xn[b, : x.shape[0]] = x
+        mean = torch.empty(self.B, M, dtype=torch.float64, device=dev)
+        var = torch.empty(self.B, M, dtype=torch.float64, device=dev)
+        info = np.zeros(self.B, dtype=np.int32)
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        rc = self.lib.gpx_batch_predict(self.handle, len(act), act.ctypes.data_as(ip),
+                                        theta.ctypes.data_as(dp), ctypes.c_void_p(Xn.data_ptr()), M,
+                                        1 if add_noise else 0, ctypes.c_void_p(mean.data_ptr()),
+                                        ctypes.c_void_p(var.data_ptr()), info.ctypes.data_as(ip),
+                                        self._stream())
+        if rc == N.GPX_NOT_PD:
+            bad = [int(b) for b in act if info[b] != 0]
+            raise N.NotPositiveDefiniteError(
+                f"Cholesky decomposition was not successful (problems {bad}, pivots "
+                f"{[int(info[b]) for b in bad]}): K + noise I is not positive definite", info)
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_batch_predict failed ({rc}): {self.ctx.last_error()}")
+        outs_m = [mean[b, : x.shape[0]] for b, x in zip(act, xs)]
+        outs_v = [var[b, : x.shape[0]] for b, x in zip(act, xs)]
+        return outs_m, outs_v, info
+
+    def last_timing(self) -> N.GpxTiming:
+        t = N.GpxTiming()
+        self.lib.gpx_batch_last_timing(self.handle, ctypes.byref(t))
+        return t

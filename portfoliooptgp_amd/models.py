@@ -1,0 +1,203 @@
+"""gpflow.models.GPR 2.9.1 surface backed by the HIP engine.
+
+Reference call sites this serves: ``gpflow.models.GPR(data=(X_tf, Y_tf), kernel=kernel)``
+(GPR/model_trainer.py:15), ``model.likelihood.variance.assign`` / ``set_trainable``
+(:16-17), ``model.training_loss`` / ``model.trainable_variables`` (:19), ``model.predict_f``
+(:20, GPR/predictor.py:6) and ``model.predict_y`` (GPR/predictor.py:7); and
+``gpflow.models.GPR((X, Y), kernel=deepcopy(k), noise_variance=v)``
+(Multi-Input_GPR/main.py:421-423, Multi-Input_GPR/models/model_trainer.py:31).
+
+Arithmetic: every logML / gradient / prediction is computed by libgpx.so on the GPU. The
+outputs are torch float64 tensors: on the CPU when the data came in as numpy / CPU tensors
+(so ``.numpy()``, arithmetic and slicing work as on the tf tensors GPflow returns), else on
+the GPU.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .engine import Engine, default_device
+from .kernels import Kernel, compile_spec
+from .likelihoods import Gaussian
+from .parameter import Parameter
+
+
+def _as_2d_cpu_or_dev(a):
+    return a
+
+
+class GPR:
+    """Exact GP regression with a Gaussian likelihood and a zero mean function."""
+
+    def __init__(self, data: Tuple, kernel: Kernel, mean_function=None,
+                 noise_variance: Optional[float] = None, likelihood: Optional[Gaussian] = None,
+                 device: Optional[int] = None):
+        if mean_function is not None:
+            raise NotImplementedError("only the zero mean function (GPflow default) is supported")
+        X, Y = data
+        self._out_cpu = not (isinstance(Y, torch.Tensor) and Y.is_cuda)
+        Xt = X if isinstance(X, torch.Tensor) else torch.as_tensor(np.asarray(X, dtype=np.float64))
+        Yt = Y if isinstance(Y, torch.Tensor) else torch.as_tensor(np.asarray(Y, dtype=np.float64))
+        Xt = Xt.to(torch.float64)
+        Yt = Yt.to(torch.float64)
+        if Xt.ndim == 1:
+            Xt = Xt[:, None]
+        if Yt.ndim == 1:
+            Yt = Yt[:, None]
+        if Yt.shape[1] != 1:
+            raise NotImplementedError("single-output GPR only (Y must be [N, 1])")
+        if Xt.shape[0] != Yt.shape[0]:
+            raise ValueError("X and Y must have the same number of rows")
+        self.data = (Xt, Yt)
+        self.kernel = kernel
+        if likelihood is None:
+            likelihood = Gaussian(1.0 if noise_variance is None else noise_variance)
+        elif noise_variance is not None:
+            raise ValueError("give either noise_variance or likelihood")
+        self.likelihood = likelihood
+        self.mean_function = None
+        self.num_latent_gps = 1
+        self.device = default_device() if device is None else int(device)
+        self._spec = compile_spec(kernel, Xt.shape[1])
+        self._engine: Optional[Engine] = None
+        self._engine_index = 0
+
+    # ---------------------------------------------------------------- structure -------
+    @property
+    def parameters(self) -> Tuple[Parameter, ...]:
+        # GPR attributes sorted: kernel < likelihood (< mean_function, which has none here)
+        return tuple(self.kernel.parameters) + tuple(self.likelihood.parameters)
+
+    @property
+    def trainable_parameters(self) -> Tuple[Parameter, ...]:
+        return tuple(p for p in self.parameters if p.trainable)
+
+    @property
+    def trainable_variables(self):
+        return tuple(p.unconstrained_variable for p in self.trainable_parameters)
+
+    def _param_paths(self):
+        return ([("GPR.kernel." + n if n else "GPR.kernel", p) for n, p in self.kernel._param_paths("")]
+                + [("GPR.likelihood.variance", self.likelihood.variance)])
+
+    @property
+    def n_kernel_params(self) -> int:
+        return int(self._spec.n_params)
+
+    def theta_row(self) -> np.ndarray:
+        """Constrained θ in the gpx layout: kernel params, then σn² at index n_params."""
+        row = np.ones(N.GPX_THETA_STRIDE, dtype=np.float64)
+        kp = self.kernel.parameters
+        for i, p in enumerate(kp):
+            row[i] = p.value
+        row[len(kp)] = self.likelihood.variance.value
+        return row
+
+    # ---------------------------------------------------------------- engine ----------
+    def _attach(self, engine: Engine, index: int) -> None:
+        self._engine, self._engine_index = engine, index
+
+    def engine(self) -> Tuple[Engine, int]:
+        if self._engine is None:
+            X, Y = self.data
+            self._engine = Engine([X], [Y], [self._spec], device=self.device)
+            self._engine_index = 0
+        return self._engine, self._engine_index
+
+    def _wrap(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.reshape(-1, 1)
+        return t.cpu() if self._out_cpu else t
+
+    # ---------------------------------------------------------------- objective -------
+    def _lml_and_grad_theta(self):
+        eng, b = self.engine()
+        theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+        theta[b] = self.theta_row()
+        lml, grad, info = eng.lml_grad([b], theta)
+        if info[b] != 0:
+            raise N.NotPositiveDefiniteError(
+                f"Cholesky decomposition was not successful: pivot {int(info[b])} of K + noise I "
+                "is not positive", info[b])
+        return float(lml[b]), grad[b]
+
+    def log_marginal_likelihood(self) -> torch.Tensor:
+        return torch.tensor(self._lml_and_grad_theta()[0], dtype=torch.float64)
+
+    def maximum_log_likelihood_objective(self) -> torch.Tensor:
+        return self.log_marginal_likelihood()
+
+    def training_loss(self) -> torch.Tensor:
+        """−logML (no priors), the closure GPR/model_trainer.py:19 hands to Scipy."""
+        return -self.log_marginal_likelihood()
+
+    def training_loss_closure(self, compile: bool = True):
+        def closure():
+            return self.training_loss()
+        closure._gpx_model = self
+        return closure
+
+    def loss_and_grad_unconstrained(self, variables=None, lml=None, grad_theta=None):
+        """(−logML, ∂(−logML)/∂u) for ``variables`` (default: trainable_variables)."""
+        if lml is None:
+            lml, grad_theta = self._lml_and_grad_theta()
+        variables = self.trainable_variables if variables is None else variables
+        pindex = {id(p): i for i, p in enumerate(self.kernel.parameters)}
+        nk = len(self.kernel.parameters)
+        g = np.empty(len(variables), dtype=np.float64)
+        for k, v in enumerate(variables):
+            p = v._param
+            if p is self.likelihood.variance:
+                gi = grad_theta[nk]
+            elif id(p) in pindex:
+                gi = grad_theta[pindex[id(p)]]
+            else:
+                raise ValueError(f"variable {v.name} is not a parameter of this model")
+            g[k] = -gi * p.dtheta_du()
+        return -float(lml), g
+
+    # ---------------------------------------------------------------- prediction ------
+    def predict_f(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
+        if full_cov or full_output_cov:
+            raise NotImplementedError("full_cov=True is not implemented (marginals only)")
+        return self._predict(Xnew, add_noise=False)
+
+    def predict_y(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
+        if full_cov or full_output_cov:
+            raise NotImplementedError("full_cov=True is not implemented (marginals only)")
+        return self._predict(Xnew, add_noise=True)
+
+    def _predict(self, Xnew, add_noise: bool):
+        eng, b = self.engine()
+        theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+        theta[b] = self.theta_row()
+        cpu_out = not (isinstance(Xnew, torch.Tensor) and Xnew.is_cuda)
+        m, v, _ = eng.predict([b], theta, [Xnew], add_noise)
+        m, v = m[0].reshape(-1, 1), v[0].reshape(-1, 1)
+        if cpu_out:
+            m, v = m.cpu(), v.cpu()
+        return m, v
+
+
+def predict_f_batch(models: Sequence[GPR], Xnews: Sequence, add_noise: bool = False):
+    """predict_f (or predict_y) for several models sharing one engine, in one device pass."""
+    eng, _ = models[0].engine()
+    idx = []
+    for m in models:
+        e, b = m.engine()
+        if e is not eng:
+            raise ValueError("models must share an engine (fit them with Scipy().minimize_batch)")
+        idx.append(b)
+    theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+    for m, b in zip(models, idx):
+        theta[b] = m.theta_row()
+    ms, vs, _ = eng.predict(idx, theta, Xnews, add_noise)
+    out = []
+    for x, m, v in zip(Xnews, ms, vs):
+        cpu_out = not (isinstance(x, torch.Tensor) and x.is_cuda)
+        m, v = m.reshape(-1, 1), v.reshape(-1, 1)
+        out.append((m.cpu(), v.cpu()) if cpu_out else (m, v))
+    return out

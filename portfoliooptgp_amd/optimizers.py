@@ -1,0 +1,189 @@
+"""gpflow.optimizers.Scipy with the same call surface, plus a lock-step batched driver.
+
+``Scipy().minimize(model.training_loss, model.trainable_variables, options=dict(maxiter=100))``
+(GPR/model_trainer.py:18-19) runs scipy's L-BFGS-B (jac=True) over the concatenated
+unconstrained variables and writes the result back, returning scipy's OptimizeResult
+(``.fun``, ``.x``, ``.nfev``, ``.nit``; ``opt_logs.fun`` at
+Multi-Input_GPR/models/model_trainer.py:40).
+
+``minimize_batch`` runs one *unmodified* scipy L-BFGS-B per model, each in its own host
+thread; whenever every still-running optimiser is waiting for a function value, the pending
+points are evaluated together in ONE batched device pass (gpx_batch_lml_grad). Each
+optimiser sees exactly the values a solo run would see, so trajectories are per-fit identical
+to sequential fitting while the device works on all fits at once.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+import scipy.optimize
+
+from . import _native as N
+from .engine import Engine
+from .kernels import compile_spec
+
+
+def _resolve_model(closure):
+    m = getattr(closure, "_gpx_model", None)
+    if m is None:
+        m = getattr(closure, "__self__", None)
+    if m is None or not hasattr(m, "loss_and_grad_unconstrained"):
+        raise TypeError("closure must be a portfoliooptgp_amd model's training_loss "
+                        "(or training_loss_closure()); gradients come from the GPU engine, "
+                        "there is no autodiff of arbitrary Python closures")
+    return m
+
+
+def _pack(variables) -> np.ndarray:
+    return np.concatenate([np.atleast_1d(v.numpy()).ravel() for v in variables]).astype(np.float64)
+
+
+def _unpack(variables, x) -> None:
+    for v, xi in zip(variables, np.asarray(x, dtype=np.float64)):
+        v.assign(xi)
+
+
+class Scipy:
+    def minimize(self, closure: Callable, variables: Sequence, method: str = "L-BFGS-B",
+                 step_callback=None, compile: bool = True, allow_unused_variables: bool = False,
+                 tf_fun_args=None, track_loss_history: bool = False, **scipy_kwargs):
+        if not callable(closure):
+            raise TypeError("The 'closure' argument is expected to be a callable object.")
+        variables = tuple(variables)
+        if not variables:
+            raise ValueError("The 'variables' argument is expected to only contain Variable instances")
+        model = _resolve_model(closure)
+        history: List[float] = []
+
+        def func(x):
+            _unpack(variables, x)
+            loss, g = model.loss_and_grad_unconstrained(variables)
+            if track_loss_history:
+                history.append(loss)
+            return loss, g
+
+        callback = None
+        if step_callback is not None:
+            def callback(xk, *args):
+                step_callback(len(history), variables, [np.asarray(v) for v in xk])
+        x0 = _pack(variables)
+        res = scipy.optimize.minimize(func, x0, jac=True, method=method, callback=callback,
+                                      **scipy_kwargs)
+        _unpack(variables, res.x)
+        if track_loss_history:
+            res.loss_history = history
+        return res
+
+    def minimize_batch(self, models: Sequence, method: str = "L-BFGS-B",
+                       engine: Optional[Engine] = None, device: Optional[int] = None,
+                       **scipy_kwargs) -> List[scipy.optimize.OptimizeResult]:
+        """Fit several GPR models concurrently (their trainable_variables), lock-step batched."""
+        models = list(models)
+        if not models:
+            return []
+        if engine is None:
+            engine = Engine([m.data[0] for m in models], [m.data[1] for m in models],
+                            [compile_spec(m.kernel, m.data[0].shape[1]) for m in models],
+                            device=device if device is not None else models[0].device)
+        for i, m in enumerate(models):
+            m._attach(engine, i)
+        step = _LockstepEvaluator(engine, models)
+        results: List[Optional[scipy.optimize.OptimizeResult]] = [None] * len(models)
+        errors: List[Optional[BaseException]] = [None] * len(models)
+
+        def worker(i: int):
+            try:
+                m = models[i]
+                variables = m.trainable_variables
+                if not variables:
+                    raise ValueError("model has no trainable variables")
+
+                def func(x):
+                    _unpack(variables, x)
+                    return step.request(i, variables)
+
+                res = scipy.optimize.minimize(func, _pack(variables), jac=True, method=method,
+                                              **scipy_kwargs)
+                _unpack(variables, res.x)
+                results[i] = res
+            except BaseException as e:  # re-raised on the caller's thread
+                errors[i] = e
+            finally:
+                step.finish(i)
+
+        threads = [threading.Thread(target=worker, args=(i,), daemon=True) for i in range(len(models))]
+        for t in threads:
+            t.start()
+        step.serve()
+        for t in threads:
+            t.join()
+        for e in errors:
+            if e is not None:
+                raise e
+        return results  # type: ignore[return-value]
+
+
+class _LockstepEvaluator:
+    """Barrier between the optimiser threads and the device: evaluates all pending points in
+    one gpx_batch_lml_grad call once every running optimiser has posted one."""
+
+    def __init__(self, engine: Engine, models):
+        self.engine = engine
+        self.models = models
+        self.cv = threading.Condition()
+        self.running = set(range(len(models)))
+        self.pending = {}
+        self.results = {}
+        self.error: Optional[BaseException] = None
+        self.rounds = 0
+
+    def request(self, i: int, variables):
+        with self.cv:
+            self.pending[i] = variables
+            self.cv.notify_all()
+            while i not in self.results:
+                self.cv.wait()
+            res = self.results.pop(i)
+        if isinstance(res, BaseException):
+            raise res
+        return res
+
+    def finish(self, i: int):
+        with self.cv:
+            self.running.discard(i)
+            self.cv.notify_all()
+
+    def serve(self):
+        eng = self.engine
+        while True:
+            with self.cv:
+                while self.running and len(self.pending) < len(self.running):
+                    self.cv.wait()
+                if not self.running:
+                    return
+                batch = dict(self.pending)
+                self.pending.clear()
+            active = sorted(batch)
+            theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+            for i in active:
+                theta[i] = self.models[i].theta_row()
+            out = {}
+            try:
+                lml, grad, info = eng.lml_grad(active, theta)
+                for i in active:
+                    if info[i] != 0:
+                        out[i] = N.NotPositiveDefiniteError(
+                            f"Cholesky decomposition was not successful (model {i}, pivot "
+                            f"{int(info[i])}): K + noise I is not positive definite", info[i])
+                    else:
+                        out[i] = self.models[i].loss_and_grad_unconstrained(
+                            batch[i], lml=lml[i], grad_theta=grad[i])
+            except BaseException as e:
+                for i in active:
+                    out[i] = e
+            self.rounds += 1
+            with self.cv:
+                self.results.update(out)
+                self.cv.notify_all()

@@ -1,0 +1,122 @@
+"""Positive parameters with GPflow 2.9.1 semantics.
+
+GPflow stores each positive parameter as an unconstrained tf.Variable u and exposes the
+constrained value θ = lower + softplus(u) (tfp.bijectors.Softplus, chained with Shift(lower)
+for the Gaussian likelihood variance, lower = 1e-6). ``gpflow.optimizers.Scipy`` optimises u
+(GPR/model_trainer.py:18-19). ``Parameter.assign`` takes a constrained value
+(GPR/model_trainer.py:16: ``model.likelihood.variance.assign(1e-5)``).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+_EPS = float(np.finfo(np.float64).eps)
+_THRESH = math.log(_EPS) + 2.0  # tfp.math.softplus_inverse threshold
+
+
+def softplus(u: float) -> float:
+    return float(np.logaddexp(0.0, u))
+
+
+def softplus_inverse(t: float) -> float:
+    """tfp.math.softplus_inverse: log(expm1(t)) with its small/large-argument branches."""
+    t = float(t)
+    if t < math.exp(_THRESH):
+        return math.log(t)
+    if t > -_THRESH:
+        return t
+    return t + math.log(-math.expm1(-t))
+
+
+def sigmoid(u: float) -> float:
+    return 0.5 * (1.0 + math.tanh(0.5 * u))
+
+
+class UnconstrainedVariable:
+    """The tf.Variable-like handle that lands in ``model.trainable_variables``."""
+
+    def __init__(self, param: "Parameter"):
+        self._param = param
+
+    @property
+    def name(self) -> str:
+        return f"{self._param.name}:0"
+
+    @property
+    def shape(self):
+        return ()
+
+    @property
+    def dtype(self):
+        return np.float64
+
+    @property
+    def trainable(self) -> bool:
+        return self._param.trainable
+
+    def numpy(self) -> np.ndarray:
+        return np.asarray(self._param.unconstrained, dtype=np.float64)
+
+    def assign(self, u) -> None:
+        self._param.set_unconstrained(float(np.asarray(u, dtype=np.float64).reshape(())))
+
+    def __repr__(self) -> str:
+        return f"<UnconstrainedVariable {self.name} u={self._param.unconstrained!r}>"
+
+
+class Parameter:
+    """A scalar positive parameter (θ = lower + softplus(u))."""
+
+    def __init__(self, value: float, lower: float = 0.0, trainable: bool = True, name: str = "parameter"):
+        value = float(np.asarray(value, dtype=np.float64).reshape(()))
+        if not value > lower:
+            raise ValueError(f"{name}: value {value} must be > {lower} (positive transform)")
+        self.lower = float(lower)
+        self.trainable = bool(trainable)
+        self.name = name
+        self._u = softplus_inverse(value - self.lower)
+        self._variable = UnconstrainedVariable(self)
+
+    # --- constrained view -------------------------------------------------------------
+    @property
+    def value(self) -> float:
+        return self.lower + softplus(self._u)
+
+    def numpy(self) -> np.float64:
+        return np.float64(self.value)
+
+    def assign(self, value) -> None:
+        value = float(np.asarray(value, dtype=np.float64).reshape(()))
+        if not value > self.lower:
+            raise ValueError(f"{self.name}: value {value} must be > {self.lower}")
+        self._u = softplus_inverse(value - self.lower)
+
+    # --- unconstrained view -----------------------------------------------------------
+    @property
+    def unconstrained(self) -> float:
+        return self._u
+
+    def set_unconstrained(self, u: float) -> None:
+        self._u = float(u)
+
+    @property
+    def unconstrained_variable(self) -> UnconstrainedVariable:
+        return self._variable
+
+    def dtheta_du(self) -> float:
+        return sigmoid(self._u)
+
+    @property
+    def transform_name(self) -> str:
+        return "Softplus" if self.lower == 0.0 else "Softplus + Shift"
+
+    def __float__(self) -> float:
+        return self.value
+
+    def __array__(self, dtype=None, copy=None):
+        return np.asarray(self.value, dtype=dtype or np.float64)
+
+    def __repr__(self) -> str:
+        return f"<Parameter {self.name}={self.value!r} trainable={self.trainable}>"
