@@ -129,8 +129,16 @@ typedef struct {
   double predict_ms;  /* predict-only kernels */
   double total_ms;
   double gemm_flops;  /* MFMA flops issued by the GEMM kernels of the last call */
+  /* cumulative since the last gpx_batch_reset_timing, profiling enabled only: the fused
+   * K^-1 = W^T W + gradient-contraction kernel (one launch per gpx_batch_lml_grad call) */
+  double contract_ms_total;
+  double contract_launches;
+  double contract_alg_flops;  /* algorithmic flops of those launches: n_active * sum_i 2(i+1)(Np-i) */
+  double eval_ms_total;       /* whole gpx_batch_lml_grad device time */
+  double evals;               /* problem-evaluations (sum of n_active) */
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
+int gpx_batch_reset_timing(gpx_batch* batch);
 int gpx_set_profiling(gpx_ctx* ctx, int enabled);
 
 #ifdef __cplusplus

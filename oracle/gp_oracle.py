@@ -53,7 +53,8 @@ def softplus(u):
 def softplus_inverse(t):
     t = np.asarray(t, dtype=np.float64)
     # log(exp(t) - 1) computed stably
-    return np.where(t > 30.0, t + np.log(-np.expm1(-t)), np.log(np.expm1(t)))
+    with np.errstate(over="ignore"):
+        return np.where(t > 30.0, t + np.log(-np.expm1(-t)), np.log(np.expm1(t)))
 
 
 def sigmoid(u):

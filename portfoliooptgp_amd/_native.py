@@ -26,7 +26,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgpx.so")
 EXPORTED_SYMBOLS = (
     "gpx_version", "gpx_create", "gpx_destroy", "gpx_last_error", "gpx_batch_create",
     "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_predict", "gpx_batch_last_timing",
-    "gpx_set_profiling",
+    "gpx_set_profiling", "gpx_batch_reset_timing",
 )
 
 
@@ -44,7 +44,10 @@ class GpxKernelSpec(ctypes.Structure):
 class GpxTiming(ctypes.Structure):
     _fields_ = [("factor_ms", ctypes.c_double), ("alpha_ms", ctypes.c_double),
                 ("grad_ms", ctypes.c_double), ("predict_ms", ctypes.c_double),
-                ("total_ms", ctypes.c_double), ("gemm_flops", ctypes.c_double)]
+                ("total_ms", ctypes.c_double), ("gemm_flops", ctypes.c_double),
+                ("contract_ms_total", ctypes.c_double), ("contract_launches", ctypes.c_double),
+                ("contract_alg_flops", ctypes.c_double), ("eval_ms_total", ctypes.c_double),
+                ("evals", ctypes.c_double)]
 
 
 class GPXError(RuntimeError):
@@ -101,6 +104,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
                                           c_int, c_void_p, c_void_p, c_int_p, c_void_p]
         lib.gpx_batch_last_timing.restype = c_int
         lib.gpx_batch_last_timing.argtypes = [c_void_p, ctypes.POINTER(GpxTiming)]
+        lib.gpx_batch_reset_timing.restype = c_int
+        lib.gpx_batch_reset_timing.argtypes = [c_void_p]
         if path is None:
             _lib = lib
         return lib

@@ -356,7 +356,9 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   g.vec = bt->alpha; g.sVec = bt->Np; g.X = bt->X; g.sX = (long long)bt->Nmax * bt->D; g.D = bt->D;
   g.specs = bt->d_specs; g.theta = bt->d_theta; g.nvalid = bt->d_n;
   g.partial = bt->partial; g.sPartial = bt->partial_stride;
+  pt.mark();
   gemm(bt, g, EPI_CONTRACT, true, false, na, s);
+  pt.mark();
   const int bm = gemm_tile(g), tt = bt->Np / bm;
   ReduceArgs r{};
   r.active = bt->d_active; r.partial = bt->partial; r.sPartial = bt->partial_stride;
@@ -372,10 +374,17 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   if (pt.on) {
     bt->timing.factor_ms = pt.ms(0, 1);
     bt->timing.alpha_ms = pt.ms(1, 2);
-    bt->timing.grad_ms = pt.ms(2, 3);
+    bt->timing.grad_ms = pt.ms(2, 5);
     bt->timing.predict_ms = 0.0;
-    bt->timing.total_ms = pt.ms(0, 3);
+    bt->timing.total_ms = pt.ms(0, 5);
     bt->timing.gemm_flops = bt->flops_acc;
+    bt->timing.contract_ms_total += pt.ms(3, 4);
+    bt->timing.contract_launches += 1.0;
+    double f = 0.0;
+    for (int i = 0; i < bt->Np; ++i) f += 2.0 * (i + 1) * (double)(bt->Np - i);
+    bt->timing.contract_alg_flops += na * f;
+    bt->timing.eval_ms_total += pt.ms(0, 5);
+    bt->timing.evals += na;
   }
   int status = GPX_OK;
   for (int i = 0; i < na; ++i) {
@@ -509,6 +518,12 @@ int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const 
   }
   if (status == GPX_NOT_PD) ctx->err = "K + noise*I is not positive definite for some problem";
   return status;
+}
+
+int gpx_batch_reset_timing(gpx_batch* bt) {
+  if (!bt) return GPX_BAD_ARG;
+  bt->timing = gpx_timing{};
+  return GPX_OK;
 }
 
 int gpx_batch_last_timing(const gpx_batch* bt, gpx_timing* out) {

@@ -153,6 +153,9 @@ class Engine:
         outs_v = [var[b, : x.shape[0]] for b, x in zip(act, xs)]
         return outs_m, outs_v, info
 
+    def reset_timing(self) -> None:
+        self.lib.gpx_batch_reset_timing(self.handle)
+
     def last_timing(self) -> N.GpxTiming:
         t = N.GpxTiming()
         self.lib.gpx_batch_last_timing(self.handle, ctypes.byref(t))

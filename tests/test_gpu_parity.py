@@ -1,0 +1,304 @@
+"""GPU parity: libgpx.so (HIP, gfx950) against the oracle and the golden fixtures.
+
+Tolerances (fp64, SURVEY.md §8c and BASELINE.json north_star "within 1e-5 relative on
+posterior mean/variance and log-ML"):
+  logML         |Δ| <= 1e-9 · max(1, |ref|)           (north-star bar: 1e-5 rel)
+  ∂loss/∂u      |Δ| <= 1e-7 · (1 + max|g_ref|)          (SURVEY: rel 1e-6)
+  mean          |Δ| <= 1e-6 · (max|ref| + 1e-12)        (bar: 1e-5 rel)
+  variance      |Δ| <= 1e-5 · |ref| + 1e-10 · σ²_max    (SURVEY: cancellation-aware)
+  fitted loss   |Δ| <= 1e-5 · |ref|
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import portfoliooptgp_amd as gpx  # noqa: E402
+from portfoliooptgp_amd import _native as N  # noqa: E402
+from portfoliooptgp_amd.engine import Engine  # noqa: E402
+from portfoliooptgp_amd.kernels import compile_spec  # noqa: E402
+from portfoliooptgp_amd.models import predict_f_batch  # noqa: E402
+from oracle import gp_oracle as O  # noqa: E402
+
+K = gpx.kernels
+
+
+def gpx_kernel(fam):
+    return {
+        "se": K.SquaredExponential, "m12": K.Matern12, "m32": K.Matern32, "m52": K.Matern52,
+        "exp": K.Exponential, "rq": K.RationalQuadratic,
+        "per": lambda: K.Periodic(K.SquaredExponential()), "lin": K.Linear,
+        "se+m12": lambda: K.SquaredExponential() + K.Matern12(),
+        "exp+per+lin": lambda: K.Exponential() + K.Periodic(K.SquaredExponential()) + K.Linear(),
+        "exp+per": lambda: K.Exponential() + K.Periodic(K.SquaredExponential()),
+        "se*m12": lambda: K.SquaredExponential() * K.Matern12(),
+    }[fam]()
+
+
+def oracle_kernel(fam):
+    from tests.test_oracle import oracle_kernel as ok
+    return ok(fam)
+
+
+@pytest.fixture(scope="module")
+def golden(golden_dir):
+    d = np.load(os.path.join(golden_dir, "kernel_cases.npz"))
+    idx = json.load(open(os.path.join(golden_dir, "kernel_cases_index.json")))
+    return d, idx
+
+
+def check_loss(got, ref):
+    assert abs(got - ref) <= 1e-9 * max(1.0, abs(ref)), (got, ref)
+
+
+def check_grad(got, ref):
+    got, ref = np.asarray(got), np.asarray(ref)
+    assert np.all(np.abs(got - ref) <= 1e-7 * (1.0 + np.abs(ref).max())), (got, ref)
+
+
+def check_mean(got, ref):
+    got, ref = np.asarray(got).ravel(), np.asarray(ref).ravel()
+    assert np.abs(got - ref).max() <= 1e-6 * (np.abs(ref).max() + 1e-12), np.abs(got - ref).max()
+
+
+def check_var(got, ref, s2max):
+    got, ref = np.asarray(got).ravel(), np.asarray(ref).ravel()
+    err = np.abs(got - ref)
+    assert np.all(err <= 1e-5 * np.abs(ref) + 1e-10 * s2max), err.max()
+
+
+def _model(d, key, trainable_noise=True):
+    dname, fam, _ = key.split("|")
+    x, y = d[f"data|{dname}|x"], d[f"data|{dname}|y"]
+    k = gpx_kernel(fam)
+    for p, v in zip(k.parameters, d[key + "|theta"]):
+        p.assign(float(v))
+    m = gpx.models.GPR(data=(x, y), kernel=k, noise_variance=float(d[key + "|noise"][0]))
+    if not trainable_noise:
+        gpx.set_trainable(m.likelihood.variance, False)
+    return m
+
+
+def test_golden_single_models(golden):
+    """Every family x dataset x θ through the single-model (B=1) path."""
+    d, idx = golden
+    for key in idx:
+        m = _model(d, key)
+        loss, g = m.loss_and_grad_unconstrained()
+        check_loss(loss, float(d[key + "|loss"][0]))
+        check_grad(g, d[key + "|grad_u"])
+        gpx.set_trainable(m.likelihood.variance, False)
+        _, g2 = m.loss_and_grad_unconstrained()
+        check_grad(g2, d[key + "|grad_u_fixed_noise"])
+        xnew = d[key + "|xnew"]
+        mu, var = m.predict_f(xnew)
+        _, vy = m.predict_y(xnew)
+        s2 = max(float(np.max(d[key + "|fvar"])), 1.0)
+        check_mean(mu.numpy(), d[key + "|fmean"])
+        check_var(var.numpy(), d[key + "|fvar"], s2)
+        check_var(vy.numpy(), d[key + "|yvar"], s2)
+
+
+def test_golden_ragged_batch(golden):
+    """All cases of all datasets in ONE engine: ragged N (1..256), mixed kernel specs."""
+    d, idx = golden
+    models = [_model(d, key) for key in idx]
+    eng = Engine([m.data[0] for m in models], [m.data[1] for m in models],
+                 [compile_spec(m.kernel, 1) for m in models])
+    theta = np.stack([m.theta_row() for m in models])
+    lml, grad, info = eng.lml_grad(list(range(len(models))), theta)
+    assert not info.any()
+    for b, (m, key) in enumerate(zip(models, idx)):
+        loss, g = m.loss_and_grad_unconstrained(lml=lml[b], grad_theta=grad[b])
+        check_loss(loss, float(d[key + "|loss"][0]))
+        check_grad(g, d[key + "|grad_u"])
+    for b, m in enumerate(models):
+        m._attach(eng, b)
+    outs = predict_f_batch(models, [d[k + "|xnew"] for k in idx])
+    for (mu, var), key in zip(outs, idx):
+        check_mean(mu.numpy(), d[key + "|fmean"])
+        check_var(var.numpy(), d[key + "|fvar"], max(float(np.max(d[key + "|fvar"])), 1.0))
+
+
+def test_survey_pin_on_gpu(golden_dir):
+    pin = json.load(open(os.path.join(golden_dir, "aapl_pin.json")))
+    d = np.load(os.path.join(golden_dir, "kernel_cases.npz"))
+    m = gpx.models.GPR(data=(d["data|aapl_d|x"], d["data|aapl_d|y"]), kernel=K.SquaredExponential())
+    m.likelihood.variance.assign(1e-5)
+    gpx.set_trainable(m.likelihood.variance, False)
+    lml = float(m.log_marginal_likelihood())
+    assert lml == pytest.approx(pin["survey_lml"], rel=1e-11)
+    _, g = m.loss_and_grad_unconstrained()
+    np.testing.assert_allclose(g, pin["survey_grad_u"], rtol=1e-9)
+
+
+def test_reference_sweep_with_shared_kernels(golden_dir):
+    """GPR/main.py d->w->m with the 8 shared kernel objects of GPR/main.py:105-114, each fit as
+    GPR/model_trainer.py:14-25 (our ModelTrainer batches the 8 fits of one timeframe)."""
+    from portfoliooptgp_amd.trainer import ModelTrainer
+    ref = json.load(open(os.path.join(golden_dir, "reference_sweep.json")))
+    d = np.load(os.path.join(golden_dir, "kernel_cases.npz"))
+    kernels = [K.SquaredExponential(), K.Matern12(), K.RationalQuadratic(), K.Exponential(),
+               K.SquaredExponential() + K.Matern12(),
+               K.Exponential() + K.Periodic(K.SquaredExponential()) + K.Linear(),
+               K.Exponential() + K.Periodic(K.SquaredExponential()),
+               K.SquaredExponential() * K.Matern12()]
+    trainer = ModelTrainer(kernels)
+    for tf in ("d", "w", "m"):
+        x, y = d[f"data|aapl_{tf}|x"], d[f"data|aapl_{tf}|y"]
+        best_kernel, best_mse, best_model = trainer.train_model(x, y)
+        rows = ref["timeframes"][tf]["fits"]
+        for k, row, res in zip(kernels, rows, trainer.last_results):
+            assert res.fun == pytest.approx(row["loss"], rel=1e-5), (tf, row)
+        assert best_mse <= 10 * ref["timeframes"][tf]["best_mse"] + 1e-9
+        assert best_kernel in kernels and best_model.kernel is best_kernel
+
+
+def test_multi_input_composite(golden_dir):
+    """C4 shape (D=5): Exponential(dims 0-3) * Exponential(dim 4) and Matern52, N=67."""
+    d = np.load(os.path.join(golden_dir, "multi_input.npz"))
+    X, Y = d["X"], d["Y"]
+    for name, k in (("expexp", K.Exponential(active_dims=slice(0, 4)) * K.Exponential(active_dims=slice(4, 5))),
+                    ("m52", K.Matern52())):
+        m = gpx.models.GPR((X, Y), kernel=k, noise_variance=1e-3)
+        gpx.set_trainable(m.likelihood, False)
+        loss, g = m.loss_and_grad_unconstrained()
+        check_loss(loss, float(d[f"{name}|loss0"][0]))
+        check_grad(g, d[f"{name}|grad0"])
+        res = gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables)
+        assert res.fun == pytest.approx(float(d[f"{name}|loss_fit"][0]), rel=1e-5)
+        mu, var = m.predict_f(X)
+        np.testing.assert_allclose(mu.numpy()[:, 0], d[f"{name}|fmean"], rtol=1e-4, atol=1e-5)
+
+
+def test_not_positive_definite_is_reported():
+    """K = σ²11ᵀ + σn²I with σ² = 1e12 rounds to rank one: pivot 2 fails, like LAPACK potrf."""
+    x = np.zeros((10, 1))
+    y = np.ones((10, 1))
+    m = gpx.models.GPR(data=(x, y), kernel=K.SquaredExponential(variance=1e12), noise_variance=1e-6)
+    with pytest.raises(N.NotPositiveDefiniteError) as e:
+        m.training_loss()
+    assert int(e.value.info) == 2
+    # the healthy problems of a batch are unaffected by a failing one
+    good = gpx.models.GPR(data=(np.arange(10.0)[:, None], y), kernel=K.SquaredExponential())
+    eng = Engine([x, good.data[0]], [y, y], [compile_spec(m.kernel, 1), compile_spec(good.kernel, 1)])
+    lml, grad, info = eng.lml_grad([0, 1], np.stack([m.theta_row(), good.theta_row()]))
+    assert info[0] == 2 and info[1] == 0 and np.isfinite(lml[1]) and np.isnan(lml[0])
+
+
+def test_lockstep_batch_equals_sequential_fits():
+    data = [O.synthetic_series(200 + 17 * i, seed=i) for i in range(4)]
+    seq = []
+    for x, y in data:
+        m = gpx.models.GPR((x, y), kernel=K.SquaredExponential())
+        m.likelihood.variance.assign(1e-5)
+        gpx.set_trainable(m.likelihood.variance, False)
+        seq.append(gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables, options=dict(maxiter=100)))
+    models = []
+    for x, y in data:
+        m = gpx.models.GPR((x, y), kernel=K.SquaredExponential())
+        m.likelihood.variance.assign(1e-5)
+        gpx.set_trainable(m.likelihood.variance, False)
+        models.append(m)
+    bat = gpx.optimizers.Scipy().minimize_batch(models, options=dict(maxiter=100))
+    for a, b in zip(seq, bat):
+        assert a.nfev == b.nfev and a.nit == b.nit
+        np.testing.assert_allclose(a.x, b.x, rtol=1e-10)
+        assert a.fun == pytest.approx(b.fun, rel=1e-12)
+
+
+def test_fit_parity_end_to_end_synthetic():
+    x, y = O.synthetic_series(256, seed=21)
+    m = gpx.models.GPR((x, y), kernel=K.SquaredExponential())
+    m.likelihood.variance.assign(1e-5)
+    gpx.set_trainable(m.likelihood.variance, False)
+    res = gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables, options=dict(maxiter=100))
+    om = O.OGPR(x, y, O.OSquaredExponential(), noise_variance=1e-5)
+    om.noise.trainable = False
+    ro = O.scipy_minimize(om, 100)
+    assert res.fun == pytest.approx(ro.fun, rel=1e-5)
+    np.testing.assert_allclose(res.x, ro.x, rtol=1e-4)
+
+
+def test_edge_sizes_and_padding():
+    """N at, just below and just above the 64-row tile, and a 1-point problem."""
+    rng = np.random.default_rng(4)
+    for n in (1, 63, 64, 65, 127, 129, 191, 300):
+        x = np.sort(rng.uniform(0, 40, n))[:, None]
+        y = rng.standard_normal((n, 1))
+        for fam in ("se", "m32"):
+            m = gpx.models.GPR((x, y), kernel=gpx_kernel(fam), noise_variance=1e-2)
+            om = O.OGPR(x, y, oracle_kernel(fam), noise_variance=1e-2)
+            loss, g = m.loss_and_grad_unconstrained()
+            lo, go = om.loss_and_grad_u()
+            check_loss(loss, lo)
+            check_grad(g, go)
+            xs = np.linspace(-5, 45, 23)[:, None]
+            mu, var = m.predict_f(xs)
+            mo, vo = om.predict_f(xs)
+            check_mean(mu.numpy(), mo)
+            check_var(var.numpy(), vo, 1.0)
+
+
+def test_large_n_against_oracle():
+    """N=2048 full comparison (the oracle finishes in about a second)."""
+    x, y = O.synthetic_series(2048, seed=2)
+    m = gpx.models.GPR((x, y), kernel=K.SquaredExponential(lengthscales=30.0, variance=0.8))
+    m.likelihood.variance.assign(1e-5)
+    om = O.OGPR(x, y, O.OSquaredExponential(lengthscales=30.0, variance=0.8), noise_variance=1e-5)
+    loss, g = m.loss_and_grad_unconstrained()
+    lo, go = om.loss_and_grad_u()
+    assert abs(loss - lo) <= 1e-7 * abs(lo)
+    assert np.all(np.abs(g - go) <= 1e-5 * (1.0 + np.abs(go).max()))
+    mu, var = m.predict_f(x[::7])
+    mo, vo = om.predict_f(x[::7])
+    check_mean(mu.numpy(), mo)
+    assert np.all(np.abs(var.numpy() - vo) <= 1e-5 * np.abs(vo) + 1e-9)
+
+
+def test_full_size_properties_n4096():
+    """BASELINE config C2 size: size-independent properties of the GPU path alone."""
+    n = 4096
+    x, y = O.synthetic_series(n, seed=0)
+    theta = (40.0, 1.3)
+    m = gpx.models.GPR((x, y), kernel=K.SquaredExponential(lengthscales=theta[0], variance=theta[1]))
+    m.likelihood.variance.assign(1e-5)
+    gpx.set_trainable(m.likelihood.variance, False)
+    lml = float(m.log_marginal_likelihood())
+    # (1) permutation invariance of logML
+    perm = np.random.default_rng(0).permutation(n)
+    mp = gpx.models.GPR((x[perm], y[perm]), kernel=K.SquaredExponential(lengthscales=theta[0], variance=theta[1]))
+    mp.likelihood.variance.assign(1e-5)
+    assert float(mp.log_marginal_likelihood()) == pytest.approx(lml, rel=1e-9)
+    # (2) gradient = central finite difference of the GPU logML itself
+    loss, g = m.loss_and_grad_unconstrained()
+    u0 = np.array([v.numpy() for v in m.trainable_variables], dtype=float)
+    h = 1e-5
+    for i in range(2):
+        for s, store in ((1, "p"), (-1, "m")):
+            u = u0.copy()
+            u[i] += s * h
+            for v, ui in zip(m.trainable_variables, u):
+                v.assign(ui)
+            if store == "p":
+                lp = float(m.training_loss())
+            else:
+                lm = float(m.training_loss())
+        fd = (lp - lm) / (2 * h)
+        assert fd == pytest.approx(g[i], rel=2e-5, abs=1e-3)
+    for v, ui in zip(m.trainable_variables, u0):
+        v.assign(ui)
+    # (3) predict_y = predict_f + σn², and far from the data the prior is recovered
+    xs = np.concatenate([x[:50], [[1e6]]])
+    mu, var = m.predict_f(xs)
+    _, vy = m.predict_y(xs)
+    np.testing.assert_allclose(vy.numpy() - var.numpy(), 1e-5, rtol=1e-9)
+    assert abs(mu.numpy()[-1, 0]) < 1e-12 and var.numpy()[-1, 0] == pytest.approx(theta[1], rel=1e-12)
+    # (4) the logML against the oracle at the full size (one eval; a few seconds on the host)
+    om = O.OGPR(x, y, O.OSquaredExponential(lengthscales=theta[0], variance=theta[1]), noise_variance=1e-5)
+    assert lml == pytest.approx(om.log_marginal_likelihood(), rel=1e-8)
