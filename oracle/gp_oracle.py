@@ -391,7 +391,7 @@ class OGPR:
         n = self.Y.shape[0]
         return float(-0.5 * np.sum(a * a) - np.sum(np.log(np.diag(L))) - 0.5 * n * LOG2PI)
 
-    def loss_and_grad_u(self) -> Tuple[float, np.ndarray]:
+    def loss_and_grad_u(self):
         """training_loss = -logML and its gradient w.r.t. the unconstrained trainables.
 
         ∂logML/∂θ = ½ αᵀ(∂K/∂θ)α − ½ tr(K⁻¹ ∂K/∂θ),  α = K⁻¹y;  ∂θ/∂u = sigmoid(u).

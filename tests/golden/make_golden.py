@@ -83,9 +83,9 @@ def kernel_cases():
                 m = O.OGPR(x, y, k, noise_variance=noise)
                 try:
                     loss, g = m.loss_and_grad_u()
-                    loss_nt = None
                     m.noise.trainable = False
                     loss_nt, g_nt = m.loss_and_grad_u()
+                    cond = float(np.linalg.cond(m._Ky()))
                     m.noise.trainable = True
                     mu, var = m.predict_f(xf)
                     _, vary = m.predict_y(xf)
@@ -97,6 +97,7 @@ def kernel_cases():
                 arrays[key + "|loss"] = np.array([loss])
                 arrays[key + "|grad_u"] = g              # noise trainable (last entry = noise)
                 arrays[key + "|grad_u_fixed_noise"] = g_nt
+                arrays[key + "|cond"] = np.array([cond])
                 arrays[key + "|xnew"] = xf
                 arrays[key + "|fmean"] = mu[:, 0]
                 arrays[key + "|fvar"] = var[:, 0]
