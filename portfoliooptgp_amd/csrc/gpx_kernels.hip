@@ -159,12 +159,15 @@ void launch_leaf(const LeafArgs& a, int n_active, hipStream_t s) {
 // lane l is C[(l>>4) + 4r][l&15] (verified on gfx950, tools/probe_f64.hip).
 // ======================================================================================
 template <int BM, bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
+__global__ __launch_bounds__(256, (BM == 128 && EPI != EPI_CONTRACT) ? 2 : 1) void gemm_kernel(GemmArgs a) {
   constexpr int BN = BM, BK = 16, S = BM + 16;
   constexpr int WT = BM / 2;
   constexpr int MT = WT / 16;
   constexpr int NLD = BM * BK / 2 / 256;  // double2 chunks per thread per operand
-  __shared__ __attribute__((aligned(16))) double smem[2 * 2 * BK * S];
+  constexpr int kMainLds = 2 * 2 * BK * S;
+  constexpr int kEpiLds = (EPI == EPI_CONTRACT)
+      ? 4 * 32 * 64 + 2 * BM * GPX_MAX_DIM + 2 * BM + GPX_THETA_STRIDE + 64 : 0;
+  __shared__ __attribute__((aligned(16))) double smem[kMainLds > kEpiLds ? kMainLds : kEpiLds];
 
   const int b = a.active[blockIdx.y];
   int ti, tj;
@@ -240,33 +243,42 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
     }
   };
 
+  auto compute = [&](int cur) {
+    const double* sA = smem + (cur * 2 + 0) * BK * S;
+    const double* sB = smem + (cur * 2 + 1) * BK * S;
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      const int kr = (kk * 4 + (lane >> 4)) * S + (lane & 15);
+      double af[MT], bf[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) af[m] = sA[kr + wr * WT + m * 16];
+#pragma unroll
+      for (int n = 0; n < MT; ++n) bf[n] = sB[kr + wc * WT + n * 16];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < MT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
+    }
+  };
+
+  // Register-staged double buffer; the last K-tile is peeled so the loop body has no
+  // conditionals (a conditional prefetch made hipcc shuttle every accumulator between AGPRs
+  // and VGPRs once per K-tile).
   const int nk = (kmax - kmin) / BK;
   if (nk > 0) {
     gload(kmin);
     swrite(0);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) gload(kmin + (kt + 1) * BK);
-      const double* sA = smem + (cur * 2 + 0) * BK * S;
-      const double* sB = smem + (cur * 2 + 1) * BK * S;
-#pragma unroll
-      for (int kk = 0; kk < BK / 4; ++kk) {
-        const int kr = (kk * 4 + (lane >> 4)) * S + (lane & 15);
-        double af[MT], bf[MT];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) af[m] = sA[kr + wr * WT + m * 16];
-#pragma unroll
-        for (int n = 0; n < MT; ++n) bf[n] = sB[kr + wc * WT + n * 16];
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int n = 0; n < MT; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
-      }
-      if (kt + 1 < nk) swrite(cur ^ 1);
+    int cur = 0;
+    for (int kt = 0; kt < nk - 1; ++kt) {
+      gload(kmin + (kt + 1) * BK);
+      compute(cur);
+      swrite(cur ^ 1);
       __syncthreads();
+      cur ^= 1;
     }
+    compute(cur);
   }
 
   if constexpr (EPI == EPI_STORE) {
@@ -287,13 +299,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   } else if constexpr (EPI == EPI_CONTRACT) {
     // Gradient contraction over this lower tile of K⁻¹ = WᵀW (acc = K⁻¹_ij):
     //   g_θ += w_ij (α_i α_j − K⁻¹_ij) ∂K_ij/∂θ,  w = 2 below the diagonal, 1 on it.
+    // The accumulators go through LDS in two halves so that the kernel-derivative code runs
+    // as a compact loop (keeping its registers out of the MFMA main loop's budget).
     const int D = a.D;
-    double* sxi = smem;                   // [BM][D]
-    double* sxj = sxi + BM * D;           // [BN][D]
-    double* sai = sxj + BN * D;           // [BM]
-    double* saj = sai + BM;               // [BN]
-    double* sth = saj + BN;               // [16]
-    double* sred = sth + GPX_THETA_STRIDE;  // [4 waves][16]
+    double* sacc = smem;                      // [4 waves][32][64]
+    double* sxi = sacc + 4 * 32 * 64;         // [BM][D]
+    double* sxj = sxi + BM * D;               // [BN][D]
+    double* sai = sxj + BN * D;               // [BM]
+    double* saj = sai + BM;                   // [BN]
+    double* sth = saj + BN;                   // [16]
+    double* sred = sth + GPX_THETA_STRIDE;    // [4 waves][16]
     __syncthreads();
     const int n = a.nvalid[b];
     const double* X = a.X + (long long)b * a.sX;
@@ -305,24 +320,37 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
     }
     if (tid < BM) { sai[tid] = al[i0 + tid]; saj[tid] = al[j0 + tid]; }
     if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
-    __syncthreads();
     const DevSpec spec = a.specs[b];
     double sums[GPX_MAX_TERMS][3];
 #pragma unroll
     for (int t = 0; t < GPX_MAX_TERMS; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
     double snoise = 0.0;
+    // wave-local image [32 rows][WT cols]; lane -> column cl, rows rg, rg + RG, ...
+    constexpr int RG = 64 / WT;
+    double* wacc = sacc + wave * (32 * 64);
+    const int cl = lane % WT, rg = lane / WT;
+    const int jl = wc * WT + cl;            // this lane's column within the tile
+    const int j = j0 + jl;
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+    for (int h = 0; h < MT / 2; ++h) {
+      // rows m = 2h, 2h+1 of this wave's MFMA tiles
 #pragma unroll
-      for (int nn = 0; nn < MT; ++nn)
+      for (int mm = 0; mm < 2; ++mm)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int il = wr * WT + m * 16 + (lane >> 4) + 4 * r;
-          const int jl = wc * WT + nn * 16 + (lane & 15);
-          const int i = i0 + il, j = j0 + jl;
+        for (int nn = 0; nn < MT; ++nn)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            wacc[(mm * 16 + (lane >> 4) + 4 * r) * WT + nn * 16 + (lane & 15)] = acc[2 * h + mm][nn][r];
+      __syncthreads();
+      if (j < n) {
+        const double aj = saj[jl];
+#pragma unroll 1
+        for (int rr = rg; rr < 32; rr += RG) {
+          const int il = wr * WT + h * 32 + rr;
+          const int i = i0 + il;
           if (i >= j && i < n) {
             const double w = (i == j) ? 1.0 : 2.0;
-            const double v = w * fma(sai[il], saj[jl], -acc[m][nn][r]);
+            const double v = w * fma(sai[il], aj, -wacc[rr * WT + cl]);
             double dk[GPX_MAX_TERMS][3];
             eval_k_grad(spec, sth, sxi + il * D, sxj + jl * D, dk);
 #pragma unroll
@@ -334,6 +362,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
             if (i == j) snoise += v;
           }
         }
+      }
+      __syncthreads();
+    }
     // block reduction of the 13 sums, then scatter to θ positions
     double vals[GPX_MAX_TERMS * 3 + 1];
 #pragma unroll
