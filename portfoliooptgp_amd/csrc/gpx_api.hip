@@ -21,9 +21,13 @@
 
 using namespace gpx;
 
+constexpr int kGroups = 2;  // concurrent pipelines per evaluation (HIP streams)
+
 struct gpx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t workers[kGroups] = {};
+  hipEvent_t fork = nullptr, join[kGroups] = {};
   std::string err;
   int profiling = 0;
 };
@@ -75,9 +79,17 @@ int fail(gpx_ctx* ctx, int code, const std::string& msg) {
 
 inline long long mat_stride(const gpx_batch* bt) { return (long long)bt->Np * bt->Np; }
 
+// One pipeline instance: a contiguous range of the device active list on one stream.
+struct Run {
+  gpx_batch* bt;
+  const int* d_act;  // device pointer into the uploaded active list
+  int na;            // problems in this range
+  hipStream_t s;
+};
+
 // MFMA flops the GEMM launcher will issue for these args (bench / roofline bookkeeping)
-double gemm_issued_flops(const GemmArgs& a) {
-  const int bm = gemm_tile(a);
+double gemm_issued_flops(const GemmArgs& a, int na) {
+  const int bm = gemm_tile(a, na);
   const int ti = a.M / bm, tj = a.N / bm;
   double f = 0.0;
   for (int x = 0; x < ti; ++x)
@@ -91,19 +103,22 @@ double gemm_issued_flops(const GemmArgs& a) {
       if (a.tri & TRI_KMIN_I) kmin = std::max(kmin, i0);
       if (kmax > kmin) f += 2.0 * bm * bm * (kmax - kmin);
     }
-  return f;
+  return f * na;
 }
 
-void gemm(gpx_batch* bt, GemmArgs a, int epi, bool ta, bool tb, int na, hipStream_t s) {
-  a.active = bt->d_active;
-  launch_gemm(a, epi, ta, tb, na, s);
-  if (bt->ctx->profiling) bt->flops_acc += na * gemm_issued_flops(a);
+void gemm(const Run& r, GemmArgs a, int epi, bool ta, bool tb) {
+  a.active = r.d_act;
+  launch_gemm(a, epi, ta, tb, r.na, r.s);
+  if (r.bt->ctx->profiling) r.bt->flops_acc += gemm_issued_flops(a, r.na);
 }
 
 GemmArgs gemm_args(const double* A, int lda, const double* B, int ldb, double* C, int ldc,
                    long long stride, int M, int N, int K, int tri, int lower, double alpha,
                    double beta) {
   GemmArgs g{};
+  // longest-K tiles first, with the K-determining tile index as the slow one
+  g.order = (tri & TRI_KMAX_J) ? ORDER_COL_DESC : (tri & TRI_KMIN_J) ? ORDER_COL_ASC
+          : (tri & TRI_KMAX_I) ? ORDER_ROW_DESC : ORDER_ROW_ASC;
   g.A = A; g.sA = stride; g.lda = lda;
   g.Bm = B; g.sB = stride; g.ldb = ldb;
   g.C = C; g.sC = stride; g.ldc = ldc;
@@ -112,63 +127,89 @@ GemmArgs gemm_args(const double* A, int lda, const double* B, int ldb, double* C
   return g;
 }
 
-// Recursive Cholesky-and-inverse on the diagonal block [off, off+n) of every active problem.
-void chol_inv(gpx_batch* bt, int off, int n, int na, hipStream_t s) {
+// Recursive Cholesky-and-inverse on the diagonal block [off, off+n) of every problem of r.
+void chol_inv(const Run& r, int off, int n) {
+  gpx_batch* bt = r.bt;
   const int Np = bt->Np;
   const long long st = mat_stride(bt);
   if (n == kLeaf) {
     LeafArgs la{};
-    la.active = bt->d_active; la.K = bt->K; la.W = bt->W; la.sMat = st; la.ld = Np; la.off = off;
+    la.active = r.d_act; la.K = bt->K; la.W = bt->W; la.sMat = st; la.ld = Np; la.off = off;
     la.ldiag = bt->ldiag; la.sVec = Np; la.info = bt->d_info;
-    launch_leaf(la, na, s);
+    launch_leaf(la, r.na, r.s);
     return;
   }
   int n1 = ((n / 2 + kLeaf - 1) / kLeaf) * kLeaf;
   if (n1 >= n) n1 = n - kLeaf;
   const int n2 = n - n1;
-  chol_inv(bt, off, n1, na, s);
+  chol_inv(r, off, n1);
   const long long o11 = (long long)off * Np + off;
   const long long o21 = (long long)(off + n1) * Np + off;
   const long long o22 = (long long)(off + n1) * Np + off + n1;
   // L21 = A21 · W11ᵀ          (opB(k,j) = W11[j][k], nonzero for k <= j)
-  gemm(bt, gemm_args(bt->K + o21, Np, bt->W + o11, Np, bt->L + o21, Np, st, n2, n1, n1,
-                     TRI_KMAX_J, 0, 1.0, 0.0), EPI_STORE, false, true, na, s);
+  gemm(r, gemm_args(bt->K + o21, Np, bt->W + o11, Np, bt->L + o21, Np, st, n2, n1, n1,
+                    TRI_KMAX_J, 0, 1.0, 0.0), EPI_STORE, false, true);
   // A22 -= L21 · L21ᵀ         (lower tiles only)
-  gemm(bt, gemm_args(bt->L + o21, Np, bt->L + o21, Np, bt->K + o22, Np, st, n2, n2, n1, 0, 1,
-                     -1.0, 1.0), EPI_STORE, false, true, na, s);
-  chol_inv(bt, off + n1, n2, na, s);
+  gemm(r, gemm_args(bt->L + o21, Np, bt->L + o21, Np, bt->K + o22, Np, st, n2, n2, n1, 0, 1,
+                    -1.0, 1.0), EPI_STORE, false, true);
+  chol_inv(r, off + n1, n2);
   // T = L21 · W11 → the dead A21 region of K   (opB(k,j) = W11[k][j], nonzero for k >= j)
-  gemm(bt, gemm_args(bt->L + o21, Np, bt->W + o11, Np, bt->K + o21, Np, st, n2, n1, n1,
-                     TRI_KMIN_J, 0, 1.0, 0.0), EPI_STORE, false, false, na, s);
+  gemm(r, gemm_args(bt->L + o21, Np, bt->W + o11, Np, bt->K + o21, Np, st, n2, n1, n1,
+                    TRI_KMIN_J, 0, 1.0, 0.0), EPI_STORE, false, false);
   // W21 = −W22 · T             (opA(i,k) = W22[i][k], nonzero for k <= i)
-  gemm(bt, gemm_args(bt->W + o22, Np, bt->K + o21, Np, bt->W + o21, Np, st, n2, n1, n2,
-                     TRI_KMAX_I, 0, -1.0, 0.0), EPI_STORE, false, false, na, s);
+  gemm(r, gemm_args(bt->W + o22, Np, bt->K + o21, Np, bt->W + o21, Np, st, n2, n1, n2,
+                    TRI_KMAX_I, 0, -1.0, 0.0), EPI_STORE, false, false);
 }
 
-// K build + factor + α for the active problems (device active list already uploaded).
-void factor_and_alpha(gpx_batch* bt, int na, hipStream_t s) {
-  const long long st = mat_stride(bt);
+// K build + recursive factor for the problems of r.
+void factor(const Run& r) {
+  gpx_batch* bt = r.bt;
   BuildArgs ba{};
-  ba.active = bt->d_active; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
+  ba.active = r.d_act; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
   ba.X = bt->X; ba.sX = (long long)bt->Nmax * bt->D; ba.X2 = bt->X; ba.sX2 = ba.sX; ba.D = bt->D;
-  ba.m2 = 0; ba.out = bt->K; ba.sOut = st; ba.ldo = bt->Np; ba.rows = ba.cols = bt->Np;
+  ba.m2 = 0; ba.out = bt->K; ba.sOut = mat_stride(bt); ba.ldo = bt->Np; ba.rows = ba.cols = bt->Np;
   ba.symmetric = 1;
-  launch_build(ba, na, s);
-  chol_inv(bt, 0, bt->Np, na, s);
+  launch_build(ba, r.na, r.s);
+  chol_inv(r, 0, bt->Np);
 }
 
-void alpha_solve(gpx_batch* bt, int na, hipStream_t s) {
+// z = W y, α = Wᵀ z
+void alpha_solve(const Run& r) {
+  gpx_batch* bt = r.bt;
   const long long st = mat_stride(bt);
   TrmvArgs t{};
-  t.active = bt->d_active; t.Wm = bt->W; t.sW = st; t.ld = bt->Np;
+  t.active = r.d_act; t.Wm = bt->W; t.sW = st; t.ld = bt->Np;
   t.x = bt->Y; t.sx = bt->Nmax; t.nvalid = bt->d_n; t.y = bt->z; t.sy = bt->Np;
   t.rows = t.cols = bt->Np; t.lower = 1;
-  launch_trmv_n(t, na, s);
+  launch_trmv_n(t, r.na, r.s);
   TrmvArgs u{};
-  u.active = bt->d_active; u.Wm = bt->W; u.sW = st; u.ld = bt->Np;
+  u.active = r.d_act; u.Wm = bt->W; u.sW = st; u.ld = bt->Np;
   u.x = bt->z; u.sx = bt->Np; u.nvalid = nullptr; u.y = bt->alpha; u.sy = bt->Np;
   u.rows = u.cols = bt->Np; u.lower = 1;
-  launch_trmv_t(u, na, s);
+  launch_trmv_t(u, r.na, r.s);
+}
+
+// fused K⁻¹ = WᵀW formation + gradient contraction over lower tiles, then the reduction
+void contract(const Run& r) {
+  gpx_batch* bt = r.bt;
+  GemmArgs g = gemm_args(bt->W, bt->Np, bt->W, bt->Np, nullptr, 0, mat_stride(bt), bt->Np, bt->Np,
+                         bt->Np, TRI_KMIN_I, 1, 1.0, 0.0);
+  g.vec = bt->alpha; g.sVec = bt->Np; g.X = bt->X; g.sX = (long long)bt->Nmax * bt->D; g.D = bt->D;
+  g.specs = bt->d_specs; g.theta = bt->d_theta; g.nvalid = bt->d_n;
+  g.partial = bt->partial; g.sPartial = bt->partial_stride;
+  gemm(r, g, EPI_CONTRACT, true, false);
+}
+
+void reduce(const Run& r) {
+  gpx_batch* bt = r.bt;
+  GemmArgs g{};
+  g.M = g.N = bt->Np; g.lower_only = 1;
+  const int bm = gemm_tile(g, r.na), tt = bt->Np / bm;
+  ReduceArgs ra{};
+  ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
+  ra.ntiles = tt * (tt + 1) / 2; ra.z = bt->z; ra.sVec = bt->Np; ra.ldiag = bt->ldiag;
+  ra.nvalid = bt->d_n; ra.specs = bt->d_specs; ra.results = bt->results; ra.Np = bt->Np;
+  launch_reduce(ra, r.na, r.s);
 }
 
 struct PhaseTimer {
@@ -231,7 +272,12 @@ int gpx_create(int device, gpx_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return GPX_HIP_ERROR;
   gpx_ctx* c = new gpx_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+  for (int g = 0; g < kGroups && ok; ++g)
+    ok = hipStreamCreateWithFlags(&c->workers[g], hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&c->join[g], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
     delete c;
     return GPX_HIP_ERROR;
   }
@@ -241,8 +287,13 @@ int gpx_create(int device, gpx_ctx** out) {
 
 int gpx_destroy(gpx_ctx* ctx) {
   if (!ctx) return GPX_BAD_ARG;
-  hipSetDevice(ctx->device);
-  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  (void)hipSetDevice(ctx->device);
+  for (int g = 0; g < kGroups; ++g) {
+    if (ctx->workers[g]) (void)hipStreamDestroy(ctx->workers[g]);
+    if (ctx->join[g]) (void)hipEventDestroy(ctx->join[g]);
+  }
+  if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return GPX_OK;
 }
@@ -342,52 +393,71 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   int rc = upload_common(bt, n_active, active, theta, s);
   if (rc != GPX_OK) return rc;
-  const int na = n_active;
-  PhaseTimer pt(ctx->profiling != 0, s);
   bt->flops_acc = 0.0;
-  pt.mark();
-  factor_and_alpha(bt, na, s);
-  pt.mark();
-  alpha_solve(bt, na, s);
-  pt.mark();
-  // fused K⁻¹ = WᵀW + gradient contraction over lower tiles
-  GemmArgs g = gemm_args(bt->W, bt->Np, bt->W, bt->Np, nullptr, 0, mat_stride(bt), bt->Np, bt->Np,
-                         bt->Np, TRI_KMIN_I, 1, 1.0, 0.0);
-  g.vec = bt->alpha; g.sVec = bt->Np; g.X = bt->X; g.sX = (long long)bt->Nmax * bt->D; g.D = bt->D;
-  g.specs = bt->d_specs; g.theta = bt->d_theta; g.nvalid = bt->d_n;
-  g.partial = bt->partial; g.sPartial = bt->partial_stride;
-  pt.mark();
-  gemm(bt, g, EPI_CONTRACT, true, false, na, s);
-  pt.mark();
-  const int bm = gemm_tile(g), tt = bt->Np / bm;
-  ReduceArgs r{};
-  r.active = bt->d_active; r.partial = bt->partial; r.sPartial = bt->partial_stride;
-  r.ntiles = tt * (tt + 1) / 2; r.z = bt->z; r.sVec = bt->Np; r.ldiag = bt->ldiag;
-  r.nvalid = bt->d_n; r.specs = bt->d_specs; r.results = bt->results; r.Np = bt->Np;
-  launch_reduce(r, na, s);
-  pt.mark();
+  // Split the active problems into up to kGroups ranges, each running the whole pipeline on
+  // its own stream: one group's latency-bound phases (64x64 leaves, small recursion levels)
+  // overlap another group's large MFMA GEMMs.
+  const int ng = n_active >= 4 ? kGroups : 1;
+  Run runs[kGroups];
+  int start = 0;
+  for (int g = 0; g < ng; ++g) {
+    const int cnt = n_active / ng + (g < n_active % ng ? 1 : 0);
+    runs[g] = Run{bt, bt->d_active + start, cnt, ng == 1 ? s : ctx->workers[g]};
+    start += cnt;
+  }
+  if (ng > 1) {
+    HIPX(ctx, hipEventRecord(ctx->fork, s));
+    for (int g = 0; g < ng; ++g) HIPX(ctx, hipStreamWaitEvent(runs[g].s, ctx->fork, 0));
+  }
+  PhaseTimer total(ctx->profiling != 0, s);
+  total.mark();
+  std::vector<PhaseTimer> pts;
+  pts.reserve(ng);
+  for (int g = 0; g < ng; ++g) pts.emplace_back(ctx->profiling != 0, runs[g].s);
+  for (int g = 0; g < ng; ++g) {
+    const Run& r = runs[g];
+    pts[g].mark();
+    factor(r);
+    pts[g].mark();
+    alpha_solve(r);
+    pts[g].mark();
+    contract(r);
+    pts[g].mark();
+    reduce(r);
+    pts[g].mark();
+  }
+  if (ng > 1) {
+    for (int g = 0; g < ng; ++g) {
+      HIPX(ctx, hipEventRecord(ctx->join[g], runs[g].s));
+      HIPX(ctx, hipStreamWaitEvent(s, ctx->join[g], 0));
+    }
+  }
+  total.mark();
   HIPX(ctx, hipGetLastError());
   HIPX(ctx, hipMemcpyAsync(bt->h_results.data(), bt->results, sizeof(double) * kResStride * bt->B,
                            hipMemcpyDeviceToHost, s));
   HIPX(ctx, hipMemcpyAsync(bt->h_info.data(), bt->d_info, sizeof(int) * bt->B, hipMemcpyDeviceToHost, s));
   HIPX(ctx, hipStreamSynchronize(s));
-  if (pt.on) {
-    bt->timing.factor_ms = pt.ms(0, 1);
-    bt->timing.alpha_ms = pt.ms(1, 2);
-    bt->timing.grad_ms = pt.ms(2, 5);
+  if (total.on) {
+    bt->timing.factor_ms = bt->timing.alpha_ms = bt->timing.grad_ms = 0.0;
+    for (int g = 0; g < ng; ++g) {
+      bt->timing.factor_ms += pts[g].ms(0, 1) / ng;
+      bt->timing.alpha_ms += pts[g].ms(1, 2) / ng;
+      bt->timing.grad_ms += pts[g].ms(2, 4) / ng;
+      bt->timing.contract_ms_total += pts[g].ms(2, 3);
+      bt->timing.contract_launches += 1.0;
+      double f = 0.0;
+      for (int i = 0; i < bt->Np; ++i) f += 2.0 * (i + 1) * (double)(bt->Np - i);
+      bt->timing.contract_alg_flops += runs[g].na * f;
+    }
     bt->timing.predict_ms = 0.0;
-    bt->timing.total_ms = pt.ms(0, 5);
+    bt->timing.total_ms = total.ms(0, 1);
     bt->timing.gemm_flops = bt->flops_acc;
-    bt->timing.contract_ms_total += pt.ms(3, 4);
-    bt->timing.contract_launches += 1.0;
-    double f = 0.0;
-    for (int i = 0; i < bt->Np; ++i) f += 2.0 * (i + 1) * (double)(bt->Np - i);
-    bt->timing.contract_alg_flops += na * f;
-    bt->timing.eval_ms_total += pt.ms(0, 5);
-    bt->timing.evals += na;
+    bt->timing.eval_ms_total += total.ms(0, 1);
+    bt->timing.evals += n_active;
   }
   int status = GPX_OK;
-  for (int i = 0; i < na; ++i) {
+  for (int i = 0; i < n_active; ++i) {
     const int b = active[i];
     const double* res = bt->h_results.data() + (size_t)b * kResStride;
     info[b] = bt->h_info[b];
@@ -435,8 +505,9 @@ int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const 
   if (!refac.empty()) {
     HIPX(ctx, hipMemcpyAsync(bt->d_active, refac.data(), sizeof(int) * refac.size(),
                              hipMemcpyHostToDevice, s));
-    factor_and_alpha(bt, (int)refac.size(), s);
-    alpha_solve(bt, (int)refac.size(), s);
+    const Run rr{bt, bt->d_active, (int)refac.size(), s};
+    factor(rr);
+    alpha_solve(rr);
     HIPX(ctx, hipMemcpyAsync(bt->d_active, active, sizeof(int) * n_active, hipMemcpyHostToDevice, s));
   }
   pt.mark();
@@ -472,7 +543,7 @@ int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const 
   // A = W · Kxs with fused column sum of squares
   GemmArgs g = gemm_args(bt->W, Np, kxs, Mp, nullptr, Mp, 0, Np, Mp, Np, TRI_KMAX_I, 0, 1.0, 0.0);
   g.sA = mat_stride(bt); g.sB = skx; g.sC = 0;
-  const int bm = gemm_tile(g);
+  const int bm = gemm_tile(g, n_active);
   const int nrt = Np / bm;
   const size_t pneed = (size_t)bt->B * nrt * Mp;
   if (bt->pvp_cap < pneed) {
@@ -482,7 +553,7 @@ int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const 
     bt->pvp_cap = pneed;
   }
   g.partial = bt->pvp; g.sPartial = (long long)nrt * Mp;
-  gemm(bt, g, EPI_COLSUMSQ, false, false, n_active, s);
+  gemm(Run{bt, bt->d_active, n_active, s}, g, EPI_COLSUMSQ, false, false);
   PredVarArgs pv{};
   pv.active = bt->d_active; pv.partial = bt->pvp; pv.sPartial = (long long)nrt * Mp;
   pv.nrowtiles = nrt; pv.ldp = Mp; pv.Xnew = Xnew; pv.sXnew = (long long)M * bt->D; pv.D = bt->D;

@@ -36,6 +36,8 @@ struct LeafArgs {
 // ---- batched fp64 MFMA GEMM -----------------------------------------------------------
 enum : int { TRI_KMAX_I = 1, TRI_KMAX_J = 2, TRI_KMIN_J = 4, TRI_KMIN_I = 8 };
 enum : int { EPI_STORE = 0, EPI_CONTRACT = 1, EPI_COLSUMSQ = 2 };
+// tile enumeration for rectangular launches (see gemm_kernel)
+enum : int { ORDER_ROW_ASC = 0, ORDER_COL_DESC = 1, ORDER_ROW_DESC = 2, ORDER_COL_ASC = 3 };
 
 struct GemmArgs {
   const int* active;
@@ -45,6 +47,7 @@ struct GemmArgs {
   int M, N, K;
   int tri;            // TRI_* flags restricting the k range per tile
   int lower_only;     // only tiles with ti >= tj
+  int order;          // ORDER_* tile enumeration (rectangular launches)
   double alpha, beta;
   // EPI_CONTRACT
   const double* vec; long long sVec;        // α vectors [B][Np]
@@ -91,6 +94,6 @@ void launch_trmv_n(const TrmvArgs& a, int n_active, hipStream_t s);   // y = M x
 void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s);   // y = Mᵀ x  (column sums)
 void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s);
 void launch_predvar(const PredVarArgs& a, int n_active, hipStream_t s);
-int gemm_tile(const GemmArgs& a);  // tile edge the launcher will use (64 or 128)
+int gemm_tile(const GemmArgs& a, int n_active);  // tile edge the launcher will use (64 or 128)
 
 }  // namespace gpx

@@ -93,55 +93,141 @@ void launch_build(const BuildArgs& a, int n_active, hipStream_t s) {
 }
 
 // ======================================================================================
-// Leaf: Cholesky of the 64x64 diagonal block at (off, off) of the (already updated) K,
-// then W11 = L11⁻¹. Writes W11 (zeros above the diagonal) and log L_ii. One WG per problem.
+// Leaf: Cholesky of the 64x64 diagonal block at (off, off) of the (already updated) K and
+// W11 = L11⁻¹. One workgroup (4 waves) per problem, blocked in 4 panels of 16:
+//   diag 16x16: wave 0 factors it and inverts it in registers (lane i = row i; broadcasts by
+//               v_readlane, no barriers), giving L_jj (for log det) and D = L_jj⁻¹;
+//   panel:      L_ij = A_ij · Dᵀ                          (f64 MFMA 16x16x4, one wave per block)
+//   trailing:   A_ik -= L_ij · L_kjᵀ                      (f64 MFMA)
+// then W = L⁻¹ block rows: W_ij = −D_i · Σ_{k=j}^{i−1} L_ik W_kj (f64 MFMA; the accumulator of
+// the first product is the B operand of the second without an LDS round trip).
+// 15 barriers in all. Writes W11 (zeros above the diagonal) and log L_ii.
 // ======================================================================================
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)(u & 0xffffffffu), l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
 __global__ __launch_bounds__(256) void leaf_kernel(LeafArgs a) {
+  constexpr int S = 66;  // row stride (doubles): 16 rows x 1 col fragment reads are conflict-free
+  __shared__ __attribute__((aligned(16))) double sA[64 * S];
+  __shared__ __attribute__((aligned(16))) double sW[64 * S];
+  __shared__ int sfail;
   const int b = a.active[blockIdx.x];
-  __shared__ double sL[64][65];
-  __shared__ double sW[64][65];
-  __shared__ double sd[64];
   const double* K = a.K + (long long)b * a.sMat;
   double* W = a.W + (long long)b * a.sMat;
   const int ld = a.ld, off = a.off, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, l4 = lane >> 4;
   for (int e = tid; e < 4096; e += 256) {
     const int r = e >> 6, c = e & 63;
-    sL[r][c] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
+    sA[r * S + c] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
+    sW[r * S + c] = 0.0;
   }
+  if (tid == 0) sfail = -1;
   __syncthreads();
-  int fail = -1;
-  for (int j = 0; j < 64; ++j) {
-    const double d = sL[j][j];
-    if (!(d > 0.0) && fail < 0) fail = j;
-    const double ljj = sqrt(d);
-    if (tid > j && tid < 64) sL[tid][j] = sL[tid][j] / ljj;
-    if (tid == 0) sd[j] = ljj;
+
+  for (int jb = 0; jb < 4; ++jb) {
+    const int c0 = jb * 16;
+    if (wave == 0) {
+      double r[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) r[k] = sA[(c0 + l15) * S + c0 + k];
+      int fail = -1;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const double piv = readlane_d(r[j], j);
+        if (!(piv > 0.0) && fail < 0) fail = j;
+        const double ljj = sqrt(piv);
+        const double inv = 1.0 / ljj;
+        r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
+#pragma unroll
+        for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], readlane_d(r[j], k), r[k]);
+      }
+      // lane l15 holds row l15 of L_jj (r[0..l15]); column l15 of D = L_jj⁻¹ by substitution
+      double w[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        double sacc = (i == l15) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < i; ++k) sacc = fma(-readlane_d(r[k], i), w[k], sacc);
+        w[i] = sacc / readlane_d(r[i], i);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sW[(c0 + i) * S + c0 + lane] = w[i];
+        a.ldiag[(long long)b * a.sVec + off + c0 + lane] = log(r[lane & 15]);
+      }
+      if (lane == 0 && fail >= 0 && sfail < 0) sfail = c0 + fail;
+    }
     __syncthreads();
-    for (int e = tid; e < 4096; e += 256) {
-      const int r = e >> 6, c = e & 63;
-      if (c > j && c <= r) sL[r][c] = fma(-sL[r][j], sL[c][j], sL[r][c]);
+    // panel: L_(ib,jb) = A_(ib,jb) · Dᵀ for ib = jb+1 .. 3, one wave per block
+    const int nblk = 3 - jb;
+    if (wave < nblk) {
+      const int r0 = (jb + 1 + wave) * 16;
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const double av = sA[(r0 + l15) * S + c0 + 4 * kk + l4];
+        const double bv = sW[(c0 + l15) * S + c0 + 4 * kk + l4];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sA[(r0 + l4 + 4 * q) * S + c0 + l15] = acc[q];
+    }
+    __syncthreads();
+    // trailing update of the lower blocks (ib, kb), jb < kb <= ib
+    const int ntr = nblk * (nblk + 1) / 2;
+    for (int t = wave; t < ntr; t += 4) {
+      int p = 0;
+      while ((p + 1) * (p + 2) / 2 <= t) ++p;
+      const int q = t - p * (p + 1) / 2;
+      const int ri = (jb + 1 + p) * 16, rk = (jb + 1 + q) * 16;
+      d4 acc;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = sA[(ri + l4 + 4 * u) * S + rk + l15];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const double av = sA[(ri + l15) * S + c0 + 4 * kk + l4];
+        const double bv = sA[(rk + l15) * S + c0 + 4 * kk + l4];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sA[(ri + l4 + 4 * u) * S + rk + l15] = acc[u];
     }
     __syncthreads();
   }
-  if (tid < 64) sL[tid][tid] = sd[tid];
-  __syncthreads();
-  // W = L⁻¹ by forward substitution; thread j owns column j (W[k][j] = 0 for k < j).
-  if (tid < 64) {
-    const int j = tid;
-    for (int i = 0; i < 64; ++i) {
-      double s = 0.0;
-      for (int k = 0; k < i; ++k) s = fma(sL[i][k], sW[k][j], s);
-      const double v = (i < j) ? 0.0 : (i == j ? 1.0 / sL[i][i] : -s / sL[i][i]);
-      sW[i][j] = v;
+  // W = L⁻¹: block rows 1..3, blocks j < i in parallel (wave j)
+  for (int i = 1; i < 4; ++i) {
+    if (wave < i) {
+      const int j = wave;
+      d4 t = {0.0, 0.0, 0.0, 0.0};
+      for (int k = j; k < i; ++k) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const double av = sA[(i * 16 + l15) * S + k * 16 + 4 * kk + l4];   // L_ik[row][k']
+          const double bv = sW[(k * 16 + 4 * kk + l4) * S + j * 16 + l15];   // W_kj[k'][col]
+          t = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, t, 0, 0, 0);
+        }
+      }
+      d4 wv = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const double av = sW[(i * 16 + l15) * S + i * 16 + 4 * kk + l4];     // D_i[row][k']
+        wv = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, t[kk], wv, 0, 0, 0);  // T[k'][col]
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sW[(i * 16 + l4 + 4 * q) * S + j * 16 + l15] = wv[q];
     }
+    __syncthreads();
   }
-  __syncthreads();
   for (int e = tid; e < 4096; e += 256) {
     const int r = e >> 6, c = e & 63;
-    W[(long long)(off + r) * ld + off + c] = sW[r][c];
+    W[(long long)(off + r) * ld + off + c] = sW[r * S + c];
   }
-  if (tid < 64) a.ldiag[(long long)b * a.sVec + off + tid] = log(sd[tid]);
-  if (tid == 0 && fail >= 0 && a.info[b] == 0) a.info[b] = off + fail + 1;
+  if (tid == 0 && sfail >= 0 && a.info[b] == 0) a.info[b] = off + sfail + 1;
 }
 
 void launch_leaf(const LeafArgs& a, int n_active, hipStream_t s) {
@@ -174,9 +260,16 @@ __global__ __launch_bounds__(256, (BM == 128 && EPI != EPI_CONTRACT) ? 2 : 1) vo
   if (a.lower_only) {
     lower_tile(blockIdx.x, ti, tj);
   } else {
-    const int ntj = a.N / BN;
-    ti = blockIdx.x / ntj;
-    tj = blockIdx.x - ti * ntj;
+    // Workgroups are dealt round-robin over the 8 XCDs: make the index that sets a tile's
+    // K range the SLOW one (so every XCD gets the same mix) and run the longest tiles first.
+    const int nti = a.M / BM, ntj = a.N / BN;
+    const int x = blockIdx.x;
+    switch (a.order) {
+      case ORDER_COL_DESC: tj = ntj - 1 - x / nti; ti = x % nti; break;
+      case ORDER_COL_ASC:  tj = x / nti; ti = x % nti; break;
+      case ORDER_ROW_DESC: ti = nti - 1 - x / ntj; tj = x % ntj; break;
+      default:             ti = x / ntj; tj = x % ntj; break;
+    }
   }
   const int i0 = ti * BM, j0 = tj * BN;
   int kmin = 0, kmax = a.K;
@@ -226,16 +319,17 @@ __global__ __launch_bounds__(256, (BM == 128 && EPI != EPI_CONTRACT) ? 2 : 1) vo
       const int c = tid + 256 * q;
       if (!TA) {
         const int row = c >> 3, kc = (c & 7) * 2;
-        sA[kc * S + row] = ra[q].x;
-        sA[(kc + 1) * S + row] = ra[q].y;
+        // transposed write: XOR-swizzle the row inside its 16-row group by k (bank spread)
+        sA[kc * S + (row ^ (kc & 15))] = ra[q].x;
+        sA[(kc + 1) * S + (row ^ ((kc + 1) & 15))] = ra[q].y;
       } else {
         const int krow = c / (BM / 2), ic = (c % (BM / 2)) * 2;
         *reinterpret_cast<d2*>(sA + krow * S + ic) = ra[q];
       }
       if (TB) {
         const int row = c >> 3, kc = (c & 7) * 2;
-        sB[kc * S + row] = rb[q].x;
-        sB[(kc + 1) * S + row] = rb[q].y;
+        sB[kc * S + (row ^ (kc & 15))] = rb[q].x;
+        sB[(kc + 1) * S + (row ^ ((kc + 1) & 15))] = rb[q].y;
       } else {
         const int krow = c / (BN / 2), jc = (c % (BN / 2)) * 2;
         *reinterpret_cast<d2*>(sB + krow * S + jc) = rb[q];
@@ -248,12 +342,15 @@ __global__ __launch_bounds__(256, (BM == 128 && EPI != EPI_CONTRACT) ? 2 : 1) vo
     const double* sB = smem + (cur * 2 + 1) * BK * S;
 #pragma unroll
     for (int kk = 0; kk < BK / 4; ++kk) {
-      const int kr = (kk * 4 + (lane >> 4)) * S + (lane & 15);
+      const int k = kk * 4 + (lane >> 4);
+      const int kr = k * S + (lane & 15);
+      const int krs = k * S + ((lane & 15) ^ (k & 15));  // swizzled image (transposed writes)
+      const int ka = TA ? kr : krs, kb = TB ? krs : kr;
       double af[MT], bf[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) af[m] = sA[kr + wr * WT + m * 16];
+      for (int m = 0; m < MT; ++m) af[m] = sA[ka + wr * WT + m * 16];
 #pragma unroll
-      for (int n = 0; n < MT; ++n) bf[n] = sB[kr + wc * WT + n * 16];
+      for (int n = 0; n < MT; ++n) bf[n] = sB[kb + wc * WT + n * 16];
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -417,8 +514,13 @@ __global__ __launch_bounds__(256, (BM == 128 && EPI != EPI_CONTRACT) ? 2 : 1) vo
   }
 }
 
-int gemm_tile(const GemmArgs& a) {
-  return (a.M % 128 == 0 && a.N % 128 == 0) ? 128 : 64;
+// 128x128 tiles when they still give every CU about two workgroups, else 64x64 tiles:
+// small recursion levels are latency-bound on a single CU per tile otherwise.
+int gemm_tile(const GemmArgs& a, int n_active) {
+  if (a.M % 128 != 0 || a.N % 128 != 0) return 64;
+  const long long t = (long long)(a.M / 128) * (a.N / 128);
+  const long long tiles = a.lower_only ? (long long)(a.M / 128) * (a.M / 128 + 1) / 2 : t;
+  return tiles * n_active >= 384 ? 128 : 64;
 }
 
 template <int BM, int EPI>
@@ -433,7 +535,7 @@ static void launch_gemm_t(const GemmArgs& a, bool ta, bool tb, int n_active, hip
 }
 
 void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hipStream_t s) {
-  const int bm = gemm_tile(a);
+  const int bm = gemm_tile(a, n_active);
   if (bm == 128) {
     if (epi == EPI_STORE) launch_gemm_t<128, EPI_STORE>(a, ta, tb, n_active, s);
     else if (epi == EPI_CONTRACT) launch_gemm_t<128, EPI_CONTRACT>(a, ta, tb, n_active, s);
