@@ -9,12 +9,14 @@ One *fit* is exactly one inner iteration of GPR/model_trainer.py:14-25 for the S
 GPflow defaults (σ²=1, ℓ=1), σn²=1e-5 fixed, scipy L-BFGS-B (maxiter=100) on the
 unconstrained variables to termination, then predict_f at the N training points.
 
-One *step* = fitting one batch of `--batch` independent series per GPU concurrently
-(lock-step batched evaluations, each series driven by its own unmodified scipy L-BFGS-B),
-followed by one batched predict_f and, for N > 1 GPUs, an RCCL all_gather of every fit's
-(θ*, loss*, nfev, last predicted mean/var) — the per-asset hand-off to the portfolio step.
+One *step* = fitting `--fits` independent series per GPU (each driven by its own unmodified
+scipy L-BFGS-B) through `--width` resident device slots with continuous batching: the
+evaluations of all resident fits run as one batched device pass, and a slot is refilled as
+soon as its fit converges and has run its predict_f. For N > 1 GPUs the step ends with an
+RCCL all_gather of every fit's (θ*, loss*, nfev, last predicted mean/var) — the per-asset
+hand-off to the portfolio step.
 Inputs are resident in HBM before the timed region. Each rank fits its own series
-(seed = rank * batch + b): weak scaling.
+(seed = rank * fits + f): weak scaling.
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N>1 the driver uses
 python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -94,7 +96,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("GPX_BENCH_BATCH", 16)))
+    ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 64)),
+                    help="independent series fitted per GPU per step")
+    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 32)),
+                    help="resident device slots (continuous-batching width)")
     ap.add_argument("--n", type=int, default=N_POINTS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -116,17 +121,18 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    B, n = args.batch, args.n
-    seeds = [rank * B + b for b in range(B)]
+    F, W, n = args.fits, args.width, args.n
+    seeds = [rank * F + f for f in range(F)]
     data = [synthetic_series(n, s) for s in seeds]
     Xd = [torch.as_tensor(x, device=dev) for x, _ in data]  # resident in HBM before timing
     Yd = [torch.as_tensor(y, device=dev) for _, y in data]
-    kern = [gpx.kernels.SquaredExponential() for _ in range(B)]
-    models = [gpx.models.GPR(data=(Xd[b], Yd[b]), kernel=kern[b], device=local_rank) for b in range(B)]
+    models = [gpx.models.GPR(data=(Xd[f], Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=local_rank)
+              for f in range(F)]
     for m in models:
         m.likelihood.variance.assign(NOISE)
         gpx.set_trainable(m.likelihood.variance, False)
-    engine = Engine(Xd, Yd, [compile_spec(m.kernel, 1) for m in models], device=local_rank)
+    # W resident device slots (continuous batching), sized for N-point problems
+    engine = Engine(Xd[:W], Yd[:W], [compile_spec(m.kernel, 1) for m in models[:W]], device=local_rank)
     engine.ctx.set_profiling(True)
     opt = gpx.optimizers.Scipy()
 
@@ -134,8 +140,8 @@ def main():
         for m in models:  # every step starts from GPflow defaults
             m.kernel.lengthscales.assign(1.0)
             m.kernel.variance.assign(1.0)
-        res = opt.minimize_batch(models, engine=engine, options=dict(maxiter=MAXITER))
-        preds = predict_f_batch(models, Xd)
+        res, preds = opt.minimize_stream(models, width=W, engine=engine, predict_train=True,
+                                         options=dict(maxiter=MAXITER))
         summary = torch.stack([
             torch.stack([
                 torch.tensor(m.kernel.lengthscales.value, device=dev, dtype=torch.float64),
@@ -175,7 +181,7 @@ def main():
     else:
         nfev_mean = float(np.mean(nfev))
 
-    total_fits = B * args.steps * world
+    total_fits = F * args.steps * world
     value = total_fits / elapsed
     contract_ms = tm.contract_ms_total / max(tm.contract_launches, 1.0)
     contract_flops = tm.contract_alg_flops / max(tm.contract_launches, 1.0)
@@ -196,7 +202,7 @@ def main():
         "data": "synthetic (C2 generator, seeded per rank/series)",
         "config": {"workload": "C2: exact GPR fit, synthetic 1-D series, N=4096, SquaredExponential, "
                                "fp64, sigma_n^2=1e-5 fixed, L-BFGS-B maxiter=100 + predict_f(X_train)",
-                   "N": n, "fits_per_gpu_per_step": B, "kernel": "SquaredExponential",
+                   "N": n, "fits_per_gpu_per_step": F, "device_slots": W, "kernel": "SquaredExponential",
                    "parallelism": f"independent fits, {world} process(es) x 1 GPU, RCCL all_gather of results"},
         "nfev_mean": nfev_mean,
         "evals_per_s": tm.evals / elapsed if world == 1 else None,

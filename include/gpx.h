@@ -102,6 +102,14 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
 int gpx_batch_destroy(gpx_batch* batch);
 
 /*
+ * Rebind slot b to a new problem: the caller has already written its inputs into row b of
+ * the X / Y arrays given at creation (n <= N_max valid points); this updates n[b] and the
+ * kernel spec and invalidates the slot's cached factor. Used to stream many fits through a
+ * fixed set of device slots (continuous batching).
+ */
+int gpx_batch_rebind(gpx_batch* batch, int b, int n, const gpx_kernel_spec* spec);
+
+/*
  * logML and ∂logML/∂θ at theta for the n_active problems listed in active (host int32).
  * Outputs are written at each active problem's row: lml[b], grad[b*GPX_THETA_STRIDE + p],
  * info[b]. stream may be NULL (library stream). Returns after the outputs are on the host.

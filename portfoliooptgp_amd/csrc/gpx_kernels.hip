@@ -245,14 +245,14 @@ void launch_leaf(const LeafArgs& a, int n_active, hipStream_t s) {
 // lane l is C[(l>>4) + 4r][l&15] (verified on gfx950, tools/probe_f64.hip).
 // ======================================================================================
 template <int BM, bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(256, (BM == 128 && EPI != EPI_CONTRACT) ? 2 : 1) void gemm_kernel(GemmArgs a) {
+__global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a) {
   constexpr int BN = BM, BK = 16, S = BM + 16;
   constexpr int WT = BM / 2;
   constexpr int MT = WT / 16;
   constexpr int NLD = BM * BK / 2 / 256;  // double2 chunks per thread per operand
   constexpr int kMainLds = 2 * 2 * BK * S;
   constexpr int kEpiLds = (EPI == EPI_CONTRACT)
-      ? 4 * 32 * 64 + 2 * BM * GPX_MAX_DIM + 2 * BM + GPX_THETA_STRIDE + 64 : 0;
+      ? 4 * 16 * WT + 2 * BM * GPX_MAX_DIM + 2 * BM + GPX_THETA_STRIDE + 64 : 0;
   __shared__ __attribute__((aligned(16))) double smem[kMainLds > kEpiLds ? kMainLds : kEpiLds];
 
   const int b = a.active[blockIdx.y];
@@ -399,8 +399,8 @@ __global__ __launch_bounds__(256, (BM == 128 && EPI != EPI_CONTRACT) ? 2 : 1) vo
     // The accumulators go through LDS in two halves so that the kernel-derivative code runs
     // as a compact loop (keeping its registers out of the MFMA main loop's budget).
     const int D = a.D;
-    double* sacc = smem;                      // [4 waves][32][64]
-    double* sxi = sacc + 4 * 32 * 64;         // [BM][D]
+    double* sacc = smem;                      // [4 waves][16][WT]
+    double* sxi = sacc + 4 * 16 * WT;         // [BM][D]
     double* sxj = sxi + BM * D;               // [BN][D]
     double* sai = sxj + BN * D;               // [BM]
     double* saj = sai + BM;                   // [BN]
@@ -422,28 +422,26 @@ __global__ __launch_bounds__(256, (BM == 128 && EPI != EPI_CONTRACT) ? 2 : 1) vo
 #pragma unroll
     for (int t = 0; t < GPX_MAX_TERMS; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
     double snoise = 0.0;
-    // wave-local image [32 rows][WT cols]; lane -> column cl, rows rg, rg + RG, ...
+    // wave-local image [16 rows][WT cols] of one MFMA row-tile per pass;
+    // lane -> column cl, rows rg, rg + RG, ...
     constexpr int RG = 64 / WT;
-    double* wacc = sacc + wave * (32 * 64);
+    double* wacc = sacc + wave * (16 * WT);
     const int cl = lane % WT, rg = lane / WT;
     const int jl = wc * WT + cl;            // this lane's column within the tile
     const int j = j0 + jl;
 #pragma unroll
-    for (int h = 0; h < MT / 2; ++h) {
-      // rows m = 2h, 2h+1 of this wave's MFMA tiles
+    for (int h = 0; h < MT; ++h) {
 #pragma unroll
-      for (int mm = 0; mm < 2; ++mm)
+      for (int nn = 0; nn < MT; ++nn)
 #pragma unroll
-        for (int nn = 0; nn < MT; ++nn)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            wacc[(mm * 16 + (lane >> 4) + 4 * r) * WT + nn * 16 + (lane & 15)] = acc[2 * h + mm][nn][r];
+        for (int r = 0; r < 4; ++r)
+          wacc[((lane >> 4) + 4 * r) * WT + nn * 16 + (lane & 15)] = acc[h][nn][r];
       __syncthreads();
       if (j < n) {
         const double aj = saj[jl];
 #pragma unroll 1
-        for (int rr = rg; rr < 32; rr += RG) {
-          const int il = wr * WT + h * 32 + rr;
+        for (int rr = rg; rr < 16; rr += RG) {
+          const int il = wr * WT + h * 16 + rr;
           const int i = i0 + il;
           if (i >= j && i < n) {
             const double w = (i == j) ? 1.0 : 2.0;

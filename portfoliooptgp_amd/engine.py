@@ -153,6 +153,25 @@ class Engine:
         outs_v = [var[b, : x.shape[0]] for b, x in zip(act, xs)]
         return outs_m, outs_v, info
 
+    def rebind(self, b: int, X, Y, spec: N.GpxKernelSpec) -> None:
+        """Load a new problem into slot b (continuous batching)."""
+        x = to_device_f64(X, self.device)
+        x = x.reshape(x.shape[0], -1)
+        y = to_device_f64(Y, self.device).reshape(-1)
+        n = x.shape[0]
+        if x.shape[1] != self.D or n > self.Nmax or y.shape[0] != n:
+            raise ValueError(f"problem does not fit slot shape (N <= {self.Nmax}, D = {self.D})")
+        self.X[b].zero_()
+        self.Y[b].zero_()
+        self.X[b, :n] = x
+        self.Y[b, :n] = y
+        torch.cuda.current_stream(self.device).synchronize()
+        self.specs[b] = spec
+        self.n[b] = n
+        rc = self.lib.gpx_batch_rebind(self.handle, int(b), int(n), ctypes.byref(spec))
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_batch_rebind failed ({rc}): {self.ctx.last_error()}")
+
     def reset_timing(self) -> None:
         self.lib.gpx_batch_reset_timing(self.handle)
 

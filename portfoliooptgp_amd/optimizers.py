@@ -14,6 +14,7 @@ to sequential fitting while the device works on all fits at once.
 """
 from __future__ import annotations
 
+import queue
 import threading
 from typing import Callable, List, Optional, Sequence
 
@@ -125,19 +126,115 @@ class Scipy:
         return results  # type: ignore[return-value]
 
 
+    def minimize_stream(self, models: Sequence, width: int, method: str = "L-BFGS-B",
+                        device: Optional[int] = None, predict_train: bool = False,
+                        engine: Optional[Engine] = None, **scipy_kwargs):
+        """Continuous batching: fit many models through ``width`` resident device slots.
+
+        Every model still runs its own unmodified scipy L-BFGS-B; at most ``width`` are
+        resident, and a slot is refilled from the queue as soon as its fit has converged, so
+        the batched evaluations stay wide until the queue drains (a lock-step batch shrinks
+        as its fits finish). With ``predict_train`` each model's predict_f at its training
+        inputs runs before its slot is released. Returns (results, predictions|None); models
+        are detached from the shared engine afterwards.
+        """
+        models = list(models)
+        if not models:
+            return [], ([] if predict_train else None)
+        width = max(1, min(int(width), len(models)))
+        D = models[0].data[0].shape[1]
+        if any(m.data[0].shape[1] != D for m in models):
+            raise ValueError("all models must have the same input dimension")
+        nmax = max(m.data[0].shape[0] for m in models)
+        if engine is None:
+            # slot shapes sized for the largest problem; slots start bound to the first models
+            seed = models[:width]
+            X0 = [np.zeros((nmax, D)) for _ in seed]
+            Y0 = [np.zeros((nmax, 1)) for _ in seed]
+            engine = Engine(X0, Y0, [compile_spec(m.kernel, D) for m in seed],
+                            device=device if device is not None else models[0].device)
+        step = _LockstepEvaluator(engine, [None] * engine.B, total=len(models))
+        free: "queue.Queue[int]" = queue.Queue()
+        for s in range(engine.B):
+            free.put(s)
+        results = [None] * len(models)
+        preds = [None] * len(models) if predict_train else None
+        errors: List[Optional[BaseException]] = [None] * len(models)
+        lib_lock = step.lib_lock
+
+        def worker(i: int):
+            m = models[i]
+            slot = free.get()
+            try:
+                with lib_lock:
+                    engine.rebind(slot, m.data[0], m.data[1], compile_spec(m.kernel, D))
+                m._attach(engine, slot)
+                step.bind(slot, m)
+                variables = m.trainable_variables
+
+                def func(x):
+                    _unpack(variables, x)
+                    return step.request(slot, variables)
+
+                res = scipy.optimize.minimize(func, _pack(variables), jac=True, method=method,
+                                              **scipy_kwargs)
+                _unpack(variables, res.x)
+                results[i] = res
+                if predict_train:
+                    step.unbind(slot)  # leave the lock-step set before the predict call
+                    theta = np.ones((engine.B, N.GPX_THETA_STRIDE))
+                    theta[slot] = m.theta_row()
+                    with lib_lock:
+                        mu, var, _ = engine.predict([slot], theta, [m.data[0]], False)
+                    preds[i] = (mu[0].reshape(-1, 1), var[0].reshape(-1, 1))
+            except BaseException as e:
+                errors[i] = e
+            finally:
+                m._engine = None
+                step.finish(slot)
+                free.put(slot)
+
+        threads = [threading.Thread(target=worker, args=(i,), daemon=True) for i in range(len(models))]
+        for t in threads:
+            t.start()
+        step.serve()
+        for t in threads:
+            t.join()
+        for e in errors:
+            if e is not None:
+                raise e
+        return results, preds
+
+
 class _LockstepEvaluator:
     """Barrier between the optimiser threads and the device: evaluates all pending points in
     one gpx_batch_lml_grad call once every running optimiser has posted one."""
 
-    def __init__(self, engine: Engine, models):
+    def __init__(self, engine: Engine, models, total: Optional[int] = None):
         self.engine = engine
-        self.models = models
+        self.models = list(models)
         self.cv = threading.Condition()
-        self.running = set(range(len(models)))
+        self.lib_lock = threading.Lock()
+        if total is None:  # fixed lock-step batch: every slot runs from the start
+            self.running = set(range(len(self.models)))
+            self.remaining = len(self.models)
+        else:              # streaming: slots join via bind() and leave via finish()
+            self.running = set()
+            self.remaining = total
         self.pending = {}
         self.results = {}
-        self.error: Optional[BaseException] = None
         self.rounds = 0
+
+    def bind(self, slot: int, model):
+        with self.cv:
+            self.models[slot] = model
+            self.running.add(slot)
+            self.cv.notify_all()
+
+    def unbind(self, slot: int):
+        with self.cv:
+            self.running.discard(slot)
+            self.cv.notify_all()
 
     def request(self, i: int, variables):
         with self.cv:
@@ -153,15 +250,16 @@ class _LockstepEvaluator:
     def finish(self, i: int):
         with self.cv:
             self.running.discard(i)
+            self.remaining -= 1
             self.cv.notify_all()
 
     def serve(self):
         eng = self.engine
         while True:
             with self.cv:
-                while self.running and len(self.pending) < len(self.running):
+                while self.remaining > 0 and (not self.running or len(self.pending) < len(self.running)):
                     self.cv.wait()
-                if not self.running:
+                if self.remaining <= 0:
                     return
                 batch = dict(self.pending)
                 self.pending.clear()
@@ -171,7 +269,8 @@ class _LockstepEvaluator:
                 theta[i] = self.models[i].theta_row()
             out = {}
             try:
-                lml, grad, info = eng.lml_grad(active, theta)
+                with self.lib_lock:
+                    lml, grad, info = eng.lml_grad(active, theta)
                 for i in active:
                     if info[i] != 0:
                         out[i] = N.NotPositiveDefiniteError(
