@@ -15,19 +15,24 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include "gpx_internal.h"
 
 using namespace gpx;
 
-constexpr int kGroups = 2;  // concurrent pipelines per evaluation (HIP streams)
+constexpr int kGroups = 4;  // max concurrent pipelines per evaluation (HIP streams)
+constexpr int kAux = 3;     // auxiliary streams for the T = L21·W11 products of depths 0..2
+constexpr int kEvents = 64;
 
 struct gpx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t workers[kGroups] = {};
+  hipStream_t aux[kAux] = {};
   hipEvent_t fork = nullptr, join[kGroups] = {};
+  hipEvent_t ev[kEvents] = {};
   std::string err;
   int profiling = 0;
 };
@@ -85,6 +90,8 @@ struct Run {
   const int* d_act;  // device pointer into the uploaded active list
   int na;            // problems in this range
   hipStream_t s;
+  bool dag = false;  // run the T products of the top recursion levels on the aux streams
+  int* next_event = nullptr;
 };
 
 // MFMA flops the GEMM launcher will issue for these args (bench / roofline bookkeeping)
@@ -128,7 +135,7 @@ GemmArgs gemm_args(const double* A, int lda, const double* B, int ldb, double* C
 }
 
 // Recursive Cholesky-and-inverse on the diagonal block [off, off+n) of every problem of r.
-void chol_inv(const Run& r, int off, int n) {
+void chol_inv(const Run& r, int off, int n, int depth = 0) {
   gpx_batch* bt = r.bt;
   const int Np = bt->Np;
   const long long st = mat_stride(bt);
@@ -142,20 +149,38 @@ void chol_inv(const Run& r, int off, int n) {
   int n1 = ((n / 2 + kLeaf - 1) / kLeaf) * kLeaf;
   if (n1 >= n) n1 = n - kLeaf;
   const int n2 = n - n1;
-  chol_inv(r, off, n1);
+  chol_inv(r, off, n1, depth + 1);
   const long long o11 = (long long)off * Np + off;
   const long long o21 = (long long)(off + n1) * Np + off;
   const long long o22 = (long long)(off + n1) * Np + off + n1;
   // L21 = A21 · W11ᵀ          (opB(k,j) = W11[j][k], nonzero for k <= j)
   gemm(r, gemm_args(bt->K + o21, Np, bt->W + o11, Np, bt->L + o21, Np, st, n2, n1, n1,
                     TRI_KMAX_J, 0, 1.0, 0.0), EPI_STORE, false, true);
+  // T = L21 · W11 → the dead A21 region of K   (opB(k,j) = W11[k][j], nonzero for k >= j).
+  // T depends only on L21 and W11, so at the top depths it runs on an auxiliary stream
+  // concurrently with the (latency-bound) recursion on A22 below.
+  const GemmArgs targs = gemm_args(bt->L + o21, Np, bt->W + o11, Np, bt->K + o21, Np, st, n2, n1,
+                                   n1, TRI_KMIN_J, 0, 1.0, 0.0);
+  gpx_ctx* ctx = bt->ctx;
+  const bool fork = r.dag && depth < kAux && r.next_event && *r.next_event + 2 <= kEvents;
+  hipEvent_t eT = nullptr;
+  if (fork) {
+    hipEvent_t eL = ctx->ev[(*r.next_event)++];
+    eT = ctx->ev[(*r.next_event)++];
+    Run ra = r;
+    ra.s = ctx->aux[depth];
+    (void)hipEventRecord(eL, r.s);
+    (void)hipStreamWaitEvent(ra.s, eL, 0);
+    gemm(ra, targs, EPI_STORE, false, false);
+    (void)hipEventRecord(eT, ra.s);
+  } else {
+    gemm(r, targs, EPI_STORE, false, false);
+  }
   // A22 -= L21 · L21ᵀ         (lower tiles only)
   gemm(r, gemm_args(bt->L + o21, Np, bt->L + o21, Np, bt->K + o22, Np, st, n2, n2, n1, 0, 1,
                     -1.0, 1.0), EPI_STORE, false, true);
-  chol_inv(r, off + n1, n2);
-  // T = L21 · W11 → the dead A21 region of K   (opB(k,j) = W11[k][j], nonzero for k >= j)
-  gemm(r, gemm_args(bt->L + o21, Np, bt->W + o11, Np, bt->K + o21, Np, st, n2, n1, n1,
-                    TRI_KMIN_J, 0, 1.0, 0.0), EPI_STORE, false, false);
+  chol_inv(r, off + n1, n2, depth + 1);
+  if (fork) (void)hipStreamWaitEvent(r.s, eT, 0);
   // W21 = −W22 · T             (opA(i,k) = W22[i][k], nonzero for k <= i)
   gemm(r, gemm_args(bt->W + o22, Np, bt->K + o21, Np, bt->W + o21, Np, st, n2, n1, n2,
                     TRI_KMAX_I, 0, -1.0, 0.0), EPI_STORE, false, false);
@@ -277,6 +302,10 @@ int gpx_create(int device, gpx_ctx** out) {
   for (int g = 0; g < kGroups && ok; ++g)
     ok = hipStreamCreateWithFlags(&c->workers[g], hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&c->join[g], hipEventDisableTiming) == hipSuccess;
+  for (int g = 0; g < kAux && ok; ++g)
+    ok = hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking) == hipSuccess;
+  for (int e = 0; e < kEvents && ok; ++e)
+    ok = hipEventCreateWithFlags(&c->ev[e], hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     delete c;
     return GPX_HIP_ERROR;
@@ -292,6 +321,10 @@ int gpx_destroy(gpx_ctx* ctx) {
     if (ctx->workers[g]) (void)hipStreamDestroy(ctx->workers[g]);
     if (ctx->join[g]) (void)hipEventDestroy(ctx->join[g]);
   }
+  for (int g = 0; g < kAux; ++g)
+    if (ctx->aux[g]) (void)hipStreamDestroy(ctx->aux[g]);
+  for (int e = 0; e < kEvents; ++e)
+    if (ctx->ev[e]) (void)hipEventDestroy(ctx->ev[e]);
   if (ctx->fork) (void)hipEventDestroy(ctx->fork);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -421,12 +454,17 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   // Split the active problems into up to kGroups ranges, each running the whole pipeline on
   // its own stream: one group's latency-bound phases (64x64 leaves, small recursion levels)
   // overlap another group's large MFMA GEMMs.
-  const int ng = n_active >= 4 ? kGroups : 1;
+  // Default: one pipeline whose recursion forks the top-level T products onto aux streams
+  // (concurrency inside the DAG). GPX_GROUPS=g instead splits the problems into g pipelines.
+  int ng = 1;
+  if (const char* e = getenv("GPX_GROUPS")) ng = atoi(e);
+  ng = std::max(1, std::min(std::min(ng, kGroups), n_active));
+  int next_event = 0;
   Run runs[kGroups];
   int start = 0;
   for (int g = 0; g < ng; ++g) {
     const int cnt = n_active / ng + (g < n_active % ng ? 1 : 0);
-    runs[g] = Run{bt, bt->d_active + start, cnt, ng == 1 ? s : ctx->workers[g]};
+    runs[g] = Run{bt, bt->d_active + start, cnt, ng == 1 ? s : ctx->workers[g], ng == 1, &next_event};
     start += cnt;
   }
   if (ng > 1) {
