@@ -94,11 +94,11 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 64)),
+    ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 128)),
                     help="independent series fitted per GPU per step")
-    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 32)),
+    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 64)),
                     help="resident device slots (continuous-batching width)")
     ap.add_argument("--n", type=int, default=N_POINTS)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -1,0 +1,136 @@
+"""Multi-GPU: independent per-asset fits sharded over ranks, results gathered once.
+
+The reference fits its assets in a sequential Python loop (GPR/main.py:23 over tickers,
+Multi-Input_GPR/main.py:535 over assets) and hands per-asset predicted means / variances to
+the portfolio step (Multi-Input_GPR/main.py:555-574 -> Portfolio(assets, predicted_values,
+predicted_variances), Multi-Input_GPR/Portfolio/portfolio.py:92-165). Here:
+
+* one process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on MI355X,
+  "gloo" for CPU tests);
+* fits are assigned to ranks longest-processing-time first on cost N³ (no communication
+  while fitting);
+* every rank fits its shard through the continuous-batching driver and predicts its
+  horizon;
+* ONE all_gather of a packed fp64 tensor (θ*, loss*, nfev, mean[H], var[H] per asset) is the
+  only data-path collective; rank 0 (or every rank) rebuilds the Portfolio input lists.
+"""
+from __future__ import annotations
+
+import heapq
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_lpt(costs: Sequence[float], world: int) -> List[List[int]]:
+    """Longest-processing-time-first assignment of items (by cost) to `world` bins."""
+    heap = [(0.0, r) for r in range(world)]
+    heapq.heapify(heap)
+    out: List[List[int]] = [[] for _ in range(world)]
+    for i in sorted(range(len(costs)), key=lambda k: (-costs[k], k)):
+        load, r = heapq.heappop(heap)
+        out[r].append(i)
+        heapq.heappush(heap, (load + float(costs[i]), r))
+    for r in out:
+        r.sort()
+    return out
+
+
+def fit_cost(n: int) -> float:
+    """Relative cost of one exact-GP fit (evaluations are O(N³))."""
+    return float(n) ** 3
+
+
+def pack_results(indices: Sequence[int], results: Sequence[dict], horizon: int, n_theta: int) -> torch.Tensor:
+    """[k, 4 + n_theta + 2H] fp64 rows: index, loss, nfev, ok, θ..., mean[H], var[H]."""
+    width = 4 + n_theta + 2 * horizon
+    t = torch.full((len(indices), width), float("nan"), dtype=torch.float64)
+    for row, (i, r) in enumerate(zip(indices, results)):
+        t[row, 0] = i
+        t[row, 1] = r["loss"]
+        t[row, 2] = r["nfev"]
+        t[row, 3] = 1.0
+        th = np.asarray(r["theta"], dtype=np.float64)[:n_theta]
+        t[row, 4:4 + len(th)] = torch.as_tensor(th)
+        t[row, 4 + n_theta:4 + n_theta + horizon] = torch.as_tensor(np.asarray(r["mean"]).reshape(-1)[:horizon])
+        t[row, 4 + n_theta + horizon:] = torch.as_tensor(np.asarray(r["var"]).reshape(-1)[:horizon])
+    return t
+
+
+def unpack_results(table: torch.Tensor, horizon: int, n_theta: int) -> Dict[int, dict]:
+    out = {}
+    for row in table.cpu().numpy():
+        if not np.isfinite(row[0]) or row[3] != 1.0:
+            continue
+        out[int(row[0])] = dict(
+            loss=float(row[1]), nfev=int(row[2]), theta=row[4:4 + n_theta].copy(),
+            mean=row[4 + n_theta:4 + n_theta + horizon].reshape(-1, 1).copy(),
+            var=row[4 + n_theta + horizon:].reshape(-1, 1).copy())
+    return out
+
+
+def all_gather_results(local: torch.Tensor, n_items: int, group=None) -> torch.Tensor:
+    """One all_gather of the packed per-asset rows (padded to the largest shard)."""
+    world = dist.get_world_size(group)
+    backend = dist.get_backend(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    k = torch.tensor([local.shape[0]], device=dev)
+    ks = [torch.zeros_like(k) for _ in range(world)]
+    dist.all_gather(ks, k, group=group)
+    kmax = int(max(int(x.item()) for x in ks))
+    pad = torch.full((kmax, local.shape[1]), float("nan"), dtype=torch.float64, device=dev)
+    pad[: local.shape[0]] = local.to(dev)
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return torch.cat(bufs).cpu()
+
+
+def portfolio_inputs(gathered: Dict[int, dict], order: Sequence[int]) -> Tuple[list, list]:
+    """Per-asset lists of per-day [1]-arrays, the shape Portfolio(...) indexes as
+    returns[i][day][0] (Multi-Input_GPR/Portfolio/portfolio.py:111-124)."""
+    means = [[np.asarray(gathered[i]["mean"][d]) for d in range(len(gathered[i]["mean"]))] for i in order]
+    varis = [[np.asarray(gathered[i]["var"][d]) for d in range(len(gathered[i]["var"]))] for i in order]
+    return means, varis
+
+
+def fit_assets(series: Sequence[Tuple[np.ndarray, np.ndarray]], horizons: Sequence[np.ndarray],
+               fit_fn: Optional[Callable] = None, n_theta: int = 2, group=None) -> Dict[int, dict]:
+    """Shard the assets over the ranks of `group`, fit the local shard with `fit_fn`
+    (default: GPU exact GPR with a SquaredExponential kernel and σn² = 1e-5 fixed, the
+    GPR/model_trainer.py:15-19 protocol, continuous-batched), predict each asset at its
+    horizon inputs and all_gather the results. Returns {asset index: result} on every rank."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    shards = shard_lpt([fit_cost(len(x)) for x, _ in series], world)
+    mine = shards[rank]
+    fit_fn = fit_fn or gpu_fit_shard
+    local = fit_fn([series[i] for i in mine], [horizons[i] for i in mine]) if mine else []
+    H = max(len(h) for h in horizons)
+    table = pack_results(mine, local, H, n_theta)
+    if world > 1:
+        table = all_gather_results(table, len(series), group)
+    return unpack_results(table, H, n_theta)
+
+
+def gpu_fit_shard(series, horizons, width: int = 32, maxiter: int = 100):
+    """Default per-rank fitter: exact GPR (SE kernel, σn² = 1e-5 fixed), L-BFGS-B through the
+    continuous-batching driver, then predict_f at each asset's horizon inputs."""
+    from . import kernels, models, optimizers
+    from .utilities import set_trainable
+
+    ms = []
+    for x, y in series:
+        m = models.GPR(data=(x, y), kernel=kernels.SquaredExponential())
+        m.likelihood.variance.assign(1e-5)
+        set_trainable(m.likelihood.variance, False)
+        ms.append(m)
+    res, _ = optimizers.Scipy().minimize_stream(ms, width=width, options=dict(maxiter=maxiter))
+    out = []
+    for m, r, h in zip(ms, res, horizons):
+        mean, var = m.predict_f(h)
+        out.append(dict(loss=float(r.fun), nfev=int(r.nfev),
+                        theta=[p.value for p in m.kernel.parameters],
+                        mean=np.asarray(mean).reshape(-1), var=np.asarray(var).reshape(-1)))
+    return out
