@@ -48,6 +48,7 @@ struct GemmArgs {
   int tri;            // TRI_* flags restricting the k range per tile
   int lower_only;     // only tiles with ti >= tj
   int order;          // ORDER_* tile enumeration (rectangular launches)
+  int n_active;       // set by the launcher (XCD-aware problem placement)
   double alpha, beta;
   // EPI_CONTRACT
   const double* vec; long long sVec;        // α vectors [B][Np]

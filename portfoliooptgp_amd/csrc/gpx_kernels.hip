@@ -255,15 +255,23 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
       ? 4 * 16 * WT + 2 * BM * GPX_MAX_DIM + 2 * BM + GPX_THETA_STRIDE + 64 : 0;
   __shared__ __attribute__((aligned(16))) double smem[kMainLds > kEpiLds ? kMainLds : kEpiLds];
 
-  const int b = a.active[blockIdx.y];
+  // XCD-aware problem placement: workgroups are dealt round-robin over the 8 XCDs (block x
+  // lands on XCD x % 8 — observed placement, used for speed only), so problem p is given
+  // blocks x ≡ p (mod 8): all tiles of a problem share one XCD's L2 instead of every XCD
+  // pulling every operand panel. Blocks past the last problem of an XCD exit at once.
+  const int nti = a.M / BM, ntj = a.N / BN;
+  const int ntl = a.lower_only ? nti * (nti + 1) / 2 : nti * ntj;
+  const int slot = blockIdx.x >> 3;
+  const int pa = (blockIdx.x & 7) + 8 * (slot / ntl);
+  if (pa >= a.n_active) return;
+  const int tile = slot % ntl;
+  const int b = a.active[pa];
   int ti, tj;
   if (a.lower_only) {
-    lower_tile(blockIdx.x, ti, tj);
+    lower_tile(tile, ti, tj);
   } else {
-    // Workgroups are dealt round-robin over the 8 XCDs: make the index that sets a tile's
-    // K range the SLOW one (so every XCD gets the same mix) and run the longest tiles first.
-    const int nti = a.M / BM, ntj = a.N / BN;
-    const int x = blockIdx.x;
+    // make the index that sets a tile's K range the SLOW one and run the longest tiles first
+    const int x = tile;
     switch (a.order) {
       case ORDER_COL_DESC: tj = ntj - 1 - x / nti; ti = x % nti; break;
       case ORDER_COL_ASC:  tj = x / nti; ti = x % nti; break;
@@ -473,7 +481,7 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
     }
     __syncthreads();
     if (tid < GPX_THETA_STRIDE) {
-      double* out = a.partial + (long long)b * a.sPartial + (long long)blockIdx.x * GPX_THETA_STRIDE;
+      double* out = a.partial + (long long)b * a.sPartial + (long long)tile * GPX_THETA_STRIDE;
       // map slot tid -> θ index
       double s = 0.0;
       int slot = -1;
@@ -522,10 +530,12 @@ int gemm_tile(const GemmArgs& a, int n_active) {
 }
 
 template <int BM, int EPI>
-static void launch_gemm_t(const GemmArgs& a, bool ta, bool tb, int n_active, hipStream_t s) {
+static void launch_gemm_t(const GemmArgs& a0, bool ta, bool tb, int n_active, hipStream_t s) {
+  GemmArgs a = a0;
+  a.n_active = n_active;
   const int ti = a.M / BM, tj = a.N / BM;
   const int ntiles = a.lower_only ? ti * (ti + 1) / 2 : ti * tj;
-  dim3 grid(ntiles, n_active);
+  dim3 grid(8 * ((n_active + 7) / 8) * ntiles);
   if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<BM, false, false, EPI>), grid, dim3(256), 0, s, a);
   else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<BM, false, true, EPI>), grid, dim3(256), 0, s, a);
   else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<BM, true, false, EPI>), grid, dim3(256), 0, s, a);
