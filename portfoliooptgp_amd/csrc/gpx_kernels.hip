@@ -255,16 +255,25 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
       ? 4 * 16 * WT + 2 * BM * GPX_MAX_DIM + 2 * BM + GPX_THETA_STRIDE + 64 : 0;
   __shared__ __attribute__((aligned(16))) double smem[kMainLds > kEpiLds ? kMainLds : kEpiLds];
 
-  // XCD-aware problem placement: workgroups are dealt round-robin over the 8 XCDs (block x
-  // lands on XCD x % 8 — observed placement, used for speed only), so problem p is given
-  // blocks x ≡ p (mod 8): all tiles of a problem share one XCD's L2 instead of every XCD
-  // pulling every operand panel. Blocks past the last problem of an XCD exit at once.
+  // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs (block x lands on
+  // XCD x % 8 — observed placement, used for speed only). The first 8·⌊na/8⌋ problems are
+  // given to the XCDs whole (⌊na/8⌋ each), so every problem's operand panels stream through ONE
+  // L2; the remaining na mod 8 problems have their tiles interleaved over all XCDs, which
+  // balances the tiles' unequal K ranges (a single problem uses the whole chip).
   const int nti = a.M / BM, ntj = a.N / BN;
   const int ntl = a.lower_only ? nti * (nti + 1) / 2 : nti * ntj;
-  const int slot = blockIdx.x >> 3;
-  const int pa = (blockIdx.x & 7) + 8 * (slot / ntl);
-  if (pa >= a.n_active) return;
-  const int tile = slot % ntl;
+  const int q = a.n_active >> 3;
+  const int xcd = blockIdx.x & 7, s = blockIdx.x >> 3;
+  int pa, tile;
+  if (s < q * ntl) {
+    pa = xcd * q + s / ntl;
+    tile = s % ntl;
+  } else {
+    const int g = (s - q * ntl) * 8 + xcd;
+    pa = 8 * q + g / ntl;
+    tile = g % ntl;
+    if (pa >= a.n_active) return;
+  }
   const int b = a.active[pa];
   int ti, tj;
   if (a.lower_only) {
@@ -535,7 +544,8 @@ static void launch_gemm_t(const GemmArgs& a0, bool ta, bool tb, int n_active, hi
   a.n_active = n_active;
   const int ti = a.M / BM, tj = a.N / BM;
   const int ntiles = a.lower_only ? ti * (ti + 1) / 2 : ti * tj;
-  dim3 grid(8 * ((n_active + 7) / 8) * ntiles);
+  const int q = n_active / 8, r = n_active % 8;
+  dim3 grid(8 * (q * ntiles + (r * ntiles + 7) / 8));
   if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<BM, false, false, EPI>), grid, dim3(256), 0, s, a);
   else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<BM, false, true, EPI>), grid, dim3(256), 0, s, a);
   else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<BM, true, false, EPI>), grid, dim3(256), 0, s, a);

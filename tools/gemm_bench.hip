@@ -29,7 +29,8 @@ int main(int argc, char** argv) {
   struct Case { const char* name; bool ta, tb; int tri, lower; int kdiv = 1; };
   Case cases[] = {{"NT full K/2", false, true, 0, 0, 2}, {"NN full K/2", false, false, 0, 0, 2},{"NN full", false, false, 0, 0}, {"NT full", false, true, 0, 0}, {"TN full", true, false, 0, 0},
                   {"NT syrk(lower)", false, true, 0, 1}, {"NT trmm kmax_j", false, true, TRI_KMAX_J, 0},
-                  {"NN trmm kmin_j", false, false, TRI_KMIN_J, 0}, {"NN trmm kmax_i", false, false, TRI_KMAX_I, 0}};
+                  {"NN trmm kmin_j", false, false, TRI_KMIN_J, 0}, {"NN trmm kmax_i", false, false, TRI_KMAX_I, 0},
+                  {"TN lauum(lower,kmin_i)", true, false, TRI_KMIN_I, 1}};
   for (auto& c : cases) {
     GemmArgs g{};
     g.active = act; g.A = A; g.sA = sz; g.lda = n; g.Bm = Bm; g.sB = sz; g.ldb = n; g.C = C; g.sC = sz; g.ldc = n;
@@ -49,14 +50,36 @@ int main(int argc, char** argv) {
       if (kmax > kmin) f += 2.0 * bm * bm * (kmax - kmin);
     }
     f *= B;
-    launch_gemm(g, EPI_STORE, c.ta, c.tb, B, 0);
-    CK(hipDeviceSynchronize());
-    const int reps = 5;
-    CK(hipEventRecord(e0));
-    for (int r = 0; r < reps; ++r) launch_gemm(g, EPI_STORE, c.ta, c.tb, B, 0);
-    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-    float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ms /= reps;
-    printf("%-18s n=%d B=%d tile=%d: %8.3f ms  %6.2f TF/s (issued)\n", c.name, n, B, bm, ms, f / ms / 1e9);
+    for (int epi = 0; epi < (c.tri == TRI_KMIN_I ? 2 : 1); ++epi) {
+      GemmArgs gg = g;
+      if (epi == 1) {  // the fused gradient contraction on the same shape (SE kernel spec)
+        static double *alpha = nullptr, *X = nullptr, *theta = nullptr, *partial = nullptr;
+        static DevSpec* spec = nullptr; static int* nv = nullptr;
+        if (!alpha) {
+          CK(hipMalloc(&alpha, (size_t)B * n * 8)); fill<<<256, 256>>>(alpha, (size_t)B * n, 7);
+          CK(hipMalloc(&X, (size_t)B * n * 8)); fill<<<256, 256>>>(X, (size_t)B * n, 8);
+          CK(hipMalloc(&theta, B * 16 * 8)); std::vector<double> th(B * 16, 1.0);
+          CK(hipMemcpy(theta, th.data(), B * 16 * 8, hipMemcpyHostToDevice));
+          CK(hipMalloc(&partial, (size_t)B * 2080 * 16 * 8));
+          DevSpec sp{}; sp.n_terms = 1; sp.combine = 0; sp.n_params = 2; sp.terms[0].kind = 1;
+          sp.terms[0].dim_start = 0; sp.terms[0].dim_count = 1; sp.terms[0].param_offset = 0;
+          std::vector<DevSpec> sps(B, sp); CK(hipMalloc(&spec, B * sizeof(DevSpec)));
+          CK(hipMemcpy(spec, sps.data(), B * sizeof(DevSpec), hipMemcpyHostToDevice));
+          std::vector<int> nn(B, n); CK(hipMalloc(&nv, B * 4)); CK(hipMemcpy(nv, nn.data(), B * 4, hipMemcpyHostToDevice));
+        }
+        gg.vec = alpha; gg.sVec = n; gg.X = X; gg.sX = n; gg.D = 1; gg.specs = spec; gg.theta = theta;
+        gg.nvalid = nv; gg.partial = partial; gg.sPartial = 2080 * 16;
+      }
+      const int ep = epi ? EPI_CONTRACT : EPI_STORE;
+      launch_gemm(gg, ep, c.ta, c.tb, B, 0);
+      CK(hipDeviceSynchronize());
+      const int reps = 5;
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r) launch_gemm(gg, ep, c.ta, c.tb, B, 0);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ms /= reps;
+      printf("%-22s%s n=%d B=%d tile=%d: %8.3f ms  %6.2f TF/s (issued)\n", c.name, epi ? " +contract" : "", n, B, bm, ms, f / ms / 1e9);
+    }
   }
   return 0;
 }
