@@ -91,6 +91,25 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
     }
 
 
+def contract_traffic(n, flops_per_launch):
+    """HBM bytes per contraction launch from the committed PMC summary of this bench command
+    (profiles/<round>_contract_traffic.json, written by tools/pmc_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes): bytes per problem x the launch's average
+    problem count (alg flops per launch / alg flops per problem). None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "*_contract_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    npad = (n + 63) // 64 * 64
+    if d.get("Np") != npad:
+        return None, None
+    per_problem = sum(2.0 * (i + 1) * (npad - i) for i in range(npad))
+    problems = flops_per_launch / per_problem
+    return d["hbm_bytes_per_problem"] * problems, os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,6 +205,7 @@ def main():
     contract_ms = tm.contract_ms_total / max(tm.contract_launches, 1.0)
     contract_flops = tm.contract_alg_flops / max(tm.contract_launches, 1.0)
     achieved = contract_flops / (contract_ms * 1e-3) / 1e12
+    traffic, traffic_src = contract_traffic(n, contract_flops)
     eval_alg = (n ** 3 + 2 * 3 * n ** 2) * tm.evals  # SURVEY §8d F_eval(N), P=2
     out = {
         "metric": "GP fits/sec (N=4096, 1-D RBF)",
@@ -214,7 +234,9 @@ def main():
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes/launch",
+            "traffic_source": traffic_src,
             "avg_launch_ms": contract_ms,
             "alg_flops_per_launch": contract_flops,
         },

@@ -11,6 +11,7 @@
  *                          (also Multi-Input_GPR/models/model_trainer.py:20-21, 36-37)
  *   gpx_batch_predict   <- model.predict_f(X, full_cov=False)        GPR/model_trainer.py:20,
  *                          GPR/predictor.py:6;  model.predict_y(X)   GPR/predictor.py:7
+ *   gpx_batch_predict_full_cov <- model.predict_f(X, full_cov=True)  test_scripts/GPR_Entropy.py:373
  *   gpx_kernel_spec     <- the kernel objects of GPR/main.py:105-114 and the composite
  *                          Exponential*Exponential of Multi-Input_GPR/main.py:118-135
  *
@@ -127,6 +128,16 @@ int gpx_batch_lml_grad(gpx_batch* batch, int n_active, const int32_t* active, co
 int gpx_batch_predict(gpx_batch* batch, int n_active, const int32_t* active, const double* theta,
                       const double* Xnew, int M, int add_noise, double* mean, double* var,
                       int32_t* info, void* stream);
+
+/*
+ * Posterior mean and FULL covariance at Xnew: GPflow GPR.predict_f(Xnew, full_cov=True)
+ * (GPflow returns the covariance as [1, M, M]; predict_y has no full_cov form in GPflow).
+ *   Xnew : device fp64 [B, M, D];  mean : device fp64 [B, M];  cov : device fp64 [B, M, M].
+ * cov[b] = k(X*,X*) − Kxsᵀ (K+σn²I)⁻¹ Kxs, formed as k(X*,X*) − AᵀA with A = L⁻¹·Kxs (MFMA).
+ */
+int gpx_batch_predict_full_cov(gpx_batch* batch, int n_active, const int32_t* active,
+                               const double* theta, const double* Xnew, int M, double* mean,
+                               double* cov, int32_t* info, void* stream);
 
 /* Timing hooks for bench.py: total device time (ms) of the last call's kernels, measured with
  * HIP events on the stream they ran on, split by phase. */

@@ -57,6 +57,8 @@ struct gpx_batch {
   // predict workspace
   double* kxs = nullptr; size_t kxs_cap = 0;
   double* pvp = nullptr; size_t pvp_cap = 0;
+  double* abuf = nullptr; size_t abuf_cap = 0;   // A = W·Kxs (full_cov, Mp > Np)
+  double* covw = nullptr; size_t covw_cap = 0;   // padded [B][Mp][Mp] covariance
   // factor cache: theta row of the last factorisation per problem
   std::vector<double> fac_theta;
   std::vector<char> fac_valid;
@@ -215,14 +217,14 @@ void alpha_solve(const Run& r) {
 }
 
 // fused K⁻¹ = WᵀW formation + gradient contraction over lower tiles, then the reduction
-void contract(const Run& r) {
+void contract(const Run& r, bool single_term) {
   gpx_batch* bt = r.bt;
   GemmArgs g = gemm_args(bt->W, bt->Np, bt->W, bt->Np, nullptr, 0, mat_stride(bt), bt->Np, bt->Np,
                          bt->Np, TRI_KMIN_I, 1, 1.0, 0.0);
   g.vec = bt->alpha; g.sVec = bt->Np; g.X = bt->X; g.sX = (long long)bt->Nmax * bt->D; g.D = bt->D;
   g.specs = bt->d_specs; g.theta = bt->d_theta; g.nvalid = bt->d_n;
   g.partial = bt->partial; g.sPartial = bt->partial_stride;
-  gemm(r, g, EPI_CONTRACT, true, false);
+  gemm(r, g, single_term ? EPI_CONTRACT1 : EPI_CONTRACT, true, false);
 }
 
 void reduce(const Run& r) {
@@ -245,17 +247,17 @@ struct PhaseTimer {
   void mark() {
     if (!on) return;
     hipEvent_t e;
-    hipEventCreate(&e);
-    hipEventRecord(e, s);
+    (void)hipEventCreate(&e);
+    (void)hipEventRecord(e, s);
     ev.push_back(e);
   }
   double ms(int i, int j) {
     float t = 0.f;
-    hipEventElapsedTime(&t, ev[i], ev[j]);
+    (void)hipEventElapsedTime(&t, ev[i], ev[j]);
     return t;
   }
   ~PhaseTimer() {
-    for (auto e : ev) hipEventDestroy(e);
+    for (auto e : ev) (void)hipEventDestroy(e);
   }
 };
 
@@ -407,12 +409,12 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
 
 int gpx_batch_destroy(gpx_batch* bt) {
   if (!bt) return GPX_BAD_ARG;
-  hipSetDevice(bt->ctx->device);
+  (void)hipSetDevice(bt->ctx->device);
   for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
                   (void*)bt->ldiag, (void*)bt->partial, (void*)bt->results, (void*)bt->d_n,
                   (void*)bt->d_specs, (void*)bt->d_theta, (void*)bt->d_active, (void*)bt->d_info,
-                  (void*)bt->kxs, (void*)bt->pvp})
-    if (p) hipFree(p);
+                  (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw})
+    if (p) (void)hipFree(p);
   delete bt;
   return GPX_OK;
 }
@@ -493,9 +495,11 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   // The contraction fills the chip by itself (Np²/2/128² tiles per problem): one launch over
   // every active problem, alone on the stream.
   const Run all{bt, bt->d_active, n_active, s};
+  bool single_term = true;
+  for (int i = 0; i < n_active; ++i) single_term = single_term && bt->specs[active[i]].n_terms == 1;
   PhaseTimer ct(ctx->profiling != 0, s);
   ct.mark();
-  contract(all);
+  contract(all, single_term);
   ct.mark();
   reduce(all);
   ct.mark();
@@ -546,12 +550,24 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   return status;
 }
 
-int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
-                      const double* Xnew, int M, int add_noise, double* mean, double* var,
-                      int32_t* info, void* stream) {
+// grow-only device workspace
+static int ensure(gpx_ctx* ctx, double*& p, size_t& cap, size_t need) {
+  if (cap >= need) return GPX_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr; cap = 0;
+  HIPX(ctx, hipMalloc(&p, need * sizeof(double)));
+  cap = need;
+  return GPX_OK;
+}
+
+// Shared body of gpx_batch_predict (var != nullptr) and gpx_batch_predict_full_cov
+// (cov != nullptr).
+static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                        const double* Xnew, int M, int add_noise, double* mean, double* var,
+                        double* cov, int32_t* info, void* stream) {
   if (!bt) return GPX_BAD_ARG;
   gpx_ctx* ctx = bt->ctx;
-  if (!Xnew || M <= 0 || !mean || !var || !info) return fail(ctx, GPX_BAD_ARG, "bad predict args");
+  if (!Xnew || M <= 0 || !mean || !(var || cov) || !info) return fail(ctx, GPX_BAD_ARG, "bad predict args");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   int rc = upload_common(bt, n_active, active, theta, s);
@@ -585,14 +601,9 @@ int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const 
   double* kxs;
   if ((size_t)Mp <= (size_t)Np) {
     kxs = bt->L;  // L is dead once W is formed
-    for (int b : refac) (void)b;
   } else {
-    if (bt->kxs_cap < need) {
-      if (bt->kxs) hipFree(bt->kxs);
-      bt->kxs = nullptr; bt->kxs_cap = 0;
-      HIPX(ctx, hipMalloc(&bt->kxs, need * sizeof(double)));
-      bt->kxs_cap = need;
-    }
+    const int e = ensure(ctx, bt->kxs, bt->kxs_cap, need);
+    if (e != GPX_OK) return e;
     kxs = bt->kxs;
   }
   const long long skx = (long long)Np * Mp;
@@ -607,17 +618,48 @@ int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const 
   t.active = bt->d_active; t.Wm = kxs; t.sW = skx; t.ld = Mp; t.x = bt->alpha; t.sx = Np;
   t.nvalid = nullptr; t.y = mean; t.sy = M; t.rows = Np; t.cols = M; t.lower = 0;
   launch_trmv_t(t, n_active, s);
+  if (cov) {
+    // A = W · Kxs stored; cov = K(X*,X*) − AᵀA (padded rows/cols of A are exactly zero)
+    double* abuf;
+    if ((size_t)Mp <= (size_t)Np) {
+      abuf = bt->K;  // K is dead once W is formed
+    } else {
+      const int e = ensure(ctx, bt->abuf, bt->abuf_cap, need);
+      if (e != GPX_OK) return e;
+      abuf = bt->abuf;
+    }
+    const long long scv = (long long)Mp * Mp;
+    {
+      const int e = ensure(ctx, bt->covw, bt->covw_cap, (size_t)bt->B * scv);
+      if (e != GPX_OK) return e;
+    }
+    BuildArgs kb = ba;
+    kb.X = Xnew; kb.sX = (long long)M * bt->D; kb.rows_valid = M; kb.out = bt->covw; kb.sOut = scv;
+    kb.ldo = Mp; kb.rows = Mp; kb.cols = Mp;
+    launch_build(kb, n_active, s);
+    const Run rr{bt, bt->d_active, n_active, s};
+    GemmArgs ga = gemm_args(bt->W, Np, kxs, Mp, abuf, Mp, 0, Np, Mp, Np, TRI_KMAX_I, 0, 1.0, 0.0);
+    ga.sA = mat_stride(bt); ga.sB = skx; ga.sC = skx;
+    gemm(rr, ga, EPI_STORE, false, false);
+    GemmArgs gc = gemm_args(abuf, Mp, abuf, Mp, bt->covw, Mp, 0, Mp, Mp, Np, 0, 0, -1.0, 1.0);
+    gc.sA = skx; gc.sB = skx; gc.sC = scv;
+    gemm(rr, gc, EPI_STORE, true, false);
+    for (int i = 0; i < n_active; ++i) {
+      const int b = active[i];
+      HIPX(ctx, hipMemcpy2DAsync(cov + (size_t)b * M * M, sizeof(double) * M,
+                                 bt->covw + (size_t)b * scv, sizeof(double) * Mp,
+                                 sizeof(double) * M, M, hipMemcpyDeviceToDevice, s));
+    }
+  } else {
   // A = W · Kxs with fused column sum of squares
   GemmArgs g = gemm_args(bt->W, Np, kxs, Mp, nullptr, Mp, 0, Np, Mp, Np, TRI_KMAX_I, 0, 1.0, 0.0);
   g.sA = mat_stride(bt); g.sB = skx; g.sC = 0;
   const int bm = gemm_tile(g, n_active);
   const int nrt = Np / bm;
   const size_t pneed = (size_t)bt->B * nrt * Mp;
-  if (bt->pvp_cap < pneed) {
-    if (bt->pvp) hipFree(bt->pvp);
-    bt->pvp = nullptr; bt->pvp_cap = 0;
-    HIPX(ctx, hipMalloc(&bt->pvp, pneed * sizeof(double)));
-    bt->pvp_cap = pneed;
+  {
+    const int e = ensure(ctx, bt->pvp, bt->pvp_cap, pneed);
+    if (e != GPX_OK) return e;
   }
   g.partial = bt->pvp; g.sPartial = (long long)nrt * Mp;
   gemm(Run{bt, bt->d_active, n_active, s}, g, EPI_COLSUMSQ, false, false);
@@ -627,6 +669,7 @@ int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const 
   pv.specs = bt->d_specs; pv.theta = bt->d_theta; pv.M = M; pv.add_noise = add_noise;
   pv.var = var; pv.sVar = M;
   launch_predvar(pv, n_active, s);
+  }
   pt.mark();
   HIPX(ctx, hipGetLastError());
   HIPX(ctx, hipMemcpyAsync(bt->h_info.data(), bt->d_info, sizeof(int) * bt->B, hipMemcpyDeviceToHost, s));
@@ -656,6 +699,21 @@ int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const 
   }
   if (status == GPX_NOT_PD) ctx->err = "K + noise*I is not positive definite for some problem";
   return status;
+}
+
+int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                      const double* Xnew, int M, int add_noise, double* mean, double* var,
+                      int32_t* info, void* stream) {
+  if (!var) return bt ? fail(bt->ctx, GPX_BAD_ARG, "bad predict args") : GPX_BAD_ARG;
+  return predict_impl(bt, n_active, active, theta, Xnew, M, add_noise, mean, var, nullptr, info,
+                      stream);
+}
+
+int gpx_batch_predict_full_cov(gpx_batch* bt, int n_active, const int32_t* active,
+                               const double* theta, const double* Xnew, int M, double* mean,
+                               double* cov, int32_t* info, void* stream) {
+  if (!cov) return bt ? fail(bt->ctx, GPX_BAD_ARG, "bad predict args") : GPX_BAD_ARG;
+  return predict_impl(bt, n_active, active, theta, Xnew, M, 0, mean, nullptr, cov, info, stream);
 }
 
 int gpx_batch_reset_timing(gpx_batch* bt) {

@@ -23,6 +23,7 @@ struct BuildArgs {
   double* out; long long sOut; int ldo;
   int rows, cols;          // padded, multiples of 64
   int symmetric;           // 1: lower tiles of K(X,X)+σn²I with identity padding
+  int rows_valid;          // >0: valid rows for every problem (K(X*,X*)), else nvalid[b]
 };
 
 // ---- leaf: 64x64 Cholesky + triangular inverse in LDS --------------------------------
@@ -35,7 +36,9 @@ struct LeafArgs {
 
 // ---- batched fp64 MFMA GEMM -----------------------------------------------------------
 enum : int { TRI_KMAX_I = 1, TRI_KMAX_J = 2, TRI_KMIN_J = 4, TRI_KMIN_I = 8 };
-enum : int { EPI_STORE = 0, EPI_CONTRACT = 1, EPI_COLSUMSQ = 2 };
+// EPI_CONTRACT1: EPI_CONTRACT specialised for single-term kernels (every active spec has
+// n_terms == 1): a quarter of the derivative registers, no spills in the epilogue.
+enum : int { EPI_STORE = 0, EPI_CONTRACT = 1, EPI_COLSUMSQ = 2, EPI_CONTRACT1 = 3 };
 // tile enumeration for rectangular launches (see gemm_kernel)
 enum : int { ORDER_ROW_ASC = 0, ORDER_COL_DESC = 1, ORDER_ROW_DESC = 2, ORDER_COL_ASC = 3 };
 

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void build_kernel(BuildArgs a) {
   __shared__ double sxj[64 * GPX_MAX_DIM];
   __shared__ double sth[GPX_THETA_STRIDE];
   const int D = a.D, tid = threadIdx.x;
-  const int n = a.nvalid[b];
+  const int n = a.rows_valid > 0 ? a.rows_valid : a.nvalid[b];
   const int ncol = a.symmetric ? n : a.m2;
   const double* X = a.X + (long long)b * a.sX;
   const double* X2 = a.symmetric ? X : a.X2 + (long long)b * a.sX2;
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
   constexpr int MT = WT / 16;
   constexpr int NLD = BM * BK / 2 / 256;  // double2 chunks per thread per operand
   constexpr int kMainLds = 2 * 2 * BK * S;
-  constexpr int kEpiLds = (EPI == EPI_CONTRACT)
+  constexpr int kEpiLds = (EPI == EPI_CONTRACT || EPI == EPI_CONTRACT1)
       ? 4 * 16 * WT + 2 * BM * GPX_MAX_DIM + 2 * BM + GPX_THETA_STRIDE + 64 : 0;
   __shared__ __attribute__((aligned(16))) double smem[kMainLds > kEpiLds ? kMainLds : kEpiLds];
 
@@ -410,7 +410,8 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
           if (a.beta != 0.0) v = fma(a.beta, C[i * ldc + j], v);
           C[i * ldc + j] = v;
         }
-  } else if constexpr (EPI == EPI_CONTRACT) {
+  } else if constexpr (EPI == EPI_CONTRACT || EPI == EPI_CONTRACT1) {
+    constexpr int NT = (EPI == EPI_CONTRACT1) ? 1 : GPX_MAX_TERMS;
     // Gradient contraction over this lower tile of K⁻¹ = WᵀW (acc = K⁻¹_ij):
     //   g_θ += w_ij (α_i α_j − K⁻¹_ij) ∂K_ij/∂θ,  w = 2 below the diagonal, 1 on it.
     // The accumulators go through LDS in two halves so that the kernel-derivative code runs
@@ -435,9 +436,9 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
     if (tid < BM) { sai[tid] = al[i0 + tid]; saj[tid] = al[j0 + tid]; }
     if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
     const DevSpec spec = a.specs[b];
-    double sums[GPX_MAX_TERMS][3];
+    double sums[NT][3];
 #pragma unroll
-    for (int t = 0; t < GPX_MAX_TERMS; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
+    for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
     double snoise = 0.0;
     // wave-local image [16 rows][WT cols] of one MFMA row-tile per pass;
     // lane -> column cl, rows rg, rg + RG, ...
@@ -463,10 +464,10 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
           if (i >= j && i < n) {
             const double w = (i == j) ? 1.0 : 2.0;
             const double v = w * fma(sai[il], aj, -wacc[rr * WT + cl]);
-            double dk[GPX_MAX_TERMS][3];
-            eval_k_grad(spec, sth, sxi + il * D, sxj + jl * D, dk);
+            double dk[NT][3];
+            eval_k_grad<NT>(spec, sth, sxi + il * D, sxj + jl * D, dk);
 #pragma unroll
-            for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+            for (int t = 0; t < NT; ++t) {
               sums[t][0] = fma(v, dk[t][0], sums[t][0]);
               sums[t][1] = fma(v, dk[t][1], sums[t][1]);
               sums[t][2] = fma(v, dk[t][2], sums[t][2]);
@@ -482,7 +483,7 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
 #pragma unroll
     for (int t = 0; t < GPX_MAX_TERMS; ++t)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) vals[t * 3 + q] = wave_sum(sums[t][q]);
+      for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wave_sum(sums[t][q]) : 0.0;
     vals[GPX_MAX_TERMS * 3] = wave_sum(snoise);
     if (lane == 0) {
 #pragma unroll
@@ -497,10 +498,10 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
       if (tid == spec.n_params) {
         slot = GPX_MAX_TERMS * 3;
       } else {
-        for (int t = 0; t < spec.n_terms; ++t) {
-          const int o = spec.terms[t].param_offset;
-          const int np = (spec.terms[t].kind == GPX_RQ || spec.terms[t].kind == GPX_PERIODIC_SE) ? 3
-                         : (spec.terms[t].kind == GPX_LINEAR ? 1 : 2);
+        const DevSpec* gs = a.specs + b;  // dynamic term index: read from memory, not a register copy
+        for (int t = 0; t < gs->n_terms; ++t) {
+          const int o = gs->terms[t].param_offset, kind = gs->terms[t].kind;
+          const int np = (kind == GPX_RQ || kind == GPX_PERIODIC_SE) ? 3 : (kind == GPX_LINEAR ? 1 : 2);
           if (tid >= o && tid < o + np) slot = t * 3 + (tid - o);
         }
       }
@@ -557,10 +558,12 @@ void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hip
   if (bm == 128) {
     if (epi == EPI_STORE) launch_gemm_t<128, EPI_STORE>(a, ta, tb, n_active, s);
     else if (epi == EPI_CONTRACT) launch_gemm_t<128, EPI_CONTRACT>(a, ta, tb, n_active, s);
+    else if (epi == EPI_CONTRACT1) launch_gemm_t<128, EPI_CONTRACT1>(a, ta, tb, n_active, s);
     else launch_gemm_t<128, EPI_COLSUMSQ>(a, ta, tb, n_active, s);
   } else {
     if (epi == EPI_STORE) launch_gemm_t<64, EPI_STORE>(a, ta, tb, n_active, s);
     else if (epi == EPI_CONTRACT) launch_gemm_t<64, EPI_CONTRACT>(a, ta, tb, n_active, s);
+    else if (epi == EPI_CONTRACT1) launch_gemm_t<64, EPI_CONTRACT1>(a, ta, tb, n_active, s);
     else launch_gemm_t<64, EPI_COLSUMSQ>(a, ta, tb, n_active, s);
   }
 }

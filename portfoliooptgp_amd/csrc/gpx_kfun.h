@@ -134,15 +134,16 @@ __device__ __forceinline__ double eval_k(const DevSpec& s, const double* __restr
 
 // K(xi, xj) and its derivatives, kept per term in statically indexed registers:
 // dk[t][q] = dK/dθ for parameter q of term t (θ index terms[t].param_offset + q).
+template <int NT = GPX_MAX_TERMS>
 __device__ __forceinline__ double eval_k_grad(const DevSpec& s, const double* __restrict__ th,
                                               const double* __restrict__ xi,
                                               const double* __restrict__ xj,
-                                              double (&dk)[GPX_MAX_TERMS][3]) {
-  const bool prod = (s.combine == GPX_PRODUCT && s.n_terms > 1);
-  double vals[GPX_MAX_TERMS];
+                                              double (&dk)[NT][3]) {
+  const bool prod = (NT > 1 && s.combine == GPX_PRODUCT && s.n_terms > 1);
+  double vals[NT];
   double acc = prod ? 1.0 : 0.0;
 #pragma unroll
-  for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+  for (int t = 0; t < NT; ++t) {
     dk[t][0] = dk[t][1] = dk[t][2] = 0.0;
     vals[t] = 1.0;
     if (t < s.n_terms) {
@@ -152,10 +153,10 @@ __device__ __forceinline__ double eval_k_grad(const DevSpec& s, const double* __
   }
   if (prod) {
 #pragma unroll
-    for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+    for (int t = 0; t < NT; ++t) {
       double others = 1.0;
 #pragma unroll
-      for (int u = 0; u < GPX_MAX_TERMS; ++u) if (u != t) others *= vals[u];
+      for (int u = 0; u < NT; ++u) if (u != t) others *= vals[u];
       dk[t][0] *= others; dk[t][1] *= others; dk[t][2] *= others;
     }
   }

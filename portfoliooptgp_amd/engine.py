@@ -118,9 +118,13 @@ class Engine:
         self.eval_count += len(act)
         return lml, grad, info
 
-    def predict(self, active: Sequence[int], theta: np.ndarray, Xnew: Sequence, add_noise: bool):
+    def predict(self, active: Sequence[int], theta: np.ndarray, Xnew: Sequence, add_noise: bool,
+                full_cov: bool = False):
         """Marginal posterior mean/var at Xnew[i] (for problem active[i]); returns lists of
-        device tensors [M_i] and info."""
+        device tensors [M_i] and info. With full_cov the second list holds the posterior
+        covariance matrices [M_i, M_i] (latent f only, as GPflow)."""
+        if full_cov and add_noise:
+            raise NotImplementedError("full covariance is only defined for predict_f")
         act = self._active(active)
         theta = np.ascontiguousarray(theta, dtype=np.float64)
         xs = [to_device_f64(x, self.device) for x in Xnew]
@@ -133,15 +137,23 @@ class Engine:
         for b, x in zip(act, xs):
             Xn[b, : x.shape[0]] = x
         mean = torch.empty(self.B, M, dtype=torch.float64, device=dev)
-        var = torch.empty(self.B, M, dtype=torch.float64, device=dev)
         info = np.zeros(self.B, dtype=np.int32)
         dp = ctypes.POINTER(ctypes.c_double)
         ip = ctypes.POINTER(ctypes.c_int32)
-        rc = self.lib.gpx_batch_predict(self.handle, len(act), act.ctypes.data_as(ip),
-                                        theta.ctypes.data_as(dp), ctypes.c_void_p(Xn.data_ptr()), M,
-                                        1 if add_noise else 0, ctypes.c_void_p(mean.data_ptr()),
-                                        ctypes.c_void_p(var.data_ptr()), info.ctypes.data_as(ip),
-                                        self._stream())
+        if full_cov:
+            var = torch.empty(self.B, M, M, dtype=torch.float64, device=dev)
+            rc = self.lib.gpx_batch_predict_full_cov(
+                self.handle, len(act), act.ctypes.data_as(ip), theta.ctypes.data_as(dp),
+                ctypes.c_void_p(Xn.data_ptr()), M, ctypes.c_void_p(mean.data_ptr()),
+                ctypes.c_void_p(var.data_ptr()), info.ctypes.data_as(ip), self._stream())
+        else:
+            var = torch.empty(self.B, M, dtype=torch.float64, device=dev)
+            rc = self.lib.gpx_batch_predict(self.handle, len(act), act.ctypes.data_as(ip),
+                                            theta.ctypes.data_as(dp), ctypes.c_void_p(Xn.data_ptr()),
+                                            M, 1 if add_noise else 0,
+                                            ctypes.c_void_p(mean.data_ptr()),
+                                            ctypes.c_void_p(var.data_ptr()),
+                                            info.ctypes.data_as(ip), self._stream())
         if rc == N.GPX_NOT_PD:
             bad = [int(b) for b in act if info[b] != 0]
             raise N.NotPositiveDefiniteError(
@@ -150,7 +162,10 @@ class Engine:
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_predict failed ({rc}): {self.ctx.last_error()}")
         outs_m = [mean[b, : x.shape[0]] for b, x in zip(act, xs)]
-        outs_v = [var[b, : x.shape[0]] for b, x in zip(act, xs)]
+        if full_cov:
+            outs_v = [var[b, : x.shape[0], : x.shape[0]] for b, x in zip(act, xs)]
+        else:
+            outs_v = [var[b, : x.shape[0]] for b, x in zip(act, xs)]
         return outs_m, outs_v, info
 
     def rebind(self, b: int, X, Y, spec: N.GpxKernelSpec) -> None:

@@ -26,10 +26,6 @@ from .likelihoods import Gaussian
 from .parameter import Parameter
 
 
-def _as_2d_cpu_or_dev(a):
-    return a
-
-
 class GPR:
     """Exact GP regression with a Gaussian likelihood and a zero mean function."""
 
@@ -161,22 +157,26 @@ class GPR:
 
     # ---------------------------------------------------------------- prediction ------
     def predict_f(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
-        if full_cov or full_output_cov:
-            raise NotImplementedError("full_cov=True is not implemented (marginals only)")
-        return self._predict(Xnew, add_noise=False)
+        """Posterior of the latent f: mean [N*,1] and var [N*,1], or with full_cov the
+        covariance [1,N*,N*] (GPflow's layout with one latent GP; full_output_cov changes
+        nothing for a single output)."""
+        return self._predict(Xnew, add_noise=False, full_cov=full_cov)
 
     def predict_y(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
         if full_cov or full_output_cov:
-            raise NotImplementedError("full_cov=True is not implemented (marginals only)")
+            # GPflow 2.9 GPModel.predict_y raises for these too
+            raise NotImplementedError("The predict_y method currently supports only the argument "
+                                      "values full_cov=False and full_output_cov=False")
         return self._predict(Xnew, add_noise=True)
 
-    def _predict(self, Xnew, add_noise: bool):
+    def _predict(self, Xnew, add_noise: bool, full_cov: bool = False):
         eng, b = self.engine()
         theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
         theta[b] = self.theta_row()
         cpu_out = not (isinstance(Xnew, torch.Tensor) and Xnew.is_cuda)
-        m, v, _ = eng.predict([b], theta, [Xnew], add_noise)
-        m, v = m[0].reshape(-1, 1), v[0].reshape(-1, 1)
+        m, v, _ = eng.predict([b], theta, [Xnew], add_noise, full_cov=full_cov)
+        m = m[0].reshape(-1, 1)
+        v = v[0].unsqueeze(0) if full_cov else v[0].reshape(-1, 1)
         if cpu_out:
             m, v = m.cpu(), v.cpu()
         return m, v

@@ -111,3 +111,14 @@ def test_no_cpu_fallback():
 def test_scipy_rejects_foreign_closures():
     with pytest.raises(TypeError):
         gpx.optimizers.Scipy().minimize(lambda: 0.0, [Parameter(1.0).unconstrained_variable])
+
+
+def test_predict_y_full_cov_not_implemented_like_gpflow():
+    """GPflow 2.9 GPModel.predict_y raises NotImplementedError for full_cov/full_output_cov;
+    predict_f(full_cov=True) is supported (GPU test_predict_full_cov)."""
+    x = np.arange(5.0)[:, None]
+    m = gpx.models.GPR((x, x), kernel=gpx.kernels.SquaredExponential())
+    with pytest.raises(NotImplementedError):
+        m.predict_y(x, full_cov=True)
+    with pytest.raises(NotImplementedError):
+        m.predict_y(x, full_output_cov=True)

@@ -359,3 +359,48 @@ def test_gradient_accuracy_vs_exact():
     kappa = float(d[key + "|cond"][0])
     assert 5e6 < kappa < 5e7
     assert err_gpu <= 5 * err_oracle, (err_gpu, err_oracle)
+
+
+def test_predict_full_cov():
+    """predict_f(full_cov=True): [1,N*,N*] covariance = k(X*,X*) − Kxsᵀ(K+σn²I)⁻¹Kxs (the
+    commented-out call at test_scripts/GPR_Entropy.py:373). Covers M below and above the
+    padded training size (the two workspace paths) and a composite kernel."""
+    rng = np.random.default_rng(11)
+    for n, msz, fam in ((100, 37, "se"), (64, 200, "m52"), (257, 130, "exp+per")):
+        x = np.sort(rng.uniform(0, 30, n))[:, None]
+        y = np.sin(x / 3.0) + 0.1 * rng.standard_normal((n, 1))
+        m = gpx.models.GPR((x, y), kernel=gpx_kernel(fam), noise_variance=1e-2)
+        om = O.OGPR(x, y, oracle_kernel(fam), noise_variance=1e-2)
+        xs = np.linspace(-3, 33, msz)[:, None]
+        mu, cov = m.predict_f(xs, full_cov=True)
+        assert tuple(cov.shape) == (1, msz, msz) and tuple(mu.shape) == (msz, 1)
+        mo, co = om.predict_f(xs, full_cov=True)
+        check_mean(mu.numpy(), mo)
+        c = cov.numpy()[0]
+        s2 = float(np.abs(np.diag(co)).max())
+        assert np.abs(c - co).max() <= 1e-5 * np.abs(co).max() + 1e-10 * s2
+        np.testing.assert_allclose(c, c.T, rtol=0, atol=1e-12 * s2)
+        _, var = m.predict_f(xs)
+        np.testing.assert_allclose(np.diag(c), var.numpy().ravel(), rtol=1e-9, atol=1e-12 * s2)
+
+
+def test_config4_shape_matern52_5d():
+    """BASELINE config C4 shape (Multi-Input_GPR: 5-D inputs, Matern-5/2, N=4096), computed in
+    fp64 (the reference's precision; see DESIGN.md on why not fp32): logML, gradient and
+    predictions against the oracle at the full size."""
+    n, d = 4096, 5
+    rng = np.random.default_rng(5)
+    x = np.cumsum(rng.standard_normal((n, d)) * 0.05, axis=0) + rng.standard_normal(d)
+    y = np.sin(x[:, :1] * 2) + 0.3 * x[:, 1:2] - 0.2 * x[:, 2:3] * x[:, 3:4] + 0.05 * rng.standard_normal((n, 1))
+    ell, var, noise = 1.7, 0.9, 1e-3
+    m = gpx.models.GPR((x, y), kernel=K.Matern52(lengthscales=ell, variance=var), noise_variance=noise)
+    om = O.OGPR(x, y, O.OMatern52(lengthscales=ell, variance=var), noise_variance=noise)
+    loss, g = m.loss_and_grad_unconstrained()
+    lo, go = om.loss_and_grad_u()
+    assert abs(loss - lo) <= 1e-9 * abs(lo)
+    assert np.all(np.abs(g - go) <= 1e-6 * (1.0 + np.abs(go).max())), (g, go)
+    xs = x[::37] + 0.01
+    mu, v = m.predict_f(xs)
+    mo, vo = om.predict_f(xs)
+    check_mean(mu.numpy(), mo)
+    assert np.all(np.abs(v.numpy() - vo) <= 1e-5 * np.abs(vo) + 1e-9)
