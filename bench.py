@@ -228,7 +228,7 @@ def main():
         "evals_per_s": tm.evals / elapsed if world == 1 else None,
         "eval_alg_tflops": eval_alg / (tm.eval_ms_total * 1e-3) / 1e12 if tm.eval_ms_total else None,
         "roofline": {
-            "kernel": "gemm_kernel<128,T,N,EPI_CONTRACT> (K^-1 = W^T W fused with the gradient contraction)",
+            "kernel": "gemm_kernel<128,T,N,EPI_CONTRACT1> (K^-1 = W^T W fused with the gradient contraction)",
             "bound": "mfma",
             "achieved": achieved,
             "peak": FP64_PEAK_TFLOPS,

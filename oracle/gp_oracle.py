@@ -106,6 +106,11 @@ class OKernel:
         """dK(X,X)/dθ for each parameter in params() order (constrained space)."""
         raise NotImplementedError
 
+    def dK_dX1(self, X, X2) -> np.ndarray:
+        """∂K(x, x')/∂x for x in X, x' in X2: [n1, n2, D] over ALL input columns (zero
+        outside active_dims). Used by the SVGP oracle for the inducing-point gradient."""
+        raise NotImplementedError
+
 
 class OStationary(OKernel):
     """IsotropicStationary: r² = Σ_d ((x_d - x'_d)/ℓ)² over active dims (GPflow
@@ -148,6 +153,20 @@ class OStationary(OKernel):
         g = self._g(r2)
         dl = var * self._dg_dr2(r2) * (-2.0 * r2 / ell)     # d r²/dℓ = -2 r²/ℓ
         return [dl, g]
+
+    def dK_dX1(self, X, X2):
+        X = np.asarray(X, np.float64)
+        X2 = np.asarray(X2, np.float64)
+        ell, var = self.lengthscales.value, self.variance.value
+        r2 = self._d2(X, X2) / (ell * ell)
+        f = var * self._dg_dr2(r2) * 2.0 / (ell * ell)        # ∂k/∂x_d = f · (x_d − x'_d)
+        out = np.zeros(X.shape[:1] + X2.shape[:1] + X.shape[1:])
+        cols = np.arange(X.shape[1])
+        if self.active_dims is not None:
+            cols = cols[self.active_dims] if isinstance(self.active_dims, slice) else np.asarray(list(self.active_dims))
+        for d in cols:
+            out[:, :, d] = f * (X[:, None, d] - X2[None, :, d])
+        return out
 
 
 class OSquaredExponential(OStationary):
@@ -282,6 +301,21 @@ class OPeriodic(OKernel):
         dp = var * g * (-0.5) * ds2dp
         return [dl, g, dp]
 
+    def dK_dX1(self, X, X2):
+        X = np.asarray(X, np.float64)
+        _, arg = self._parts(X, X2)
+        ell, p = self.base.lengthscales.value, self.period.value
+        k = self.K(X, X2)
+        # ∂k/∂x_d = k · (−½) · 2 sin cos · (π/p) / ℓ²
+        part = -k[:, :, None] * np.sin(arg) * np.cos(arg) * (math.pi / p) / (ell * ell)
+        out = np.zeros(k.shape + X.shape[1:])
+        cols = np.arange(X.shape[1])
+        ad = self.base.active_dims
+        if ad is not None:
+            cols = cols[ad] if isinstance(ad, slice) else np.asarray(list(ad))
+        out[:, :, cols] = part
+        return out
+
 
 class OLinear(OKernel):
     def __init__(self, variance=1.0, active_dims=None):
@@ -306,6 +340,17 @@ class OLinear(OKernel):
     def dK(self, X):
         return [self._xx(X, None)]
 
+    def dK_dX1(self, X, X2):
+        X = np.asarray(X, np.float64)
+        X2 = np.asarray(X2, np.float64)
+        out = np.zeros((X.shape[0], X2.shape[0], X.shape[1]))
+        cols = np.arange(X.shape[1])
+        if self.active_dims is not None:
+            cols = cols[self.active_dims] if isinstance(self.active_dims, slice) else np.asarray(list(self.active_dims))
+        for d in cols:
+            out[:, :, d] = self.variance.value * X2[None, :, d]
+        return out
+
 
 class OSum(OKernel):
     def __init__(self, kernels: Sequence[OKernel]):
@@ -322,6 +367,9 @@ class OSum(OKernel):
 
     def dK(self, X):
         return [d for k in self.kernels for d in k.dK(X)]
+
+    def dK_dX1(self, X, X2):
+        return sum(k.dK_dX1(X, X2) for k in self.kernels)
 
 
 class OProduct(OKernel):
@@ -353,6 +401,17 @@ class OProduct(OKernel):
                     others = others * Ks_s
             res.extend(others * d for d in k.dK(X))
         return res
+
+    def dK_dX1(self, X, X2):
+        Ks = [k.K(X, X2) for k in self.kernels]
+        out = 0.0
+        for t, k in enumerate(self.kernels):
+            others = np.ones_like(Ks[0])
+            for s_, Ks_s in enumerate(Ks):
+                if s_ != t:
+                    others = others * Ks_s
+            out = out + others[:, :, None] * k.dK_dX1(X, X2)
+        return out
 
 
 # ----------------------------------------------------------------------------------------
