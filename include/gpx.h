@@ -160,6 +160,47 @@ int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);
 int gpx_set_profiling(gpx_ctx* ctx, int enabled);
 
+/* ---------------------------------------------------------------------------------------
+ * SVGP: gpflow.models.SVGP(kernel, Gaussian(σn²), inducing_variable=Z, num_data=...) with
+ * GPflow's defaults (whiten=True, full lower-triangular q_sqrt, zero mean, one latent GP) —
+ * test_scripts/SVGP.py:461-478 (M=120), :515-540 (M=20), test_scripts/GPR.py:118-138.
+ *   gpx_svgp_elbo_grad  <- training_loss_closure((X, Y)) value + gradient, fed to
+ *                          gpflow.optimizers.Scipy().minimize (test_scripts/SVGP.py:471-474)
+ *   gpx_svgp_predict    <- model.predict_f(X_test) / predict_y          (SVGP.py:478)
+ *
+ * One gpx_svgp holds one shard of the data: X [N, D] and Y [N] (device, fp64, caller-owned).
+ * n_total = rows over all shards (= N on one GPU); the ELBO's data term is scaled by
+ * num_data / n_total like GPflow's minibatch scaling. Per evaluation:
+ *   theta  host [16]: kernel params (gpx_kernel_spec layout) then σn² at theta[n_params]
+ *   Z      host [M, D]   inducing inputs;   q_mu host [M];   q_sqrt host [M, M] row-major,
+ *          lower triangle used (the FillTriangular-constrained value)
+ * Outputs (host): elbo; grad_theta [16] (∂ELBO/∂θ constrained, σn² at n_params);
+ *   grad_Z [M, D]; grad_qmu [M]; grad_qsqrt [M, M] (lower triangle, upper zero).
+ * Sharded use: gpx_svgp_eval_local on every shard, sum the gpx_svgp_partials() device
+ * buffers over shards (one all-reduce), then gpx_svgp_eval_finish. gpx_svgp_elbo_grad is
+ * local + finish for the unsharded case (n_total == N).
+ */
+typedef struct gpx_svgp gpx_svgp;
+int gpx_svgp_create(gpx_ctx* ctx, int N, int M, int D, const double* X, const double* Y,
+                    const gpx_kernel_spec* spec, double num_data, long long n_total,
+                    gpx_svgp** out);
+int gpx_svgp_destroy(gpx_svgp* svgp);
+/* the partial-sum buffer (device, fp64, len doubles) and a way to substitute a caller-owned
+ * one (e.g. a torch tensor that torch.distributed all-reduces in place) */
+int gpx_svgp_partials(gpx_svgp* svgp, double** dev_ptr, long long* len);
+int gpx_svgp_bind_partials(gpx_svgp* svgp, double* dev_ptr, long long len);
+int gpx_svgp_eval_local(gpx_svgp* svgp, const double* theta, const double* Z, const double* q_mu,
+                        const double* q_sqrt, int32_t* info, void* stream);
+int gpx_svgp_eval_finish(gpx_svgp* svgp, double* elbo, double* grad_theta, double* grad_Z,
+                         double* grad_qmu, double* grad_qsqrt, void* stream);
+int gpx_svgp_elbo_grad(gpx_svgp* svgp, const double* theta, const double* Z, const double* q_mu,
+                       const double* q_sqrt, double* elbo, double* grad_theta, double* grad_Z,
+                       double* grad_qmu, double* grad_qsqrt, int32_t* info, void* stream);
+/* predict_f (add_noise = 0) / predict_y (1) at Xnew (device [Mn, D]) -> mean, var (device [Mn]) */
+int gpx_svgp_predict(gpx_svgp* svgp, const double* theta, const double* Z, const double* q_mu,
+                     const double* q_sqrt, const double* Xnew, int Mn, int add_noise, double* mean,
+                     double* var, int32_t* info, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,11 +11,11 @@ gfx950 in ``libgpx.so`` behind the C ABI of ``include/gpx.h``.
     gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables, options=dict(maxiter=100))
     mean, var = m.predict_f(X)
 """
-from . import _native, kernels, likelihoods, models, optimizers, utilities
+from . import _native, inducing_variables, kernels, likelihoods, models, optimizers, utilities
 from ._native import GPXError, NotPositiveDefiniteError
 from .parameter import Parameter
 from .utilities import print_summary, set_trainable
 
-__all__ = ["kernels", "likelihoods", "models", "optimizers", "utilities", "Parameter",
+__all__ = ["inducing_variables", "kernels", "likelihoods", "models", "optimizers", "utilities", "Parameter",
            "set_trainable", "print_summary", "GPXError", "NotPositiveDefiniteError"]
 __version__ = "0.1.0"

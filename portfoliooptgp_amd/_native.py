@@ -28,6 +28,8 @@ EXPORTED_SYMBOLS = (
     "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_predict", "gpx_batch_predict_full_cov",
     "gpx_batch_last_timing",
     "gpx_set_profiling", "gpx_batch_reset_timing", "gpx_batch_rebind",
+    "gpx_svgp_create", "gpx_svgp_destroy", "gpx_svgp_partials", "gpx_svgp_bind_partials",
+    "gpx_svgp_eval_local", "gpx_svgp_eval_finish", "gpx_svgp_elbo_grad", "gpx_svgp_predict",
 )
 
 
@@ -82,6 +84,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib = ctypes.CDLL(p)
         c_int, c_void_p, c_double_p = ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)
         c_int_p = ctypes.POINTER(ctypes.c_int32)
+        c_double = ctypes.c_double
         lib.gpx_version.restype = ctypes.c_char_p
         lib.gpx_version.argtypes = []
         lib.gpx_create.restype = c_int
@@ -112,6 +115,29 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_rebind.argtypes = [c_void_p, c_int, c_int, ctypes.POINTER(GpxKernelSpec)]
         lib.gpx_batch_reset_timing.restype = c_int
         lib.gpx_batch_reset_timing.argtypes = [c_void_p]
+        spec_p = ctypes.POINTER(GpxKernelSpec)
+        lib.gpx_svgp_create.restype = c_int
+        lib.gpx_svgp_create.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, spec_p,
+                                        c_double, ctypes.c_longlong, ctypes.POINTER(c_void_p)]
+        lib.gpx_svgp_destroy.restype = c_int
+        lib.gpx_svgp_destroy.argtypes = [c_void_p]
+        lib.gpx_svgp_partials.restype = c_int
+        lib.gpx_svgp_partials.argtypes = [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(ctypes.c_longlong)]
+        lib.gpx_svgp_bind_partials.restype = c_int
+        lib.gpx_svgp_bind_partials.argtypes = [c_void_p, c_void_p, ctypes.c_longlong]
+        lib.gpx_svgp_eval_local.restype = c_int
+        lib.gpx_svgp_eval_local.argtypes = [c_void_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                            c_int_p, c_void_p]
+        lib.gpx_svgp_eval_finish.restype = c_int
+        lib.gpx_svgp_eval_finish.argtypes = [c_void_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                             c_double_p, c_void_p]
+        lib.gpx_svgp_elbo_grad.restype = c_int
+        lib.gpx_svgp_elbo_grad.argtypes = [c_void_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                           c_double_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                           c_int_p, c_void_p]
+        lib.gpx_svgp_predict.restype = c_int
+        lib.gpx_svgp_predict.argtypes = [c_void_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                         c_void_p, c_int, c_int, c_void_p, c_void_p, c_int_p, c_void_p]
         if path is None:
             _lib = lib
         return lib

@@ -18,83 +18,14 @@
 #include <cstdlib>
 #include <string>
 #include <vector>
-#include "gpx_internal.h"
+#include "gpx_host.h"
 
 using namespace gpx;
 
-constexpr int kGroups = 4;  // max concurrent pipelines per evaluation (HIP streams)
-constexpr int kAux = 3;     // auxiliary streams for the T = L21·W11 products of depths 0..2
-constexpr int kEvents = 64;
-
-struct gpx_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t workers[kGroups] = {};
-  hipStream_t aux[kAux] = {};
-  hipEvent_t fork = nullptr, join[kGroups] = {};
-  hipEvent_t ev[kEvents] = {};
-  std::string err;
-  int profiling = 0;
-};
-
-struct gpx_batch {
-  gpx_ctx* ctx = nullptr;
-  int B = 0, Nmax = 0, D = 0, Np = 0;
-  const double* X = nullptr;
-  const double* Y = nullptr;
-  std::vector<int> n;
-  std::vector<gpx_kernel_spec> specs;
-  int* d_n = nullptr;
-  DevSpec* d_specs = nullptr;
-  double* d_theta = nullptr;
-  int* d_active = nullptr;
-  int* d_info = nullptr;
-  double *K = nullptr, *L = nullptr, *W = nullptr;     // [B][Np][Np]
-  double *z = nullptr, *alpha = nullptr, *ldiag = nullptr;  // [B][Np]
-  double* partial = nullptr;       // [B][ntiles64][16]
-  long long partial_stride = 0;
-  double* results = nullptr;       // [B][kResStride]
-  // predict workspace
-  double* kxs = nullptr; size_t kxs_cap = 0;
-  double* pvp = nullptr; size_t pvp_cap = 0;
-  double* abuf = nullptr; size_t abuf_cap = 0;   // A = W·Kxs (full_cov, Mp > Np)
-  double* covw = nullptr; size_t covw_cap = 0;   // padded [B][Mp][Mp] covariance
-  // factor cache: theta row of the last factorisation per problem
-  std::vector<double> fac_theta;
-  std::vector<char> fac_valid;
-  std::vector<double> h_results;
-  std::vector<int> h_info;
-  gpx_timing timing{};
-  double flops_acc = 0.0;
-};
-
-namespace {
+namespace gpx {
 
 const char* kVersion = "gpx 0.1.0 (gfx950, fp64 MFMA)";
 
-int fail(gpx_ctx* ctx, int code, const std::string& msg) {
-  if (ctx) ctx->err = msg;
-  return code;
-}
-
-#define HIPX(ctx, expr)                                                               \
-  do {                                                                                \
-    hipError_t e_ = (expr);                                                           \
-    if (e_ != hipSuccess)                                                             \
-      return fail(ctx, GPX_HIP_ERROR, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
-inline long long mat_stride(const gpx_batch* bt) { return (long long)bt->Np * bt->Np; }
-
-// One pipeline instance: a contiguous range of the device active list on one stream.
-struct Run {
-  gpx_batch* bt;
-  const int* d_act;  // device pointer into the uploaded active list
-  int na;            // problems in this range
-  hipStream_t s;
-  bool dag = false;  // run the T products of the top recursion levels on the aux streams
-  int* next_event = nullptr;
-};
 
 // MFMA flops the GEMM launcher will issue for these args (bench / roofline bookkeeping)
 double gemm_issued_flops(const GemmArgs& a, int na) {
@@ -137,7 +68,7 @@ GemmArgs gemm_args(const double* A, int lda, const double* B, int ldb, double* C
 }
 
 // Recursive Cholesky-and-inverse on the diagonal block [off, off+n) of every problem of r.
-void chol_inv(const Run& r, int off, int n, int depth = 0) {
+void chol_inv(const Run& r, int off, int n, int depth) {
   gpx_batch* bt = r.bt;
   const int Np = bt->Np;
   const long long st = mat_stride(bt);
@@ -239,27 +170,6 @@ void reduce(const Run& r) {
   launch_reduce(ra, r.na, r.s);
 }
 
-struct PhaseTimer {
-  bool on;
-  hipStream_t s;
-  std::vector<hipEvent_t> ev;
-  PhaseTimer(bool enabled, hipStream_t st) : on(enabled), s(st) {}
-  void mark() {
-    if (!on) return;
-    hipEvent_t e;
-    (void)hipEventCreate(&e);
-    (void)hipEventRecord(e, s);
-    ev.push_back(e);
-  }
-  double ms(int i, int j) {
-    float t = 0.f;
-    (void)hipEventElapsedTime(&t, ev[i], ev[j]);
-    return t;
-  }
-  ~PhaseTimer() {
-    for (auto e : ev) (void)hipEventDestroy(e);
-  }
-};
 
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                   hipStream_t s) {
@@ -284,7 +194,7 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
   return GPX_OK;
 }
 
-}  // namespace
+}  // namespace gpx
 
 extern "C" {
 
@@ -550,15 +460,6 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   return status;
 }
 
-// grow-only device workspace
-static int ensure(gpx_ctx* ctx, double*& p, size_t& cap, size_t need) {
-  if (cap >= need) return GPX_OK;
-  if (p) (void)hipFree(p);
-  p = nullptr; cap = 0;
-  HIPX(ctx, hipMalloc(&p, need * sizeof(double)));
-  cap = need;
-  return GPX_OK;
-}
 
 // Shared body of gpx_batch_predict (var != nullptr) and gpx_batch_predict_full_cov
 // (cov != nullptr).

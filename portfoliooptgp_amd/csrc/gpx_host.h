@@ -1,0 +1,125 @@
+// gpx_host.h — host-side internals shared by the exact-GP (gpx_api.hip) and SVGP
+// (gpx_svgp.hip) orchestration: context / batch state, error plumbing and the device
+// building blocks (K build + recursive Cholesky-and-inverse, batched MFMA GEMM).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string>
+#include <vector>
+#include "gpx_internal.h"
+
+constexpr int kGroups = 4;  // max concurrent pipelines per evaluation (HIP streams)
+constexpr int kAux = 3;     // auxiliary streams for the T = L21·W11 products of depths 0..2
+constexpr int kEvents = 64;
+
+struct gpx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t workers[kGroups] = {};
+  hipStream_t aux[kAux] = {};
+  hipEvent_t fork = nullptr, join[kGroups] = {};
+  hipEvent_t ev[kEvents] = {};
+  std::string err;
+  int profiling = 0;
+};
+
+struct gpx_batch {
+  gpx_ctx* ctx = nullptr;
+  int B = 0, Nmax = 0, D = 0, Np = 0;
+  const double* X = nullptr;
+  const double* Y = nullptr;
+  std::vector<int> n;
+  std::vector<gpx_kernel_spec> specs;
+  int* d_n = nullptr;
+  gpx::DevSpec* d_specs = nullptr;
+  double* d_theta = nullptr;
+  int* d_active = nullptr;
+  int* d_info = nullptr;
+  double *K = nullptr, *L = nullptr, *W = nullptr;     // [B][Np][Np]
+  double *z = nullptr, *alpha = nullptr, *ldiag = nullptr;  // [B][Np]
+  double* partial = nullptr;       // [B][ntiles64][16]
+  long long partial_stride = 0;
+  double* results = nullptr;       // [B][kResStride]
+  // predict workspace
+  double* kxs = nullptr; size_t kxs_cap = 0;
+  double* pvp = nullptr; size_t pvp_cap = 0;
+  double* abuf = nullptr; size_t abuf_cap = 0;   // A = W·Kxs (full_cov, Mp > Np)
+  double* covw = nullptr; size_t covw_cap = 0;   // padded [B][Mp][Mp] covariance
+  // factor cache: theta row of the last factorisation per problem
+  std::vector<double> fac_theta;
+  std::vector<char> fac_valid;
+  std::vector<double> h_results;
+  std::vector<int> h_info;
+  gpx_timing timing{};
+  double flops_acc = 0.0;
+};
+
+namespace gpx {
+
+inline int fail(gpx_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+#define HIPX(ctx, expr)                                                               \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(ctx, GPX_HIP_ERROR, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+inline long long mat_stride(const gpx_batch* bt) { return (long long)bt->Np * bt->Np; }
+
+// One pipeline instance: a contiguous range of the device active list on one stream.
+struct Run {
+  gpx_batch* bt;
+  const int* d_act;  // device pointer into the uploaded active list
+  int na;            // problems in this range
+  hipStream_t s;
+  bool dag = false;  // run the T products of the top recursion levels on the aux streams
+  int* next_event = nullptr;
+};
+
+struct PhaseTimer {
+  bool on;
+  hipStream_t s;
+  std::vector<hipEvent_t> ev;
+  PhaseTimer(bool enabled, hipStream_t st) : on(enabled), s(st) {}
+  void mark() {
+    if (!on) return;
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    (void)hipEventRecord(e, s);
+    ev.push_back(e);
+  }
+  double ms(int i, int j) {
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, ev[i], ev[j]);
+    return t;
+  }
+  ~PhaseTimer() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+  }
+};
+
+// grow-only device workspace
+inline int ensure(gpx_ctx* ctx, double*& p, size_t& cap, size_t need) {
+  if (cap >= need) return GPX_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr; cap = 0;
+  HIPX(ctx, hipMalloc(&p, need * sizeof(double)));
+  cap = need;
+  return GPX_OK;
+}
+
+double gemm_issued_flops(const GemmArgs& a, int na);
+void gemm(const Run& r, GemmArgs a, int epi, bool ta, bool tb);
+GemmArgs gemm_args(const double* A, int lda, const double* B, int ldb, double* C, int ldc,
+                   long long stride, int M, int N, int K, int tri, int lower, double alpha,
+                   double beta);
+void chol_inv(const Run& r, int off, int n, int depth = 0);
+void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W = L⁻¹)
+void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z
+int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                  hipStream_t s);
+
+}  // namespace gpx

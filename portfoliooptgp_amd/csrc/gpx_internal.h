@@ -100,4 +100,68 @@ void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s);
 void launch_predvar(const PredVarArgs& a, int n_active, hipStream_t s);
 int gemm_tile(const GemmArgs& a, int n_active);  // tile edge the launcher will use (64 or 128)
 
+// ---- SVGP (gpx_svgp_kernels.hip) -----------------------------------------------------
+// Row-organised derivative contraction over an M×N (or M×M) index set:
+//   Kbar_ij = u_i g_j (optional) + Y_ij (or ½(Y_ij + Y_ji) when sym)
+//   θ:  Σ_ij Kbar_ij ∂k(z_i, x_j)/∂θ          -> part_theta [blocks][16]
+//   z:  zscale Σ_j Kbar_ij ∂k(z_i, x_j)/∂z_i  -> part_z [chunks][Mp*D]
+//   w:  Σ_j k(z_i, x_j) g_j (optional)         -> part_w [chunks][Mp]
+struct RowsArgs {
+  const double* Zr; const double* Xc; int D;
+  int nrows, ncols;
+  const double* Y; int ldy; int sym;
+  const double* u; const double* g;
+  double zscale;
+  const DevSpec* spec; const double* theta;
+  int chunk;
+  double* part_theta; double* part_z; double* part_w;
+  int Mp;
+};
+
+// g_j = s (y_j − μ_j)/σ²; block partials [blocks][kResidW]: 0..15 c Σ ∂k_jj/∂θ (θ layout),
+// 16 Σ (y−μ)², 17 Σ k_jj.
+constexpr int kResidW = 20;
+struct ResidArgs {
+  const double* X; const double* Y; const double* mu; int D; int n; int npad;
+  const DevSpec* spec; const double* theta;
+  double scale;            // num_data / n_total
+  double* g;               // [npad], zero beyond n
+  double* part;            // [blocks][kResidW]
+};
+
+// dst[c] (+)= Σ_b src[b*stride + c], c < width
+struct SumArgs {
+  const double* src; long long stride; int nb; long long width;
+  double* dst; int accumulate;
+};
+
+// Elementwise M×M tail of the ELBO gradient (valid i, j < m):
+//   Phi = Φ(−(q âᵀ + 2c X1)), Rbar = tril(2c GR − R + diag(1/R_ii)), trace partials of Sm1∘Ĝ
+struct SvgpFinalArgs {
+  const double* X1; const double* GR; const double* R; const double* Sm1; const double* Gh;
+  const double* q; const double* ahat; double c2;
+  int m, ld;
+  double* Phi; double* Rbar; double* part_tr;   // part_tr [blocks]
+};
+
+struct SvgpPredVarArgs {
+  const double* pA; const double* pB; int nrt; int ldp;   // COLSUMSQ partials [nrt][ldp]
+  const double* Xnew; int D; int M;
+  const DevSpec* spec; const double* theta; int add_noise;
+  double* var;
+};
+
+void launch_rows(const RowsArgs& a, hipStream_t s);
+int rows_chunk_for(int D);              // column chunk for RowsArgs.chunk
+int rows_blocks(const RowsArgs& a);     // number of part_theta rows written
+int rows_chunks(const RowsArgs& a);     // number of part_z / part_w chunks written
+void launch_resid(const ResidArgs& a, hipStream_t s);
+int resid_blocks(int npad);
+void launch_sum(const SumArgs& a, hipStream_t s);
+void launch_svgp_final(const SvgpFinalArgs& a, hipStream_t s);
+int svgp_final_blocks(int m);
+void launch_diag_add(double* A, int ld, int n, double v, hipStream_t s);
+void launch_symmetrize_lower(double* A, int ld, int n, hipStream_t s);
+void launch_svgp_predvar(const SvgpPredVarArgs& a, hipStream_t s);
+
 }  // namespace gpx

@@ -163,6 +163,121 @@ __device__ __forceinline__ double eval_k_grad(const DevSpec& s, const double* __
   return acc;
 }
 
+// ∂K(xi, xj)/∂xi over the first DM input columns (zero outside each term's active dims);
+// the SVGP inducing-point gradient. Product rule applied term by term:
+// (P, G) ← (P·v_t, G·v_t + P·g_t).
+template <int DM>
+__device__ __forceinline__ double eval_term_dx1(const gpx_term& t, const double* __restrict__ th,
+                                                const double* __restrict__ xi,
+                                                const double* __restrict__ xj, double (&g)[DM]) {
+  const int d0 = t.dim_start, dn = t.dim_count;
+#pragma unroll
+  for (int d = 0; d < DM; ++d) g[d] = 0.0;
+  switch (t.kind) {
+    case GPX_LINEAR: {
+      double s = 0.0;
+      for (int d = 0; d < dn; ++d) s = fma(xi[d0 + d], xj[d0 + d], s);
+#pragma unroll
+      for (int d = 0; d < DM; ++d)
+        if (d >= d0 && d < d0 + dn) g[d] = th[0] * xj[d];
+      return th[0] * s;
+    }
+    case GPX_PERIODIC_SE: {
+      const double ell = th[0], var = th[1], p = th[2];
+      const double inv_l2 = 1.0 / (ell * ell);
+      double s2 = 0.0;
+      for (int d = 0; d < dn; ++d) {
+        const double sn = sin(M_PI * (xi[d0 + d] - xj[d0 + d]) / p);
+        s2 = fma(sn, sn, s2);
+      }
+      const double k = var * exp(-0.5 * s2 * inv_l2);
+#pragma unroll
+      for (int d = 0; d < DM; ++d)
+        if (d >= d0 && d < d0 + dn) {
+          double sn, cs;
+          sincos(M_PI * (xi[d] - xj[d]) / p, &sn, &cs);
+          g[d] = -k * sn * cs * (M_PI / p) * inv_l2;
+        }
+      return k;
+    }
+    default: break;
+  }
+  const bool rq = (t.kind == GPX_RQ);
+  const double ell = rq ? th[1] : th[0];
+  const double var = rq ? th[2] : th[1];
+  double d2 = 0.0;
+  for (int d = 0; d < dn; ++d) {
+    const double diff = xi[d0 + d] - xj[d0 + d];
+    d2 = fma(diff, diff, d2);
+  }
+  const double inv_l2 = 1.0 / (ell * ell);
+  const double r2 = d2 * inv_l2;
+  double k, dgdr2;  // K = var·g(r²), dgdr2 = var·g'(r²)
+  switch (t.kind) {
+    case GPX_SE: { k = var * exp(-0.5 * r2); dgdr2 = -0.5 * k; break; }
+    case GPX_RQ: {
+      const double a = th[0];
+      const double b = 1.0 + 0.5 * r2 / a;
+      k = var * exp(-a * log(b));
+      dgdr2 = -0.5 * k / b;
+      break;
+    }
+    default: {
+      const bool clamped = !(r2 > 1e-36);
+      const double r = sqrt(clamped ? 1e-36 : r2);
+      double gv, dh;
+      switch (t.kind) {
+        case GPX_MATERN12: { gv = exp(-r); dh = -gv; break; }
+        case GPX_EXPONENTIAL: { gv = exp(-0.5 * r); dh = -0.5 * gv; break; }
+        case GPX_MATERN32: {
+          const double sq3 = 1.7320508075688772, e = exp(-sq3 * r);
+          gv = (1.0 + sq3 * r) * e; dh = -3.0 * r * e; break;
+        }
+        default: {
+          const double sq5 = 2.23606797749979, e = exp(-sq5 * r);
+          gv = (1.0 + sq5 * r + (5.0 / 3.0) * r * r) * e;
+          dh = -(5.0 / 3.0) * r * (1.0 + sq5 * r) * e;
+          break;
+        }
+      }
+      k = var * gv;
+      dgdr2 = clamped ? 0.0 : var * dh / (2.0 * r);
+      break;
+    }
+  }
+  const double f = 2.0 * dgdr2 * inv_l2;
+#pragma unroll
+  for (int d = 0; d < DM; ++d)
+    if (d >= d0 && d < d0 + dn) g[d] = f * (xi[d] - xj[d]);
+  return k;
+}
+
+template <int DM>
+__device__ __forceinline__ double eval_k_dx1(const DevSpec& s, const double* __restrict__ th,
+                                             const double* __restrict__ xi,
+                                             const double* __restrict__ xj, double (&g)[DM]) {
+  const bool prod = (s.combine == GPX_PRODUCT && s.n_terms > 1);
+  double P = prod ? 1.0 : 0.0;
+#pragma unroll
+  for (int d = 0; d < DM; ++d) g[d] = 0.0;
+#pragma unroll
+  for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+    if (t >= s.n_terms) break;
+    double gt[DM];
+    const double v = eval_term_dx1<DM>(s.terms[t], th + s.terms[t].param_offset, xi, xj, gt);
+    if (prod) {
+#pragma unroll
+      for (int d = 0; d < DM; ++d) g[d] = fma(g[d], v, P * gt[d]);
+      P *= v;
+    } else {
+#pragma unroll
+      for (int d = 0; d < DM; ++d) g[d] += gt[d];
+      P += v;
+    }
+  }
+  return P;
+}
+
 // K_diag(x): σ² for stationary terms, σ² Σ x² for Linear.
 __device__ __forceinline__ double eval_kdiag(const DevSpec& s, const double* __restrict__ th,
                                              const double* __restrict__ x) {

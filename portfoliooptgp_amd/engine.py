@@ -194,3 +194,113 @@ class Engine:
         t = N.GpxTiming()
         self.lib.gpx_batch_last_timing(self.handle, ctypes.byref(t))
         return t
+
+
+class SVGPEngine:
+    """Device state of one SVGP data shard (include/gpx.h gpx_svgp): X [N, D] / Y [N]
+    resident in HBM, Kmn / workspace owned by the library, and the per-shard partial-sum
+    buffer as a torch tensor (so torch.distributed can all-reduce it in place)."""
+
+    def __init__(self, X, Y, spec: N.GpxKernelSpec, M: int, num_data: float,
+                 n_total: Optional[int] = None, device: Optional[int] = None):
+        self.device = require_gpu(device)
+        self.ctx = N.Context.get(self.device)
+        self.lib = self.ctx.lib
+        x = to_device_f64(X, self.device)
+        self.X = x.reshape(x.shape[0], -1).contiguous()
+        self.Y = to_device_f64(Y, self.device).reshape(-1).contiguous()
+        self.N, self.D = self.X.shape
+        if self.Y.shape[0] != self.N:
+            raise ValueError("X and Y must have the same number of rows")
+        if self.D > N.GPX_MAX_DIM:
+            raise NotImplementedError(f"input dimension {self.D} > {N.GPX_MAX_DIM}")
+        self.M = int(M)
+        self.n_total = int(self.N if n_total is None else n_total)
+        self.spec = spec
+        torch.cuda.synchronize(self.device)
+        h = ctypes.c_void_p()
+        rc = self.lib.gpx_svgp_create(self.ctx.handle, self.N, self.M, self.D,
+                                      ctypes.c_void_p(self.X.data_ptr()), ctypes.c_void_p(self.Y.data_ptr()),
+                                      ctypes.byref(self.spec), float(num_data), self.n_total, ctypes.byref(h))
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_svgp_create failed ({rc}): {self.ctx.last_error()}")
+        self.handle = h
+        ptr, ln = ctypes.c_void_p(), ctypes.c_longlong()
+        self.lib.gpx_svgp_partials(h, ctypes.byref(ptr), ctypes.byref(ln))
+        self.partials = torch.zeros(int(ln.value), dtype=torch.float64, device=f"cuda:{self.device}")
+        rc = self.lib.gpx_svgp_bind_partials(h, ctypes.c_void_p(self.partials.data_ptr()), int(ln.value))
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_svgp_bind_partials failed ({rc}): {self.ctx.last_error()}")
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.lib.gpx_svgp_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @staticmethod
+    def _host(a, shape) -> np.ndarray:
+        return np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(shape))
+
+    def _args(self, theta, Z, q_mu, q_sqrt):
+        M, D = self.M, self.D
+        self._keep = (self._host(theta, (N.GPX_THETA_STRIDE,)), self._host(Z, (M, D)),
+                      self._host(q_mu, (M,)), self._host(q_sqrt, (M, M)))
+        dp = ctypes.POINTER(ctypes.c_double)
+        return [a.ctypes.data_as(dp) for a in self._keep]
+
+    def _raise(self, rc, what, info):
+        if rc == N.GPX_NOT_PD:
+            raise N.NotPositiveDefiniteError(
+                f"Cholesky decomposition was not successful (pivot {int(info.value)}): "
+                "Kuu + jitter I is not positive definite", int(info.value))
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"{what} failed ({rc}): {self.ctx.last_error()}")
+
+    def eval_local(self, theta, Z, q_mu, q_sqrt) -> None:
+        info = ctypes.c_int32(0)
+        rc = self.lib.gpx_svgp_eval_local(self.handle, *self._args(theta, Z, q_mu, q_sqrt),
+                                          ctypes.byref(info), self._stream())
+        self._raise(rc, "gpx_svgp_eval_local", info)
+
+    def eval_finish(self):
+        M, D = self.M, self.D
+        elbo = np.zeros(1)
+        gth = np.zeros(N.GPX_THETA_STRIDE)
+        gZ = np.zeros((M, D))
+        gq = np.zeros(M)
+        gR = np.zeros((M, M))
+        dp = ctypes.POINTER(ctypes.c_double)
+        rc = self.lib.gpx_svgp_eval_finish(self.handle, elbo.ctypes.data_as(dp), gth.ctypes.data_as(dp),
+                                           gZ.ctypes.data_as(dp), gq.ctypes.data_as(dp),
+                                           gR.ctypes.data_as(dp), self._stream())
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_svgp_eval_finish failed ({rc}): {self.ctx.last_error()}")
+        return float(elbo[0]), gth, gZ, gq, gR
+
+    def elbo_grad(self, theta, Z, q_mu, q_sqrt):
+        """ELBO and ∂ELBO/∂(θ, Z, q_mu, q_sqrt) (constrained space) on this shard alone."""
+        self.eval_local(theta, Z, q_mu, q_sqrt)
+        return self.eval_finish()
+
+    def predict(self, theta, Z, q_mu, q_sqrt, Xnew, add_noise: bool):
+        x = to_device_f64(Xnew, self.device)
+        x = x.reshape(x.shape[0], -1).contiguous()
+        if x.shape[1] != self.D:
+            raise ValueError(f"Xnew must have {self.D} columns")
+        Mn = x.shape[0]
+        mean = torch.empty(Mn, dtype=torch.float64, device=x.device)
+        var = torch.empty(Mn, dtype=torch.float64, device=x.device)
+        info = ctypes.c_int32(0)
+        rc = self.lib.gpx_svgp_predict(self.handle, *self._args(theta, Z, q_mu, q_sqrt),
+                                       ctypes.c_void_p(x.data_ptr()), Mn, 1 if add_noise else 0,
+                                       ctypes.c_void_p(mean.data_ptr()), ctypes.c_void_p(var.data_ptr()),
+                                       ctypes.byref(info), self._stream())
+        self._raise(rc, "gpx_svgp_predict", info)
+        return mean, var

@@ -201,3 +201,169 @@ def predict_f_batch(models: Sequence[GPR], Xnews: Sequence, add_noise: bool = Fa
         m, v = m.reshape(-1, 1), v.reshape(-1, 1)
         out.append((m.cpu(), v.cpu()) if cpu_out else (m, v))
     return out
+
+
+class SVGP:
+    """gpflow.models.SVGP with a Gaussian likelihood and GPflow's defaults (whiten=True, full
+    q_sqrt, zero mean, one latent GP) — the cells at test_scripts/SVGP.py:461-478 and
+    test_scripts/GPR.py:118-138::
+
+        m = SVGP(kernel=k, likelihood=Gaussian(variance=1e-4), inducing_variable=Z, num_data=N)
+        set_trainable(m.likelihood.variance, False)
+        Scipy().minimize(m.training_loss_closure((X, Y)), m.trainable_variables,
+                         options=dict(maxiter=100))
+        mean, var = m.predict_f(X_test)
+
+    ELBO, gradients and predictions come from libgpx.so (gpx_svgp_*); trainable variables
+    are ordered as tf.Module flattens SVGP: inducing_variable.Z, kernel.*, likelihood.variance,
+    q_mu, q_sqrt (FillTriangular-unconstrained)."""
+
+    def __init__(self, kernel: Kernel, likelihood: Gaussian, inducing_variable, *, mean_function=None,
+                 num_latent_gps: int = 1, q_diag: bool = False, q_mu=None, q_sqrt=None,
+                 whiten: bool = True, num_data: Optional[int] = None, device: Optional[int] = None):
+        from .inducing_variables import InducingPoints
+        from .parameter import ArrayParameter
+        if mean_function is not None:
+            raise NotImplementedError("only the zero mean function (GPflow default) is supported")
+        if num_latent_gps != 1 or q_diag or not whiten:
+            raise NotImplementedError("SVGP supports GPflow's defaults: one latent GP, full q_sqrt, whiten=True")
+        if not isinstance(likelihood, Gaussian):
+            raise NotImplementedError("SVGP supports the Gaussian likelihood")
+        self.kernel = kernel
+        self.likelihood = likelihood
+        self.inducing_variable = (inducing_variable if isinstance(inducing_variable, InducingPoints)
+                                  else InducingPoints(inducing_variable))
+        M = self.inducing_variable.num_inducing
+        self.num_data = num_data
+        self.num_latent_gps = 1
+        self.whiten = True
+        self.q_mu = ArrayParameter(np.zeros((M, 1)) if q_mu is None else np.asarray(q_mu).reshape(M, 1),
+                                   name="q_mu")
+        self.q_sqrt = ArrayParameter(np.eye(M)[None] if q_sqrt is None else q_sqrt,
+                                     transform="triangular", name="q_sqrt")
+        self.device = default_device() if device is None else int(device)
+        self._engines = {}
+
+    # ---------------------------------------------------------------- structure -------
+    @property
+    def parameters(self):
+        return ((self.inducing_variable.Z,) + tuple(self.kernel.parameters)
+                + tuple(self.likelihood.parameters) + (self.q_mu, self.q_sqrt))
+
+    @property
+    def trainable_parameters(self):
+        return tuple(p for p in self.parameters if p.trainable)
+
+    @property
+    def trainable_variables(self):
+        return tuple(p.unconstrained_variable for p in self.trainable_parameters)
+
+    def _param_paths(self):
+        return ([("SVGP.inducing_variable.Z", self.inducing_variable.Z)]
+                + [("SVGP.kernel." + n if n else "SVGP.kernel", p) for n, p in self.kernel._param_paths("")]
+                + [("SVGP.likelihood.variance", self.likelihood.variance),
+                   ("SVGP.q_mu", self.q_mu), ("SVGP.q_sqrt", self.q_sqrt)])
+
+    @property
+    def M(self) -> int:
+        return self.inducing_variable.num_inducing
+
+    def theta_row(self) -> np.ndarray:
+        row = np.ones(N.GPX_THETA_STRIDE, dtype=np.float64)
+        kp = self.kernel.parameters
+        for i, p in enumerate(kp):
+            row[i] = p.value
+        row[len(kp)] = self.likelihood.variance.value
+        return row
+
+    def _state(self):
+        return (self.theta_row(), self.inducing_variable.Z.value, self.q_mu.value.reshape(-1),
+                self.q_sqrt.value[0])
+
+    # ---------------------------------------------------------------- engine ----------
+    def engine(self, data=None) -> "SVGPEngine":
+        from .engine import SVGPEngine
+        if data is None:
+            if self._engines:
+                return next(iter(self._engines.values()))[0]
+            Z = self.inducing_variable.Z.value
+            data = (Z[:1], np.zeros((1, 1)))
+        X, Y = data
+        key = (id(X), id(Y))
+        hit = self._engines.get(key)
+        if hit is None or hit[1] is not X or hit[2] is not Y:
+            Xa = X if isinstance(X, torch.Tensor) else np.asarray(X, dtype=np.float64)
+            n = int(Xa.shape[0])
+            D = 1 if Xa.ndim == 1 else int(Xa.shape[1])
+            eng = SVGPEngine(X, Y, compile_spec(self.kernel, D), self.M,
+                             num_data=float(self.num_data if self.num_data is not None else n),
+                             device=self.device)
+            hit = (eng, X, Y)
+            self._engines = {key: hit}
+        return hit[0]
+
+    # ---------------------------------------------------------------- objective -------
+    def _elbo_and_grads(self, data):
+        eng = self.engine(data)
+        return eng.elbo_grad(*self._state())
+
+    def elbo(self, data) -> torch.Tensor:
+        return torch.tensor(self._elbo_and_grads(data)[0], dtype=torch.float64)
+
+    def maximum_log_likelihood_objective(self, data) -> torch.Tensor:
+        return self.elbo(data)
+
+    def training_loss(self, data) -> torch.Tensor:
+        return -self.elbo(data)
+
+    def training_loss_closure(self, data, compile: bool = True):
+        def closure():
+            return self.training_loss(data)
+        closure._gpx_model = self
+        closure._gpx_loss_and_grad = lambda variables=None: self.loss_and_grad_unconstrained(data, variables)
+        return closure
+
+    def grads_to_unconstrained(self, variables, elbo, gth, gZ, gq, gR):
+        """(−ELBO, ∂(−ELBO)/∂u flattened in ``variables`` order)."""
+        kp = self.kernel.parameters
+        pindex = {id(p): i for i, p in enumerate(kp)}
+        parts = []
+        for v in variables:
+            p = v._param
+            if p is self.inducing_variable.Z:
+                parts.append(-np.asarray(gZ).ravel())
+            elif p is self.likelihood.variance:
+                parts.append(np.array([-gth[len(kp)] * p.dtheta_du()]))
+            elif id(p) in pindex:
+                parts.append(np.array([-gth[pindex[id(p)]] * p.dtheta_du()]))
+            elif p is self.q_mu:
+                parts.append(-np.asarray(gq).ravel())
+            elif p is self.q_sqrt:
+                parts.append(-p.grad_to_unconstrained(gR).ravel())
+            else:
+                raise ValueError(f"variable {v.name} is not a parameter of this model")
+        return -float(elbo), np.concatenate(parts)
+
+    def loss_and_grad_unconstrained(self, data, variables=None):
+        variables = self.trainable_variables if variables is None else variables
+        return self.grads_to_unconstrained(variables, *self._elbo_and_grads(data))
+
+    # ---------------------------------------------------------------- prediction ------
+    def predict_f(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
+        if full_cov or full_output_cov:
+            raise NotImplementedError("SVGP.predict_f supports full_cov=False (marginals)")
+        return self._predict(Xnew, False)
+
+    def predict_y(self, Xnew, full_cov: bool = False, full_output_cov: bool = False):
+        if full_cov or full_output_cov:
+            raise NotImplementedError("The predict_y method currently supports only the argument "
+                                      "values full_cov=False and full_output_cov=False")
+        return self._predict(Xnew, True)
+
+    def _predict(self, Xnew, add_noise: bool):
+        cpu_out = not (isinstance(Xnew, torch.Tensor) and Xnew.is_cuda)
+        m, v = self.engine().predict(*self._state(), Xnew, add_noise)
+        m, v = m.reshape(-1, 1), v.reshape(-1, 1)
+        if cpu_out:
+            m, v = m.cpu(), v.cpu()
+        return m, v

@@ -27,6 +27,8 @@ from .kernels import compile_spec
 
 
 def _resolve_model(closure):
+    if hasattr(closure, "_gpx_loss_and_grad"):  # closures that carry their data (SVGP)
+        return closure
     m = getattr(closure, "_gpx_model", None)
     if m is None:
         m = getattr(closure, "__self__", None)
@@ -42,8 +44,13 @@ def _pack(variables) -> np.ndarray:
 
 
 def _unpack(variables, x) -> None:
-    for v, xi in zip(variables, np.asarray(x, dtype=np.float64)):
-        v.assign(xi)
+    x = np.asarray(x, dtype=np.float64)
+    o = 0
+    for v in variables:
+        shape = tuple(v.shape)
+        n = int(np.prod(shape)) if shape else 1
+        v.assign(x[o] if not shape else x[o:o + n].reshape(shape))
+        o += n
 
 
 class Scipy:
@@ -58,9 +65,11 @@ class Scipy:
         model = _resolve_model(closure)
         history: List[float] = []
 
+        lg = getattr(model, "_gpx_loss_and_grad", None) or model.loss_and_grad_unconstrained
+
         def func(x):
             _unpack(variables, x)
-            loss, g = model.loss_and_grad_unconstrained(variables)
+            loss, g = lg(variables)
             if track_loss_history:
                 history.append(loss)
             return loss, g

@@ -120,3 +120,121 @@ class Parameter:
 
     def __repr__(self) -> str:
         return f"<Parameter {self.name}={self.value!r} trainable={self.trainable}>"
+
+
+# ----------------------------------------------------------------------------------------
+# array-valued parameters (SVGP: inducing inputs Z, q_mu, q_sqrt)
+# ----------------------------------------------------------------------------------------
+def fill_triangular(x: np.ndarray) -> np.ndarray:
+    """tfp.math.fill_triangular(x, upper=False): the vector → lower-triangular layout that
+    tfp.bijectors.FillTriangular (GPflow's ``triangular()`` transform of q_sqrt) uses."""
+    x = np.asarray(x, dtype=np.float64)
+    m = x.shape[-1]
+    n = (math.isqrt(8 * m + 1) - 1) // 2
+    if n * (n + 1) // 2 != m:
+        raise ValueError(f"fill_triangular: {m} is not a triangular number")
+    return np.tril(np.concatenate([x[n:], x[::-1]]).reshape(n, n))
+
+
+def fill_triangular_inverse(L: np.ndarray) -> np.ndarray:
+    """tfp.math.fill_triangular_inverse(L, upper=False)."""
+    L = np.asarray(L, dtype=np.float64)
+    n = L.shape[-1]
+    tri = L[:-1, :]
+    rest = (tri + tri[::-1, ::-1]).reshape(-1)[: n * (n + 1) // 2 - n]
+    return np.concatenate([L[-1, ::-1], rest])
+
+
+class ArrayVariable:
+    """Unconstrained tf.Variable-like handle of an ArrayParameter."""
+
+    def __init__(self, param: "ArrayParameter"):
+        self._param = param
+
+    @property
+    def name(self) -> str:
+        return f"{self._param.name}:0"
+
+    @property
+    def shape(self):
+        return self._param.unconstrained.shape
+
+    @property
+    def dtype(self):
+        return np.float64
+
+    @property
+    def trainable(self) -> bool:
+        return self._param.trainable
+
+    def numpy(self) -> np.ndarray:
+        return self._param.unconstrained.copy()
+
+    def assign(self, u) -> None:
+        self._param.set_unconstrained(np.asarray(u, dtype=np.float64).reshape(self.shape))
+
+
+class ArrayParameter:
+    """A GPflow Parameter holding an array with the identity transform (Z, q_mu) or
+    FillTriangular (q_sqrt: constrained [1, M, M] lower-triangular, unconstrained
+    [1, M(M+1)/2])."""
+
+    def __init__(self, value, transform: str = "identity", trainable: bool = True,
+                 name: str = "parameter"):
+        self.transform = transform
+        self.trainable = bool(trainable)
+        self.name = name
+        self.assign(value)
+        self._variable = ArrayVariable(self)
+
+    @property
+    def value(self) -> np.ndarray:
+        if self.transform == "triangular":
+            return np.stack([fill_triangular(r) for r in self._u])
+        return self._u.copy()
+
+    def numpy(self) -> np.ndarray:
+        return self.value
+
+    def assign(self, value) -> None:
+        v = np.array(value, dtype=np.float64)
+        if self.transform == "triangular":
+            if v.ndim == 2:
+                v = v[None]
+            self._u = np.stack([fill_triangular_inverse(np.tril(r)) for r in v])
+        else:
+            self._u = v
+
+    @property
+    def shape(self):
+        return self.value.shape
+
+    @property
+    def unconstrained(self) -> np.ndarray:
+        return self._u
+
+    def set_unconstrained(self, u) -> None:
+        self._u = np.array(u, dtype=np.float64).reshape(self._u.shape)
+
+    @property
+    def unconstrained_variable(self) -> ArrayVariable:
+        return self._variable
+
+    def grad_to_unconstrained(self, g: np.ndarray) -> np.ndarray:
+        """Chain rule for the transform: ∂/∂u from ∂/∂value (same layout as ``unconstrained``)."""
+        if self.transform == "triangular":
+            g = np.asarray(g, dtype=np.float64)
+            if g.ndim == 2:
+                g = g[None]
+            return np.stack([fill_triangular_inverse(np.tril(r)) for r in g])
+        return np.asarray(g, dtype=np.float64).reshape(self._u.shape)
+
+    @property
+    def transform_name(self) -> str:
+        return "FillTriangular" if self.transform == "triangular" else "Identity"
+
+    def __array__(self, dtype=None, copy=None):
+        return np.asarray(self.value, dtype=dtype or np.float64)
+
+    def __repr__(self) -> str:
+        return f"<ArrayParameter {self.name} shape={self.shape} trainable={self.trainable}>"

@@ -2,12 +2,14 @@
 (GPR/model_trainer.py:2,17; GPR/main.py:40-44)."""
 from __future__ import annotations
 
-from .parameter import Parameter
+import numpy as np
+
+from .parameter import ArrayParameter, Parameter
 
 
 def set_trainable(obj, flag: bool) -> None:
     """Set ``trainable`` on a Parameter or on every Parameter of a kernel/likelihood/model."""
-    if isinstance(obj, Parameter):
+    if isinstance(obj, (Parameter, ArrayParameter)):
         obj.trainable = bool(flag)
         return
     params = getattr(obj, "parameters", None)
@@ -22,7 +24,12 @@ def summary_rows(model):
     paths = model._param_paths() if hasattr(model, "_param_paths") else [
         (n, p) for n, p in model._param_paths("")]
     for name, p in paths:
-        rows.append((name, "Parameter", p.transform_name, p.trainable, "()", "float64", p.value))
+        if isinstance(p, ArrayParameter):
+            v = p.value
+            rows.append((name, "Parameter", p.transform_name, p.trainable, str(tuple(v.shape)), "float64",
+                         np.array2string(v.ravel()[:3], precision=4) + ("..." if v.size > 3 else "")))
+        else:
+            rows.append((name, "Parameter", p.transform_name, p.trainable, "()", "float64", p.value))
     return rows
 
 

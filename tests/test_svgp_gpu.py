@@ -1,0 +1,160 @@
+"""SVGP on the GPU (libgpx.so gpx_svgp_*) against the SVGP oracle (oracle/svgp_oracle.py).
+
+Tolerances (fp64; the north-star bar is 1e-5 relative on ELBO / posterior moments):
+  ELBO          |Δ| <= 1e-9 · |ref|        (1e-7 on the ill-conditioned Kuu case)
+  gradients     |Δ| <= 1e-7 · (1 + max|g_ref|) per block (Z, θ, q_mu, q_sqrt); 1e-5 on the
+                ill-conditioned case (cond(Kuu + 1e-6 I) ~ 1e8 amplifies rounding in ANY
+                implementation: the oracle's L⁻¹ route and the device's W-route differ there)
+  predictions   |Δ| <= 1e-7 · max|ref| (+1e-10)
+"""
+import numpy as np
+import pytest
+import scipy.optimize
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import portfoliooptgp_amd as gpx  # noqa: E402
+from portfoliooptgp_amd.engine import SVGPEngine  # noqa: E402
+from portfoliooptgp_amd.kernels import compile_spec  # noqa: E402
+from oracle import gp_oracle as O  # noqa: E402
+from oracle import svgp_oracle as S  # noqa: E402
+from tests.test_gpu_parity import gpx_kernel, oracle_kernel  # noqa: E402
+
+
+def _case(n, M, D, fam, seed, zgrid=False, ell=None):
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(0, 10, (n, D))
+    Y = np.sin(X[:, :1]) + 0.3 * np.cos(2 * X[:, -1:]) + 0.05 * rng.standard_normal((n, 1))
+    Z = np.linspace(0, 10, M)[:, None].repeat(D, 1) if zgrid else rng.uniform(0, 10, (M, D))
+    R = np.tril(rng.standard_normal((M, M)) * 0.05)
+    R[np.diag_indices(M)] = rng.uniform(0.3, 1.0, M)
+    q = rng.standard_normal(M) * 0.5
+    gk, ok = gpx_kernel(fam), oracle_kernel(fam)
+    if ell is not None:
+        gk.lengthscales.assign(ell)
+        ok.lengthscales.value = ell
+    return X, Y, Z, q, R, gk, ok
+
+
+def _device_eval(X, Y, Z, q, R, gk, noise, num_data):
+    m = gpx.models.SVGP(kernel=gk, likelihood=gpx.likelihoods.Gaussian(variance=noise),
+                        inducing_variable=Z, num_data=num_data, q_mu=q, q_sqrt=R[None])
+    return m, m._elbo_and_grads((X, Y))
+
+
+def _check(got, ref, tol_rel):
+    elbo, gth, gZ, gq, gR = got
+    relbo, rg = ref
+    assert abs(elbo - relbo) <= tol_rel[0] * abs(relbo), (elbo, relbo)
+    np_ = len(rg["theta"])
+    for name, a, b in (("theta", gth[:np_], rg["theta"]), ("noise", gth[np_], rg["noise"]),
+                       ("Z", gZ, rg["Z"]), ("q_mu", gq, rg["q_mu"]), ("q_sqrt", gR, rg["q_sqrt"])):
+        a, b = np.asarray(a), np.asarray(b)
+        err = np.abs(a - b).max()
+        assert err <= tol_rel[1] * (1.0 + np.abs(b).max()), (name, err, np.abs(b).max())
+
+
+@pytest.mark.parametrize("n,M,D,fam,seed", [
+    (300, 20, 1, "se", 0),
+    (257, 13, 1, "exp+per+lin", 1),
+    (200, 70, 2, "se*m12", 2),
+    (1500, 100, 3, "m52", 3),
+    (999, 64, 1, "rq", 4),
+    (130, 1, 1, "m32", 5),
+])
+def test_elbo_and_gradients_vs_oracle(n, M, D, fam, seed):
+    X, Y, Z, q, R, gk, ok = _case(n, M, D, fam, seed)
+    _, got = _device_eval(X, Y, Z, q, R, gk, 0.05, n)
+    om = S.OSVGP(ok, Z, num_data=n, noise_variance=0.05, q_mu=q, q_sqrt=R)
+    _check(got, om.elbo_and_grads(X, Y), (1e-9, 1e-7))
+
+
+def test_minibatch_scale_and_ill_conditioned_grid():
+    """num_data ≠ N (GPflow's minibatch scaling) and the reference's inducing layout
+    (np.linspace grid, test_scripts/SVGP.py:464) with a long lengthscale: Kuu is near-singular."""
+    X, Y, Z, q, R, gk, ok = _case(2000, 120, 1, "se", 6, zgrid=True, ell=3.0)
+    _, got = _device_eval(X, Y, Z, q, R, gk, 1e-2, 50000)
+    om = S.OSVGP(ok, Z, num_data=50000, noise_variance=1e-2, q_mu=q, q_sqrt=R)
+    _check(got, om.elbo_and_grads(X, Y), (1e-7, 1e-5))
+
+
+def test_predict_f_and_predict_y():
+    X, Y, Z, q, R, gk, ok = _case(400, 90, 2, "m32", 7)
+    m = gpx.models.SVGP(kernel=gk, likelihood=gpx.likelihoods.Gaussian(variance=1e-3),
+                        inducing_variable=Z, num_data=400, q_mu=q, q_sqrt=R[None])
+    om = S.OSVGP(ok, Z, num_data=400, noise_variance=1e-3, q_mu=q, q_sqrt=R)
+    xs = np.random.default_rng(8).uniform(-1, 11, (333, 2))
+    mu, var = m.predict_f(xs)
+    mo, vo = om.predict_f(xs)
+    assert np.abs(mu.numpy() - mo).max() <= 1e-7 * np.abs(mo).max() + 1e-10
+    assert np.abs(var.numpy() - vo).max() <= 1e-7 * np.abs(vo).max() + 1e-10
+    _, vy = m.predict_y(xs)
+    np.testing.assert_allclose(vy.numpy() - var.numpy(), 1e-3, rtol=1e-9)
+
+
+def test_sharded_partials_equal_single_shard():
+    """Two shards' partial buffers summed (what the all-reduce does) then finished equal the
+    unsharded evaluation — the multi-GPU decomposition, on one device."""
+    X, Y, Z, q, R, gk, _ = _case(3001, 77, 1, "se", 9)
+    spec = compile_spec(gk, 1)
+    theta = np.ones(16)
+    theta[:2] = [p.value for p in gk.parameters]
+    theta[2] = 0.02
+    full = SVGPEngine(X, Y, spec, 77, num_data=3001).elbo_grad(theta, Z, q, R)
+    a = SVGPEngine(X[:1400], Y[:1400], spec, 77, num_data=3001, n_total=3001)
+    b = SVGPEngine(X[1400:], Y[1400:], spec, 77, num_data=3001, n_total=3001)
+    a.eval_local(theta, Z, q, R)
+    b.eval_local(theta, Z, q, R)
+    a.partials += b.partials
+    got = a.eval_finish()
+    assert got[0] == pytest.approx(full[0], rel=1e-12)
+    for x, y in zip(got[1:], full[1:]):
+        np.testing.assert_allclose(x, y, rtol=1e-9, atol=1e-9 * (1 + np.abs(y).max()))
+
+
+def test_scipy_fit_tracks_oracle_fit():
+    """The reference protocol (likelihood variance frozen, Scipy L-BFGS-B) for a few
+    iterations: the device-driven fit follows the oracle-driven one."""
+    X, Y, Z, q, R, gk, ok = _case(500, 15, 1, "se", 10)
+    m = gpx.models.SVGP(kernel=gk, likelihood=gpx.likelihoods.Gaussian(variance=1e-2),
+                        inducing_variable=Z, num_data=500)
+    gpx.set_trainable(m.likelihood.variance, False)
+    res = gpx.optimizers.Scipy().minimize(m.training_loss_closure((X, Y)), m.trainable_variables,
+                                          options=dict(maxiter=8))
+    om = S.OSVGP(ok, Z, num_data=500, noise_variance=1e-2)
+    om.noise.trainable = False
+
+    def f(u):
+        om.set_u(u)
+        return om.loss_and_grad_u(X, Y)
+
+    ref = scipy.optimize.minimize(f, om.get_u(), jac=True, method="L-BFGS-B", options=dict(maxiter=8))
+    assert res.nit == ref.nit
+    assert res.fun == pytest.approx(ref.fun, rel=1e-7)
+
+
+def test_c5_size_known_answer_and_oracle_elbo():
+    """BASELINE config C5 shape (N=65536, M=1024, inducing grid as test_scripts/SVGP.py:464):
+    (1) at GPflow's initial q = N(0, I) the ELBO has a closed form (μ=0, v=k_nn, KL=0);
+    (2) at a random q the ELBO matches the oracle's forward pass at full size."""
+    n, M = 65536, 1024
+    rng = np.random.default_rng(11)
+    X = np.sort(rng.uniform(0, 360, (n, 1)), axis=0)
+    Y = np.sin(X / 20.0) + 0.1 * rng.standard_normal((n, 1))
+    Z = np.linspace(0, 360, M)[:, None]
+    k = gpx.kernels.SquaredExponential(lengthscales=2.0, variance=1.0)
+    m = gpx.models.SVGP(kernel=k, likelihood=gpx.likelihoods.Gaussian(variance=1e-4),
+                        inducing_variable=Z, num_data=n)
+    elbo0 = float(m.elbo((X, Y)))
+    want = np.sum(-0.5 * np.log(2 * np.pi * 1e-4) - 0.5 * (Y[:, 0] ** 2 + 1.0) / 1e-4)
+    assert elbo0 == pytest.approx(want, rel=1e-12)
+    q = rng.standard_normal(M) * 0.3
+    R = np.tril(rng.standard_normal((M, M)) * 1e-3)
+    R[np.diag_indices(M)] = rng.uniform(0.05, 0.2, M)
+    m.q_mu.assign(q[:, None])
+    m.q_sqrt.assign(R[None])
+    elbo = float(m.elbo((X, Y)))
+    om = S.OSVGP(O.OSquaredExponential(lengthscales=2.0, variance=1.0), Z, num_data=n,
+                 noise_variance=1e-4, q_mu=q, q_sqrt=R)
+    assert elbo == pytest.approx(om.elbo(X, Y), rel=1e-7)
