@@ -108,9 +108,10 @@ def test_sharded_partials_equal_single_shard():
     b.eval_local(theta, Z, q, R)
     a.partials += b.partials
     got = a.eval_finish()
-    assert got[0] == pytest.approx(full[0], rel=1e-12)
+    # equal up to summation order (the G and k_nn sums are split differently)
+    assert got[0] == pytest.approx(full[0], rel=1e-9)
     for x, y in zip(got[1:], full[1:]):
-        np.testing.assert_allclose(x, y, rtol=1e-9, atol=1e-9 * (1 + np.abs(y).max()))
+        np.testing.assert_allclose(x, y, rtol=1e-8, atol=1e-8 * (1 + np.abs(y).max()))
 
 
 def test_scipy_fit_tracks_oracle_fit():
