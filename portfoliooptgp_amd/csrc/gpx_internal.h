@@ -151,7 +151,7 @@ struct SvgpPredVarArgs {
   double* var;
 };
 
-void launch_rows(const RowsArgs& a, hipStream_t s);
+void launch_rows(const RowsArgs& a, bool single_term, hipStream_t s);
 int rows_chunk_for(int D);              // column chunk for RowsArgs.chunk
 int rows_blocks(const RowsArgs& a);     // number of part_theta rows written
 int rows_chunks(const RowsArgs& a);     // number of part_z / part_w chunks written

@@ -52,7 +52,9 @@ struct gpx_svgp {
   double *Kms = nullptr, *V = nullptr, *pA = nullptr, *pB = nullptr;
   size_t kms_cap = 0, pa_cap = 0, pb_cap = 0;
   // host staging
-  std::vector<double> h_q, h_R, h_pad, h_part_small, h_fin, h_ahat, h_Rbar;
+  std::vector<double> h_q, h_part_small, h_fin, h_ahat;
+  double* h_R = nullptr;     // pinned [Mp][Mp] q_sqrt staging (upper part stays zero)
+  double* h_Rbar = nullptr;  // pinned [Mp][Mp] ∂ELBO/∂q_sqrt staging
   std::vector<double> h_theta;
   double h_nloc = 0.0;
   int h_info = 0;
@@ -75,7 +77,7 @@ void sum_into(const double* src, long long stride, int nb, long long width, doub
   launch_sum(a, s);
 }
 
-// theta check + uploads shared by the ELBO and predict paths; leaves W (kmm->W) and u = Wᵀ q.
+// theta check + uploads shared by the ELBO and predict paths (all on stream s).
 int prelude(gpx_svgp* sv, const double* theta, const double* Z, const double* q_mu,
             const double* q_sqrt, hipStream_t s) {
   gpx_ctx* ctx = sv->ctx;
@@ -97,19 +99,24 @@ int prelude(gpx_svgp* sv, const double* theta, const double* Z, const double* q_
   HIPX(ctx, hipMemcpyAsync(sv->dZ, Z, sizeof(double) * M * sv->D, hipMemcpyHostToDevice, s));
   sv->h_q.assign(Mp, 0.0);
   std::memcpy(sv->h_q.data(), q_mu, sizeof(double) * M);
-  sv->h_R.assign((size_t)Mp * Mp, 0.0);
   for (int i = 0; i < M; ++i)
     std::memcpy(&sv->h_R[(size_t)i * Mp], q_sqrt + (size_t)i * M, sizeof(double) * (i + 1));
   HIPX(ctx, hipMemcpyAsync(sv->dq, sv->h_q.data(), sizeof(double) * Mp, hipMemcpyHostToDevice, s));
-  HIPX(ctx, hipMemcpyAsync(sv->dR, sv->h_R.data(), sizeof(double) * Mp * Mp, hipMemcpyHostToDevice, s));
+  HIPX(ctx, hipMemcpyAsync(sv->dR, sv->h_R, sizeof(double) * Mp * Mp, hipMemcpyHostToDevice, s));
+  return GPX_OK;
+}
+
+// Kmm = k(Z,Z) + jitter I -> W = L⁻¹ (recursive Cholesky-and-inverse), u = Wᵀ q_mu.
+void factor_u(gpx_svgp* sv, hipStream_t s) {
   const Run r{sv->kmm, sv->kmm->d_active, 1, s};
   factor(r);
   TrmvArgs t{};
-  t.active = sv->kmm->d_active; t.Wm = sv->kmm->W; t.sW = 0; t.ld = Mp; t.x = sv->dq; t.sx = 0;
-  t.nvalid = nullptr; t.y = sv->u; t.sy = 0; t.rows = t.cols = Mp; t.lower = 1;
+  t.active = sv->kmm->d_active; t.Wm = sv->kmm->W; t.sW = 0; t.ld = sv->Mp; t.x = sv->dq; t.sx = 0;
+  t.nvalid = nullptr; t.y = sv->u; t.sy = 0; t.rows = t.cols = sv->Mp; t.lower = 1;
   launch_trmv_t(t, 1, s);
-  return GPX_OK;
 }
+
+bool single_term(const gpx_svgp* sv) { return sv->spec.n_terms == 1; }
 
 int check_info(gpx_svgp* sv, int32_t* info, hipStream_t s) {
   gpx_ctx* ctx = sv->ctx;
@@ -175,6 +182,10 @@ int gpx_svgp_create(gpx_ctx* ctx, int N, int M, int D, const double* X, const do
   for (double** p : vecs)
     if (hipMalloc(p, sizeof(double) * Mp) != hipSuccess || hipMemset(*p, 0, sizeof(double) * Mp) != hipSuccess)
       return bail("out of device memory for M vectors");
+  if (hipHostMalloc(&sv->h_R, sizeof(double) * mm) != hipSuccess ||
+      hipHostMalloc(&sv->h_Rbar, sizeof(double) * mm) != hipSuccess)
+    return bail("out of pinned host memory");
+  std::memset(sv->h_R, 0, sizeof(double) * mm);
   const size_t mn = (size_t)Mp * sv->Ncols;
   if (hipMalloc(&sv->Kmn, sizeof(double) * mn) != hipSuccess ||
       hipMalloc(&sv->Ybuf, sizeof(double) * mn) != hipSuccess ||
@@ -205,6 +216,8 @@ int gpx_svgp_destroy(gpx_svgp* sv) {
   if (!sv) return GPX_BAD_ARG;
   (void)hipSetDevice(sv->ctx->device);
   if (sv->kmm) gpx_batch_destroy(sv->kmm);
+  if (sv->h_R) (void)hipHostFree(sv->h_R);
+  if (sv->h_Rbar) (void)hipHostFree(sv->h_Rbar);
   for (void* p : {(void*)sv->dZ, (void*)sv->dYdummy, (void*)sv->d_theta, (void*)sv->dq, (void*)sv->dR,
                   (void*)sv->u, (void*)sv->mu, (void*)sv->g, (void*)sv->Sm1, (void*)sv->T, (void*)sv->P,
                   (void*)sv->Gh, (void*)sv->X1, (void*)sv->GR, (void*)sv->Phi, (void*)sv->Sb,
@@ -249,14 +262,9 @@ int gpx_svgp_eval_local(gpx_svgp* sv, const double* theta, const double* Z, cons
   const double c2 = -scale / s2;  // 2c
   const Run r{sv->kmm, sv->kmm->d_active, 1, s};
   double* W = sv->kmm->W;
-  // S − I = q_sqrt q_sqrtᵀ − I;  P = Wᵀ (S − I) W
-  gemm(r, gemm_args(sv->dR, Mp, sv->dR, Mp, sv->Sm1, Mp, 0, Mp, Mp, Mp, TRI_KMAX_I | TRI_KMAX_J, 0,
-                    1.0, 0.0), EPI_STORE, false, true);
-  launch_diag_add(sv->Sm1, Mp, M, -1.0, s);
-  gemm(r, gemm_args(sv->Sm1, Mp, W, Mp, sv->T, Mp, 0, Mp, Mp, Mp, TRI_KMIN_J, 0, 1.0, 0.0), EPI_STORE,
-       false, false);
-  gemm(r, gemm_args(W, Mp, sv->T, Mp, sv->P, Mp, 0, Mp, Mp, Mp, TRI_KMIN_I, 0, 1.0, 0.0), EPI_STORE,
-       true, false);
+  hipStream_t sa = ctx->aux[0];
+  hipEvent_t e_up = ctx->ev[kEvents - 2], e_m = ctx->ev[kEvents - 1];
+  HIPX(ctx, hipEventRecord(e_up, s));
   // Kmn = k(Z, X) (rows ≥ M and columns ≥ N are zero)
   BuildArgs ba{};
   ba.active = sv->kmm->d_active; ba.specs = sv->kmm->d_specs; ba.theta = sv->d_theta;
@@ -264,6 +272,32 @@ int gpx_svgp_eval_local(gpx_svgp* sv, const double* theta, const double* Z, cons
   ba.m2 = sv->N; ba.out = sv->Kmn; ba.sOut = 0; ba.ldo = Nc; ba.rows = Mp; ba.cols = Nc;
   ba.symmetric = 0; ba.rows_valid = 0;
   launch_build(ba, 1, s);
+  // G = Kmn Kmnᵀ (lower), split-K over nc column chunks, then summed
+  {
+    const Run rk{sv->kmm, sv->d_iota, sv->nc, s};
+    GemmArgs gg = gemm_args(sv->Kmn, Nc, sv->Kmn, Nc, sv->Gpart, Mp, 0, Mp, Mp, sv->chunkK, 0, 1, 1.0, 0.0);
+    gg.sA = sv->chunkK; gg.sB = sv->chunkK; gg.sC = (long long)Mp * Mp;
+    gemm(rk, gg, EPI_STORE, false, true);
+    sum_into(sv->Gpart, (long long)Mp * Mp, sv->nc, (long long)Mp * Mp, sv->part + sv->off_G, 0, s);
+  }
+  // The M×M chain (latency-bound recursive factorisation, then S − I and P) runs on an
+  // auxiliary stream while the main stream builds Kmn and runs the split-K SYRK for G
+  // (enqueued first, so the chain's many small launches do not delay the big ones).
+  HIPX(ctx, hipStreamWaitEvent(sa, e_up, 0));
+  {
+    const Run ra{sv->kmm, sv->kmm->d_active, 1, sa};
+    factor_u(sv, sa);
+    // S − I = q_sqrt q_sqrtᵀ − I;  P = Wᵀ (S − I) W
+    gemm(ra, gemm_args(sv->dR, Mp, sv->dR, Mp, sv->Sm1, Mp, 0, Mp, Mp, Mp, TRI_KMAX_I | TRI_KMAX_J, 0,
+                       1.0, 0.0), EPI_STORE, false, true);
+    launch_diag_add(sv->Sm1, Mp, M, -1.0, sa);
+    gemm(ra, gemm_args(sv->Sm1, Mp, W, Mp, sv->T, Mp, 0, Mp, Mp, Mp, TRI_KMIN_J, 0, 1.0, 0.0), EPI_STORE,
+         false, false);
+    gemm(ra, gemm_args(W, Mp, sv->T, Mp, sv->P, Mp, 0, Mp, Mp, Mp, TRI_KMIN_I, 0, 1.0, 0.0), EPI_STORE,
+         true, false);
+    HIPX(ctx, hipEventRecord(e_m, sa));
+  }
+  HIPX(ctx, hipStreamWaitEvent(s, e_m, 0));
   // μ = Kmnᵀ u
   TrmvArgs t{};
   t.active = sv->kmm->d_active; t.Wm = sv->Kmn; t.sW = 0; t.ld = Nc; t.x = sv->u; t.sx = 0;
@@ -278,14 +312,6 @@ int gpx_svgp_eval_local(gpx_svgp* sv, const double* theta, const double* Z, cons
   sum_into(sv->pres, kResidW, nrb, GPX_THETA_STRIDE, sv->part + sv->off_th, 0, s);
   sum_into(sv->pres + 16, kResidW, nrb, 2, sv->part + sv->off_sc, 0, s);
   HIPX(ctx, hipMemcpyAsync(sv->part + sv->off_sc + 2, &sv->h_nloc, sizeof(double), hipMemcpyHostToDevice, s));
-  // G = Kmn Kmnᵀ (lower), split-K over nc column chunks, then summed
-  {
-    const Run rk{sv->kmm, sv->d_iota, sv->nc, s};
-    GemmArgs gg = gemm_args(sv->Kmn, Nc, sv->Kmn, Nc, sv->Gpart, Mp, 0, Mp, Mp, sv->chunkK, 0, 1, 1.0, 0.0);
-    gg.sA = sv->chunkK; gg.sB = sv->chunkK; gg.sC = (long long)Mp * Mp;
-    gemm(rk, gg, EPI_STORE, false, true);
-    sum_into(sv->Gpart, (long long)Mp * Mp, sv->nc, (long long)Mp * Mp, sv->part + sv->off_G, 0, s);
-  }
   // Y = 2c P Kmn
   gemm(r, gemm_args(sv->P, Mp, sv->Kmn, Nc, sv->Ybuf, Nc, 0, Mp, Nc, Mp, 0, 0, c2, 0.0), EPI_STORE,
        false, false);
@@ -299,7 +325,7 @@ int gpx_svgp_eval_local(gpx_svgp* sv, const double* theta, const double* Z, cons
   ro.part_theta = sv->pth; ro.part_z = sv->pz; ro.part_w = sv->pw;
   HIPX(ctx, hipMemsetAsync(sv->pz, 0, sizeof(double) * rows_chunks(ro) * Mp * D, s));
   HIPX(ctx, hipMemsetAsync(sv->pw, 0, sizeof(double) * rows_chunks(ro) * Mp, s));
-  launch_rows(ro, s);
+  launch_rows(ro, single_term(sv), s);
   sum_into(sv->pth, GPX_THETA_STRIDE, rows_blocks(ro), GPX_THETA_STRIDE, sv->part + sv->off_th, 1, s);
   sum_into(sv->pz, (long long)Mp * D, rows_chunks(ro), (long long)Mp * D, sv->part + sv->off_z, 0, s);
   sum_into(sv->pw, Mp, rows_chunks(ro), Mp, sv->part + sv->off_w, 0, s);
@@ -355,7 +381,7 @@ int gpx_svgp_eval_finish(gpx_svgp* sv, double* elbo, double* grad_theta, double*
   if (rc != GPX_OK) return rc;
   ro.part_theta = sv->pth; ro.part_z = sv->pz; ro.part_w = nullptr;
   HIPX(ctx, hipMemsetAsync(sv->pz, 0, sizeof(double) * rows_chunks(ro) * Mp * D, s));
-  launch_rows(ro, s);
+  launch_rows(ro, single_term(sv), s);
   sum_into(sv->pth, GPX_THETA_STRIDE, rows_blocks(ro), GPX_THETA_STRIDE, sv->fin, 0, s);
   sum_into(sv->pz, (long long)Mp * D, rows_chunks(ro), (long long)Mp * D, sv->fin + GPX_THETA_STRIDE, 0, s);
   sum_into(sv->ptr, 1, svgp_final_blocks(M), 1, sv->fin + GPX_THETA_STRIDE + (long long)Mp * D, 0, s);
@@ -369,8 +395,7 @@ int gpx_svgp_eval_finish(gpx_svgp* sv, double* elbo, double* grad_theta, double*
   HIPX(ctx, hipMemcpyAsync(sv->h_fin.data(), sv->fin, sizeof(double) * sv->h_fin.size(), hipMemcpyDeviceToHost, s));
   sv->h_ahat.resize(Mp);
   HIPX(ctx, hipMemcpyAsync(sv->h_ahat.data(), sv->ahat, sizeof(double) * Mp, hipMemcpyDeviceToHost, s));
-  sv->h_Rbar.resize((size_t)Mp * Mp);
-  HIPX(ctx, hipMemcpyAsync(sv->h_Rbar.data(), sv->Rbar, sizeof(double) * Mp * Mp, hipMemcpyDeviceToHost, s));
+  HIPX(ctx, hipMemcpyAsync(sv->h_Rbar, sv->Rbar, sizeof(double) * Mp * Mp, hipMemcpyDeviceToHost, s));
   HIPX(ctx, hipStreamSynchronize(s));
   const double* pth = sv->h_part_small.data();
   const double* pz = pth + GPX_THETA_STRIDE;
@@ -425,6 +450,7 @@ int gpx_svgp_predict(gpx_svgp* sv, const double* theta, const double* Z, const d
   sv->local_done = false;
   int rc = prelude(sv, theta, Z, q_mu, q_sqrt, s);
   if (rc != GPX_OK) return rc;
+  factor_u(sv, s);
   const int Mp = sv->Mp, D = sv->D;
   const int Mnp = (Mn + 63) / 64 * 64;
   const Run r{sv->kmm, sv->kmm->d_active, 1, s};

@@ -30,14 +30,14 @@ __device__ int theta_slot(const DevSpec* gs, int p) {
 }
 
 // Block reduction of the per-lane sums[4][3] into out[16] (θ layout).
-__device__ void reduce_theta(double (&sums)[GPX_MAX_TERMS][3], const DevSpec* gs, double* sred,
-                             double* out) {
+template <int NT>
+__device__ void reduce_theta(double (&sums)[NT][3], const DevSpec* gs, double* sred, double* out) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int t = 0; t < GPX_MAX_TERMS; ++t)
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const double v = wsum(sums[t][q]);
+      const double v = t < NT ? wsum(sums[t < NT ? t : 0][q]) : 0.0;
       if (lane == 0) sred[wave * 16 + t * 3 + q] = v;
     }
   __syncthreads();
@@ -47,7 +47,7 @@ __device__ void reduce_theta(double (&sums)[GPX_MAX_TERMS][3], const DevSpec* gs
   }
 }
 
-template <int DM>
+template <int DM, int NT>
 __global__ __launch_bounds__(256) void rows_kernel(RowsArgs a) {
   __shared__ double sx[kRowsLds];
   __shared__ double sz[kRowsPerBlock * GPX_MAX_DIM];
@@ -66,9 +66,9 @@ __global__ __launch_bounds__(256) void rows_kernel(RowsArgs a) {
   if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[tid];
   __syncthreads();
   const DevSpec spec = *a.spec;
-  double sums[GPX_MAX_TERMS][3];
+  double sums[NT][3];
 #pragma unroll
-  for (int t = 0; t < GPX_MAX_TERMS; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
+  for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
   for (int rr = 0; rr < 4; ++rr) {
     const int il = wave * 4 + rr;
     const int i = r0 + il;
@@ -87,10 +87,10 @@ __global__ __launch_bounds__(256) void rows_kernel(RowsArgs a) {
         const double y = a.Y[(long long)i * a.ldy + j];
         kb += a.sym ? 0.5 * (y + a.Y[(long long)j * a.ldy + i]) : y;
       }
-      double dk[GPX_MAX_TERMS][3];
-      const double kv = eval_k_grad<GPX_MAX_TERMS>(spec, sth, zi, xj, dk);
+      double dk[NT][3];
+      const double kv = eval_k_grad<NT>(spec, sth, zi, xj, dk);
 #pragma unroll
-      for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+      for (int t = 0; t < NT; ++t) {
         sums[t][0] = fma(kb, dk[t][0], sums[t][0]);
         sums[t][1] = fma(kb, dk[t][1], sums[t][1]);
         sums[t][2] = fma(kb, dk[t][2], sums[t][2]);
@@ -162,12 +162,37 @@ __global__ __launch_bounds__(256) void resid_kernel(ResidArgs a) {
   if (tid == 0) { out[16] = s_sq; out[17] = s_kd; out[18] = 0.0; out[19] = 0.0; }
 }
 
+// wide outputs: one thread per column, the nb rows unrolled by 4 (independent loads in flight)
 __global__ __launch_bounds__(256) void sum_kernel(SumArgs a) {
   const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
   if (c >= a.width) return;
-  double s = 0.0;
-  for (int b = 0; b < a.nb; ++b) s += a.src[(long long)b * a.stride + c];
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int b = 0;
+  for (; b + 4 <= a.nb; b += 4) {
+    s0 += a.src[(long long)b * a.stride + c];
+    s1 += a.src[(long long)(b + 1) * a.stride + c];
+    s2 += a.src[(long long)(b + 2) * a.stride + c];
+    s3 += a.src[(long long)(b + 3) * a.stride + c];
+  }
+  for (; b < a.nb; ++b) s0 += a.src[(long long)b * a.stride + c];
+  const double s = (s0 + s1) + (s2 + s3);
   a.dst[c] = a.accumulate ? a.dst[c] + s : s;
+}
+
+// narrow outputs over many rows (θ partials of thousands of blocks): one block per column,
+// the rows strided over the block, fixed-order tree reduction
+__global__ __launch_bounds__(256) void sum_narrow_kernel(SumArgs a) {
+  __shared__ double sred[4];
+  const long long c = blockIdx.x;
+  double s = 0.0;
+  for (int b = threadIdx.x; b < a.nb; b += 256) s += a.src[(long long)b * a.stride + c];
+  s = wsum(s);
+  if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double t = (sred[0] + sred[1]) + (sred[2] + sred[3]);
+    a.dst[c] = a.accumulate ? a.dst[c] + t : t;
+  }
 }
 
 __global__ __launch_bounds__(256) void svgp_final_kernel(SvgpFinalArgs a) {
@@ -236,13 +261,21 @@ int rows_blocks(const RowsArgs& a) {
 
 int rows_chunks(const RowsArgs& a) { return (a.ncols + a.chunk - 1) / a.chunk; }
 
-void launch_rows(const RowsArgs& a, hipStream_t s) {
+template <int NT>
+static void launch_rows_nt(const RowsArgs& a, hipStream_t s) {
   dim3 grid((a.nrows + kRowsPerBlock - 1) / kRowsPerBlock, rows_chunks(a));
-  if (a.D <= 1) hipLaunchKernelGGL(rows_kernel<1>, grid, dim3(256), 0, s, a);
-  else if (a.D <= 2) hipLaunchKernelGGL(rows_kernel<2>, grid, dim3(256), 0, s, a);
-  else if (a.D <= 4) hipLaunchKernelGGL(rows_kernel<4>, grid, dim3(256), 0, s, a);
-  else if (a.D <= 8) hipLaunchKernelGGL(rows_kernel<8>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(rows_kernel<16>, grid, dim3(256), 0, s, a);
+  if (a.D <= 1) hipLaunchKernelGGL((rows_kernel<1, NT>), grid, dim3(256), 0, s, a);
+  else if (a.D <= 2) hipLaunchKernelGGL((rows_kernel<2, NT>), grid, dim3(256), 0, s, a);
+  else if (a.D <= 4) hipLaunchKernelGGL((rows_kernel<4, NT>), grid, dim3(256), 0, s, a);
+  else if (a.D <= 8) hipLaunchKernelGGL((rows_kernel<8, NT>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((rows_kernel<16, NT>), grid, dim3(256), 0, s, a);
+}
+
+// single-term kernels (the common case) use the 1-term derivative path: a quarter of the
+// derivative registers
+void launch_rows(const RowsArgs& a, bool single_term, hipStream_t s) {
+  if (single_term) launch_rows_nt<1>(a, s);
+  else launch_rows_nt<GPX_MAX_TERMS>(a, s);
 }
 
 int resid_blocks(int npad) { return (npad + 255) / 256; }
@@ -252,7 +285,10 @@ void launch_resid(const ResidArgs& a, hipStream_t s) {
 }
 
 void launch_sum(const SumArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(sum_kernel, dim3((unsigned)((a.width + 255) / 256)), dim3(256), 0, s, a);
+  if (a.width <= 64 && a.nb > 64)
+    hipLaunchKernelGGL(sum_narrow_kernel, dim3((unsigned)a.width), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(sum_kernel, dim3((unsigned)((a.width + 255) / 256)), dim3(256), 0, s, a);
 }
 
 int svgp_final_blocks(int m) { return (int)(((long long)m * m + 255) / 256); }
