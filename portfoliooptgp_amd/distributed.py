@@ -134,3 +134,51 @@ def gpu_fit_shard(series, horizons, width: int = 32, maxiter: int = 100):
                         theta=[p.value for p in m.kernel.parameters],
                         mean=np.asarray(mean).reshape(-1), var=np.asarray(var).reshape(-1)))
     return out
+
+
+# ----------------------------------------------------------------------------------------
+# SVGP over N shards (BASELINE config C5 at 8 GPUs; SURVEY.md §8 e)
+# ----------------------------------------------------------------------------------------
+def shard_rows(n: int, world: int, rank: int) -> slice:
+    """Contiguous, balanced row block of rank (sizes differ by at most one)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return slice(lo, lo + base + (1 if rank < extra else 0))
+
+
+def svgp_elbo_grad(engine, theta, Z, q_mu, q_sqrt, group=None):
+    """One sharded SVGP evaluation: this rank's partial sums (Kmn-side: G = Kmn Kmnᵀ, Kmn g_μ,
+    θ/Z contractions, residual sums), ONE all_reduce of the packed partial buffer in place, then
+    the replicated O(M³) tail. Every rank returns the same (ELBO, ∂θ, ∂Z, ∂q_mu, ∂q_sqrt)."""
+    engine.eval_local(theta, Z, q_mu, q_sqrt)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(engine.partials, op=dist.ReduceOp.SUM, group=group)
+    return engine.eval_finish()
+
+
+def fit_svgp_sharded(model, X_local, Y_local, n_total: int, group=None, engine=None, **scipy_kwargs):
+    """Fit ``model`` (models.SVGP) on data sharded by rows over the ranks of ``group``: every
+    rank runs the same scipy L-BFGS-B on the all-reduced (hence identical) ELBO gradient, so
+    the replicated variational parameters stay bit-identical across ranks. ``engine`` may be
+    injected (tests); by default an SVGPEngine on this rank's rows with n_total set."""
+    from .engine import SVGPEngine
+    from .kernels import compile_spec
+    from .optimizers import Scipy
+    if engine is None:
+        Xl = np.asarray(X_local, dtype=np.float64) if not isinstance(X_local, torch.Tensor) else X_local
+        D = 1 if Xl.ndim == 1 else int(Xl.shape[1])
+        engine = SVGPEngine(X_local, Y_local, compile_spec(model.kernel, D), model.M,
+                            num_data=float(model.num_data if model.num_data is not None else n_total),
+                            n_total=n_total, device=model.device)
+
+    def loss_and_grad(variables=None):
+        variables = model.trainable_variables if variables is None else variables
+        out = svgp_elbo_grad(engine, *model._state(), group=group)
+        return model.grads_to_unconstrained(variables, *out)
+
+    def closure():
+        return torch.tensor(loss_and_grad()[0], dtype=torch.float64)
+
+    closure._gpx_loss_and_grad = loss_and_grad
+    closure._gpx_model = model
+    return Scipy().minimize(closure, model.trainable_variables, **scipy_kwargs)

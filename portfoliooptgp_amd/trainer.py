@@ -133,3 +133,53 @@ class MultiInputTrainer:
 
     def train_best_model(self, X_tf, Y_tf):
         return ModelTrainer(self.kernel_combinations).train_model(X_tf, Y_tf)
+
+
+def refit_steps(X_full, Y_full, n_train: int, composite_kernels: Sequence, is_fixed: bool = True,
+                mean: float = 0.0, std: float = 1.0, noise_variance: float = 1e-3,
+                starting_variances=(1e-5, 1e-3, 1e-1, 1.0)):
+    """The iterative refit of Multi-Input_GPR/main.py:414-456 (``run_step_4``), batched.
+
+    For every step i in [n_train, len(Y_full)) and every composite kernel, the reference fits a
+    fresh GPR (``deepcopy(kernel)``) on the first i rows — noise fixed at 1e-3 and
+    ``ModelTrainer.train_model`` (scipy defaults, no maxiter) when ``is_fixed``, else the
+    4-restart ``train_likelihood`` — keeps the model of the LAST kernel of the loop, predicts
+    f at the first i+1 rows and keeps the last row, de-normalised (mean·std + μ, var·std²).
+    All (step × kernel × restart) fits are independent: here they run as ONE lock-step batch
+    (ragged N = n_train … len−1), each the same scipy trajectory it would be alone.
+
+    Returns (f_means, f_vars, actual_returns): lists of [1]-arrays, as run_step_4's first
+    three outputs.
+    """
+    X_full = _np(X_full)
+    Y_full = _np(Y_full).reshape(-1, 1)
+    steps = list(range(n_train, len(Y_full)))
+    kernels = list(composite_kernels)
+    if not steps or not kernels:
+        return [], [], []
+    starts = [noise_variance] if is_fixed else list(starting_variances)
+    models, index = [], []
+    for si, i in enumerate(steps):
+        for ki, k in enumerate(kernels):
+            for v in starts:
+                m = M.GPR((X_full[:i], Y_full[:i]), kernel=deepcopy(k), noise_variance=v)
+                set_trainable(m.likelihood, not is_fixed)
+                models.append(m)
+                index.append((si, ki))
+    logs = Scipy().minimize_batch(models)
+    # per step: the last kernel's model (best restart by final loss, strict <, first wins)
+    chosen = []
+    for si in range(len(steps)):
+        best, best_loss = None, float("inf")
+        for m, r, (s, k) in zip(models, logs, index):
+            if s == si and k == len(kernels) - 1 and r.fun < best_loss:
+                best, best_loss = m, r.fun
+        chosen.append(best)
+    preds = M.predict_f_batch(chosen, [X_full[: i + 1] for i in steps])
+    f_means, f_vars, actual = [], [], []
+    for i, (fm, fv) in zip(steps, preds):
+        fm, fv = _np(fm), _np(fv)
+        f_means.append(fm[-1] * std + mean)
+        f_vars.append(fv[-1] * std ** 2)
+        actual.append(Y_full[i] * std + mean)
+    return f_means, f_vars, actual

@@ -96,3 +96,67 @@ def test_two_rank_gloo_gather_matches_single_process():
             assert loss == pytest.approx(r["loss"]) and nfev == r["nfev"]
             assert means[i][0] == pytest.approx(float(series[i][1].mean()))
     assert outs[0][1] == outs[1][1]
+
+
+def _svgp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import gp_oracle as O
+        from tests.svgp_numpy_shard import NumpySVGPShard
+        X, Y, Z, qm, R = _svgp_data()
+        sl = D.shard_rows(len(X), world, rank)
+        eng = NumpySVGPShard(O.OSquaredExponential(lengthscales=1.3, variance=0.8), X[sl], Y[sl],
+                             len(Z), num_data=len(X), n_total=len(X))
+        theta = np.ones(16)
+        theta[:3] = [1.3, 0.8, 0.05]
+        out = D.svgp_elbo_grad(eng, theta, Z, qm, R)
+        q.put((rank, out[0], [np.asarray(a).tolist() for a in out[1:]]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _svgp_data():
+    rng = np.random.default_rng(21)
+    X = rng.uniform(0, 10, (103, 1))
+    Y = np.sin(X) + 0.1 * rng.standard_normal((103, 1))
+    Z = rng.uniform(0, 10, (7, 1))
+    R = np.tril(rng.standard_normal((7, 7)) * 0.1)
+    R[np.diag_indices(7)] = rng.uniform(0.4, 1.0, 7)
+    return X, Y, Z, rng.standard_normal(7) * 0.3, R
+
+
+def test_shard_rows_partition():
+    for n, w in ((10, 3), (65536, 8), (5, 8)):
+        sl = [D.shard_rows(n, w, r) for r in range(w)]
+        assert sum(s.stop - s.start for s in sl) == n
+        assert all(sl[i].stop == sl[i + 1].start for i in range(w - 1))
+
+
+def test_two_rank_gloo_svgp_allreduce_matches_oracle():
+    """C5's multi-GPU decomposition: each rank's partial sums over its rows, one all_reduce,
+    the replicated finish — equal to the single-process oracle ELBO and gradients."""
+    from oracle import gp_oracle as O
+    from oracle import svgp_oracle as S
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_svgp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X, Y, Z, qm, R = _svgp_data()
+    om = S.OSVGP(O.OSquaredExponential(lengthscales=1.3, variance=0.8), Z, num_data=len(X),
+                 noise_variance=0.05, q_mu=qm, q_sqrt=R)
+    elbo, g = om.elbo_and_grads(X, Y)
+    for rank, e, (gth, gZ, gq, gR) in outs:
+        assert e == pytest.approx(elbo, rel=1e-10)
+        np.testing.assert_allclose(gth[:2], g["theta"], rtol=1e-7, atol=1e-8)
+        assert gth[2] == pytest.approx(g["noise"], rel=1e-7)
+        np.testing.assert_allclose(np.asarray(gZ), g["Z"], rtol=1e-7, atol=1e-8)
+        np.testing.assert_allclose(gq, g["q_mu"], rtol=1e-7, atol=1e-8)
+        np.testing.assert_allclose(np.asarray(gR), g["q_sqrt"], rtol=1e-7, atol=1e-8)
+    assert outs[0][1] == outs[1][1]

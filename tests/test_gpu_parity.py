@@ -404,3 +404,24 @@ def test_config4_shape_matern52_5d():
     mo, vo = om.predict_f(xs)
     check_mean(mu.numpy(), mo)
     assert np.all(np.abs(v.numpy() - vo) <= 1e-5 * np.abs(vo) + 1e-9)
+
+
+def test_refit_steps_matches_sequential_oracle_loop(golden_dir):
+    """Multi-Input_GPR/main.py:414-456 (run_step_4) on the C4-shaped fixture: steps i = 63..66,
+    Exponential(dims 0-3) × Exponential(dim 4), noise fixed at 1e-3, scipy defaults — the
+    batched refit against the oracle fitting each step in sequence."""
+    from portfoliooptgp_amd.trainer import refit_steps
+    d = np.load(os.path.join(golden_dir, "multi_input.npz"))
+    X, Y = d["X"], d["Y"]
+    comp = K.Exponential(active_dims=slice(0, 4)) * K.Exponential(active_dims=slice(4, 5))
+    fm, fv, act = refit_steps(X, Y, 63, [comp], is_fixed=True, mean=0.01, std=2.0)
+    assert len(fm) == len(X) - 63
+    for j, i in enumerate(range(63, len(X))):
+        ok = O.OProduct([O.OExponential(active_dims=slice(0, 4)), O.OExponential(active_dims=slice(4, 5))])
+        om = O.OGPR(X[:i], Y[:i], ok, noise_variance=1e-3)
+        om.noise.trainable = False
+        O.scipy_minimize(om, maxiter=None)
+        mo, vo = om.predict_f(X[: i + 1])
+        assert fm[j][0] == pytest.approx(mo[-1, 0] * 2.0 + 0.01, rel=1e-4, abs=1e-6)
+        assert fv[j][0] == pytest.approx(vo[-1, 0] * 4.0, rel=1e-4, abs=1e-8)
+        assert act[j][0] == pytest.approx(Y[i, 0] * 2.0 + 0.01, rel=1e-15)

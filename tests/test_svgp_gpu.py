@@ -159,3 +159,22 @@ def test_c5_size_known_answer_and_oracle_elbo():
     om = S.OSVGP(O.OSquaredExponential(lengthscales=2.0, variance=1.0), Z, num_data=n,
                  noise_variance=1e-4, q_mu=q, q_sqrt=R)
     assert elbo == pytest.approx(om.elbo(X, Y), rel=1e-7)
+
+
+def test_fit_svgp_sharded_single_rank_equals_model_fit():
+    """distributed.fit_svgp_sharded with one rank (no process group) is the plain model fit."""
+    from portfoliooptgp_amd.distributed import fit_svgp_sharded
+    X, Y, Z, q, R, gk, _ = _case(700, 12, 1, "se", 12)
+
+    def model():
+        m = gpx.models.SVGP(kernel=gpx_kernel("se"), likelihood=gpx.likelihoods.Gaussian(variance=1e-2),
+                            inducing_variable=Z, num_data=700)
+        gpx.set_trainable(m.likelihood.variance, False)
+        return m
+
+    a, b = model(), model()
+    ra = gpx.optimizers.Scipy().minimize(a.training_loss_closure((X, Y)), a.trainable_variables,
+                                         options=dict(maxiter=6))
+    rb = fit_svgp_sharded(b, X, Y, n_total=700, options=dict(maxiter=6))
+    assert ra.fun == rb.fun and ra.nit == rb.nit
+    np.testing.assert_array_equal(a.q_sqrt.value, b.q_sqrt.value)
