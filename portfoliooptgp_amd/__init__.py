@@ -11,7 +11,7 @@ gfx950 in ``libgpx.so`` behind the C ABI of ``include/gpx.h``.
     gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables, options=dict(maxiter=100))
     mean, var = m.predict_f(X)
 """
-from . import _native, inducing_variables, kernels, likelihoods, models, optimizers, utilities
+from . import _native, data, inducing_variables, kernels, likelihoods, models, optimizers, utilities
 from ._native import GPXError, NotPositiveDefiniteError
 from .parameter import Parameter
 from .utilities import print_summary, set_trainable

@@ -10,6 +10,8 @@
   upsample_predictions as host post-processing).
 * ``MultiInputTrainer`` — Multi-Input_GPR/models/model_trainer.py:17-72 (train_model,
   train_likelihood with 4 noise restarts picking the lowest opt_logs.fun, train_best_model).
+* ``BlendOptimizer`` — GPR/optimizer.py:5-28 (the α/β SLSQP of the timeframe blend).
+* ``refit_steps`` — Multi-Input_GPR/main.py:414-456 (run_step_4's refit loop), batched.
 """
 from __future__ import annotations
 
@@ -93,6 +95,31 @@ class Predictor:
         p = _np(predictions).reshape(-1)
         s = pd.Series(p, index=xs).reindex(xd).interpolate(method="linear")
         return torch.as_tensor(s.values.reshape(-1, 1), dtype=torch.float64)
+
+
+class BlendOptimizer:
+    """Timeframe-blend weights (GPR/optimizer.py:5-28): SLSQP over (α, β) ∈ [0,1]², α + β ≤ 1,
+    from (0.33, 0.33), minimising MSE(Y, α·f_d + β·f_w + (1−α−β)·f_m) + λ(|α| + |β|). Host
+    code: two variables, evaluated on the blended device predictions."""
+
+    def __init__(self, lambda_: float = 0.01):
+        self.lambda_ = float(lambda_)
+        self.initial_weights = [0.33, 0.33]
+        self.bounds = [(0, 1), (0, 1)]
+        self.constraints = {"type": "ineq", "fun": lambda w: 1 - sum(w)}
+
+    def loss_fn(self, weights, Y, f_daily, f_weekly, f_monthly) -> float:
+        a, b = weights
+        y = _np(Y).reshape(len(_np(Y)), -1)
+        blend = a * _np(f_daily) + b * _np(f_weekly) + (1.0 - a - b) * _np(f_monthly)
+        return mean_squared_error(y, blend.reshape(y.shape)) + self.lambda_ * (abs(a) + abs(b))
+
+    def optimize_weights(self, Y_tf, f_mean_daily, f_mean_weekly, f_mean_monthly) -> np.ndarray:
+        import scipy.optimize
+        res = scipy.optimize.minimize(
+            lambda w: self.loss_fn(w, Y_tf, f_mean_daily, f_mean_weekly, f_mean_monthly),
+            self.initial_weights, method="SLSQP", bounds=self.bounds, constraints=self.constraints)
+        return res.x
 
 
 class MultiInputTrainer:

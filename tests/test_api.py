@@ -122,3 +122,18 @@ def test_predict_y_full_cov_not_implemented_like_gpflow():
         m.predict_y(x, full_cov=True)
     with pytest.raises(NotImplementedError):
         m.predict_y(x, full_output_cov=True)
+
+
+def test_blend_optimizer_recovers_weights_and_respects_constraints():
+    """GPR/optimizer.py semantics: SLSQP, bounds [0,1]², α+β ≤ 1, L1 penalty λ."""
+    from portfoliooptgp_amd.trainer import BlendOptimizer
+    rng = np.random.default_rng(0)
+    fd, fw, fm = (rng.standard_normal((200, 1)) for _ in range(3))
+    Y = 0.5 * fd + 0.3 * fw + 0.2 * fm
+    w = BlendOptimizer(lambda_=1e-8).optimize_weights(Y, fd, fw, fm)
+    np.testing.assert_allclose(w, [0.5, 0.3], atol=1e-4)
+    w = BlendOptimizer(lambda_=0.01).optimize_weights(3 * fd + 3 * fw, fd, fw, fm)
+    assert np.all(w >= -1e-9) and np.all(w <= 1 + 1e-9) and w.sum() <= 1 + 1e-9
+    opt = BlendOptimizer(0.01)
+    assert opt.loss_fn([0.2, 0.3], Y, fd, fw, fm) == pytest.approx(
+        float(np.mean((Y - (0.2 * fd + 0.3 * fw + 0.5 * fm)) ** 2)) + 0.01 * 0.5)
