@@ -130,6 +130,16 @@ int gpx_batch_predict(gpx_batch* batch, int n_active, const int32_t* active, con
                       int32_t* info, void* stream);
 
 /*
+ * gpx_batch_predict at each problem's own training inputs (GPR/model_trainer.py:20,
+ * predict_f(X_train)) in O(N²) from the factor: with Kxs = K_y − σn²I, GPflow's
+ * Kxsᵀα = y − σn²α and k_jj − colsum((L⁻¹Kxs)²)_j = σn² − σn⁴ [K_y⁻¹]_jj exactly.
+ *   mean, var : device fp64 [B, N_max] (rows < n[b] written).
+ */
+int gpx_batch_predict_train(gpx_batch* batch, int n_active, const int32_t* active,
+                            const double* theta, int add_noise, double* mean, double* var,
+                            int32_t* info, void* stream);
+
+/*
  * Posterior mean and FULL covariance at Xnew: GPflow GPR.predict_f(Xnew, full_cov=True)
  * (GPflow returns the covariance as [1, M, M]; predict_y has no full_cov form in GPflow).
  *   Xnew : device fp64 [B, M, D];  mean : device fp64 [B, M];  cov : device fp64 [B, M, M].

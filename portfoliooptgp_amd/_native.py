@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgpx.so")
 # every symbol include/gpx.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
     "gpx_version", "gpx_create", "gpx_destroy", "gpx_last_error", "gpx_batch_create",
-    "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_predict", "gpx_batch_predict_full_cov",
+    "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_predict", "gpx_batch_predict_full_cov", "gpx_batch_predict_train",
     "gpx_batch_last_timing",
     "gpx_set_profiling", "gpx_batch_reset_timing", "gpx_batch_rebind",
     "gpx_svgp_create", "gpx_svgp_destroy", "gpx_svgp_partials", "gpx_svgp_bind_partials",
@@ -109,6 +109,9 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_predict_full_cov.restype = c_int
         lib.gpx_batch_predict_full_cov.argtypes = [c_void_p, c_int, c_int_p, c_double_p, c_void_p,
                                                    c_int, c_void_p, c_void_p, c_int_p, c_void_p]
+        lib.gpx_batch_predict_train.restype = c_int
+        lib.gpx_batch_predict_train.argtypes = [c_void_p, c_int, c_int_p, c_double_p, c_int, c_void_p,
+                                                c_void_p, c_int_p, c_void_p]
         lib.gpx_batch_last_timing.restype = c_int
         lib.gpx_batch_last_timing.argtypes = [c_void_p, ctypes.POINTER(GpxTiming)]
         lib.gpx_batch_rebind.restype = c_int

@@ -465,10 +465,11 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
 // (cov != nullptr).
 static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                         const double* Xnew, int M, int add_noise, double* mean, double* var,
-                        double* cov, int32_t* info, void* stream) {
+                        double* cov, int32_t* info, void* stream, bool train = false) {
   if (!bt) return GPX_BAD_ARG;
   gpx_ctx* ctx = bt->ctx;
-  if (!Xnew || M <= 0 || !mean || !(var || cov) || !info) return fail(ctx, GPX_BAD_ARG, "bad predict args");
+  if ((!train && (!Xnew || M <= 0)) || !mean || !(var || cov) || !info)
+    return fail(ctx, GPX_BAD_ARG, "bad predict args");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   int rc = upload_common(bt, n_active, active, theta, s);
@@ -496,6 +497,14 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   }
   pt.mark();
   const int Np = bt->Np;
+  if (train) {
+    TrainPredArgs ta{};
+    ta.active = bt->d_active; ta.W = bt->W; ta.sW = mat_stride(bt); ta.ld = Np;
+    ta.alpha = bt->alpha; ta.sVec = Np; ta.Y = bt->Y; ta.sY = bt->Nmax; ta.nvalid = bt->d_n;
+    ta.specs = bt->d_specs; ta.theta = bt->d_theta; ta.add_noise = add_noise;
+    ta.mean = mean; ta.var = var; ta.sOut = bt->Nmax;
+    launch_train_pred(ta, n_active, Np, s);
+  } else {
   const int Mp = ((M + 63) / 64) * 64;
   // cross-covariance workspace [B][Np][Mp]
   const size_t need = (size_t)bt->B * Np * Mp;
@@ -571,6 +580,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   pv.var = var; pv.sVar = M;
   launch_predvar(pv, n_active, s);
   }
+  }
   pt.mark();
   HIPX(ctx, hipGetLastError());
   HIPX(ctx, hipMemcpyAsync(bt->h_info.data(), bt->d_info, sizeof(int) * bt->B, hipMemcpyDeviceToHost, s));
@@ -608,6 +618,12 @@ int gpx_batch_predict(gpx_batch* bt, int n_active, const int32_t* active, const 
   if (!var) return bt ? fail(bt->ctx, GPX_BAD_ARG, "bad predict args") : GPX_BAD_ARG;
   return predict_impl(bt, n_active, active, theta, Xnew, M, add_noise, mean, var, nullptr, info,
                       stream);
+}
+
+int gpx_batch_predict_train(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                            int add_noise, double* mean, double* var, int32_t* info, void* stream) {
+  return predict_impl(bt, n_active, active, theta, nullptr, 0, add_noise, mean, var, nullptr, info,
+                      stream, true);
 }
 
 int gpx_batch_predict_full_cov(gpx_batch* bt, int n_active, const int32_t* active,

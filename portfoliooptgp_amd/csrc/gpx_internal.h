@@ -71,6 +71,21 @@ struct TrmvArgs {
   int lower;                       // 1: triangular (skip known zeros)
 };
 
+// predict_f / predict_y at the training inputs from the cached factor, O(N²):
+//   mean_j = y_j − σn² α_j,  var_j = σn² − σn⁴ [K_y⁻¹]_jj  (+σn² for predict_y),
+// [K_y⁻¹]_jj = Σ_i W_ij² — algebraically GPflow's Kxsᵀα and k_jj − colsum((L⁻¹Kxs)²) with
+// Kxs = K_y − σn²I.
+struct TrainPredArgs {
+  const int* active;
+  const double* W; long long sW; int ld;
+  const double* alpha; long long sVec;
+  const double* Y; long long sY;
+  const int* nvalid;
+  const DevSpec* specs; const double* theta;
+  int add_noise;
+  double* mean; double* var; long long sOut;
+};
+
 struct ReduceArgs {
   const int* active;
   const double* partial; long long sPartial; int ntiles;
@@ -97,6 +112,7 @@ void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hip
 void launch_trmv_n(const TrmvArgs& a, int n_active, hipStream_t s);   // y = M x   (row dots)
 void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s);   // y = Mᵀ x  (column sums)
 void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s);
+void launch_train_pred(const TrainPredArgs& a, int n_active, int Np, hipStream_t s);
 void launch_predvar(const PredVarArgs& a, int n_active, hipStream_t s);
 int gemm_tile(const GemmArgs& a, int n_active);  // tile edge the launcher will use (64 or 128)
 

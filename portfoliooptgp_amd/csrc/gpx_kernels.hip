@@ -354,25 +354,31 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
     }
   };
 
+  // Fragment reads are software-pipelined one k-step ahead (two register sets), so the
+  // LDS latency of step kk+1 hides under the 16 MFMAs of step kk.
   auto compute = [&](int cur) {
     const double* sA = smem + (cur * 2 + 0) * BK * S;
     const double* sB = smem + (cur * 2 + 1) * BK * S;
-#pragma unroll
-    for (int kk = 0; kk < BK / 4; ++kk) {
+    double af[2][MT], bf[2][MT];
+    auto fload = [&](int kk, int slot) {
       const int k = kk * 4 + (lane >> 4);
       const int kr = k * S + (lane & 15);
       const int krs = k * S + ((lane & 15) ^ (k & 15));  // swizzled image (transposed writes)
       const int ka = TA ? kr : krs, kb = TB ? krs : kr;
-      double af[MT], bf[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) af[m] = sA[ka + wr * WT + m * 16];
+      for (int m = 0; m < MT; ++m) af[slot][m] = sA[ka + wr * WT + m * 16];
 #pragma unroll
-      for (int n = 0; n < MT; ++n) bf[n] = sB[kb + wc * WT + n * 16];
+      for (int n = 0; n < MT; ++n) bf[slot][n] = sB[kb + wc * WT + n * 16];
+    };
+    fload(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      if (kk + 1 < BK / 4) fload(kk + 1, (kk + 1) & 1);
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < MT; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk & 1][m], bf[kk & 1][n], acc[m][n], 0, 0, 0);
     }
   };
 
@@ -612,6 +618,36 @@ __global__ __launch_bounds__(256) void trmv_t_kernel(TrmvArgs a) {
   __syncthreads();
   if (wave == 0 && j < a.cols)
     a.y[(long long)b * a.sy + j] = sred[0][lane] + sred[1][lane] + sred[2][lane] + sred[3][lane];
+}
+
+__global__ __launch_bounds__(256) void train_pred_kernel(TrainPredArgs a) {
+  const int b = a.active[blockIdx.y];
+  const double* W = a.W + (long long)b * a.sW;
+  __shared__ double sred[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  const int n = a.nvalid[b];
+  double s = 0.0;
+  if (j < n) {
+    for (int i = blockIdx.x * 64 + wave; i < n; i += 4) {
+      const double w = W[(long long)i * a.ld + j];
+      s = fma(w, w, s);
+    }
+  }
+  sred[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && j < n) {
+    const double kinv = (sred[0][lane] + sred[1][lane]) + (sred[2][lane] + sred[3][lane]);
+    const double s2 = a.theta[b * GPX_THETA_STRIDE + a.specs[b].n_params];
+    a.mean[(long long)b * a.sOut + j] = fma(-s2, a.alpha[(long long)b * a.sVec + j], a.Y[(long long)b * a.sY + j]);
+    double v = fma(-s2 * s2, kinv, s2);
+    if (a.add_noise) v += s2;
+    a.var[(long long)b * a.sOut + j] = v;
+  }
+}
+
+void launch_train_pred(const TrainPredArgs& a, int n_active, int Np, hipStream_t s) {
+  hipLaunchKernelGGL(train_pred_kernel, dim3(Np / 64, n_active), dim3(256), 0, s, a);
 }
 
 void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s) {

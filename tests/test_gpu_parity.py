@@ -425,3 +425,35 @@ def test_refit_steps_matches_sequential_oracle_loop(golden_dir):
         assert fm[j][0] == pytest.approx(mo[-1, 0] * 2.0 + 0.01, rel=1e-4, abs=1e-6)
         assert fv[j][0] == pytest.approx(vo[-1, 0] * 4.0, rel=1e-4, abs=1e-8)
         assert act[j][0] == pytest.approx(Y[i, 0] * 2.0 + 0.01, rel=1e-15)
+
+
+def test_predict_at_training_inputs_fast_path(golden):
+    """predict_f/predict_y at the model's own X (GPR/model_trainer.py:20) take the O(N²) path
+    (y − σn²α, σn² − σn⁴[K⁻¹]_jj); it agrees with the golden fixtures (whose xnew starts with
+    the training inputs), with the general path and, at N=2048, with the oracle."""
+    d, idx = golden
+    for key in [k for k in idx if k.endswith("|random")]:
+        m = _model(d, key)
+        x = m.data[0].numpy()
+        n = len(x)
+        xnew = d[key + "|xnew"]
+        assert np.array_equal(xnew[:n], x)
+        cond = d[key + "|cond"][0]
+        mu, var = m.predict_f(x)
+        _, vy = m.predict_y(x)
+        s2 = max(float(np.max(d[key + "|fvar"])), 1.0)
+        check_mean(mu.numpy(), d[key + "|fmean"][:n], cond)
+        check_var(var.numpy(), d[key + "|fvar"][:n], s2)
+        check_var(vy.numpy(), d[key + "|yvar"][:n], s2)
+        mg, vg = m.predict_f(xnew)                 # general (Kxs GEMM) path
+        check_mean(mu.numpy(), mg.numpy()[:n], cond)
+        check_var(var.numpy(), vg.numpy()[:n], s2)
+    # full size, ill-conditioned (σn² = 1e-5, the bench protocol)
+    xs, ys = O.synthetic_series(2048, seed=3)
+    m = gpx.models.GPR((xs, ys), kernel=K.SquaredExponential(lengthscales=30.0, variance=0.8))
+    m.likelihood.variance.assign(1e-5)
+    om = O.OGPR(xs, ys, O.OSquaredExponential(lengthscales=30.0, variance=0.8), noise_variance=1e-5)
+    mu, var = m.predict_f(xs)
+    mo, vo = om.predict_f(xs)
+    assert np.abs(mu.numpy() - mo).max() <= 1e-6 * np.abs(mo).max()
+    assert np.abs(var.numpy() - vo).max() <= 1e-9
