@@ -117,8 +117,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 128)),
                     help="independent series fitted per GPU per step")
-    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 64)),
+    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 128)),
                     help="resident device slots (continuous-batching width)")
+    ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 2)),
+                    help="alternating device batches (host/device overlap)")
     ap.add_argument("--n", type=int, default=N_POINTS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -155,12 +157,16 @@ def main():
     engine.ctx.set_profiling(True)
     opt = gpx.optimizers.Scipy()
 
+    traces = []
+
     def one_step():
         for m in models:  # every step starts from GPflow defaults
             m.kernel.lengthscales.assign(1.0)
             m.kernel.variance.assign(1.0)
-        res, preds = opt.minimize_stream(models, width=W, engine=engine, predict_train=True,
+        res, preds = opt.minimize_stream(models, width=W, engine=engine, predict_train=True, groups=args.groups,
                                          options=dict(maxiter=MAXITER))
+        if getattr(opt, "last_trace", None):
+            traces.append(opt.last_trace)
         summary = torch.stack([
             torch.stack([
                 torch.tensor(m.kernel.lengthscales.value, device=dev, dtype=torch.float64),
@@ -222,7 +228,8 @@ def main():
         "data": "synthetic (C2 generator, seeded per rank/series)",
         "config": {"workload": "C2: exact GPR fit, synthetic 1-D series, N=4096, SquaredExponential, "
                                "fp64, sigma_n^2=1e-5 fixed, L-BFGS-B maxiter=100 + predict_f(X_train)",
-                   "N": n, "fits_per_gpu_per_step": F, "device_slots": W, "kernel": "SquaredExponential",
+                   "N": n, "fits_per_gpu_per_step": F, "device_slots": W, "device_batches": args.groups,
+                   "kernel": "SquaredExponential",
                    "parallelism": f"independent fits, {world} process(es) x 1 GPU, RCCL all_gather of results"},
         "nfev_mean": nfev_mean,
         "evals_per_s": tm.evals / elapsed if world == 1 else None,
@@ -244,6 +251,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, nfev_mean)
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if traces and rank == 0:
+        with open(os.environ.get("GPX_TRACE_OUT", "rounds_trace.json"), "w") as f:
+            json.dump([[[t, b] for t, b in tr] for tr in traces], f)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

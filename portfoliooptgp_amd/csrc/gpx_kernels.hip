@@ -583,17 +583,29 @@ __global__ __launch_bounds__(256) void trmv_n_kernel(TrmvArgs a) {
   const double* x = a.x + (long long)b * a.sx;
   const int nx = a.nvalid ? a.nvalid[b] : a.cols;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int rr = 0; rr < 16; ++rr) {
-    const int i = blockIdx.x * 64 + wave * 16 + rr;
-    if (i >= a.rows) break;
-    const int kend = a.lower ? min(i + 1, a.cols) : a.cols;
-    double s = 0.0;
+  // four rows at a time per wave: four independent load streams in flight
+  for (int rr = 0; rr < 16; rr += 4) {
+    const int i0 = blockIdx.x * 64 + wave * 16 + rr;
+    if (i0 >= a.rows) break;
+    const int kend = a.lower ? min(i0 + 4, a.cols) : a.cols;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    const double* r0 = M + (long long)i0 * a.ld;
     for (int k = lane; k < kend; k += 64) {
       const double xv = (k < nx) ? x[k] : 0.0;
-      s = fma(M[(long long)i * a.ld + k], xv, s);
+      // rows beyond a.rows or entries above the diagonal read as zero
+      if (!a.lower || k <= i0) s0 = fma(r0[k], xv, s0);
+      if (i0 + 1 < a.rows && (!a.lower || k <= i0 + 1)) s1 = fma(r0[a.ld + k], xv, s1);
+      if (i0 + 2 < a.rows && (!a.lower || k <= i0 + 2)) s2 = fma(r0[2 * a.ld + k], xv, s2);
+      if (i0 + 3 < a.rows && (!a.lower || k <= i0 + 3)) s3 = fma(r0[3 * (long long)a.ld + k], xv, s3);
     }
-    s = wave_sum(s);
-    if (lane == 0) a.y[(long long)b * a.sy + i] = s;
+    s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2); s3 = wave_sum(s3);
+    if (lane == 0) {
+      double* y = a.y + (long long)b * a.sy;
+      y[i0] = s0;
+      if (i0 + 1 < a.rows) y[i0 + 1] = s1;
+      if (i0 + 2 < a.rows) y[i0 + 2] = s2;
+      if (i0 + 3 < a.rows) y[i0 + 3] = s3;
+    }
   }
 }
 

@@ -124,10 +124,14 @@ __device__ __forceinline__ double eval_term(const gpx_term& t, const double* __r
 __device__ __forceinline__ double eval_k(const DevSpec& s, const double* __restrict__ th,
                                          const double* __restrict__ xi,
                                          const double* __restrict__ xj) {
-  double acc = (s.combine == GPX_PRODUCT && s.n_terms > 1) ? 1.0 : 0.0;
-  for (int t = 0; t < s.n_terms; ++t) {
+  const bool prod = (s.combine == GPX_PRODUCT && s.n_terms > 1);
+  double acc = prod ? 1.0 : 0.0;
+  // static term index (a runtime-indexed register copy of the spec would live in scratch)
+#pragma unroll
+  for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+    if (t >= s.n_terms) break;
     const double v = eval_term<false>(s.terms[t], th + s.terms[t].param_offset, xi, xj, nullptr);
-    if (s.combine == GPX_PRODUCT && s.n_terms > 1) acc *= v; else acc += v;
+    if (prod) acc *= v; else acc += v;
   }
   return acc;
 }

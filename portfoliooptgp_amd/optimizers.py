@@ -14,8 +14,10 @@ to sequential fitting while the device works on all fits at once.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
+import time
 from typing import Callable, List, Optional, Sequence
 
 import numpy as np
@@ -137,14 +139,15 @@ class Scipy:
 
     def minimize_stream(self, models: Sequence, width: int, method: str = "L-BFGS-B",
                         device: Optional[int] = None, predict_train: bool = False,
-                        engine: Optional[Engine] = None, **scipy_kwargs):
+                        engine: Optional[Engine] = None, groups: int = 1, **scipy_kwargs):
         """Continuous batching: fit many models through ``width`` resident device slots.
 
         Every model still runs its own unmodified scipy L-BFGS-B; at most ``width`` are
         resident, and a slot is refilled from the queue as soon as its fit has converged, so
         the batched evaluations stay wide until the queue drains (a lock-step batch shrinks
         as its fits finish). With ``predict_train`` each model's predict_f at its training
-        inputs runs before its slot is released. Returns (results, predictions|None); models
+        inputs runs before its slot is released. ``groups`` > 1 splits the slots into that many
+        alternating device batches so the host work of one overlaps the device work of the other. Returns (results, predictions|None); models
         are detached from the shared engine afterwards.
         """
         models = list(models)
@@ -162,7 +165,7 @@ class Scipy:
             Y0 = [np.zeros((nmax, 1)) for _ in seed]
             engine = Engine(X0, Y0, [compile_spec(m.kernel, D) for m in seed],
                             device=device if device is not None else models[0].device)
-        step = _LockstepEvaluator(engine, [None] * engine.B, total=len(models))
+        step = _LockstepEvaluator(engine, [None] * engine.B, total=len(models), groups=groups)
         free: "queue.Queue[int]" = queue.Queue()
         for s in range(engine.B):
             free.put(s)
@@ -209,6 +212,7 @@ class Scipy:
         step.serve()
         for t in threads:
             t.join()
+        self.last_trace = step.trace
         for e in errors:
             if e is not None:
                 raise e
@@ -219,20 +223,32 @@ class _LockstepEvaluator:
     """Barrier between the optimiser threads and the device: evaluates all pending points in
     one gpx_batch_lml_grad call once every running optimiser has posted one."""
 
-    def __init__(self, engine: Engine, models, total: Optional[int] = None):
+    def __init__(self, engine: Engine, models, total: Optional[int] = None, groups: int = 1):
         self.engine = engine
         self.models = list(models)
+        # slots are split into `groups` (slot % groups); each group has its own server thread
+        # and device calls, so one group's host-side work (scipy steps, result unpacking)
+        # overlaps the other group's device evaluation
+        self.groups = max(1, int(groups))
         self.cv = threading.Condition()
         self.lib_lock = threading.Lock()
         if total is None:  # fixed lock-step batch: every slot runs from the start
             self.running = set(range(len(self.models)))
             self.remaining = len(self.models)
+            self.initial = len(self.models)
         else:              # streaming: slots join via bind() and leave via finish()
             self.running = set()
             self.remaining = total
+            self.initial = min(len(self.models), total)
         self.pending = {}
         self.results = {}
         self.rounds = 0
+        # slots of the previous device call; only these (if still running) are waited for —
+        # a fit bound since then joins whichever round it posts in time for, so rebinding a
+        # slot never stalls the device
+        self.last_batch = [None] * self.groups
+        # GPX_TRACE_ROUNDS=1: (time, batch size) per device call, for bench diagnostics
+        self.trace = [] if os.environ.get("GPX_TRACE_ROUNDS") else None
 
     def bind(self, slot: int, model):
         with self.cv:
@@ -262,17 +278,49 @@ class _LockstepEvaluator:
             self.remaining -= 1
             self.cv.notify_all()
 
+    def _ready(self, g: int) -> bool:
+        G = self.groups
+        if not any(i % G == g for i in self.pending):
+            return False
+        run = {i for i in self.running if i % G == g}
+        if self.last_batch[g] is None:  # first round: wait for the group's initial slots
+            init = sum(1 for s in range(self.initial) if s % G == g)
+            return len(run) >= min(init, self.remaining) and all(i in self.pending for i in run)
+        return all(i in self.pending for i in self.last_batch[g] & run)
+
     def serve(self):
+        if self.groups == 1:
+            return self._serve(0)
+        errs = []
+
+        def run(g):
+            try:
+                self._serve(g)
+            except BaseException as e:  # pragma: no cover - surfaced below
+                errs.append(e)
+        helpers = [threading.Thread(target=run, args=(g,), daemon=True) for g in range(1, self.groups)]
+        for t in helpers:
+            t.start()
+        run(0)
+        for t in helpers:
+            t.join()
+        if errs:
+            raise errs[0]
+
+    def _serve(self, g: int):
         eng = self.engine
+        G = self.groups
         while True:
             with self.cv:
-                while self.remaining > 0 and (not self.running or len(self.pending) < len(self.running)):
+                while self.remaining > 0 and not self._ready(g):
                     self.cv.wait()
                 if self.remaining <= 0:
                     return
-                batch = dict(self.pending)
-                self.pending.clear()
+                batch = {i: self.pending.pop(i) for i in [i for i in self.pending if i % G == g]}
+                self.last_batch[g] = set(batch)
             active = sorted(batch)
+            if self.trace is not None:
+                self.trace.append((time.perf_counter(), len(active)))
             theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
             for i in active:
                 theta[i] = self.models[i].theta_row()
@@ -291,7 +339,7 @@ class _LockstepEvaluator:
             except BaseException as e:
                 for i in active:
                     out[i] = e
-            self.rounds += 1
             with self.cv:
+                self.rounds += 1
                 self.results.update(out)
                 self.cv.notify_all()

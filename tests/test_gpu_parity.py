@@ -237,14 +237,15 @@ def test_stream_fits_equal_solo_fits():
         m = make(x, y)
         r = gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables, options=dict(maxiter=100))
         solo.append((r, m.predict_f(x)))
-    models = [make(x, y) for x, y in data]
-    res, preds = gpx.optimizers.Scipy().minimize_stream(models, width=3, predict_train=True,
-                                                        options=dict(maxiter=100))
-    for (r0, (mu0, v0)), r1, (mu1, v1) in zip(solo, res, preds):
-        assert r0.nfev == r1.nfev
-        np.testing.assert_allclose(r0.x, r1.x, rtol=1e-9)
-        np.testing.assert_allclose(mu0.numpy()[:, 0], mu1.cpu().numpy()[:, 0], rtol=1e-9, atol=1e-12)
-        np.testing.assert_allclose(v0.numpy()[:, 0], v1.cpu().numpy()[:, 0], rtol=1e-7, atol=1e-12)
+    for width, groups in ((3, 1), (4, 2)):
+        models = [make(x, y) for x, y in data]
+        res, preds = gpx.optimizers.Scipy().minimize_stream(models, width=width, predict_train=True,
+                                                            groups=groups, options=dict(maxiter=100))
+        for (r0, (mu0, v0)), r1, (mu1, v1) in zip(solo, res, preds):
+            assert r0.nfev == r1.nfev
+            np.testing.assert_allclose(r0.x, r1.x, rtol=1e-9)
+            np.testing.assert_allclose(mu0.numpy()[:, 0], mu1.cpu().numpy()[:, 0], rtol=1e-9, atol=1e-12)
+            np.testing.assert_allclose(v0.numpy()[:, 0], v1.cpu().numpy()[:, 0], rtol=1e-7, atol=1e-12)
     # models are detached and still usable on their own
     mu, _ = models[0].predict_f(data[0][0])
     np.testing.assert_allclose(mu.numpy()[:, 0], solo[0][1][0].numpy()[:, 0], rtol=1e-9, atol=1e-12)
