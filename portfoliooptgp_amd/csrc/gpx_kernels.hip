@@ -307,25 +307,28 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
 #pragma unroll
     for (int n = 0; n < MT; ++n) acc[m][n] = (d4){0.0, 0.0, 0.0, 0.0};
 
+  // Operand loads are buffer loads: the K-tile origin is a wave-uniform base (SGPR buffer
+  // descriptor rebuilt per K-tile with scalar arithmetic) and each lane's byte offset inside
+  // the tile is a loop-invariant 32-bit VGPR — no per-load 64-bit address arithmetic.
   d2 ra[NLD], rb[NLD];
+  int offa[NLD], offb[NLD];
+#pragma unroll
+  for (int q = 0; q < NLD; ++q) {
+    const int c = tid + 256 * q;
+    if (!TA) offa[q] = (int)(((c >> 3) * lda + (c & 7) * 2) * 8);
+    else offa[q] = (int)(((c / (BM / 2)) * lda + (c % (BM / 2)) * 2) * 8);
+    if (TB) offb[q] = (int)(((c >> 3) * ldb + (c & 7) * 2) * 8);
+    else offb[q] = (int)(((c / (BN / 2)) * ldb + (c % (BN / 2)) * 2) * 8);
+  }
   auto gload = [&](int k0) {
+    const double* pa = TA ? A + (long long)k0 * lda + i0 : A + (long long)i0 * lda + k0;
+    const double* pb = TB ? B + (long long)j0 * ldb + k0 : B + (long long)k0 * ldb + j0;
+    const auto rsa = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(pa), (short)0, 0x7fffffff, 0x00020000);
+    const auto rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(pb), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
-      const int c = tid + 256 * q;
-      if (!TA) {
-        const int row = c >> 3, kc = (c & 7) * 2;
-        ra[q] = *reinterpret_cast<const d2*>(A + (long long)(i0 + row) * lda + k0 + kc);
-      } else {
-        const int krow = c / (BM / 2), ic = (c % (BM / 2)) * 2;
-        ra[q] = *reinterpret_cast<const d2*>(A + (long long)(k0 + krow) * lda + i0 + ic);
-      }
-      if (TB) {
-        const int row = c >> 3, kc = (c & 7) * 2;
-        rb[q] = *reinterpret_cast<const d2*>(B + (long long)(j0 + row) * ldb + k0 + kc);
-      } else {
-        const int krow = c / (BN / 2), jc = (c % (BN / 2)) * 2;
-        rb[q] = *reinterpret_cast<const d2*>(B + (long long)(k0 + krow) * ldb + j0 + jc);
-      }
+      ra[q] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rsa, offa[q], 0, 0));
+      rb[q] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rsb, offb[q], 0, 0));
     }
   };
   auto swrite = [&](int buf) {

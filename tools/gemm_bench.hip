@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 #include "../portfoliooptgp_amd/csrc/gpx_internal.h"
 using namespace gpx;
@@ -18,6 +19,7 @@ __global__ void fill(double* p, size_t n, unsigned seed) {
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 2048;
   const int B = argc > 2 ? atoi(argv[2]) : 8;
+  const char* only = argc > 3 ? argv[3] : nullptr;   // run only the case with this name prefix
   const size_t sz = (size_t)n * n;
   double *A, *Bm, *C;
   CK(hipMalloc(&A, sz * B * 8)); CK(hipMalloc(&Bm, sz * B * 8)); CK(hipMalloc(&C, sz * B * 8));
@@ -32,6 +34,7 @@ int main(int argc, char** argv) {
                   {"NN trmm kmin_j", false, false, TRI_KMIN_J, 0}, {"NN trmm kmax_i", false, false, TRI_KMAX_I, 0},
                   {"TN lauum(lower,kmin_i)", true, false, TRI_KMIN_I, 1}};
   for (auto& c : cases) {
+    if (only && std::string(c.name).rfind(only, 0) != 0) continue;
     GemmArgs g{};
     g.active = act; g.A = A; g.sA = sz; g.lda = n; g.Bm = Bm; g.sB = sz; g.ldb = n; g.C = C; g.sC = sz; g.ldc = n;
     g.M = g.N = n; g.K = n / c.kdiv; g.tri = c.tri; g.lower_only = c.lower;
@@ -70,7 +73,7 @@ int main(int argc, char** argv) {
         gg.vec = alpha; gg.sVec = n; gg.X = X; gg.sX = n; gg.D = 1; gg.specs = spec; gg.theta = theta;
         gg.nvalid = nv; gg.partial = partial; gg.sPartial = 2080 * 16;
       }
-      const int ep = epi ? EPI_CONTRACT : EPI_STORE;
+      const int ep = epi ? EPI_CONTRACT1 : EPI_STORE;
       launch_gemm(gg, ep, c.ta, c.tb, B, 0);
       CK(hipDeviceSynchronize());
       const int reps = 5;
