@@ -137,23 +137,31 @@ def main():
     from portfoliooptgp_amd.kernels import compile_spec
     from portfoliooptgp_amd.models import predict_f_batch
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device(f"cuda:{local_rank}")
+    # GPX_BENCH_BACKEND=gloo + GPX_DEVICE=0: rehearsal of the multi-rank path with every rank
+    # on one GPU (collectives on host tensors); the real run is RCCL, one GPU per rank
+    backend = os.environ.get("GPX_BENCH_BACKEND", "nccl")
+    gpu = int(os.environ["GPX_DEVICE"])
+    torch.cuda.set_device(gpu)
+    dev = torch.device(f"cuda:{gpu}")
+    cdev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     F, W, n = args.fits, args.width, args.n
     seeds = [rank * F + f for f in range(F)]
     data = [synthetic_series(n, s) for s in seeds]
     Xd = [torch.as_tensor(x, device=dev) for x, _ in data]  # resident in HBM before timing
     Yd = [torch.as_tensor(y, device=dev) for _, y in data]
-    models = [gpx.models.GPR(data=(Xd[f], Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=local_rank)
+    models = [gpx.models.GPR(data=(Xd[f], Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=gpu)
               for f in range(F)]
     for m in models:
         m.likelihood.variance.assign(NOISE)
         gpx.set_trainable(m.likelihood.variance, False)
     # W resident device slots (continuous batching), sized for N-point problems
-    engine = Engine(Xd[:W], Yd[:W], [compile_spec(m.kernel, 1) for m in models[:W]], device=local_rank)
+    engine = Engine(Xd[:W], Yd[:W], [compile_spec(m.kernel, 1) for m in models[:W]], device=gpu)
     engine.ctx.set_profiling(True)
     opt = gpx.optimizers.Scipy()
 
@@ -175,6 +183,7 @@ def main():
                 torch.tensor(float(r.nfev), device=dev, dtype=torch.float64),
                 p[0][-1, 0], p[1][-1, 0]]) for m, r, p in zip(models, res, preds)])
         if world > 1:
+            summary = summary.to(cdev)
             gathered = [torch.empty_like(summary) for _ in range(world)]
             dist.all_gather(gathered, summary)
             summary = torch.cat(gathered)
@@ -197,10 +206,10 @@ def main():
     elapsed = time.perf_counter() - t0
     tm = engine.last_timing()
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        nf = torch.tensor([float(sum(nfev)), float(len(nfev))], device=dev, dtype=torch.float64)
+        nf = torch.tensor([float(sum(nfev)), float(len(nfev))], device=cdev, dtype=torch.float64)
         dist.all_reduce(nf)
         nfev_mean = float(nf[0] / nf[1])
     else:
