@@ -126,10 +126,11 @@ def gpu_fit_shard(series, horizons, width: int = 32, maxiter: int = 100):
         m.likelihood.variance.assign(1e-5)
         set_trainable(m.likelihood.variance, False)
         ms.append(m)
-    res, _ = optimizers.Scipy().minimize_stream(ms, width=width, options=dict(maxiter=maxiter))
+    res, preds = optimizers.Scipy().minimize_stream(ms, width=min(width, len(ms)), predict_inputs=list(horizons),
+                                                    options=dict(maxiter=maxiter))
     out = []
-    for m, r, h in zip(ms, res, horizons):
-        mean, var = m.predict_f(h)
+    for m, r, (mean, var) in zip(ms, res, preds):
+        mean, var = mean.cpu().numpy(), var.cpu().numpy()
         out.append(dict(loss=float(r.fun), nfev=int(r.nfev),
                         theta=[p.value for p in m.kernel.parameters],
                         mean=np.asarray(mean).reshape(-1), var=np.asarray(var).reshape(-1)))

@@ -139,14 +139,16 @@ class Scipy:
 
     def minimize_stream(self, models: Sequence, width: int, method: str = "L-BFGS-B",
                         device: Optional[int] = None, predict_train: bool = False,
-                        engine: Optional[Engine] = None, groups: int = 1, **scipy_kwargs):
+                        engine: Optional[Engine] = None, groups: int = 1,
+                        predict_inputs: Optional[Sequence] = None, **scipy_kwargs):
         """Continuous batching: fit many models through ``width`` resident device slots.
 
         Every model still runs its own unmodified scipy L-BFGS-B; at most ``width`` are
         resident, and a slot is refilled from the queue as soon as its fit has converged, so
         the batched evaluations stay wide until the queue drains (a lock-step batch shrinks
         as its fits finish). With ``predict_train`` each model's predict_f at its training
-        inputs runs before its slot is released. ``groups`` > 1 splits the slots into that many
+        inputs (or at ``predict_inputs[i]`` when given) runs before its slot is released.
+        ``groups`` > 1 splits the slots into that many
         alternating device batches so the host work of one overlaps the device work of the other. Returns (results, predictions|None); models
         are detached from the shared engine afterwards.
         """
@@ -170,6 +172,10 @@ class Scipy:
         for s in range(engine.B):
             free.put(s)
         results = [None] * len(models)
+        if predict_inputs is not None:
+            predict_train = True
+            if len(predict_inputs) != len(models):
+                raise ValueError("predict_inputs needs one Xnew per model")
         preds = [None] * len(models) if predict_train else None
         errors: List[Optional[BaseException]] = [None] * len(models)
         lib_lock = step.lib_lock
@@ -196,8 +202,9 @@ class Scipy:
                     step.unbind(slot)  # leave the lock-step set before the predict call
                     theta = np.ones((engine.B, N.GPX_THETA_STRIDE))
                     theta[slot] = m.theta_row()
+                    xp = m.data[0] if predict_inputs is None else predict_inputs[i]
                     with lib_lock:
-                        mu, var, _ = engine.predict([slot], theta, [m.data[0]], False)
+                        mu, var, _ = engine.predict([slot], theta, [xp], False)
                     preds[i] = (mu[0].reshape(-1, 1), var[0].reshape(-1, 1))
             except BaseException as e:
                 errors[i] = e

@@ -458,3 +458,28 @@ def test_predict_at_training_inputs_fast_path(golden):
     mo, vo = om.predict_f(xs)
     assert np.abs(mu.numpy() - mo).max() <= 1e-6 * np.abs(mo).max()
     assert np.abs(var.numpy() - vo).max() <= 1e-9
+
+
+def test_config3_twenty_series_fit_assets():
+    """BASELINE config C3 shape on one GPU: 20 series × N=2048 through distributed.fit_assets
+    (LPT shard = everything on this rank, continuous batching, predict at the horizon). Each
+    fit equals its solo fit; the reported loss equals the oracle's −logML at the fitted θ."""
+    from portfoliooptgp_amd import distributed as Dist
+    series = [O.synthetic_series(2048, seed=100 + i) for i in range(20)]
+    horizons = [np.arange(2048, 2053, dtype=np.float64)[:, None] for _ in series]
+    res = Dist.fit_assets(series, horizons)
+    assert sorted(res) == list(range(20))
+    for i in (0, 13):
+        x, y = series[i]
+        m = gpx.models.GPR((x, y), kernel=K.SquaredExponential())
+        m.likelihood.variance.assign(1e-5)
+        gpx.set_trainable(m.likelihood.variance, False)
+        r = gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables, options=dict(maxiter=100))
+        # batched and solo runs may use different GEMM tile sizes: equal up to rounding
+        assert res[i]["loss"] == pytest.approx(r.fun, rel=1e-10) and res[i]["nfev"] == r.nfev
+        mu, var = m.predict_f(horizons[i])
+        np.testing.assert_allclose(res[i]["mean"][:, 0], mu.numpy()[:, 0], rtol=1e-7, atol=1e-10)
+        np.testing.assert_allclose(res[i]["var"][:, 0], var.numpy()[:, 0], rtol=1e-7, atol=1e-12)
+        ell, s2 = res[i]["theta"][:2]
+        om = O.OGPR(x, y, O.OSquaredExponential(lengthscales=ell, variance=s2), noise_variance=1e-5)
+        assert res[i]["loss"] == pytest.approx(-om.log_marginal_likelihood(), rel=1e-8)
