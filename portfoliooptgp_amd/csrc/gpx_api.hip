@@ -98,10 +98,10 @@ void chol_inv(const Run& r, int off, int n, int depth) {
   const bool fork = r.dag && depth < kAux && r.next_event && *r.next_event + 2 <= kEvents;
   hipEvent_t eT = nullptr;
   if (fork) {
-    hipEvent_t eL = ctx->ev[(*r.next_event)++];
-    eT = ctx->ev[(*r.next_event)++];
+    hipEvent_t eL = bt->ev[(*r.next_event)++];
+    eT = bt->ev[(*r.next_event)++];
     Run ra = r;
-    ra.s = ctx->aux[depth];
+    ra.s = bt->aux[depth];
     (void)hipEventRecord(eL, r.s);
     (void)hipStreamWaitEvent(ra.s, eL, 0);
     gemm(ra, targs, EPI_STORE, false, false);
@@ -303,6 +303,12 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
   if (hipMemset(bt->W, 0, mat) != hipSuccess || hipMemset(bt->L, 0, mat) != hipSuccess ||
       hipMemset(bt->K, 0, mat) != hipSuccess)
     return cleanup("memset failed");
+  for (int g = 0; g < kAux; ++g)
+    if (hipStreamCreateWithFlags(&bt->aux[g], hipStreamNonBlocking) != hipSuccess)
+      return cleanup("stream creation failed");
+  for (int e = 0; e < kEvents; ++e)
+    if (hipEventCreateWithFlags(&bt->ev[e], hipEventDisableTiming) != hipSuccess)
+      return cleanup("event creation failed");
   std::vector<DevSpec> ds(B);
   for (int b = 0; b < B; ++b) std::memcpy(&ds[b], &specs[b], sizeof(DevSpec));
   static_assert(sizeof(DevSpec) == sizeof(gpx_kernel_spec), "spec layout");
@@ -325,6 +331,10 @@ int gpx_batch_destroy(gpx_batch* bt) {
                   (void*)bt->d_specs, (void*)bt->d_theta, (void*)bt->d_active, (void*)bt->d_info,
                   (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw})
     if (p) (void)hipFree(p);
+  for (int g = 0; g < kAux; ++g)
+    if (bt->aux[g]) (void)hipStreamDestroy(bt->aux[g]);
+  for (int e = 0; e < kEvents; ++e)
+    if (bt->ev[e]) (void)hipEventDestroy(bt->ev[e]);
   delete bt;
   return GPX_OK;
 }

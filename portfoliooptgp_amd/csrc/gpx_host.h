@@ -51,6 +51,10 @@ struct gpx_batch {
   std::vector<int> h_info;
   gpx_timing timing{};
   double flops_acc = 0.0;
+  // per-batch auxiliary streams and events (the recursion's T-product forks), so that
+  // independent batches of one context can evaluate concurrently on different streams
+  hipStream_t aux[kAux] = {};
+  hipEvent_t ev[kEvents] = {};
 };
 
 namespace gpx {

@@ -262,8 +262,8 @@ int gpx_svgp_eval_local(gpx_svgp* sv, const double* theta, const double* Z, cons
   const double c2 = -scale / s2;  // 2c
   const Run r{sv->kmm, sv->kmm->d_active, 1, s};
   double* W = sv->kmm->W;
-  hipStream_t sa = ctx->aux[0];
-  hipEvent_t e_up = ctx->ev[kEvents - 2], e_m = ctx->ev[kEvents - 1];
+  hipStream_t sa = sv->kmm->aux[0];
+  hipEvent_t e_up = sv->kmm->ev[kEvents - 2], e_m = sv->kmm->ev[kEvents - 1];
   HIPX(ctx, hipEventRecord(e_up, s));
   // Kmn = k(Z, X) (rows ≥ M and columns ≥ N are zero)
   BuildArgs ba{};

@@ -22,6 +22,7 @@ from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 import scipy.optimize
+import torch
 
 from . import _native as N
 from .engine import Engine
@@ -139,7 +140,7 @@ class Scipy:
 
     def minimize_stream(self, models: Sequence, width: int, method: str = "L-BFGS-B",
                         device: Optional[int] = None, predict_train: bool = False,
-                        engine: Optional[Engine] = None, groups: int = 1,
+                        engine=None, groups: int = 1,
                         predict_inputs: Optional[Sequence] = None, **scipy_kwargs):
         """Continuous batching: fit many models through ``width`` resident device slots.
 
@@ -148,28 +149,37 @@ class Scipy:
         the batched evaluations stay wide until the queue drains (a lock-step batch shrinks
         as its fits finish). With ``predict_train`` each model's predict_f at its training
         inputs (or at ``predict_inputs[i]`` when given) runs before its slot is released.
-        ``groups`` > 1 splits the slots into that many
-        alternating device batches so the host work of one overlaps the device work of the other. Returns (results, predictions|None); models
-        are detached from the shared engine afterwards.
+
+        ``groups`` > 1 splits the slots into that many independent device batches, each its
+        own engine (gpx_batch) evaluated from its own server thread on its own HIP stream:
+        the groups' evaluations run concurrently on the GPU (one group's latency-bound
+        phases overlap another's large GEMMs) and one group's host work overlaps the others'
+        device work. ``engine`` may be one Engine (groups then alternate on it) or a list of
+        ``groups`` Engines. Returns (results, predictions|None); models are detached afterwards.
         """
         models = list(models)
         if not models:
             return [], ([] if predict_train else None)
         width = max(1, min(int(width), len(models)))
+        groups = max(1, min(int(groups), width))
         D = models[0].data[0].shape[1]
         if any(m.data[0].shape[1] != D for m in models):
             raise ValueError("all models must have the same input dimension")
         nmax = max(m.data[0].shape[0] for m in models)
+        dev = device if device is not None else models[0].device
         if engine is None:
-            # slot shapes sized for the largest problem; slots start bound to the first models
-            seed = models[:width]
-            X0 = [np.zeros((nmax, D)) for _ in seed]
-            Y0 = [np.zeros((nmax, 1)) for _ in seed]
-            engine = Engine(X0, Y0, [compile_spec(m.kernel, D) for m in seed],
-                            device=device if device is not None else models[0].device)
-        step = _LockstepEvaluator(engine, [None] * engine.B, total=len(models), groups=groups)
+            # slot shapes sized for the largest problem; one engine per group
+            per = -(-width // groups)
+            engines = []
+            for g in range(groups):
+                seed = models[g * per:(g + 1) * per] or models[:1]
+                engines.append(Engine([np.zeros((nmax, D)) for _ in seed], [np.zeros((nmax, 1)) for _ in seed],
+                                      [compile_spec(m.kernel, D) for m in seed], device=dev))
+        else:
+            engines = list(engine) if isinstance(engine, (list, tuple)) else [engine]
+        step = _LockstepEvaluator(engines, None, total=len(models), groups=groups)
         free: "queue.Queue[int]" = queue.Queue()
-        for s in range(engine.B):
+        for s in range(step.n_slots):
             free.put(s)
         results = [None] * len(models)
         if predict_inputs is not None:
@@ -178,15 +188,15 @@ class Scipy:
                 raise ValueError("predict_inputs needs one Xnew per model")
         preds = [None] * len(models) if predict_train else None
         errors: List[Optional[BaseException]] = [None] * len(models)
-        lib_lock = step.lib_lock
 
         def worker(i: int):
             m = models[i]
             slot = free.get()
+            eng, local, lock = step.slot_engine(slot)
             try:
-                with lib_lock:
-                    engine.rebind(slot, m.data[0], m.data[1], compile_spec(m.kernel, D))
-                m._attach(engine, slot)
+                with lock:
+                    eng.rebind(local, m.data[0], m.data[1], compile_spec(m.kernel, D))
+                m._attach(eng, local)
                 step.bind(slot, m)
                 variables = m.trainable_variables
 
@@ -200,11 +210,11 @@ class Scipy:
                 results[i] = res
                 if predict_train:
                     step.unbind(slot)  # leave the lock-step set before the predict call
-                    theta = np.ones((engine.B, N.GPX_THETA_STRIDE))
-                    theta[slot] = m.theta_row()
+                    theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+                    theta[local] = m.theta_row()
                     xp = m.data[0] if predict_inputs is None else predict_inputs[i]
-                    with lib_lock:
-                        mu, var, _ = engine.predict([slot], theta, [xp], False)
+                    with lock:
+                        mu, var, _ = eng.predict([local], theta, [xp], False)
                     preds[i] = (mu[0].reshape(-1, 1), var[0].reshape(-1, 1))
             except BaseException as e:
                 errors[i] = e
@@ -230,15 +240,29 @@ class _LockstepEvaluator:
     """Barrier between the optimiser threads and the device: evaluates all pending points in
     one gpx_batch_lml_grad call once every running optimiser has posted one."""
 
-    def __init__(self, engine: Engine, models, total: Optional[int] = None, groups: int = 1):
-        self.engine = engine
+    def __init__(self, engine, models, total: Optional[int] = None, groups: int = 1):
+        # engine: one Engine (slots = its rows; groups alternate on it) or a list of Engines
+        # (one per group; global slot s lives in engines[s % G] at row s // G)
+        self.engines = list(engine) if isinstance(engine, (list, tuple)) else [engine]
+        self.engine = self.engines[0]
+        if len(self.engines) > 1:
+            G = len(self.engines)
+            self.n_slots = G * min(e.B for e in self.engines)
+            self.locks = [threading.Lock() for _ in self.engines]
+            self.streams = [torch.cuda.Stream(device=e.device) for e in self.engines]
+        else:
+            self.n_slots = self.engine.B
+            self.locks = [threading.Lock()]
+            self.streams = [None]
+        if models is None:
+            models = [None] * self.n_slots
         self.models = list(models)
         # slots are split into `groups` (slot % groups); each group has its own server thread
         # and device calls, so one group's host-side work (scipy steps, result unpacking)
         # overlaps the other group's device evaluation
-        self.groups = max(1, int(groups))
+        self.groups = len(self.engines) if len(self.engines) > 1 else max(1, int(groups))
         self.cv = threading.Condition()
-        self.lib_lock = threading.Lock()
+        self.lib_lock = self.locks[0]
         if total is None:  # fixed lock-step batch: every slot runs from the start
             self.running = set(range(len(self.models)))
             self.remaining = len(self.models)
@@ -256,6 +280,13 @@ class _LockstepEvaluator:
         self.last_batch = [None] * self.groups
         # GPX_TRACE_ROUNDS=1: (time, batch size) per device call, for bench diagnostics
         self.trace = [] if os.environ.get("GPX_TRACE_ROUNDS") else None
+
+    def slot_engine(self, s: int):
+        """(engine, row in that engine, its lock) of global slot s."""
+        if len(self.engines) == 1:
+            return self.engine, s, self.locks[0]
+        G = len(self.engines)
+        return self.engines[s % G], s // G, self.locks[s % G]
 
     def bind(self, slot: int, model):
         with self.cv:
@@ -315,8 +346,12 @@ class _LockstepEvaluator:
             raise errs[0]
 
     def _serve(self, g: int):
-        eng = self.engine
         G = self.groups
+        multi = len(self.engines) > 1
+        eng = self.engines[g] if multi else self.engine
+        lock = self.locks[g] if multi else self.locks[0]
+        if multi:
+            torch.cuda.set_stream(self.streams[g])  # this thread's device calls use stream g
         while True:
             with self.cv:
                 while self.remaining > 0 and not self._ready(g):
@@ -328,21 +363,22 @@ class _LockstepEvaluator:
             active = sorted(batch)
             if self.trace is not None:
                 self.trace.append((time.perf_counter(), len(active)))
+            rows = [i // G for i in active] if multi else active
             theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
-            for i in active:
-                theta[i] = self.models[i].theta_row()
+            for i, r in zip(active, rows):
+                theta[r] = self.models[i].theta_row()
             out = {}
             try:
-                with self.lib_lock:
-                    lml, grad, info = eng.lml_grad(active, theta)
-                for i in active:
-                    if info[i] != 0:
+                with lock:
+                    lml, grad, info = eng.lml_grad(rows, theta)
+                for i, r in zip(active, rows):
+                    if info[r] != 0:
                         out[i] = N.NotPositiveDefiniteError(
                             f"Cholesky decomposition was not successful (model {i}, pivot "
-                            f"{int(info[i])}): K + noise I is not positive definite", info[i])
+                            f"{int(info[r])}): K + noise I is not positive definite", info[r])
                     else:
                         out[i] = self.models[i].loss_and_grad_unconstrained(
-                            batch[i], lml=lml[i], grad_theta=grad[i])
+                            batch[i], lml=lml[r], grad_theta=grad[r])
             except BaseException as e:
                 for i in active:
                     out[i] = e
