@@ -487,3 +487,33 @@ def test_config3_twenty_series_fit_assets():
         ell, s2 = res[i]["theta"][:2]
         om = O.OGPR(x, y, O.OSquaredExponential(lengthscales=ell, variance=s2), noise_variance=1e-5)
         assert res[i]["loss"] == pytest.approx(-om.log_marginal_likelihood(), rel=1e-8)
+
+
+def test_n8192_logml_and_gradient_properties():
+    """N = 8192 (twice config C2): logML against the oracle's Cholesky, gradient against central
+    differences of the device logML, predict at the training inputs vs the general path."""
+    n = 8192
+    x, y = O.synthetic_series(n, seed=9)
+    k = K.SquaredExponential(lengthscales=50.0, variance=1.1)
+    m = gpx.models.GPR((x, y), kernel=k, noise_variance=1e-2)
+    gpx.set_trainable(m.likelihood.variance, False)
+    loss, g = m.loss_and_grad_unconstrained()
+    om = O.OGPR(x, y, O.OSquaredExponential(lengthscales=50.0, variance=1.1), noise_variance=1e-2)
+    assert -loss == pytest.approx(om.log_marginal_likelihood(), rel=1e-10)
+    u0 = np.array([v.numpy() for v in m.trainable_variables], dtype=float)
+    h = 1e-4
+    for i in range(2):
+        vals = []
+        for sgn in (1, -1):
+            u = u0.copy()
+            u[i] += sgn * h
+            for v, ui in zip(m.trainable_variables, u):
+                v.assign(ui)
+            vals.append(float(m.training_loss()))
+        assert (vals[0] - vals[1]) / (2 * h) == pytest.approx(g[i], rel=1e-5, abs=1e-4)
+    for v, ui in zip(m.trainable_variables, u0):
+        v.assign(ui)
+    mu, var = m.predict_f(x)
+    mg, vg = m.predict_f(np.concatenate([x, x[:1]]))
+    np.testing.assert_allclose(mu.numpy(), mg.numpy()[:-1], rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(var.numpy(), vg.numpy()[:-1], rtol=1e-6, atol=1e-10)

@@ -32,7 +32,8 @@ int main(int argc, char** argv) {
   Case cases[] = {{"NT full K/2", false, true, 0, 0, 2}, {"NN full K/2", false, false, 0, 0, 2},{"NN full", false, false, 0, 0}, {"NT full", false, true, 0, 0}, {"TN full", true, false, 0, 0},
                   {"NT syrk(lower)", false, true, 0, 1}, {"NT trmm kmax_j", false, true, TRI_KMAX_J, 0},
                   {"NN trmm kmin_j", false, false, TRI_KMIN_J, 0}, {"NN trmm kmax_i", false, false, TRI_KMAX_I, 0},
-                  {"TN lauum(lower,kmin_i)", true, false, TRI_KMIN_I, 1}};
+                  {"TN lauum(lower,kmin_i)", true, false, TRI_KMIN_I, 1},
+                  {"TN syrk(lower)", true, false, 0, 1}, {"NT lauum(lower,kmin_i)", false, true, TRI_KMIN_I, 1}};
   for (auto& c : cases) {
     if (only && std::string(c.name).rfind(only, 0) != 0) continue;
     GemmArgs g{};
