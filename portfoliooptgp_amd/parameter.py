@@ -125,24 +125,49 @@ class Parameter:
 # ----------------------------------------------------------------------------------------
 # array-valued parameters (SVGP: inducing inputs Z, q_mu, q_sqrt)
 # ----------------------------------------------------------------------------------------
+_TRI_CACHE = {}
+
+
+def _tri_index(n: int):
+    """(flat positions of the lower triangle of an n×n matrix, the vector index stored at each)
+    for tfp's fill_triangular layout, computed once per n (a gather/scatter pair then replaces
+    the concatenate/reverse/reshape of the definition below)."""
+    hit = _TRI_CACHE.get(n)
+    if hit is None:
+        m = n * (n + 1) // 2
+        x = np.arange(m, dtype=np.float64)
+        full = np.tril(np.concatenate([x[n:], x[::-1]]).reshape(n, n))
+        r, c = np.tril_indices(n)
+        flat = r * n + c
+        hit = (flat, full.reshape(-1)[flat].astype(np.int64))
+        _TRI_CACHE[n] = hit
+    return hit
+
+
 def fill_triangular(x: np.ndarray) -> np.ndarray:
     """tfp.math.fill_triangular(x, upper=False): the vector → lower-triangular layout that
-    tfp.bijectors.FillTriangular (GPflow's ``triangular()`` transform of q_sqrt) uses."""
+    tfp.bijectors.FillTriangular (GPflow's ``triangular()`` transform of q_sqrt) uses:
+    L = tril(reshape(concat(x[n:], reverse(x)), [n, n]))."""
     x = np.asarray(x, dtype=np.float64)
     m = x.shape[-1]
     n = (math.isqrt(8 * m + 1) - 1) // 2
     if n * (n + 1) // 2 != m:
         raise ValueError(f"fill_triangular: {m} is not a triangular number")
-    return np.tril(np.concatenate([x[n:], x[::-1]]).reshape(n, n))
+    flat, src = _tri_index(n)
+    L = np.zeros(n * n)
+    L[flat] = x[src]
+    return L.reshape(n, n)
 
 
 def fill_triangular_inverse(L: np.ndarray) -> np.ndarray:
-    """tfp.math.fill_triangular_inverse(L, upper=False)."""
+    """tfp.math.fill_triangular_inverse(L, upper=False) (the lower triangle of L, gathered back
+    into fill_triangular's vector order)."""
     L = np.asarray(L, dtype=np.float64)
     n = L.shape[-1]
-    tri = L[:-1, :]
-    rest = (tri + tri[::-1, ::-1]).reshape(-1)[: n * (n + 1) // 2 - n]
-    return np.concatenate([L[-1, ::-1], rest])
+    flat, src = _tri_index(n)
+    x = np.empty(n * (n + 1) // 2)
+    x[src] = L.reshape(-1)[flat]
+    return x
 
 
 class ArrayVariable:
