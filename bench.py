@@ -10,9 +10,12 @@ GPflow defaults (σ²=1, ℓ=1), σn²=1e-5 fixed, scipy L-BFGS-B (maxiter=100) 
 unconstrained variables to termination, then predict_f at the N training points.
 
 One *step* = fitting `--fits` independent series per GPU (each driven by its own unmodified
-scipy L-BFGS-B) through `--width` resident device slots with continuous batching: the
-evaluations of all resident fits run as one batched device pass, and a slot is refilled as
-soon as its fit converges and has run its predict_f. For N > 1 GPUs the step ends with an
+scipy L-BFGS-B, from a fresh GPR model at GPflow defaults) through `--width` resident device
+slots with continuous batching: the evaluations of all resident fits run as batched device
+passes (`--groups` concurrent device batches), and a slot is refilled as soon as its fit
+converges and has run its predict_f. The K timed steps are streamed back to back through the
+slots (the next step's fits take slots as the previous step's finish; no drain between steps),
+bracketed by one barrier + synchronize on each side. For N > 1 GPUs the step ends with an
 RCCL all_gather of every fit's (θ*, loss*, nfev, last predicted mean/var) — the per-asset
 hand-off to the portfolio step.
 Inputs are resident in HBM before the timed region. Each rank fits its own series
@@ -155,27 +158,33 @@ def main():
     data = [synthetic_series(n, s) for s in seeds]
     Xd = [torch.as_tensor(x, device=dev) for x, _ in data]  # resident in HBM before timing
     Yd = [torch.as_tensor(y, device=dev) for _, y in data]
-    models = [gpx.models.GPR(data=(Xd[f], Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=gpu)
+    def make_models():
+        # GPflow defaults (σ²=1, ℓ=1), σn² = 1e-5 frozen — GPR/model_trainer.py:15-17
+        ms = [gpx.models.GPR(data=(Xd[f], Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=gpu)
               for f in range(F)]
-    for m in models:
-        m.likelihood.variance.assign(NOISE)
-        gpx.set_trainable(m.likelihood.variance, False)
+        for m in ms:
+            m.likelihood.variance.assign(NOISE)
+            gpx.set_trainable(m.likelihood.variance, False)
+        return ms
+
     # W resident device slots (continuous batching), sized for N-point problems, split into
     # `groups` independent device batches evaluated concurrently on their own streams
     G = max(1, args.groups)
     per = W // G
+    proto = make_models()
     engines = [Engine(Xd[g * per:(g + 1) * per], Yd[g * per:(g + 1) * per],
-                      [compile_spec(m.kernel, 1) for m in models[g * per:(g + 1) * per]], device=gpu)
+                      [compile_spec(m.kernel, 1) for m in proto[g * per:(g + 1) * per]], device=gpu)
                for g in range(G)]
     engines[0].ctx.set_profiling(True)
     opt = gpx.optimizers.Scipy()
 
     traces = []
 
-    def one_step():
-        for m in models:  # every step starts from GPflow defaults
-            m.kernel.lengthscales.assign(1.0)
-            m.kernel.variance.assign(1.0)
+    def run_steps(k):
+        """k steps (k × F fits, each from GPflow defaults) streamed back to back through the
+        slots — the next step's fits fill slots as the previous step's finish, no drain in
+        between — then every fit's summary row, all_gathered across ranks."""
+        models = [m for _ in range(k) for m in make_models()]
         res, preds = opt.minimize_stream(models, width=W, engine=engines, predict_train=True, groups=G,
                                          options=dict(maxiter=MAXITER))
         if getattr(opt, "last_trace", None):
@@ -194,18 +203,16 @@ def main():
             summary = torch.cat(gathered)
         return res, summary
 
-    for _ in range(args.warmup):
-        one_step()
+    if args.warmup > 0:
+        run_steps(args.warmup)
     for e in engines:
         e.reset_timing()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    nfev = []
-    for _ in range(args.steps):
-        res, summary = one_step()
-        nfev.extend(r.nfev for r in res)
+    res, summary = run_steps(args.steps)
+    nfev = [r.nfev for r in res]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
