@@ -194,7 +194,9 @@ class Scipy:
             slot = free.get()
             eng, local, lock = step.slot_engine(slot)
             try:
-                with lock:
+                # the slot is idle, so loading the new problem needs no engine lock: its copies
+                # run on a side stream while the group's evaluation of other slots proceeds
+                with torch.cuda.stream(torch.cuda.Stream(device=eng.device)):
                     eng.rebind(local, m.data[0], m.data[1], compile_spec(m.kernel, D))
                 m._attach(eng, local)
                 step.bind(slot, m)
@@ -210,12 +212,10 @@ class Scipy:
                 results[i] = res
                 if predict_train:
                     step.unbind(slot)  # leave the lock-step set before the predict call
-                    theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
-                    theta[local] = m.theta_row()
                     xp = m.data[0] if predict_inputs is None else predict_inputs[i]
-                    with lock:
-                        mu, var, _ = eng.predict([local], theta, [xp], False)
-                    preds[i] = (mu[0].reshape(-1, 1), var[0].reshape(-1, 1))
+                    # executed by the slot's server thread between its device calls
+                    mu, var = step.predict(slot, m.theta_row(), xp)
+                    preds[i] = (mu.reshape(-1, 1), var.reshape(-1, 1))
             except BaseException as e:
                 errors[i] = e
             finally:
@@ -274,6 +274,9 @@ class _LockstepEvaluator:
         self.pending = {}
         self.results = {}
         self.rounds = 0
+        # predict requests of finished fits, run by the slot's server thread between device
+        # calls (no engine-lock wait behind a whole evaluation)
+        self.admin = [[] for _ in range(self.groups)]
         # slots of the previous device call; only these (if still running) are waited for —
         # a fit bound since then joins whichever round it posts in time for, so rebinding a
         # slot never stalls the device
@@ -309,6 +312,35 @@ class _LockstepEvaluator:
         if isinstance(res, BaseException):
             raise res
         return res
+
+    def predict(self, slot: int, theta_row, Xnew):
+        G = self.groups
+        job = {"slot": slot, "theta": np.asarray(theta_row, dtype=np.float64), "x": Xnew, "out": None}
+        with self.cv:
+            self.admin[slot % G].append(job)
+            self.cv.notify_all()
+            while job["out"] is None:
+                self.cv.wait()
+        if isinstance(job["out"], BaseException):
+            raise job["out"]
+        return job["out"]
+
+    def _run_admin(self, g: int, eng, lock, multi: bool):
+        with self.cv:
+            jobs, self.admin[g] = self.admin[g], []
+        G = self.groups
+        for job in jobs:
+            try:
+                row = job["slot"] // G if multi else job["slot"]
+                theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+                theta[row] = job["theta"]
+                with lock:
+                    mu, var, _ = eng.predict([row], theta, [job["x"]], False)
+                job["out"] = (mu[0], var[0])
+            except BaseException as e:
+                job["out"] = e
+        with self.cv:
+            self.cv.notify_all()
 
     def finish(self, i: int):
         with self.cv:
@@ -354,10 +386,17 @@ class _LockstepEvaluator:
             torch.cuda.set_stream(self.streams[g])  # this thread's device calls use stream g
         while True:
             with self.cv:
-                while self.remaining > 0 and not self._ready(g):
+                while self.remaining > 0 and not self._ready(g) and not self.admin[g]:
                     self.cv.wait()
-                if self.remaining <= 0:
+                if self.remaining <= 0 and not self.admin[g]:
                     return
+                run_admin = bool(self.admin[g])
+            if run_admin:
+                self._run_admin(g, eng, lock, multi)
+                continue
+            with self.cv:
+                if not self._ready(g):
+                    continue
                 batch = {i: self.pending.pop(i) for i in [i for i in self.pending if i % G == g]}
                 self.last_batch[g] = set(batch)
             active = sorted(batch)
