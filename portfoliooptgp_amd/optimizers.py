@@ -277,6 +277,13 @@ class _LockstepEvaluator:
         # predict requests of finished fits, run by the slot's server thread between device
         # calls (no engine-lock wait behind a whole evaluation)
         self.admin = [[] for _ in range(self.groups)]
+        # stagger: group g ≥ 1 starts its first device call g/G of a group-0 call after group 0's
+        # first call returns, so the concurrent batches run out of phase (one batch's
+        # latency-bound recursion levels under the other's large GEMMs); started in phase they
+        # stay in phase
+        self.rounds_g = [0] * self.groups
+        self.first_call = threading.Event()
+        self.first_call_s = 0.0
         # slots of the previous device call; only these (if still running) are waited for —
         # a fit bound since then joins whichever round it posts in time for, so rebinding a
         # slot never stalls the device
@@ -378,6 +385,13 @@ class _LockstepEvaluator:
             raise errs[0]
 
     def _serve(self, g: int):
+        try:
+            self._serve_loop(g)
+        finally:
+            if g == 0:
+                self.first_call.set()
+
+    def _serve_loop(self, g: int):
         G = self.groups
         multi = len(self.engines) > 1
         eng = self.engines[g] if multi else self.engine
@@ -399,9 +413,13 @@ class _LockstepEvaluator:
                     continue
                 batch = {i: self.pending.pop(i) for i in [i for i in self.pending if i % G == g]}
                 self.last_batch[g] = set(batch)
+            if multi and g > 0 and self.rounds_g[g] == 0:
+                self.first_call.wait(timeout=10.0)
+                time.sleep(self.first_call_s * g / G)
             active = sorted(batch)
             if self.trace is not None:
                 self.trace.append((time.perf_counter(), len(active)))
+            t_call = time.perf_counter()
             rows = [i // G for i in active] if multi else active
             theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
             for i, r in zip(active, rows):
@@ -421,6 +439,10 @@ class _LockstepEvaluator:
             except BaseException as e:
                 for i in active:
                     out[i] = e
+            if g == 0 and self.rounds_g[0] == 0:
+                self.first_call_s = time.perf_counter() - t_call
+                self.first_call.set()
+            self.rounds_g[g] += 1
             with self.cv:
                 self.rounds += 1
                 self.results.update(out)
