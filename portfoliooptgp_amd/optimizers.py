@@ -14,6 +14,7 @@ to sequential fitting while the device works on all fits at once.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import queue
 import threading
@@ -27,6 +28,15 @@ import torch
 from . import _native as N
 from .engine import Engine
 from .kernels import compile_spec
+
+
+def _new_stream(device):
+    """A HIP stream from torch's pool (None without a device: the CPU test doubles)."""
+    return torch.cuda.Stream(device=device) if torch.cuda.is_available() else None
+
+
+def _stream_ctx(stream):
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
 
 def _resolve_model(closure):
@@ -196,7 +206,7 @@ class Scipy:
             try:
                 # the slot is idle, so loading the new problem needs no engine lock: its copies
                 # run on a side stream while the group's evaluation of other slots proceeds
-                with torch.cuda.stream(torch.cuda.Stream(device=eng.device)):
+                with _stream_ctx(_new_stream(eng.device)):
                     eng.rebind(local, m.data[0], m.data[1], compile_spec(m.kernel, D))
                 m._attach(eng, local)
                 step.bind(slot, m)
@@ -249,7 +259,7 @@ class _LockstepEvaluator:
             G = len(self.engines)
             self.n_slots = G * min(e.B for e in self.engines)
             self.locks = [threading.Lock() for _ in self.engines]
-            self.streams = [torch.cuda.Stream(device=e.device) for e in self.engines]
+            self.streams = [_new_stream(e.device) for e in self.engines]
         else:
             self.n_slots = self.engine.B
             self.locks = [threading.Lock()]
@@ -396,7 +406,7 @@ class _LockstepEvaluator:
         multi = len(self.engines) > 1
         eng = self.engines[g] if multi else self.engine
         lock = self.locks[g] if multi else self.locks[0]
-        if multi:
+        if multi and self.streams[g] is not None:
             torch.cuda.set_stream(self.streams[g])  # this thread's device calls use stream g
         while True:
             with self.cv:

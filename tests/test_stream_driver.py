@@ -1,0 +1,84 @@
+"""The streaming / lock-step drivers of optimizers.Scipy on the CPU with a stand-in engine:
+every fit must see exactly the trajectory it would see alone, whatever the slot count, the
+number of concurrent device batches, and the refill order (the device arithmetic is covered
+by the GPU tests; this pins the host-side scheduling: barriers, rebinding, predict requests)."""
+import numpy as np
+import pytest
+import scipy.optimize
+import torch
+
+import portfoliooptgp_amd as gpx
+from portfoliooptgp_amd import _native as N
+
+
+class FakeEngine:
+    """lml(θ) = −Σ_p (log θ_p − log t_p)² with per-problem targets t from the bound data."""
+
+    def __init__(self, B):
+        self.B, self.device = B, 0
+        self.target = np.ones((B, 2))
+        self.calls = []
+
+    def rebind(self, b, X, Y, spec):
+        y = np.asarray(Y, dtype=np.float64).reshape(-1)
+        self.target[b] = [1.0 + abs(y.mean()) * 3.0, 0.5 + y.std()]
+
+    def lml_grad(self, rows, theta):
+        self.calls.append(len(rows))
+        lml = np.full(self.B, np.nan)
+        grad = np.full((self.B, N.GPX_THETA_STRIDE), np.nan)
+        info = np.zeros(self.B, dtype=np.int32)
+        for r in rows:
+            d = np.log(theta[r, :2]) - np.log(self.target[r])
+            lml[r] = -np.sum(d * d)
+            grad[r] = 0.0
+            grad[r, :2] = -2.0 * d / theta[r, :2]
+        return lml, grad, info
+
+    def predict(self, rows, theta, xs, add_noise):
+        return ([torch.full((len(x),), float(theta[r, 0])) for r, x in zip(rows, xs)],
+                [torch.full((len(x),), float(theta[r, 1])) for r, x in zip(rows, xs)], None)
+
+
+def _models(k):
+    rng = np.random.default_rng(0)
+    out = []
+    for i in range(k):
+        x = np.arange(10.0)[:, None]
+        y = rng.standard_normal((10, 1)) * (1 + i % 3) + 0.2 * i
+        m = gpx.models.GPR((x, y), kernel=gpx.kernels.SquaredExponential())
+        m.likelihood.variance.assign(1e-5)
+        gpx.set_trainable(m.likelihood.variance, False)
+        out.append(m)
+    return out
+
+
+def _solo(m):
+    eng = FakeEngine(1)
+    eng.rebind(0, m.data[0], m.data[1], None)
+    v = m.trainable_variables
+
+    def f(u):
+        for var, ui in zip(v, u):
+            var.assign(ui)
+        th = np.ones((1, N.GPX_THETA_STRIDE))
+        th[0] = m.theta_row()
+        lml, g, _ = eng.lml_grad([0], th)
+        return m.loss_and_grad_unconstrained(v, lml=lml[0], grad_theta=g[0])
+    return scipy.optimize.minimize(f, np.array([x.numpy() for x in v], dtype=float), jac=True,
+                                   method="L-BFGS-B")
+
+
+@pytest.mark.parametrize("width,groups,engines", [(3, 1, 1), (4, 2, 1), (4, 2, 2), (6, 3, 3)])
+def test_stream_equals_solo(width, groups, engines):
+    ms = _models(11)
+    ref = [_solo(m) for m in _models(11)]
+    per = width // engines
+    eng = [FakeEngine(per) for _ in range(engines)]
+    res, preds = gpx.optimizers.Scipy().minimize_stream(
+        ms, width=width, engine=eng if engines > 1 else eng[0], groups=groups, predict_train=True)
+    for r, r0, m, p in zip(res, ref, ms, preds):
+        assert r.nfev == r0.nfev
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+        assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
+    assert max(max(e.calls) for e in eng) <= per
