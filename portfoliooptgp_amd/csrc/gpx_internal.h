@@ -58,6 +58,9 @@ struct GemmArgs {
   const double* X; long long sX; int D;
   const DevSpec* specs; const double* theta; const int* nvalid;
   double* partial; long long sPartial;      // [B][ntiles][16] / [B][rowtiles][ldc]
+  // host-side only: when set, the launch is timestamped at the kernel's actual start and end
+  // (hipExtLaunchKernel), excluding any wait for resources held by other streams
+  hipEvent_t ev_start, ev_stop;
 };
 
 // ---- vectors --------------------------------------------------------------------------

@@ -11,6 +11,7 @@
 //   reduce_kernel       logML and ½Σ(αα−K⁻¹)∘∂K/∂θ from per-tile partials (deterministic)
 // and for predict_f: the cross-covariance build, mean = Kxsᵀα, and W·Kxs with a fused
 // column-sum-of-squares epilogue (EPI_COLSUMSQ) for the variance.
+#include <hip/hip_ext.h>
 #include "gpx_internal.h"
 
 namespace gpx {
@@ -556,6 +557,12 @@ static void launch_gemm_t(const GemmArgs& a0, bool ta, bool tb, int n_active, hi
   const int ntiles = a.lower_only ? ti * (ti + 1) / 2 : ti * tj;
   const int q = n_active / 8, r = n_active % 8;
   dim3 grid(8 * (q * ntiles + (r * ntiles + 7) / 8));
+  if (a.ev_start) {
+    auto k = (!ta && !tb) ? gemm_kernel<BM, false, false, EPI> : (!ta && tb) ? gemm_kernel<BM, false, true, EPI>
+           : (ta && !tb) ? gemm_kernel<BM, true, false, EPI> : gemm_kernel<BM, true, true, EPI>;
+    hipExtLaunchKernelGGL(k, grid, dim3(256), 0, s, a.ev_start, a.ev_stop, 0, a);
+    return;
+  }
   if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<BM, false, false, EPI>), grid, dim3(256), 0, s, a);
   else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<BM, false, true, EPI>), grid, dim3(256), 0, s, a);
   else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<BM, true, false, EPI>), grid, dim3(256), 0, s, a);
