@@ -94,7 +94,6 @@ void chol_inv(const Run& r, int off, int n, int depth) {
   // concurrently with the (latency-bound) recursion on A22 below.
   const GemmArgs targs = gemm_args(bt->L + o21, Np, bt->W + o11, Np, bt->K + o21, Np, st, n2, n1,
                                    n1, TRI_KMIN_J, 0, 1.0, 0.0);
-  gpx_ctx* ctx = bt->ctx;
   const bool fork = r.dag && depth < kAux && r.next_event && *r.next_event + 2 <= kEvents;
   hipEvent_t eT = nullptr;
   if (fork) {
