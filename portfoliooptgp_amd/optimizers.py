@@ -395,9 +395,13 @@ class _LockstepEvaluator:
             raise errs[0]
 
     def _serve(self, g: int):
+        # group 0 is served on the caller's thread: restore its current stream afterwards
+        prev = torch.cuda.current_stream() if (len(self.engines) > 1 and self.streams[g] is not None) else None
         try:
             self._serve_loop(g)
         finally:
+            if prev is not None:
+                torch.cuda.set_stream(prev)
             if g == 0:
                 self.first_call.set()
 
