@@ -153,7 +153,13 @@ def svgp_elbo_grad(engine, theta, Z, q_mu, q_sqrt, group=None):
     the replicated O(M³) tail. Every rank returns the same (ELBO, ∂θ, ∂Z, ∂q_mu, ∂q_sqrt)."""
     engine.eval_local(theta, Z, q_mu, q_sqrt)
     if dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(engine.partials, op=dist.ReduceOp.SUM, group=group)
+        buf = engine.partials
+        if buf.is_cuda and dist.get_backend(group) != "nccl":   # gloo: reduce a host copy
+            host = buf.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            buf.copy_(host)
+        else:
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
     return engine.eval_finish()
 
 
