@@ -333,6 +333,7 @@ int gpx_batch_destroy(gpx_batch* bt) {
     if (p) (void)hipFree(p);
   for (int g = 0; g < kAux; ++g)
     if (bt->aux[g]) (void)hipStreamDestroy(bt->aux[g]);
+  if (bt->hp) (void)hipStreamDestroy(bt->hp);
   for (int e = 0; e < kEvents; ++e)
     if (bt->ev[e]) (void)hipEventDestroy(bt->ev[e]);
   delete bt;
@@ -432,10 +433,31 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     HIPX(ctx, hipEventCreate(&kev[0]));
     HIPX(ctx, hipEventCreate(&kev[1]));
   }
+  // optional: run the contraction on a highest-priority stream so that, with several batches
+  // evaluating concurrently, its workgroups are dispatched ahead of the other batches' kernels
+  static const bool prio = [] {
+    const char* e = getenv("GPX_CONTRACT_PRIORITY");
+    return e && atoi(e) != 0;
+  }();
+  Run cr = all;
+  if (prio) {
+    if (!bt->hp) {
+      int lo = 0, hi = 0;
+      HIPX(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPX(ctx, hipStreamCreateWithPriority(&bt->hp, hipStreamNonBlocking, hi));
+    }
+    HIPX(ctx, hipEventRecord(bt->ev[kEvents - 4], s));
+    HIPX(ctx, hipStreamWaitEvent(bt->hp, bt->ev[kEvents - 4], 0));
+    cr.s = bt->hp;
+  }
   ct.mark();
-  contract(all, single_term, kev[0], kev[1]);
+  contract(cr, single_term, kev[0], kev[1]);
   ct.mark();
-  reduce(all);
+  reduce(cr);
+  if (prio) {
+    HIPX(ctx, hipEventRecord(bt->ev[kEvents - 3], bt->hp));
+    HIPX(ctx, hipStreamWaitEvent(s, bt->ev[kEvents - 3], 0));
+  }
   ct.mark();
   total.mark();
   HIPX(ctx, hipGetLastError());

@@ -55,6 +55,7 @@ struct gpx_batch {
   // independent batches of one context can evaluate concurrently on different streams
   hipStream_t aux[kAux] = {};
   hipEvent_t ev[kEvents] = {};
+  hipStream_t hp = nullptr;   // highest-priority stream for the contraction (GPX_CONTRACT_PRIORITY)
 };
 
 namespace gpx {
