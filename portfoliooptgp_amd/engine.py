@@ -329,3 +329,41 @@ class SVGPEngine:
                                        ctypes.byref(info), self._stream())
         self._raise(rc, "gpx_svgp_predict", info)
         return mean, var
+
+
+# ----------------------------------------------------------------------------------------
+# pooled single-problem engines for models used on their own (no batch engine attached)
+# ----------------------------------------------------------------------------------------
+_SOLO_POOL: "OrderedDict" = None
+_SOLO_POOL_MAX = 8
+
+
+def solo_engine(model) -> Engine:
+    """A B=1 engine for `model`'s shape, shared by every model of that (device, padded N, D):
+    the reference fits many models one after another (GPR/main.py's ticker × timeframe ×
+    kernel loop), and a fresh N×N workspace per model would grow device memory without
+    bound. The model's data is rebound into the slot when another model used it last (the
+    cached factor is dropped then, so results never mix)."""
+    global _SOLO_POOL
+    import weakref
+    from collections import OrderedDict
+    if _SOLO_POOL is None:
+        _SOLO_POOL = OrderedDict()
+    X, Y = model.data
+    n, D = int(X.shape[0]), int(X.shape[1])
+    key = (int(model.device), (n + 63) // 64 * 64, D)
+    eng = _SOLO_POOL.get(key)
+    if eng is None:
+        npad = key[1]
+        eng = Engine([torch.zeros(npad, D, dtype=torch.float64)], [torch.zeros(npad, 1, dtype=torch.float64)],
+                     [model._spec], device=model.device)
+        eng._owner = None
+        _SOLO_POOL[key] = eng
+        while len(_SOLO_POOL) > _SOLO_POOL_MAX:
+            _SOLO_POOL.popitem(last=False)
+    _SOLO_POOL.move_to_end(key)
+    owner = eng._owner() if eng._owner is not None else None
+    if owner is not model:
+        eng.rebind(0, X, Y, model._spec)
+        eng._owner = weakref.ref(model)
+    return eng

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .engine import Engine, default_device
+from .engine import Engine, default_device, solo_engine
 from .kernels import Kernel, compile_spec
 from .likelihoods import Gaussian
 from .parameter import Parameter
@@ -98,10 +98,10 @@ class GPR:
         self._engine, self._engine_index = engine, index
 
     def engine(self) -> Tuple[Engine, int]:
+        """(engine, slot): the batch engine this model was attached to, else a pooled
+        single-problem engine for its shape (engine.solo_engine)."""
         if self._engine is None:
-            X, Y = self.data
-            self._engine = Engine([X], [Y], [self._spec], device=self.device)
-            self._engine_index = 0
+            return solo_engine(self), 0
         return self._engine, self._engine_index
 
     def _wrap(self, t: torch.Tensor) -> torch.Tensor:
@@ -183,7 +183,10 @@ class GPR:
 
 
 def predict_f_batch(models: Sequence[GPR], Xnews: Sequence, add_noise: bool = False):
-    """predict_f (or predict_y) for several models sharing one engine, in one device pass."""
+    """predict_f (or predict_y) for several models sharing one engine, in one device pass.
+    Models not attached to a shared batch engine are predicted one by one."""
+    if any(m._engine is None for m in models):
+        return [(m.predict_y(x) if add_noise else m.predict_f(x)) for m, x in zip(models, Xnews)]
     eng, _ = models[0].engine()
     idx = []
     for m in models:
