@@ -517,3 +517,23 @@ def test_n8192_logml_and_gradient_properties():
     mg, vg = m.predict_f(np.concatenate([x, x[:1]]))
     np.testing.assert_allclose(mu.numpy(), mg.numpy()[:-1], rtol=1e-7, atol=1e-9)
     np.testing.assert_allclose(var.numpy(), vg.numpy()[:-1], rtol=1e-6, atol=1e-10)
+
+
+def test_pooled_solo_engines_interleaved_models():
+    """Models used on their own share a pooled single-problem engine per shape; interleaving
+    two same-shaped models rebinds the slot and never mixes their data or cached factors."""
+    xa, ya = O.synthetic_series(300, seed=21)
+    xb, yb = O.synthetic_series(290, seed=22)          # same padded size (320)
+    a = gpx.models.GPR((xa, ya), kernel=K.SquaredExponential(lengthscales=7.0), noise_variance=1e-3)
+    b = gpx.models.GPR((xb, yb), kernel=K.Matern32(lengthscales=4.0), noise_variance=1e-2)
+    la1, ga1 = a.loss_and_grad_unconstrained()
+    ma1, _ = a.predict_f(xa[:5] + 0.5)
+    lb1, gb1 = b.loss_and_grad_unconstrained()
+    la2, ga2 = a.loss_and_grad_unconstrained()
+    mb1, _ = b.predict_f(xb)
+    ma2, _ = a.predict_f(xa[:5] + 0.5)
+    assert a.engine()[0] is b.engine()[0]
+    assert la1 == la2 and np.array_equal(ga1, ga2) and np.array_equal(ma1.numpy(), ma2.numpy())
+    ob = O.OGPR(xb, yb, O.OMatern32(lengthscales=4.0), noise_variance=1e-2)
+    assert lb1 == pytest.approx(ob.loss_and_grad_u()[0], rel=1e-10)
+    check_mean(mb1.numpy(), ob.predict_f(xb)[0])
