@@ -423,8 +423,10 @@ int gpx_svgp_eval_finish(gpx_svgp* sv, double* elbo, double* grad_theta, double*
   for (int m = 0; m < M; ++m)
     for (int d = 0; d < D; ++d) grad_Z[(size_t)m * D + d] = pz[(size_t)m * D + d] + fz[(size_t)m * D + d];
   for (int m = 0; m < M; ++m) grad_qmu[m] = sv->h_ahat[m] - sv->h_q[m];
-  for (int i = 0; i < M; ++i)
-    for (int j = 0; j < M; ++j) grad_qsqrt[(size_t)i * M + j] = (j <= i) ? sv->h_Rbar[(size_t)i * Mp + j] : 0.0;
+  for (int i = 0; i < M; ++i) {
+    std::memcpy(grad_qsqrt + (size_t)i * M, sv->h_Rbar + (size_t)i * Mp, sizeof(double) * (i + 1));
+    std::memset(grad_qsqrt + (size_t)i * M + i + 1, 0, sizeof(double) * (M - i - 1));
+  }
   return GPX_OK;
 }
 
