@@ -388,7 +388,9 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
 
   // Register-staged double buffer; the last K-tile is peeled so the loop body has no
   // conditionals (a conditional prefetch made hipcc shuttle every accumulator between AGPRs
-  // and VGPRs once per K-tile).
+  // and VGPRs once per K-tile). (Splitting the loop into load-only / load+compute phases to
+  // skip a wave's all-zero k-tiles in triangular tiles cost 7 % on full GEMMs through the
+  // compiler's scheduling of the main loop, more than the skipped work.)
   const int nk = (kmax - kmin) / BK;
   if (nk > 0) {
     gload(kmin);
@@ -540,13 +542,14 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
   }
 }
 
-// 128x128 tiles when they still give every CU about two workgroups, else 64x64 tiles:
-// small recursion levels are latency-bound on a single CU per tile otherwise.
+// 128x128 tiles for operands of at least 512x512, else 64x64 tiles (small recursion levels are
+// latency-bound on a single CU per tile otherwise). The choice depends on the shape only, not
+// on how many problems share the launch, so a problem's arithmetic — and therefore its fit —
+// is bit-identical whichever other problems are batched with it (same padded size Np).
 int gemm_tile(const GemmArgs& a, int n_active) {
+  (void)n_active;
   if (a.M % 128 != 0 || a.N % 128 != 0) return 64;
-  const long long t = (long long)(a.M / 128) * (a.N / 128);
-  const long long tiles = a.lower_only ? (long long)(a.M / 128) * (a.M / 128 + 1) / 2 : t;
-  return tiles * n_active >= 384 ? 128 : 64;
+  return (a.M >= 512 && a.N >= 512) ? 128 : 64;
 }
 
 template <int BM, int EPI>
@@ -587,34 +590,54 @@ void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hip
 // ======================================================================================
 // y = M x (row dot products; lower: k <= i). 64 rows per WG, 16 rows per wave.
 // ======================================================================================
+// Both matrix-vector kernels are HBM streams over W's lower triangle; a workgroup's rate is set
+// by the loads each wave keeps in flight (latency-bound otherwise, and the long-row workgroups
+// set the kernel's tail), so each wave runs 8 independent row (column) streams and the longest
+// workgroups are dispatched first.
 __global__ __launch_bounds__(256) void trmv_n_kernel(TrmvArgs a) {
+  constexpr int R = 8;
   const int b = a.active[blockIdx.y];
   const double* M = a.Wm + (long long)b * a.sW;
   const double* x = a.x + (long long)b * a.sx;
   const int nx = a.nvalid ? a.nvalid[b] : a.cols;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // four rows at a time per wave: four independent load streams in flight
-  for (int rr = 0; rr < 16; rr += 4) {
-    const int i0 = blockIdx.x * 64 + wave * 16 + rr;
+  const int rb = (a.lower ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x);  // longest rows first
+  for (int rr = 0; rr < 16; rr += R) {
+    const int i0 = rb * 64 + wave * 16 + rr;
     if (i0 >= a.rows) break;
-    const int kend = a.lower ? min(i0 + 4, a.cols) : a.cols;
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    double s[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) s[q] = 0.0;
     const double* r0 = M + (long long)i0 * a.ld;
-    for (int k = lane; k < kend; k += 64) {
-      const double xv = (k < nx) ? x[k] : 0.0;
-      // rows beyond a.rows or entries above the diagonal read as zero
-      if (!a.lower || k <= i0) s0 = fma(r0[k], xv, s0);
-      if (i0 + 1 < a.rows && (!a.lower || k <= i0 + 1)) s1 = fma(r0[a.ld + k], xv, s1);
-      if (i0 + 2 < a.rows && (!a.lower || k <= i0 + 2)) s2 = fma(r0[2 * a.ld + k], xv, s2);
-      if (i0 + 3 < a.rows && (!a.lower || k <= i0 + 3)) s3 = fma(r0[3 * (long long)a.ld + k], xv, s3);
+    // full part: k < i0 is inside every row's triangle (and k < cols), no per-row checks
+    const int kfull = a.lower ? min(i0, a.cols) : a.cols;
+    const bool rows_ok = i0 + R <= a.rows;
+    int k = lane;
+    if (rows_ok) {
+      for (; k < kfull; k += 64) {
+        const double xv = (k < nx) ? x[k] : 0.0;
+        double m[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) m[q] = r0[(long long)q * a.ld + k];
+#pragma unroll
+        for (int q = 0; q < R; ++q) s[q] = fma(m[q], xv, s[q]);
+      }
     }
-    s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2); s3 = wave_sum(s3);
+    // remainder: entries above the diagonal and rows beyond a.rows read as zero
+    const int kend = a.lower ? min(i0 + R, a.cols) : a.cols;
+    for (; k < kend; k += 64) {
+      const double xv = (k < nx) ? x[k] : 0.0;
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+        if (i0 + q < a.rows && (!a.lower || k <= i0 + q)) s[q] = fma(r0[(long long)q * a.ld + k], xv, s[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) s[q] = wave_sum(s[q]);
     if (lane == 0) {
       double* y = a.y + (long long)b * a.sy;
-      y[i0] = s0;
-      if (i0 + 1 < a.rows) y[i0 + 1] = s1;
-      if (i0 + 2 < a.rows) y[i0 + 2] = s2;
-      if (i0 + 3 < a.rows) y[i0 + 3] = s3;
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+        if (i0 + q < a.rows) y[i0 + q] = s[q];
     }
   }
 }
@@ -623,8 +646,10 @@ void launch_trmv_n(const TrmvArgs& a, int n_active, hipStream_t s) {
   hipLaunchKernelGGL(trmv_n_kernel, dim3((a.rows + 63) / 64, n_active), dim3(256), 0, s, a);
 }
 
-// y = Mᵀ x (column sums; lower: i >= j). 64 columns per WG, rows split over 4 waves.
+// y = Mᵀ x (column sums; lower: i >= j). 64 columns per WG, rows split over 4 waves, 8 row
+// loads in flight per lane. Column block 0 (the longest) has the lowest block index.
 __global__ __launch_bounds__(256) void trmv_t_kernel(TrmvArgs a) {
+  constexpr int R = 8;
   const int b = a.active[blockIdx.y];
   const double* M = a.Wm + (long long)b * a.sW;
   const double* x = a.x + (long long)b * a.sx;
@@ -632,11 +657,25 @@ __global__ __launch_bounds__(256) void trmv_t_kernel(TrmvArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int j0 = blockIdx.x * 64, j = j0 + lane;
   const int istart = a.lower ? j0 : 0;
-  double s = 0.0;
+  double s[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) s[q] = 0.0;
   if (j < a.cols) {
-    for (int i = istart + wave; i < a.rows; i += 4) s = fma(M[(long long)i * a.ld + j], x[i], s);
+    int i = istart + wave;
+    for (; i + 4 * (R - 1) < a.rows; i += 4 * R) {
+      double m[R], xv[R];
+#pragma unroll
+      for (int q = 0; q < R; ++q) { m[q] = M[(long long)(i + 4 * q) * a.ld + j]; xv[q] = x[i + 4 * q]; }
+#pragma unroll
+      for (int q = 0; q < R; ++q) s[q] = fma(m[q], xv[q], s[q]);
+    }
+    for (; i < a.rows; i += 4) s[0] = fma(M[(long long)i * a.ld + j], x[i], s[0]);
   }
-  sred[wave][lane] = s;
+  // fixed-order combine (deterministic)
+  double t = 0.0;
+#pragma unroll
+  for (int q = 0; q < R; ++q) t += s[q];
+  sred[wave][lane] = t;
   __syncthreads();
   if (wave == 0 && j < a.cols)
     a.y[(long long)b * a.sy + j] = sred[0][lane] + sred[1][lane] + sred[2][lane] + sred[3][lane];
