@@ -188,9 +188,6 @@ class Scipy:
         else:
             engines = list(engine) if isinstance(engine, (list, tuple)) else [engine]
         step = _LockstepEvaluator(engines, None, total=len(models), groups=groups)
-        free: "queue.Queue[int]" = queue.Queue()
-        for s in range(step.n_slots):
-            free.put(s)
         results = [None] * len(models)
         if predict_inputs is not None:
             predict_train = True
@@ -199,9 +196,23 @@ class Scipy:
         preds = [None] * len(models) if predict_train else None
         errors: List[Optional[BaseException]] = [None] * len(models)
 
-        def worker(i: int):
+        order: "queue.Queue[int]" = queue.Queue()
+        for i in range(len(models)):
+            order.put(i)
+
+        def slot_worker(slot: int):
+            # one host thread per device slot (not per model): it fits the queued models one
+            # after another in its slot, so the thread count is the slot count however many
+            # models are streamed
+            while True:
+                try:
+                    i = order.get_nowait()
+                except queue.Empty:
+                    return
+                fit_in_slot(i, slot)
+
+        def fit_in_slot(i: int, slot: int):
             m = models[i]
-            slot = free.get()
             eng, local, lock = step.slot_engine(slot)
             try:
                 # the slot is idle, so loading the new problem needs no engine lock: its copies
@@ -231,9 +242,9 @@ class Scipy:
             finally:
                 m._engine = None
                 step.finish(slot)
-                free.put(slot)
 
-        threads = [threading.Thread(target=worker, args=(i,), daemon=True) for i in range(len(models))]
+        n_workers = min(step.n_slots, len(models))
+        threads = [threading.Thread(target=slot_worker, args=(s,), daemon=True) for s in range(n_workers)]
         for t in threads:
             t.start()
         step.serve()
@@ -283,6 +294,7 @@ class _LockstepEvaluator:
             self.initial = min(len(self.models), total)
         self.pending = {}
         self.results = {}
+        self.ready_ev = {}  # slot -> threading.Event set when its result is posted
         self.rounds = 0
         # predict requests of finished fits, run by the slot's server thread between device
         # calls (no engine-lock wait behind a whole evaluation)
@@ -319,12 +331,23 @@ class _LockstepEvaluator:
             self.running.discard(slot)
             self.cv.notify_all()
 
+    def _slot_event(self, i: int) -> threading.Event:
+        ev = self.ready_ev.get(i)
+        if ev is None:
+            ev = self.ready_ev.setdefault(i, threading.Event())
+        return ev
+
     def request(self, i: int, variables):
+        # the optimiser thread waits on its own slot's event: the condition variable only
+        # wakes the server threads (with hundreds of optimiser threads on one condition,
+        # every notify_all woke them all)
+        ev = self._slot_event(i)
+        ev.clear()
         with self.cv:
             self.pending[i] = variables
             self.cv.notify_all()
-            while i not in self.results:
-                self.cv.wait()
+        ev.wait()
+        with self.cv:
             res = self.results.pop(i)
         if isinstance(res, BaseException):
             raise res
@@ -332,12 +355,12 @@ class _LockstepEvaluator:
 
     def predict(self, slot: int, theta_row, Xnew):
         G = self.groups
-        job = {"slot": slot, "theta": np.asarray(theta_row, dtype=np.float64), "x": Xnew, "out": None}
+        job = {"slot": slot, "theta": np.asarray(theta_row, dtype=np.float64), "x": Xnew, "out": None,
+               "done": threading.Event()}
         with self.cv:
             self.admin[slot % G].append(job)
             self.cv.notify_all()
-            while job["out"] is None:
-                self.cv.wait()
+        job["done"].wait()
         if isinstance(job["out"], BaseException):
             raise job["out"]
         return job["out"]
@@ -356,8 +379,7 @@ class _LockstepEvaluator:
                 job["out"] = (mu[0], var[0])
             except BaseException as e:
                 job["out"] = e
-        with self.cv:
-            self.cv.notify_all()
+            job["done"].set()
 
     def finish(self, i: int):
         with self.cv:
@@ -461,3 +483,5 @@ class _LockstepEvaluator:
                 self.rounds += 1
                 self.results.update(out)
                 self.cv.notify_all()
+            for i in out:
+                self._slot_event(i).set()
