@@ -19,7 +19,11 @@ namespace gpx {
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-// linear index -> (ti, tj) of the lower-triangular tile enumeration (ti >= tj)
+// linear index -> (ti, tj) of the lower-triangular tile enumeration (ti >= tj), row-major:
+// a row's tiles share their A panel and start their k loops together, so its panel k-slabs are
+// served from L2 in step. (A grouped order — 8 rows taken column by column, fewer distinct
+// panels resident — was measured 7 % slower on the contraction: tiles of different rows start
+// at different k, so the shared column panels are no longer read in step.)
 __device__ __forceinline__ void lower_tile(int idx, int& ti, int& tj) {
   int t = (int)((sqrt(8.0 * (double)idx + 1.0) - 1.0) * 0.5);
   while ((t + 1) * (t + 2) / 2 <= idx) ++t;
@@ -388,9 +392,11 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
 
   // Register-staged double buffer; the last K-tile is peeled so the loop body has no
   // conditionals (a conditional prefetch made hipcc shuttle every accumulator between AGPRs
-  // and VGPRs once per K-tile). (Splitting the loop into load-only / load+compute phases to
-  // skip a wave's all-zero k-tiles in triangular tiles cost 7 % on full GEMMs through the
-  // compiler's scheduling of the main loop, more than the skipped work.)
+  // and VGPRs once per K-tile). Skipping a wave's all-zero k-tiles in triangular tiles (its
+  // quadrant starts WT after the tile's k range) was measured twice and dropped: as a loop split
+  // it cost 7 % on full GEMMs through the main loop's scheduling; as guarded peeled head/tail
+  // iterations it left the body intact but gained < 1.5 % (the co-resident workgroup's waves,
+  // barrier-coupled to their own tile, cannot use the freed MFMA slots).
   const int nk = (kmax - kmin) / BK;
   if (nk > 0) {
     gload(kmin);
