@@ -171,6 +171,23 @@ void reduce(const Run& r) {
 }
 
 
+// The batch's auxiliary streams (the forked T products of the recursion) take the priority of
+// the stream the caller evaluates on, so a batch submitted on a high-priority stream is high
+// priority throughout. Called at the start of an evaluation, when the aux streams are idle (the
+// previous evaluation joined them before returning).
+int match_aux_priority(gpx_batch* bt, hipStream_t s) {
+  int p = 0;
+  if (hipStreamGetPriority(s, &p) != hipSuccess) p = 0;
+  if (p == bt->aux_priority) return GPX_OK;
+  for (int g = 0; g < kAux; ++g) {
+    if (bt->aux[g]) HIPX(bt->ctx, hipStreamDestroy(bt->aux[g]));
+    bt->aux[g] = nullptr;
+    HIPX(bt->ctx, hipStreamCreateWithPriority(&bt->aux[g], hipStreamNonBlocking, p));
+  }
+  bt->aux_priority = p;
+  return GPX_OK;
+}
+
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                   hipStream_t s) {
   gpx_ctx* ctx = bt->ctx;
@@ -372,6 +389,8 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   int rc = upload_common(bt, n_active, active, theta, s);
+  if (rc != GPX_OK) return rc;
+  rc = match_aux_priority(bt, s);
   if (rc != GPX_OK) return rc;
   bt->flops_acc = 0.0;
   // Split the active problems into up to kGroups ranges, each running the whole pipeline on

@@ -53,6 +53,7 @@ struct gpx_batch {
   double flops_acc = 0.0;
   // per-batch auxiliary streams and events (the recursion's T-product forks), so that
   // independent batches of one context can evaluate concurrently on different streams
+  int aux_priority = 0;       // priority the aux streams were created with
   hipStream_t aux[kAux] = {};
   hipEvent_t ev[kEvents] = {};
   hipStream_t hp = nullptr;   // highest-priority stream for the contraction (GPX_CONTRACT_PRIORITY)
