@@ -72,11 +72,18 @@ void chol_inv(const Run& r, int off, int n, int depth) {
   gpx_batch* bt = r.bt;
   const int Np = bt->Np;
   const long long st = mat_stride(bt);
-  if (n == kLeaf) {
+  // GPX_LEAF128=0 recurses down to 64-leaves instead (A/B measurements)
+  static const bool leaf128 = [] {
+    const char* e = getenv("GPX_LEAF128");
+    return !(e && atoi(e) == 0);
+  }();
+  if (n == kLeaf || (leaf128 && n == 2 * kLeaf)) {
     LeafArgs la{};
     la.active = r.d_act; la.K = bt->K; la.W = bt->W; la.sMat = st; la.ld = Np; la.off = off;
     la.ldiag = bt->ldiag; la.sVec = Np; la.info = bt->d_info;
-    launch_leaf(la, r.na, r.s);
+    // a 128-node is factored and inverted by one fused kernel (no 64x64 GEMM launches)
+    if (n == kLeaf) launch_leaf(la, r.na, r.s);
+    else launch_leaf128(la, r.na, r.s);
     return;
   }
   int n1 = ((n / 2 + kLeaf - 1) / kLeaf) * kLeaf;

@@ -111,6 +111,7 @@ struct PredVarArgs {
 
 void launch_build(const BuildArgs& a, int n_active, hipStream_t s);
 void launch_leaf(const LeafArgs& a, int n_active, hipStream_t s);
+void launch_leaf128(const LeafArgs& a, int n_active, hipStream_t s);  // 128x128 block, fused
 void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hipStream_t s);
 void launch_trmv_n(const TrmvArgs& a, int n_active, hipStream_t s);   // y = M x   (row dots)
 void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s);   // y = Mᵀ x  (column sums)
