@@ -242,22 +242,25 @@ void launch_leaf(const LeafArgs& a, int n_active, hipStream_t s) {
 // ======================================================================================
 // Leaf128: Cholesky + triangular inverse of a 128x128 diagonal block in ONE launch (replaces
 // two 64-leaves and the four 64x64 GEMMs of a 128-node of the recursion: 6 dependent launches
-// of a latency-bound chain become 1). One workgroup of 8 waves per problem; the lower 16x16
-// blocks of A (then L) and of W live in LDS, packed by block (36 blocks each, rows padded to 17
-// doubles: 2 x 36 x 272 x 8 B = 153 KiB). Right-looking over 8 block columns:
-//   diag:     wave 0 factors A_jj and inverts it in registers (as leaf_kernel) -> D_j = L_jj⁻¹
-//   panel:    L_ij = A_ij · D_jᵀ                 (f64 MFMA, one wave per block)
-//   trailing: A_ik -= L_ij · L_kjᵀ, j < k <= i   (f64 MFMA, blocks over the 8 waves)
-// then W_ij = −D_i · Σ_{k=j}^{i−1} L_ik W_kj block row by block row (W_jj = D_j). 31 barriers.
+// of a latency-bound chain become 1). One 4-wave workgroup per problem. The lower 16x16 blocks
+// live in ONE packed LDS array (36 blocks, rows padded to 17 doubles: 78 KiB), so the leaf fits
+// on a CU beside a GEMM workgroup (73.7 KiB, 256 VGPRs per wave) of the concurrent batch or of
+// the recursion's forked T product — a 153 KiB two-array version waited for wholly free CUs.
+// Each slot holds A, then L (off-diagonal) or D_j = L_jj⁻¹ (diagonal; L_jj itself is only
+// needed for log det), then W: right-looking over 8 block columns
+//   diag:     wave 0 factors A_jj and inverts it in registers (as leaf_kernel) -> D_j
+//   panel:    L_ij = A_ij · D_jᵀ                 (f64 MFMA)
+//   trailing: A_ik -= L_ij · L_kjᵀ, j < k <= i   (f64 MFMA, blocks over the 4 waves)
+// then W_ij = −D_i · Σ_{k=j}^{i−1} L_ik W_kj block row by block row (W_jj = D_j): a row's blocks
+// are formed in registers, then written over that row's L blocks after a barrier.
 // ======================================================================================
 namespace {
 constexpr int L8 = 8, LBS = 16 * 17;   // blocks per side, block stride (doubles)
 __device__ __forceinline__ int lblk(int bi, int bj) { return (bi * (bi + 1) / 2 + bj) * LBS; }
 }  // namespace
 
-__global__ __launch_bounds__(512) void leaf128_kernel(LeafArgs a) {
-  __shared__ __attribute__((aligned(16))) double sA[36 * LBS];
-  __shared__ __attribute__((aligned(16))) double sW[36 * LBS];
+__global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
+  __shared__ __attribute__((aligned(16))) double sS[36 * LBS];
   __shared__ int sfail;
   const int b = a.active[blockIdx.x];
   const double* K = a.K + (long long)b * a.sMat;
@@ -266,22 +269,21 @@ __global__ __launch_bounds__(512) void leaf128_kernel(LeafArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, l4 = lane >> 4;
   // lower 128x128 of A (row pieces of 128 B, coalesced); blocks above the diagonal not stored
-  for (int e = tid; e < 128 * 128; e += 512) {
+  for (int e = tid; e < 128 * 128; e += 256) {
     const int r = e >> 7, c = e & 127;
     if (c > (r | 15)) continue;
-    const int o = lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15);
-    sA[o] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
-    sW[o] = 0.0;
+    sS[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] =
+        (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
   }
   if (tid == 0) sfail = -1;
   __syncthreads();
 
   for (int jb = 0; jb < L8; ++jb) {
+    const int dj = lblk(jb, jb);
     if (wave == 0) {
-      const int dj = lblk(jb, jb);
       double r[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) r[k] = sA[dj + l15 * 17 + k];
+      for (int k = 0; k < 16; ++k) r[k] = sS[dj + l15 * 17 + k];
       int fail = -1;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
@@ -301,33 +303,34 @@ __global__ __launch_bounds__(512) void leaf128_kernel(LeafArgs a) {
         for (int k = 0; k < i; ++k) sacc = fma(-readlane_d(r[k], i), w[k], sacc);
         w[i] = sacc / readlane_d(r[i], i);
       }
+      // D_j over A_jj (this wave read the whole block into registers above)
       if (lane < 16) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sW[dj + i * 17 + lane] = w[i];
+        for (int i = 0; i < 16; ++i) sS[dj + i * 17 + lane] = w[i];
         a.ldiag[(long long)b * a.sVec + off + jb * 16 + lane] = log(r[lane & 15]);
       }
       if (lane == 0 && fail >= 0 && sfail < 0) sfail = jb * 16 + fail;
     }
     __syncthreads();
-    // panel: L_(ib,jb) = A_(ib,jb) · D_jbᵀ, one wave per block
+    // panel: L_(ib,jb) = A_(ib,jb) · D_jbᵀ, in place
     const int nblk = L8 - 1 - jb;
-    if (wave < nblk) {
-      const int pb = lblk(jb + 1 + wave, jb), dj = lblk(jb, jb);
+    for (int t = wave; t < nblk; t += 4) {
+      const int pb = lblk(jb + 1 + t, jb);
       d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const double av = sA[pb + l15 * 17 + 4 * kk + l4];
-        const double bv = sW[dj + l15 * 17 + 4 * kk + l4];
+        const double av = sS[pb + l15 * 17 + 4 * kk + l4];
+        const double bv = sS[dj + l15 * 17 + 4 * kk + l4];
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
-      // the wave has read all its operands before the MFMA results exist: in-place is safe
+      // the wave's operand reads precede its MFMA results: the in-place update is safe
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sA[pb + (l4 + 4 * q) * 17 + l15] = acc[q];
+      for (int q = 0; q < 4; ++q) sS[pb + (l4 + 4 * q) * 17 + l15] = acc[q];
     }
     __syncthreads();
     // trailing update of the lower blocks (ib, kb), jb < kb <= ib
     const int ntr = nblk * (nblk + 1) / 2;
-    for (int t = wave; t < ntr; t += 8) {
+    for (int t = wave; t < ntr; t += 4) {
       int p = 0;
       while ((p + 1) * (p + 2) / 2 <= t) ++p;
       const int q = t - p * (p + 1) / 2;
@@ -335,56 +338,67 @@ __global__ __launch_bounds__(512) void leaf128_kernel(LeafArgs a) {
       const int ob = lblk(bi, bk), li = lblk(bi, jb), lk = lblk(bk, jb);
       d4 acc;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = sA[ob + (l4 + 4 * u) * 17 + l15];
+      for (int u = 0; u < 4; ++u) acc[u] = sS[ob + (l4 + 4 * u) * 17 + l15];
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const double av = sA[li + l15 * 17 + 4 * kk + l4];
-        const double bv = sA[lk + l15 * 17 + 4 * kk + l4];
+        const double av = sS[li + l15 * 17 + 4 * kk + l4];
+        const double bv = sS[lk + l15 * 17 + 4 * kk + l4];
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) sA[ob + (l4 + 4 * u) * 17 + l15] = acc[u];
+      for (int u = 0; u < 4; ++u) sS[ob + (l4 + 4 * u) * 17 + l15] = acc[u];
     }
     __syncthreads();
   }
-  // W = L⁻¹ block rows 1..7: blocks j < i in parallel (wave j)
+  // W = L⁻¹ block rows 1..7; blocks j < i of a row (j = wave, wave + 4) in registers first
   for (int i = 1; i < L8; ++i) {
-    if (wave < i) {
-      const int j = wave;
-      d4 t = {0.0, 0.0, 0.0, 0.0};
-      for (int k = j; k < i; ++k) {
-        const int lik = lblk(i, k), wkj = lblk(k, j);
+    d4 wv[2];
+    const int di = lblk(i, i);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = wave + 4 * h;
+      wv[h] = (d4){0.0, 0.0, 0.0, 0.0};
+      if (j < i) {
+        d4 t = {0.0, 0.0, 0.0, 0.0};
+        for (int k = j; k < i; ++k) {
+          const int lik = lblk(i, k), wkj = lblk(k, j);   // L_ik; W_kj (row k < i done; W_jj = D_j)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const double av = sS[lik + l15 * 17 + 4 * kk + l4];
+            const double bv = sS[wkj + (4 * kk + l4) * 17 + l15];
+            t = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, t, 0, 0, 0);
+          }
+        }
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
-          const double av = sA[lik + l15 * 17 + 4 * kk + l4];     // L_ik[row][k']
-          const double bv = sW[wkj + (4 * kk + l4) * 17 + l15];   // W_kj[k'][col]
-          t = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, t, 0, 0, 0);
+          const double av = sS[di + l15 * 17 + 4 * kk + l4];   // D_i[row][k']
+          wv[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, t[kk], wv[h], 0, 0, 0);
         }
       }
-      const int di = lblk(i, i);
-      d4 wv = {0.0, 0.0, 0.0, 0.0};
+    }
+    __syncthreads();   // every wave has read row i's L blocks
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const double av = sW[di + l15 * 17 + 4 * kk + l4];       // D_i[row][k']
-        wv = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, t[kk], wv, 0, 0, 0);  // T[k'][col]
+    for (int h = 0; h < 2; ++h) {
+      const int j = wave + 4 * h;
+      if (j < i) {
+        const int wij = lblk(i, j);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sS[wij + (l4 + 4 * q) * 17 + l15] = wv[h][q];
       }
-      const int wij = lblk(i, j);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sW[wij + (l4 + 4 * q) * 17 + l15] = wv[q];
     }
     __syncthreads();
   }
   // the whole 128x128 block of W, zeros above the diagonal
-  for (int e = tid; e < 128 * 128; e += 512) {
+  for (int e = tid; e < 128 * 128; e += 256) {
     const int r = e >> 7, c = e & 127;
-    const double v = (c <= r) ? sW[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] : 0.0;
+    const double v = (c <= r) ? sS[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] : 0.0;
     W[(long long)(off + r) * ld + off + c] = v;
   }
   if (tid == 0 && sfail >= 0 && a.info[b] == 0) a.info[b] = off + sfail + 1;
 }
 
 void launch_leaf128(const LeafArgs& a, int n_active, hipStream_t s) {
-  hipLaunchKernelGGL(leaf128_kernel, dim3(n_active), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(leaf128_kernel, dim3(n_active), dim3(256), 0, s, a);
 }
 
 // ======================================================================================
