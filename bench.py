@@ -81,6 +81,12 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
     m.predict_f(x)
     t_pred = time.perf_counter() - t0
     t_fit = nfev_per_fit * t_eval + t_pred
+    cpu_model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
+    except OSError:
+        pass
     return {
         "value": 1.0 / t_fit,
         "unit": "fits/s",
@@ -91,6 +97,8 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
                    f"at N={n}; fit time = mean GPU nfev/fit ({nfev_per_fit:.1f}) x eval + predict"),
         "eval_s": t_eval,
         "predict_s": t_pred,
+        "cpu_model": cpu_model,
+        "host_cpus_visible": len(os.sched_getaffinity(0)),
     }
 
 
