@@ -41,6 +41,60 @@ __device__ __forceinline__ double wave_sum(double v) {
 // ======================================================================================
 // K build (and cross-covariance Kxs for predict)
 // ======================================================================================
+// value of a single-term isotropic stationary kernel at scaled squared distance r2 = d²/ℓ²
+// (same formulas and 1e-36 clamp as eval_term in gpx_kfun.h)
+template <int KIND>
+__device__ __forceinline__ double stationary_value(double r2, double var) {
+  if constexpr (KIND == GPX_SE) {
+    return var * exp(-0.5 * r2);
+  } else {
+    const double r = sqrt(r2 > 1e-36 ? r2 : 1e-36);
+    if constexpr (KIND == GPX_MATERN12) return var * exp(-r);
+    if constexpr (KIND == GPX_EXPONENTIAL) return var * exp(-0.5 * r);
+    if constexpr (KIND == GPX_MATERN32) {
+      const double s = 1.7320508075688772;
+      return var * ((1.0 + s * r) * exp(-s * r));
+    }
+    if constexpr (KIND == GPX_MATERN52) {
+      const double s = 2.23606797749979;
+      return var * ((1.0 + s * r + (5.0 / 3.0) * r * r) * exp(-s * r));
+    }
+  }
+  return 0.0;
+}
+
+template <int KIND>
+__device__ __forceinline__ void build_stationary(const BuildArgs& a, const DevSpec& spec,
+                                                 const double* sth, const double* sxi,
+                                                 const double* sxj, double noise, int n, int ncol,
+                                                 int ti, int tj, double* out) {
+  const gpx_term& t = spec.terms[0];
+  const double* th = sth + t.param_offset;
+  const double ell = th[0], var = th[1];
+  const double inv_l2 = 1.0 / (ell * ell);
+  const int D = a.D, d0 = t.dim_start, dn = t.dim_count;
+  const int c = threadIdx.x & 63;
+  const int gj = tj * 64 + c;
+  for (int q = 0; q < 16; ++q) {
+    const int r = (threadIdx.x >> 6) + 4 * q;
+    const int gi = ti * 64 + r;
+    double v;
+    const bool valid = a.symmetric ? (gi < n && gj < n) : (gi < n && gj < ncol);
+    if (valid) {
+      double d2 = 0.0;
+      for (int d = 0; d < dn; ++d) {
+        const double diff = sxi[r * D + d0 + d] - sxj[c * D + d0 + d];
+        d2 = fma(diff, diff, d2);
+      }
+      v = stationary_value<KIND>(d2 * inv_l2, var);
+      if (a.symmetric && gi == gj) v += noise;
+    } else {
+      v = (a.symmetric && gi == gj) ? 1.0 : 0.0;
+    }
+    out[(long long)gi * a.ldo + gj] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void build_kernel(BuildArgs a) {
   const int b = a.active[blockIdx.y];
   int ti, tj;
@@ -72,7 +126,20 @@ __global__ __launch_bounds__(256) void build_kernel(BuildArgs a) {
   double* out = a.out + (long long)b * a.sOut;
   const int c = tid & 63;
   const int gj = tj * 64 + c;
-#pragma unroll 4
+  // single-term isotropic stationary kernels (the reference's SE / Matern / Exponential sweeps)
+  // take a compact loop with 1/ℓ² hoisted: the generic term interpreter below unrolls into tens
+  // of KiB of code per kernel, which thrashed the instruction cache of this HBM-write kernel
+  const int k0 = spec.terms[0].kind;
+  if (spec.n_terms == 1 && k0 >= GPX_SE && k0 <= GPX_EXPONENTIAL) {
+    switch (k0) {
+      case GPX_SE:          build_stationary<GPX_SE>(a, spec, sth, sxi, sxj, noise, n, ncol, ti, tj, out); return;
+      case GPX_MATERN12:    build_stationary<GPX_MATERN12>(a, spec, sth, sxi, sxj, noise, n, ncol, ti, tj, out); return;
+      case GPX_MATERN32:    build_stationary<GPX_MATERN32>(a, spec, sth, sxi, sxj, noise, n, ncol, ti, tj, out); return;
+      case GPX_MATERN52:    build_stationary<GPX_MATERN52>(a, spec, sth, sxi, sxj, noise, n, ncol, ti, tj, out); return;
+      default:              build_stationary<GPX_EXPONENTIAL>(a, spec, sth, sxi, sxj, noise, n, ncol, ti, tj, out); return;
+    }
+  }
+#pragma unroll 1
   for (int q = 0; q < 16; ++q) {
     const int r = (tid >> 6) + 4 * q;
     const int gi = ti * 64 + r;
