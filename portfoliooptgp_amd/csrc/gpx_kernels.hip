@@ -182,6 +182,16 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
+// 1/sqrt(x) from the hardware estimate and two Newton steps (each doubles the ~22 correct bits):
+// within an ulp or two of 1/sqrt, and one multiply gives sqrt(x) = x/sqrt(x). Replaces a
+// correctly rounded sqrt and a division on the leaves' serial 16-step diagonal chain.
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * fma(-0.5 * x, y * y, 1.5);
+  y = y * fma(-0.5 * x, y * y, 1.5);
+  return y;
+}
+
 __global__ __launch_bounds__(256) void leaf_kernel(LeafArgs a) {
   constexpr int S = 66;  // row stride (doubles): 16 rows x 1 col fragment reads are conflict-free
   __shared__ __attribute__((aligned(16))) double sA[64 * S];
@@ -193,10 +203,21 @@ __global__ __launch_bounds__(256) void leaf_kernel(LeafArgs a) {
   const int ld = a.ld, off = a.off, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, l4 = lane >> 4;
-  for (int e = tid; e < 4096; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    sA[r * S + c] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
-    sW[r * S + c] = 0.0;
+  // 8 independent loads in flight per thread (a load-then-store loop serialises on latency)
+#pragma unroll 1
+  for (int e0 = tid; e0 < 4096; e0 += 256 * 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 256 * u, r = e >> 6, c = e & 63;
+      v[u] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 256 * u, r = e >> 6, c = e & 63;
+      sA[r * S + c] = v[u];
+      sW[r * S + c] = 0.0;
+    }
   }
   if (tid == 0) sfail = -1;
   __syncthreads();
@@ -208,12 +229,14 @@ __global__ __launch_bounds__(256) void leaf_kernel(LeafArgs a) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) r[k] = sA[(c0 + l15) * S + c0 + k];
       int fail = -1;
+      double invd[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const double piv = readlane_d(r[j], j);
         if (!(piv > 0.0) && fail < 0) fail = j;
-        const double ljj = sqrt(piv);
-        const double inv = 1.0 / ljj;
+        const double inv = rsqrt_nr(piv);
+        const double ljj = piv * inv;
+        invd[j] = inv;
         r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
 #pragma unroll
         for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], readlane_d(r[j], k), r[k]);
@@ -225,7 +248,7 @@ __global__ __launch_bounds__(256) void leaf_kernel(LeafArgs a) {
         double sacc = (i == l15) ? 1.0 : 0.0;
 #pragma unroll
         for (int k = 0; k < i; ++k) sacc = fma(-readlane_d(r[k], i), w[k], sacc);
-        w[i] = sacc / readlane_d(r[i], i);
+        w[i] = sacc * invd[i];
       }
       if (lane < 16) {
 #pragma unroll
@@ -336,11 +359,20 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, l4 = lane >> 4;
   // lower 128x128 of A (row pieces of 128 B, coalesced); blocks above the diagonal not stored
-  for (int e = tid; e < 128 * 128; e += 256) {
-    const int r = e >> 7, c = e & 127;
-    if (c > (r | 15)) continue;
-    sS[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] =
-        (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
+  // 8 independent loads in flight per thread (a load-then-store loop serialises on latency)
+#pragma unroll 1
+  for (int e0 = tid; e0 < 128 * 128; e0 += 256 * 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 256 * u, r = e >> 7, c = e & 127;
+      v[u] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 256 * u, r = e >> 7, c = e & 127;
+      if (c <= (r | 15)) sS[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] = v[u];
+    }
   }
   if (tid == 0) sfail = -1;
   __syncthreads();
@@ -352,12 +384,14 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) r[k] = sS[dj + l15 * 17 + k];
       int fail = -1;
+      double invd[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const double piv = readlane_d(r[j], j);
         if (!(piv > 0.0) && fail < 0) fail = j;
-        const double ljj = sqrt(piv);
-        const double inv = 1.0 / ljj;
+        const double inv = rsqrt_nr(piv);
+        const double ljj = piv * inv;
+        invd[j] = inv;
         r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
 #pragma unroll
         for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], readlane_d(r[j], k), r[k]);
@@ -368,7 +402,7 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
         double sacc = (i == l15) ? 1.0 : 0.0;
 #pragma unroll
         for (int k = 0; k < i; ++k) sacc = fma(-readlane_d(r[k], i), w[k], sacc);
-        w[i] = sacc / readlane_d(r[i], i);
+        w[i] = sacc * invd[i];
       }
       // D_j over A_jj (this wave read the whole block into registers above)
       if (lane < 16) {
