@@ -72,6 +72,7 @@ struct TrmvArgs {
   double* y; long long sy;         // output
   int rows, cols;                  // operator dims
   int lower;                       // 1: triangular (skip known zeros)
+  int n_active;                    // set by the launcher (1-D grid: blocks x problems)
 };
 
 // predict_f / predict_y at the training inputs from the cached factor, O(N²):

@@ -865,12 +865,16 @@ void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hip
 // workgroups are dispatched first.
 __global__ __launch_bounds__(256) void trmv_n_kernel(TrmvArgs a) {
   constexpr int R = 8;
-  const int b = a.active[blockIdx.y];
+  // 1-D grid, block index major: every problem's longest rows are dispatched before any
+  // problem's shorter ones (no long-row workgroup is left for the tail)
+  const int na = a.n_active, nb = (a.rows + 63) / 64;
+  const int blk = (int)blockIdx.x / na;
+  const int b = a.active[(int)blockIdx.x - blk * na];
   const double* M = a.Wm + (long long)b * a.sW;
   const double* x = a.x + (long long)b * a.sx;
   const int nx = a.nvalid ? a.nvalid[b] : a.cols;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int rb = (a.lower ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x);  // longest rows first
+  const int rb = a.lower ? nb - 1 - blk : blk;  // longest rows first
   for (int rr = 0; rr < 16; rr += R) {
     const int i0 = rb * 64 + wave * 16 + rr;
     if (i0 >= a.rows) break;
@@ -912,19 +916,24 @@ __global__ __launch_bounds__(256) void trmv_n_kernel(TrmvArgs a) {
 }
 
 void launch_trmv_n(const TrmvArgs& a, int n_active, hipStream_t s) {
-  hipLaunchKernelGGL(trmv_n_kernel, dim3((a.rows + 63) / 64, n_active), dim3(256), 0, s, a);
+  TrmvArgs t = a;
+  t.n_active = n_active;
+  hipLaunchKernelGGL(trmv_n_kernel, dim3((a.rows + 63) / 64 * n_active), dim3(256), 0, s, t);
 }
 
 // y = Mᵀ x (column sums; lower: i >= j). 64 columns per WG, rows split over 4 waves, 8 row
 // loads in flight per lane. Column block 0 (the longest) has the lowest block index.
 __global__ __launch_bounds__(256) void trmv_t_kernel(TrmvArgs a) {
   constexpr int R = 8;
-  const int b = a.active[blockIdx.y];
+  // 1-D grid, column block major (block 0, the longest column, first for every problem)
+  const int na = a.n_active;
+  const int blk = (int)blockIdx.x / na;
+  const int b = a.active[(int)blockIdx.x - blk * na];
   const double* M = a.Wm + (long long)b * a.sW;
   const double* x = a.x + (long long)b * a.sx;
   __shared__ double sred[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j0 = blockIdx.x * 64, j = j0 + lane;
+  const int j0 = blk * 64, j = j0 + lane;
   const int istart = a.lower ? j0 : 0;
   double s[R];
 #pragma unroll
@@ -981,7 +990,9 @@ void launch_train_pred(const TrainPredArgs& a, int n_active, int Np, hipStream_t
 }
 
 void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s) {
-  hipLaunchKernelGGL(trmv_t_kernel, dim3((a.cols + 63) / 64, n_active), dim3(256), 0, s, a);
+  TrmvArgs t = a;
+  t.n_active = n_active;
+  hipLaunchKernelGGL(trmv_t_kernel, dim3((a.cols + 63) / 64 * n_active), dim3(256), 0, s, t);
 }
 
 // ======================================================================================
