@@ -307,6 +307,9 @@ def main():
                      if G > 1 else "one device batch"),
             "achieved_isolated": iso,
             "frac_isolated": iso / FP64_PEAK_TFLOPS if iso else None,
+            # the whole path: F_eval(N) x evaluations / wall time of the timed steps
+            "achieved_job": eval_alg / elapsed / 1e12 if world == 1 else None,
+            "frac_job": eval_alg / elapsed / 1e12 / FP64_PEAK_TFLOPS if world == 1 else None,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
