@@ -16,7 +16,9 @@ predicted_variances), Multi-Input_GPR/Portfolio/portfolio.py:92-165). Here:
 """
 from __future__ import annotations
 
+import hashlib
 import heapq
+import os
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -95,20 +97,68 @@ def portfolio_inputs(gathered: Dict[int, dict], order: Sequence[int]) -> Tuple[l
     return means, varis
 
 
+def asset_fingerprint(x, y, horizon) -> str:
+    """Content hash of one asset's fit inputs (training series and prediction inputs)."""
+    h = hashlib.sha1()
+    for a in (x, y, horizon):
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+        h.update(str(a.shape).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
+def _load_checkpoint(path: str, H: int, n_theta: int) -> Dict[str, dict]:
+    """{fingerprint: result} of a previous run's rank file (absent or unreadable: empty)."""
+    if not os.path.exists(path):
+        return {}
+    try:
+        with np.load(path, allow_pickle=False) as z:
+            if int(z["H"]) != H or int(z["n_theta"]) != n_theta:
+                return {}
+            rows = unpack_results(torch.as_tensor(z["table"]), H, n_theta)
+            fps = [str(f) for f in z["fingerprints"]]
+            index = [int(i) for i in z["table"][:, 0]]
+    except (OSError, KeyError, ValueError):
+        return {}
+    return {fp: rows[i] for fp, i in zip(fps, index) if i in rows}
+
+
+def _save_checkpoint(path: str, table: torch.Tensor, fingerprints: Sequence[str], H: int, n_theta: int):
+    tmp = path + ".tmp.npz"
+    np.savez(tmp, table=table.numpy(), fingerprints=np.asarray(list(fingerprints), dtype="U40"),
+             H=np.int64(H), n_theta=np.int64(n_theta))
+    os.replace(tmp, path)
+
+
 def fit_assets(series: Sequence[Tuple[np.ndarray, np.ndarray]], horizons: Sequence[np.ndarray],
-               fit_fn: Optional[Callable] = None, n_theta: int = 2, group=None) -> Dict[int, dict]:
+               fit_fn: Optional[Callable] = None, n_theta: int = 2, group=None,
+               checkpoint: Optional[str] = None) -> Dict[int, dict]:
     """Shard the assets over the ranks of `group`, fit the local shard with `fit_fn`
     (default: GPU exact GPR with a SquaredExponential kernel and σn² = 1e-5 fixed, the
     GPR/model_trainer.py:15-19 protocol, continuous-batched), predict each asset at its
-    horizon inputs and all_gather the results. Returns {asset index: result} on every rank."""
+    horizon inputs and all_gather the results. Returns {asset index: result} on every rank.
+
+    ``checkpoint``: path prefix of per-rank result files (``<prefix>.rank<r>.npz``, θ*, loss*,
+    nfev and the horizon predictions of each fitted asset, keyed by a content hash of its
+    inputs). A rerun with the same prefix (say after a crash of another rank) fits only the
+    assets whose results are missing, so a long multi-asset sweep resumes at asset
+    granularity; changed inputs are refitted. The reference has no checkpointing."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     shards = shard_lpt([fit_cost(len(x)) for x, _ in series], world)
     mine = shards[rank]
     fit_fn = fit_fn or gpu_fit_shard
-    local = fit_fn([series[i] for i in mine], [horizons[i] for i in mine]) if mine else []
     H = max(len(h) for h in horizons)
+    fps = {i: asset_fingerprint(series[i][0], series[i][1], horizons[i]) for i in mine} if checkpoint else {}
+    path = f"{checkpoint}.rank{rank}.npz" if checkpoint else None
+    done = _load_checkpoint(path, H, n_theta) if checkpoint else {}
+    todo = [i for i in mine if fps.get(i) not in done]
+    fitted = fit_fn([series[i] for i in todo], [horizons[i] for i in todo]) if todo else []
+    by_index = dict(zip(todo, fitted))
+    local = [by_index[i] if i in by_index else done[fps[i]] for i in mine]
     table = pack_results(mine, local, H, n_theta)
+    if checkpoint:
+        _save_checkpoint(path, table, [fps[i] for i in mine], H, n_theta)
     if world > 1:
         table = all_gather_results(table, len(series), group)
     return unpack_results(table, H, n_theta)

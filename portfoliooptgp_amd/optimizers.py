@@ -52,6 +52,27 @@ def _resolve_model(closure):
     return m
 
 
+def _not_pd_policy(on_not_pd: str):
+    """GPflow/TF raise when the Cholesky of K + σn²I fails (tf.linalg.cholesky →
+    InvalidArgumentError inside Scipy.minimize); on_not_pd="inf" instead reports an infinite
+    loss (zero gradient) for that point, so L-BFGS-B's line search backs off and the fit goes on."""
+    if on_not_pd not in ("raise", "inf"):
+        raise ValueError("on_not_pd must be 'raise' (GPflow's behaviour) or 'inf'")
+    return on_not_pd == "inf"
+
+
+def _guarded(fn, as_inf: bool):
+    if not as_inf:
+        return fn
+
+    def g(x):
+        try:
+            return fn(x)
+        except N.NotPositiveDefiniteError:
+            return float("inf"), np.zeros_like(np.asarray(x, dtype=np.float64))
+    return g
+
+
 def _pack(variables) -> np.ndarray:
     return np.concatenate([np.atleast_1d(v.numpy()).ravel() for v in variables]).astype(np.float64)
 
@@ -69,7 +90,9 @@ def _unpack(variables, x) -> None:
 class Scipy:
     def minimize(self, closure: Callable, variables: Sequence, method: str = "L-BFGS-B",
                  step_callback=None, compile: bool = True, allow_unused_variables: bool = False,
-                 tf_fun_args=None, track_loss_history: bool = False, **scipy_kwargs):
+                 tf_fun_args=None, track_loss_history: bool = False, on_not_pd: str = "raise",
+                 **scipy_kwargs):
+        as_inf = _not_pd_policy(on_not_pd)
         if not callable(closure):
             raise TypeError("The 'closure' argument is expected to be a callable object.")
         variables = tuple(variables)
@@ -92,8 +115,8 @@ class Scipy:
             def callback(xk, *args):
                 step_callback(len(history), variables, [np.asarray(v) for v in xk])
         x0 = _pack(variables)
-        res = scipy.optimize.minimize(func, x0, jac=True, method=method, callback=callback,
-                                      **scipy_kwargs)
+        res = scipy.optimize.minimize(_guarded(func, as_inf), x0, jac=True, method=method,
+                                      callback=callback, **scipy_kwargs)
         _unpack(variables, res.x)
         if track_loss_history:
             res.loss_history = history
@@ -101,8 +124,9 @@ class Scipy:
 
     def minimize_batch(self, models: Sequence, method: str = "L-BFGS-B",
                        engine: Optional[Engine] = None, device: Optional[int] = None,
-                       **scipy_kwargs) -> List[scipy.optimize.OptimizeResult]:
+                       on_not_pd: str = "raise", **scipy_kwargs) -> List[scipy.optimize.OptimizeResult]:
         """Fit several GPR models concurrently (their trainable_variables), lock-step batched."""
+        as_inf = _not_pd_policy(on_not_pd)
         models = list(models)
         if not models:
             return []
@@ -127,8 +151,8 @@ class Scipy:
                     _unpack(variables, x)
                     return step.request(i, variables)
 
-                res = scipy.optimize.minimize(func, _pack(variables), jac=True, method=method,
-                                              **scipy_kwargs)
+                res = scipy.optimize.minimize(_guarded(func, as_inf), _pack(variables), jac=True,
+                                              method=method, **scipy_kwargs)
                 _unpack(variables, res.x)
                 results[i] = res
             except BaseException as e:  # re-raised on the caller's thread
@@ -151,7 +175,8 @@ class Scipy:
     def minimize_stream(self, models: Sequence, width: int, method: str = "L-BFGS-B",
                         device: Optional[int] = None, predict_train: bool = False,
                         engine=None, groups: int = 1,
-                        predict_inputs: Optional[Sequence] = None, **scipy_kwargs):
+                        predict_inputs: Optional[Sequence] = None, on_not_pd: str = "raise",
+                        **scipy_kwargs):
         """Continuous batching: fit many models through ``width`` resident device slots.
 
         Every model still runs its own unmodified scipy L-BFGS-B; at most ``width`` are
@@ -167,6 +192,7 @@ class Scipy:
         device work. ``engine`` may be one Engine (groups then alternate on it) or a list of
         ``groups`` Engines. Returns (results, predictions|None); models are detached afterwards.
         """
+        as_inf = _not_pd_policy(on_not_pd)
         models = list(models)
         if not models:
             return [], ([] if predict_train else None)
@@ -227,8 +253,8 @@ class Scipy:
                     _unpack(variables, x)
                     return step.request(slot, variables)
 
-                res = scipy.optimize.minimize(func, _pack(variables), jac=True, method=method,
-                                              **scipy_kwargs)
+                res = scipy.optimize.minimize(_guarded(func, as_inf), _pack(variables), jac=True,
+                                              method=method, **scipy_kwargs)
                 _unpack(variables, res.x)
                 results[i] = res
                 if predict_train:

@@ -160,3 +160,31 @@ def test_two_rank_gloo_svgp_allreduce_matches_oracle():
         np.testing.assert_allclose(gq, g["q_mu"], rtol=1e-7, atol=1e-8)
         np.testing.assert_allclose(np.asarray(gR), g["q_sqrt"], rtol=1e-7, atol=1e-8)
     assert outs[0][1] == outs[1][1]
+
+
+def test_fit_assets_checkpoint_resumes_at_asset_granularity(tmp_path):
+    """A rerun with the same checkpoint prefix fits only the assets without a stored result;
+    an asset whose inputs changed is refitted; results equal a fresh run's."""
+    series = [_series(k) for k in range(5)]
+    horizons = [np.arange(len(s[0]), len(s[0]) + 3, dtype=np.float64)[:, None] for s in series]
+    calls = []
+
+    def counting_fit(ss, hs):
+        calls.append(len(ss))
+        return _stand_in_fit(ss, hs)
+
+    prefix = str(tmp_path / "sweep")
+    fresh = D.fit_assets(series, horizons, fit_fn=_stand_in_fit)
+    first = D.fit_assets(series, horizons, fit_fn=counting_fit, checkpoint=prefix)
+    again = D.fit_assets(series, horizons, fit_fn=counting_fit, checkpoint=prefix)
+    assert calls == [5]                       # the rerun fitted nothing
+    x2, y2 = series[2]
+    series[2] = (x2, y2 + 1.0)
+    changed = D.fit_assets(series, horizons, fit_fn=counting_fit, checkpoint=prefix)
+    assert calls == [5, 1]                    # only the changed asset
+    for res in (first, again):
+        for i in range(5):
+            assert res[i]["loss"] == fresh[i]["loss"]
+            np.testing.assert_array_equal(res[i]["mean"], fresh[i]["mean"])
+    assert changed[2]["loss"] == pytest.approx(float(np.sum((y2 + 1.0) ** 2)))
+    assert changed[0]["loss"] == fresh[0]["loss"]

@@ -82,3 +82,31 @@ def test_stream_equals_solo(width, groups, engines):
         np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
         assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
     assert max(max(e.calls) for e in eng) <= per
+
+
+class NotPDEngine(FakeEngine):
+    """As FakeEngine, but K + σn²I 'fails to factor' once the lengthscale passes 2.5."""
+
+    def lml_grad(self, rows, theta):
+        lml, grad, info = super().lml_grad(rows, theta)
+        for r in rows:
+            if theta[r, 0] > 2.5:
+                info[r] = 7
+        return lml, grad, info
+
+
+def test_not_positive_definite_raises_like_gpflow_or_backs_off():
+    """Default: a failed factorisation raises (GPflow: tf.linalg.cholesky's InvalidArgumentError
+    escapes Scipy.minimize). on_not_pd="inf": the point gets an infinite loss, L-BFGS-B's line
+    search backs off and the fit ends inside the factorisable region."""
+    ms = _models(4)
+    for m in ms:
+        m.kernel.lengthscales.assign(1.0)
+    with pytest.raises(N.NotPositiveDefiniteError):
+        gpx.optimizers.Scipy().minimize_stream(_models(4), width=2, engine=NotPDEngine(2))
+    res, _ = gpx.optimizers.Scipy().minimize_stream(ms, width=2, engine=NotPDEngine(2), on_not_pd="inf")
+    for r, m in zip(res, ms):
+        assert np.isfinite(r.fun)
+        assert m.kernel.lengthscales.value <= 2.5
+    with pytest.raises(ValueError):
+        gpx.optimizers.Scipy().minimize_stream(_models(1), width=1, engine=NotPDEngine(1), on_not_pd="ignore")

@@ -19,8 +19,10 @@ __global__ void fill(double* p, size_t n, unsigned seed) {
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 2048;
   const int B = argc > 2 ? atoi(argv[2]) : 8;
-  const char* only = argc > 3 ? argv[3] : nullptr;   // run only the case with this name prefix
-  const size_t sz = (size_t)n * n;
+  // run only the cases with this name prefix ("all": every case)
+  const char* only = (argc > 3 && std::string(argv[3]) != "all") ? argv[3] : nullptr;
+  const int ld = n + (argc > 4 ? atoi(argv[4]) : 0);  // leading dimension (row padding test)
+  const size_t sz = (size_t)n * ld;
   double *A, *Bm, *C;
   CK(hipMalloc(&A, sz * B * 8)); CK(hipMalloc(&Bm, sz * B * 8)); CK(hipMalloc(&C, sz * B * 8));
   fill<<<1024, 256>>>(A, sz * B, 1); fill<<<1024, 256>>>(Bm, sz * B, 2); fill<<<1024, 256>>>(C, sz * B, 3);
@@ -37,7 +39,7 @@ int main(int argc, char** argv) {
   for (auto& c : cases) {
     if (only && std::string(c.name).rfind(only, 0) != 0) continue;
     GemmArgs g{};
-    g.active = act; g.A = A; g.sA = sz; g.lda = n; g.Bm = Bm; g.sB = sz; g.ldb = n; g.C = C; g.sC = sz; g.ldc = n;
+    g.active = act; g.A = A; g.sA = sz; g.lda = ld; g.Bm = Bm; g.sB = sz; g.ldb = ld; g.C = C; g.sC = sz; g.ldc = ld;
     g.M = g.N = n; g.K = n / c.kdiv; g.tri = c.tri; g.lower_only = c.lower;
     g.order = (c.tri & TRI_KMAX_J) ? ORDER_COL_DESC : (c.tri & TRI_KMIN_J) ? ORDER_COL_ASC
             : (c.tri & TRI_KMAX_I) ? ORDER_ROW_DESC : ORDER_ROW_ASC; g.alpha = -1.0; g.beta = 1.0;
@@ -82,7 +84,7 @@ int main(int argc, char** argv) {
       for (int r = 0; r < reps; ++r) launch_gemm(gg, ep, c.ta, c.tb, B, 0);
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ms /= reps;
-      printf("%-22s%s n=%d B=%d tile=%d: %8.3f ms  %6.2f TF/s (issued)\n", c.name, epi ? " +contract" : "", n, B, bm, ms, f / ms / 1e9);
+      printf("%-22s%s n=%d ld=%d B=%d tile=%d: %8.3f ms  %6.2f TF/s (issued)\n", c.name, epi ? " +contract" : "", n, ld, B, bm, ms, f / ms / 1e9);
     }
   }
   return 0;
