@@ -63,6 +63,36 @@ __device__ __forceinline__ double stationary_value(double r2, double var) {
   return 0.0;
 }
 
+// value derivatives (∂K/∂ℓ, ∂K/∂σ²) of a single-term isotropic stationary kernel at r2 = d²/ℓ²,
+// with 1/ℓ precomputed by the caller (same formulas and clamp as eval_term<true>)
+__device__ __forceinline__ void stationary_grad(int kind, double r2, double var, double inv_ell,
+                                                double (&dk)[3]) {
+  dk[2] = 0.0;
+  if (kind == GPX_SE) {
+    const double g = exp(-0.5 * r2);
+    dk[0] = var * g * r2 * inv_ell;
+    dk[1] = g;
+    return;
+  }
+  const bool clamped = !(r2 > 1e-36);
+  const double r = sqrt(clamped ? 1e-36 : r2);
+  double g, dgdr;
+  if (kind == GPX_MATERN12) {
+    g = exp(-r); dgdr = -g;
+  } else if (kind == GPX_EXPONENTIAL) {
+    g = exp(-0.5 * r); dgdr = -0.5 * g;
+  } else if (kind == GPX_MATERN32) {
+    const double sq3 = 1.7320508075688772, e = exp(-sq3 * r);
+    g = (1.0 + sq3 * r) * e; dgdr = -3.0 * r * e;
+  } else {
+    const double sq5 = 2.23606797749979, e = exp(-sq5 * r);
+    g = (1.0 + sq5 * r + (5.0 / 3.0) * r * r) * e;
+    dgdr = -(5.0 / 3.0) * r * (1.0 + sq5 * r) * e;
+  }
+  dk[0] = clamped ? 0.0 : var * dgdr * (-r * inv_ell);
+  dk[1] = g;
+}
+
 template <int KIND>
 __device__ __forceinline__ void build_stationary(const BuildArgs& a, const DevSpec& spec,
                                                  const double* sth, const double* sxi,
@@ -728,6 +758,14 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
     const int cl = lane % WT, rg = lane / WT;
     const int jl = wc * WT + cl;            // this lane's column within the tile
     const int j = j0 + jl;
+    // single-term isotropic stationary specs (the SE / Matern / Exponential fits): ℓ-dependent
+    // factors hoisted out of the per-element derivative (no division per element)
+    const int fkind = spec.terms[0].kind;
+    const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
+    const int fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
+    const double fell = a.theta[b * GPX_THETA_STRIDE + spec.terms[0].param_offset];
+    const double fvar = a.theta[b * GPX_THETA_STRIDE + spec.terms[0].param_offset + 1];
+    const double finv_ell = 1.0 / fell, finv_l2 = finv_ell * finv_ell;
 #pragma unroll
     for (int h = 0; h < MT; ++h) {
 #pragma unroll
@@ -746,7 +784,16 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
             const double w = (i == j) ? 1.0 : 2.0;
             const double v = w * fma(sai[il], aj, -wacc[rr * WT + cl]);
             double dk[NT][3];
-            eval_k_grad<NT>(spec, sth, sxi + il * D, sxj + jl * D, dk);
+            if (fast) {
+              double d2 = 0.0;
+              for (int d = 0; d < fdn; ++d) {
+                const double diff = sxi[il * D + fd0 + d] - sxj[jl * D + fd0 + d];
+                d2 = fma(diff, diff, d2);
+              }
+              stationary_grad(fkind, d2 * finv_l2, fvar, finv_ell, dk[0]);
+            } else {
+              eval_k_grad<NT>(spec, sth, sxi + il * D, sxj + jl * D, dk);
+            }
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
               sums[t][0] = fma(v, dk[t][0], sums[t][0]);
