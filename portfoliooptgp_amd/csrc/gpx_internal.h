@@ -88,6 +88,7 @@ struct TrainPredArgs {
   const DevSpec* specs; const double* theta;
   int add_noise;
   double* mean; double* var; long long sOut;
+  int n_active;                    // set by the launcher (1-D grid: blocks x problems)
 };
 
 struct ReduceArgs {

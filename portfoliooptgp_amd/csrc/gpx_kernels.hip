@@ -1007,20 +1007,38 @@ __global__ __launch_bounds__(256) void trmv_t_kernel(TrmvArgs a) {
 }
 
 __global__ __launch_bounds__(256) void train_pred_kernel(TrainPredArgs a) {
-  const int b = a.active[blockIdx.y];
+  // (K⁻¹)_jj = Σ_{i≥j} W_ij²: a column stream over W's lower triangle like trmv_t — 1-D grid,
+  // column block major (the longest columns of every problem first), 8 loads in flight per lane
+  constexpr int R = 8;
+  const int na = a.n_active;
+  const int blk = (int)blockIdx.x / na;
+  const int b = a.active[(int)blockIdx.x - blk * na];
   const double* W = a.W + (long long)b * a.sW;
   __shared__ double sred[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j = blockIdx.x * 64 + lane;
+  const int j = blk * 64 + lane;
   const int n = a.nvalid[b];
-  double s = 0.0;
+  double s[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) s[q] = 0.0;
   if (j < n) {
-    for (int i = blockIdx.x * 64 + wave; i < n; i += 4) {
+    int i = blk * 64 + wave;
+    for (; i + 4 * (R - 1) < n; i += 4 * R) {
+      double w[R];
+#pragma unroll
+      for (int q = 0; q < R; ++q) w[q] = W[(long long)(i + 4 * q) * a.ld + j];
+#pragma unroll
+      for (int q = 0; q < R; ++q) s[q] = fma(w[q], w[q], s[q]);
+    }
+    for (; i < n; i += 4) {
       const double w = W[(long long)i * a.ld + j];
-      s = fma(w, w, s);
+      s[0] = fma(w, w, s[0]);
     }
   }
-  sred[wave][lane] = s;
+  double t = 0.0;
+#pragma unroll
+  for (int q = 0; q < R; ++q) t += s[q];
+  sred[wave][lane] = t;
   __syncthreads();
   if (wave == 0 && j < n) {
     const double kinv = (sred[0][lane] + sred[1][lane]) + (sred[2][lane] + sred[3][lane]);
@@ -1033,7 +1051,9 @@ __global__ __launch_bounds__(256) void train_pred_kernel(TrainPredArgs a) {
 }
 
 void launch_train_pred(const TrainPredArgs& a, int n_active, int Np, hipStream_t s) {
-  hipLaunchKernelGGL(train_pred_kernel, dim3(Np / 64, n_active), dim3(256), 0, s, a);
+  TrainPredArgs t = a;
+  t.n_active = n_active;
+  hipLaunchKernelGGL(train_pred_kernel, dim3(Np / 64 * n_active), dim3(256), 0, s, t);
 }
 
 void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s) {
