@@ -154,7 +154,7 @@ void alpha_solve(const Run& r) {
 }
 
 // fused K⁻¹ = WᵀW formation + gradient contraction over lower tiles, then the reduction
-void contract(const Run& r, bool single_term, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+void contract(const Run& r, int max_terms, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   gpx_batch* bt = r.bt;
   GemmArgs g = gemm_args(bt->W, bt->Np, bt->W, bt->Np, nullptr, 0, mat_stride(bt), bt->Np, bt->Np,
                          bt->Np, TRI_KMIN_I, 1, 1.0, 0.0);
@@ -162,7 +162,7 @@ void contract(const Run& r, bool single_term, hipEvent_t ev0 = nullptr, hipEvent
   g.specs = bt->d_specs; g.theta = bt->d_theta; g.nvalid = bt->d_n;
   g.partial = bt->partial; g.sPartial = bt->partial_stride;
   g.ev_start = ev0; g.ev_stop = ev1;
-  gemm(r, g, single_term ? EPI_CONTRACT1 : EPI_CONTRACT, true, false);
+  gemm(r, g, max_terms <= 1 ? EPI_CONTRACT1 : max_terms == 2 ? EPI_CONTRACT2 : EPI_CONTRACT, true, false);
 }
 
 void reduce(const Run& r) {
@@ -442,8 +442,8 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   // The contraction fills the chip by itself (Np²/2/128² tiles per problem): one launch over
   // every active problem, alone on the stream.
   const Run all{bt, bt->d_active, n_active, s};
-  bool single_term = true;
-  for (int i = 0; i < n_active; ++i) single_term = single_term && bt->specs[active[i]].n_terms == 1;
+  int max_terms = 1;
+  for (int i = 0; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[active[i]].n_terms);
   PhaseTimer ct(ctx->profiling != 0, s);
   // the contraction kernel is timestamped at its actual start/end (hipExtLaunchKernel), so
   // its duration excludes any wait behind kernels of other streams (concurrent batches)
@@ -477,7 +477,7 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     cr.s = bt->hp;
   }
   ct.mark();
-  contract(cr, single_term, kev[0], kev[1]);
+  contract(cr, max_terms, kev[0], kev[1]);
   ct.mark();
   reduce(cr);
   if (prio) {

@@ -38,7 +38,7 @@ struct LeafArgs {
 enum : int { TRI_KMAX_I = 1, TRI_KMAX_J = 2, TRI_KMIN_J = 4, TRI_KMIN_I = 8 };
 // EPI_CONTRACT1: EPI_CONTRACT specialised for single-term kernels (every active spec has
 // n_terms == 1): a quarter of the derivative registers, no spills in the epilogue.
-enum : int { EPI_STORE = 0, EPI_CONTRACT = 1, EPI_COLSUMSQ = 2, EPI_CONTRACT1 = 3 };
+enum : int { EPI_STORE = 0, EPI_CONTRACT = 1, EPI_COLSUMSQ = 2, EPI_CONTRACT1 = 3, EPI_CONTRACT2 = 4 };
 // tile enumeration for rectangular launches (see gemm_kernel)
 enum : int { ORDER_ROW_ASC = 0, ORDER_COL_DESC = 1, ORDER_ROW_DESC = 2, ORDER_COL_ASC = 3 };
 

@@ -549,7 +549,7 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
   constexpr int MT = WT / 16;
   constexpr int NLD = BM * BK / 2 / 256;  // double2 chunks per thread per operand
   constexpr int kMainLds = 2 * 2 * BK * S;
-  constexpr int kEpiLds = (EPI == EPI_CONTRACT || EPI == EPI_CONTRACT1)
+  constexpr int kEpiLds = (EPI == EPI_CONTRACT || EPI == EPI_CONTRACT1 || EPI == EPI_CONTRACT2)
       ? 4 * 16 * WT + 2 * BM * GPX_MAX_DIM + 2 * BM + GPX_THETA_STRIDE + 64 : 0;
   __shared__ __attribute__((aligned(16))) double smem[kMainLds > kEpiLds ? kMainLds : kEpiLds];
 
@@ -721,8 +721,10 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
           if (a.beta != 0.0) v = fma(a.beta, C[i * ldc + j], v);
           C[i * ldc + j] = v;
         }
-  } else if constexpr (EPI == EPI_CONTRACT || EPI == EPI_CONTRACT1) {
-    constexpr int NT = (EPI == EPI_CONTRACT1) ? 1 : GPX_MAX_TERMS;
+  } else if constexpr (EPI == EPI_CONTRACT || EPI == EPI_CONTRACT1 || EPI == EPI_CONTRACT2) {
+    // derivative registers sized for the batch's largest spec: 1 term (SE / Matern sweeps),
+    // 2 terms (sums / products such as Multi-Input_GPR's Exponential x Exponential) or 4
+    constexpr int NT = (EPI == EPI_CONTRACT1) ? 1 : (EPI == EPI_CONTRACT2) ? 2 : GPX_MAX_TERMS;
     // Gradient contraction over this lower tile of K⁻¹ = WᵀW (acc = K⁻¹_ij):
     //   g_θ += w_ij (α_i α_j − K⁻¹_ij) ∂K_ij/∂θ,  w = 2 below the diagonal, 1 on it.
     // The accumulators go through LDS in two halves so that the kernel-derivative code runs
@@ -894,11 +896,13 @@ void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hip
     if (epi == EPI_STORE) launch_gemm_t<128, EPI_STORE>(a, ta, tb, n_active, s);
     else if (epi == EPI_CONTRACT) launch_gemm_t<128, EPI_CONTRACT>(a, ta, tb, n_active, s);
     else if (epi == EPI_CONTRACT1) launch_gemm_t<128, EPI_CONTRACT1>(a, ta, tb, n_active, s);
+    else if (epi == EPI_CONTRACT2) launch_gemm_t<128, EPI_CONTRACT2>(a, ta, tb, n_active, s);
     else launch_gemm_t<128, EPI_COLSUMSQ>(a, ta, tb, n_active, s);
   } else {
     if (epi == EPI_STORE) launch_gemm_t<64, EPI_STORE>(a, ta, tb, n_active, s);
     else if (epi == EPI_CONTRACT) launch_gemm_t<64, EPI_CONTRACT>(a, ta, tb, n_active, s);
     else if (epi == EPI_CONTRACT1) launch_gemm_t<64, EPI_CONTRACT1>(a, ta, tb, n_active, s);
+    else if (epi == EPI_CONTRACT2) launch_gemm_t<64, EPI_CONTRACT2>(a, ta, tb, n_active, s);
     else launch_gemm_t<64, EPI_COLSUMSQ>(a, ta, tb, n_active, s);
   }
 }
