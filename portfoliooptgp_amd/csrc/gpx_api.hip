@@ -48,6 +48,7 @@ double gemm_issued_flops(const GemmArgs& a, int na) {
 
 void gemm(const Run& r, GemmArgs a, int epi, bool ta, bool tb) {
   a.active = r.d_act;
+  a.small_tiles = r.bt->small_tiles;
   launch_gemm(a, epi, ta, tb, r.na, r.s);
   if (r.bt->ctx->profiling) r.bt->flops_acc += gemm_issued_flops(a, r.na);
 }
@@ -168,7 +169,7 @@ void contract(const Run& r, int max_terms, hipEvent_t ev0 = nullptr, hipEvent_t 
 void reduce(const Run& r) {
   gpx_batch* bt = r.bt;
   GemmArgs g{};
-  g.M = g.N = bt->Np; g.lower_only = 1;
+  g.M = g.N = bt->Np; g.lower_only = 1; g.small_tiles = bt->small_tiles;  // as gemm() launches it
   const int bm = gemm_tile(g, r.na), tt = bt->Np / bm;
   ReduceArgs ra{};
   ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
@@ -638,6 +639,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   // A = W · Kxs with fused column sum of squares
   GemmArgs g = gemm_args(bt->W, Np, kxs, Mp, nullptr, Mp, 0, Np, Mp, Np, TRI_KMAX_I, 0, 1.0, 0.0);
   g.sA = mat_stride(bt); g.sB = skx; g.sC = 0;
+  g.small_tiles = bt->small_tiles;  // the tile size gemm() will launch with
   const int bm = gemm_tile(g, n_active);
   const int nrt = Np / bm;
   const size_t pneed = (size_t)bt->B * nrt * Mp;

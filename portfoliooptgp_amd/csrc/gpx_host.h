@@ -54,6 +54,7 @@ struct gpx_batch {
   // per-batch auxiliary streams and events (the recursion's T-product forks), so that
   // independent batches of one context can evaluate concurrently on different streams
   int aux_priority = 0;       // priority the aux streams were created with
+  int small_tiles = 0;        // GEMM tiles by workgroup count (set for the SVGP's B=1 Kmm batch)
   hipStream_t aux[kAux] = {};
   hipEvent_t ev[kEvents] = {};
   hipStream_t hp = nullptr;   // highest-priority stream for the contraction (GPX_CONTRACT_PRIORITY)

@@ -51,6 +51,7 @@ struct GemmArgs {
   int tri;            // TRI_* flags restricting the k range per tile
   int lower_only;     // only tiles with ti >= tj
   int order;          // ORDER_* tile enumeration (rectangular launches)
+  int small_tiles;    // pick the tile size by workgroup count (single-problem launches: SVGP)
   int n_active;       // set by the launcher (XCD-aware problem placement)
   double alpha, beta;
   // EPI_CONTRACT

@@ -865,8 +865,14 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
 // on how many problems share the launch, so a problem's arithmetic — and therefore its fit —
 // is bit-identical whichever other problems are batched with it (same padded size Np).
 int gemm_tile(const GemmArgs& a, int n_active) {
-  (void)n_active;
   if (a.M % 128 != 0 || a.N % 128 != 0) return 64;
+  if (a.small_tiles) {
+    // launches of a single problem (the SVGP's M x M chain): 128-tiles only when they still
+    // put a workgroup on every CU — 64 tiles of 128 on 256 CUs left three quarters idle
+    const long long t = a.lower_only ? (long long)(a.M / 128) * (a.M / 128 + 1) / 2
+                                     : (long long)(a.M / 128) * (a.N / 128);
+    return t * n_active >= 256 ? 128 : 64;
+  }
   return (a.M >= 512 && a.N >= 512) ? 128 : 64;
 }
 

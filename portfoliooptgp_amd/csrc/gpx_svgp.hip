@@ -167,6 +167,7 @@ int gpx_svgp_create(gpx_ctx* ctx, int N, int M, int D, const double* X, const do
     gpx_svgp_destroy(sv);
     return rc;
   }
+  sv->kmm->small_tiles = 1;   // every M x M launch here is one problem: size tiles to fill the chip
   const size_t mm = (size_t)Mp * Mp;
   sv->off_G = 0;
   sv->off_w = (long long)mm;
@@ -475,6 +476,7 @@ int gpx_svgp_predict(gpx_svgp* sv, const double* theta, const double* Z, const d
   launch_trmv_t(t, 1, s);
   // column sums of squares of A = W Kms and B = V Kms
   GemmArgs ga = gemm_args(W, Mp, sv->Kms, Mnp, nullptr, Mnp, 0, Mp, Mnp, Mp, TRI_KMAX_I, 0, 1.0, 0.0);
+  ga.small_tiles = sv->kmm->small_tiles;  // the tile size gemm() will launch with
   const int nrt = Mp / gemm_tile(ga, 1);
   rc = ensure(ctx, sv->pA, sv->pa_cap, (size_t)nrt * Mnp);
   if (rc != GPX_OK) return rc;
