@@ -132,7 +132,8 @@ def main():
                     help="resident device slots (continuous-batching width)")
     ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 2)),
                     help="alternating device batches (host/device overlap)")
-    ap.add_argument("--n", type=int, default=N_POINTS)
+    ap.add_argument("--points", "--n", dest="n", type=int, default=N_POINTS,
+                    help="points per series (use --points under torch.distributed.run, whose parser takes --n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -240,11 +241,14 @@ def main():
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        nf = torch.tensor([float(sum(nfev)), float(len(nfev))], device=cdev, dtype=torch.float64)
+        nf = torch.tensor([float(sum(nfev)), float(len(nfev)), float(tm.evals)], device=cdev,
+                          dtype=torch.float64)
         dist.all_reduce(nf)
         nfev_mean = float(nf[0] / nf[1])
+        evals_all = float(nf[2])  # device evaluations over all ranks
     else:
         nfev_mean = float(np.mean(nfev))
+        evals_all = float(tm.evals)
 
     total_fits = F * args.steps * world
     value = total_fits / elapsed
@@ -265,7 +269,7 @@ def main():
     contract_flops = tm.contract_alg_flops / max(tm.contract_launches, 1.0)
     achieved = contract_flops / (contract_ms * 1e-3) / 1e12
     traffic, traffic_src = contract_traffic(n, contract_flops)
-    eval_alg = (n ** 3 + 2 * 3 * n ** 2) * tm.evals  # SURVEY §8d F_eval(N), P=2
+    eval_alg = (n ** 3 + 2 * 3 * n ** 2) * evals_all  # SURVEY §8d F_eval(N), P=2, all ranks
     out = {
         "metric": "GP fits/sec (N=4096, 1-D RBF)",
         "value": value,
@@ -285,9 +289,9 @@ def main():
                    "kernel": "SquaredExponential",
                    "parallelism": f"independent fits, {world} process(es) x 1 GPU, RCCL all_gather of results"},
         "nfev_mean": nfev_mean,
-        "evals_per_s": tm.evals / elapsed if world == 1 else None,
+        "evals_per_s": evals_all / elapsed,
         # whole-job algorithmic rate: F_eval(N) x evaluations / wall time of the timed steps
-        "eval_alg_tflops": eval_alg / elapsed / 1e12 if world == 1 else None,
+        "eval_alg_tflops": eval_alg / elapsed / 1e12,
         "roofline": {
             "kernel": "gemm_kernel<128,T,N,EPI_CONTRACT1> (K^-1 = W^T W fused with the gradient contraction)",
             "bound": "mfma",
@@ -308,8 +312,9 @@ def main():
             "achieved_isolated": iso,
             "frac_isolated": iso / FP64_PEAK_TFLOPS if iso else None,
             # the whole path: F_eval(N) x evaluations / wall time of the timed steps
-            "achieved_job": eval_alg / elapsed / 1e12 if world == 1 else None,
-            "frac_job": eval_alg / elapsed / 1e12 / FP64_PEAK_TFLOPS if world == 1 else None,
+            # per GPU: the whole-job algorithmic rate over all ranks ÷ the number of GPUs
+            "achieved_job": eval_alg / elapsed / 1e12 / world,
+            "frac_job": eval_alg / elapsed / 1e12 / world / FP64_PEAK_TFLOPS,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
