@@ -12,10 +12,11 @@ gfx950 in ``libgpx.so`` behind the C ABI of ``include/gpx.h``.
     mean, var = m.predict_f(X)
 """
 from . import _native, data, inducing_variables, kernels, likelihoods, models, optimizers, utilities
-from ._native import GPXError, NotPositiveDefiniteError
+from ._native import GPXError, InvalidParameterError, NotPositiveDefiniteError
 from .parameter import Parameter
 from .utilities import print_summary, set_trainable
 
 __all__ = ["inducing_variables", "kernels", "likelihoods", "models", "optimizers", "utilities", "Parameter",
-           "set_trainable", "print_summary", "GPXError", "NotPositiveDefiniteError"]
+           "set_trainable", "print_summary", "GPXError", "InvalidParameterError",
+           "NotPositiveDefiniteError"]
 __version__ = "0.1.0"

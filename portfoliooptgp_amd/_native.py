@@ -57,6 +57,14 @@ class GPXError(RuntimeError):
     pass
 
 
+INFO_BAD_THETA = -1  # info code of a problem whose θ was screened out on the host
+
+
+class InvalidParameterError(GPXError):
+    """A constrained hyperparameter left (0, ∞) — softplus(u) underflows to 0 for u < -745 after
+    an extreme L-BFGS-B step. The problem is not evaluated (the rest of its batch is)."""
+
+
 class NotPositiveDefiniteError(GPXError):
     """K + σn²I is not positive definite (GPflow raises tf.errors.InvalidArgumentError from
     tf.linalg.cholesky in the same situation)."""

@@ -42,6 +42,25 @@ def to_device_f64(a, device: int) -> torch.Tensor:
     return t.to(device=f"cuda:{device}", dtype=torch.float64).contiguous()
 
 
+def _rows(x: torch.Tensor, D: int) -> torch.Tensor:
+    """[M, D] view of prediction inputs (a 1-D input is one column; an empty one has D columns)."""
+    if x.numel() == 0:
+        return x if x.ndim == 2 else x.reshape(0, D)
+    return x.reshape(x.shape[0], -1)
+
+
+def screen_theta(act: np.ndarray, theta: np.ndarray, n_params: np.ndarray, info: np.ndarray) -> np.ndarray:
+    """Active rows whose constrained θ (kernel parameters + σn²) are all finite and > 0; the
+    others get info = INFO_BAD_THETA and stay out of the device call, so one fit whose softplus
+    underflowed does not fail its whole batch (gpx_batch_lml_grad rejects the call otherwise)."""
+    ok = np.array([bool(np.all(np.isfinite(theta[b, : n_params[b] + 1]) & (theta[b, : n_params[b] + 1] > 0.0)))
+                   for b in act], dtype=bool)
+    if ok.all():
+        return act
+    info[act[~ok]] = N.INFO_BAD_THETA
+    return np.ascontiguousarray(act[ok])
+
+
 class Engine:
     def __init__(self, Xs: Sequence, Ys: Sequence, specs: Sequence[N.GpxKernelSpec],
                  device: Optional[int] = None):
@@ -100,13 +119,18 @@ class Engine:
         return np.ascontiguousarray(np.asarray(active, dtype=np.int32))
 
     def lml_grad(self, active: Sequence[int], theta: np.ndarray):
-        """logML [B], ∂logML/∂θ [B, 16], info [B] for the active rows (others untouched)."""
+        """logML [B], ∂logML/∂θ [B, 16], info [B] for the active rows (others untouched).
+        info[b] > 0: the LAPACK-style failing pivot; info[b] == INFO_BAD_THETA: θ of problem b
+        is not finite and > 0, so b was left out of the device call (the others still run)."""
         act = self._active(active)
         theta = np.ascontiguousarray(theta, dtype=np.float64)
         assert theta.shape == (self.B, N.GPX_THETA_STRIDE)
         lml = np.full(self.B, np.nan)
         grad = np.full((self.B, N.GPX_THETA_STRIDE), np.nan)
         info = np.zeros(self.B, dtype=np.int32)
+        act = screen_theta(act, theta, self.n_params, info)
+        if len(act) == 0:
+            return lml, grad, info
         dp = ctypes.POINTER(ctypes.c_double)
         ip = ctypes.POINTER(ctypes.c_int32)
         rc = self.lib.gpx_batch_lml_grad(self.handle, len(act), act.ctypes.data_as(ip),
@@ -127,8 +151,7 @@ class Engine:
             raise NotImplementedError("full covariance is only defined for predict_f")
         act = self._active(active)
         theta = np.ascontiguousarray(theta, dtype=np.float64)
-        xs = [to_device_f64(x, self.device) for x in Xnew]
-        xs = [x.reshape(x.shape[0], -1) for x in xs]
+        xs = [_rows(to_device_f64(x, self.device), self.D) for x in Xnew]
         if any(x.shape[1] != self.D for x in xs):
             raise ValueError(f"Xnew must have {self.D} columns")
         if not full_cov and all(
@@ -136,6 +159,10 @@ class Engine:
             return self._predict_train(act, theta, add_noise)
         M = max(x.shape[0] for x in xs)
         dev = f"cuda:{self.device}"
+        if M == 0:  # every Xnew is empty: empty outputs, as GPflow returns [0, 1] tensors
+            e = torch.empty(0, dtype=torch.float64, device=dev)
+            ev = torch.empty(0, 0, dtype=torch.float64, device=dev) if full_cov else e
+            return [e for _ in act], [ev for _ in act], np.zeros(self.B, dtype=np.int32)
         Xn = torch.zeros(self.B, M, self.D, dtype=torch.float64, device=dev)
         for b, x in zip(act, xs):
             Xn[b, : x.shape[0]] = x
@@ -207,6 +234,7 @@ class Engine:
         self.Y[b, :n] = y
         torch.cuda.current_stream(self.device).synchronize()
         self.specs[b] = spec
+        self.n_params[b] = spec.n_params
         self.n[b] = n
         rc = self.lib.gpx_batch_rebind(self.handle, int(b), int(n), ctypes.byref(spec))
         if rc != N.GPX_OK:
@@ -315,13 +343,14 @@ class SVGPEngine:
         return self.eval_finish()
 
     def predict(self, theta, Z, q_mu, q_sqrt, Xnew, add_noise: bool):
-        x = to_device_f64(Xnew, self.device)
-        x = x.reshape(x.shape[0], -1).contiguous()
+        x = _rows(to_device_f64(Xnew, self.device), self.D).contiguous()
         if x.shape[1] != self.D:
             raise ValueError(f"Xnew must have {self.D} columns")
         Mn = x.shape[0]
         mean = torch.empty(Mn, dtype=torch.float64, device=x.device)
         var = torch.empty(Mn, dtype=torch.float64, device=x.device)
+        if Mn == 0:  # empty Xnew: empty outputs (GPflow returns [0, 1] tensors)
+            return mean, var
         info = ctypes.c_int32(0)
         rc = self.lib.gpx_svgp_predict(self.handle, *self._args(theta, Z, q_mu, q_sqrt),
                                        ctypes.c_void_p(x.data_ptr()), Mn, 1 if add_noise else 0,

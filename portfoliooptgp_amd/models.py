@@ -48,6 +48,10 @@ class GPR:
             raise NotImplementedError("single-output GPR only (Y must be [N, 1])")
         if Xt.shape[0] != Yt.shape[0]:
             raise ValueError("X and Y must have the same number of rows")
+        if Xt.shape[0] == 0:
+            # GPflow would return the prior; the device engine needs at least one training point
+            # (an empty factorisation has nothing to run on the GPU), so refuse it up front
+            raise ValueError("GPR needs at least one training point (X has 0 rows)")
         self.data = (Xt, Yt)
         self.kernel = kernel
         if likelihood is None:
@@ -114,6 +118,8 @@ class GPR:
         theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
         theta[b] = self.theta_row()
         lml, grad, info = eng.lml_grad([b], theta)
+        if info[b] == N.INFO_BAD_THETA:
+            raise N.InvalidParameterError(f"hyperparameters out of (0, inf): {theta[b, :eng.n_params[b] + 1]}")
         if info[b] != 0:
             raise N.NotPositiveDefiniteError(
                 f"Cholesky decomposition was not successful: pivot {int(info[b])} of K + noise I "

@@ -55,7 +55,9 @@ def _resolve_model(closure):
 def _not_pd_policy(on_not_pd: str):
     """GPflow/TF raise when the Cholesky of K + σn²I fails (tf.linalg.cholesky →
     InvalidArgumentError inside Scipy.minimize); on_not_pd="inf" instead reports an infinite
-    loss (zero gradient) for that point, so L-BFGS-B's line search backs off and the fit goes on."""
+    loss (zero gradient) for that point, so L-BFGS-B's line search backs off and the fit goes on.
+    The same holds for a point whose constrained hyperparameters left (0, inf) (softplus
+    underflow after an extreme step: InvalidParameterError)."""
     if on_not_pd not in ("raise", "inf"):
         raise ValueError("on_not_pd must be 'raise' (GPflow's behaviour) or 'inf'")
     return on_not_pd == "inf"
@@ -68,7 +70,7 @@ def _guarded(fn, as_inf: bool):
     def g(x):
         try:
             return fn(x)
-        except N.NotPositiveDefiniteError:
+        except (N.NotPositiveDefiniteError, N.InvalidParameterError):
             return float("inf"), np.zeros_like(np.asarray(x, dtype=np.float64))
     return g
 
@@ -491,7 +493,10 @@ class _LockstepEvaluator:
                 with lock:
                     lml, grad, info = eng.lml_grad(rows, theta)
                 for i, r in zip(active, rows):
-                    if info[r] != 0:
+                    if info[r] == N.INFO_BAD_THETA:
+                        out[i] = N.InvalidParameterError(
+                            f"model {i}: hyperparameters out of (0, inf): {theta[r, :eng.n_params[r] + 1]}")
+                    elif info[r] != 0:
                         out[i] = N.NotPositiveDefiniteError(
                             f"Cholesky decomposition was not successful (model {i}, pivot "
                             f"{int(info[r])}): K + noise I is not positive definite", info[r])

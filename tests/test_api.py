@@ -108,6 +108,12 @@ def test_no_cpu_fallback():
         gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables)
 
 
+def test_empty_training_set_is_refused():
+    """0 training rows: refused at construction (the device engine needs a point to factorise)."""
+    with pytest.raises(ValueError, match="at least one training point"):
+        gpx.models.GPR((np.zeros((0, 1)), np.zeros((0, 1))), kernel=gpx.kernels.SquaredExponential())
+
+
 def test_scipy_rejects_foreign_closures():
     with pytest.raises(TypeError):
         gpx.optimizers.Scipy().minimize(lambda: 0.0, [Parameter(1.0).unconstrained_variable])

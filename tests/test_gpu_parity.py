@@ -424,6 +424,19 @@ def test_predict_full_cov():
         np.testing.assert_allclose(np.diag(c), var.numpy().ravel(), rtol=1e-9, atol=1e-12 * s2)
 
 
+def test_empty_prediction_inputs():
+    """Xnew with 0 rows gives empty [0,1] outputs ([1,0,0] with full_cov), as GPflow does."""
+    x = np.arange(10.0)[:, None]
+    m = gpx.models.GPR((x, np.sin(x)), kernel=K.SquaredExponential(), noise_variance=1e-2)
+    e = np.zeros((0, 1))
+    for mu, var in (m.predict_f(e), m.predict_y(e)):
+        assert tuple(mu.shape) == (0, 1) and tuple(var.shape) == (0, 1)
+    mu, cov = m.predict_f(e, full_cov=True)
+    assert tuple(mu.shape) == (0, 1) and tuple(cov.shape) == (1, 0, 0)
+    mu, var = m.predict_f(x[:3])  # the model still predicts normally afterwards
+    assert tuple(mu.shape) == (3, 1) and np.all(np.isfinite(var.numpy()))
+
+
 def test_config4_shape_matern52_5d():
     """BASELINE config C4 shape (Multi-Input_GPR: 5-D inputs, Matern-5/2, N=4096), computed in
     fp64 (the reference's precision; see DESIGN.md on why not fp32): logML, gradient and

@@ -17,6 +17,7 @@ class FakeEngine:
     def __init__(self, B):
         self.B, self.device = B, 0
         self.target = np.ones((B, 2))
+        self.n_params = np.full(B, 2)
         self.calls = []
 
     def rebind(self, b, X, Y, spec):
@@ -110,3 +111,37 @@ def test_not_positive_definite_raises_like_gpflow_or_backs_off():
         assert m.kernel.lengthscales.value <= 2.5
     with pytest.raises(ValueError):
         gpx.optimizers.Scipy().minimize_stream(_models(1), width=1, engine=NotPDEngine(1), on_not_pd="ignore")
+
+
+class BadThetaEngine(FakeEngine):
+    """As FakeEngine, but the lengthscale counts as out of (0, ∞) once it passes 2.5 (the
+    device engine's host-side screen marks such rows INFO_BAD_THETA and skips them)."""
+
+    def lml_grad(self, rows, theta):
+        lml, grad, info = super().lml_grad(rows, theta)
+        for r in rows:
+            if theta[r, 0] > 2.5:
+                info[r] = N.INFO_BAD_THETA
+        return lml, grad, info
+
+
+def test_out_of_domain_hyperparameters_fail_one_fit_only():
+    """A fit whose θ leaves (0, ∞) raises InvalidParameterError (default) or backs off
+    (on_not_pd="inf"); with "inf" every fit of the batch finishes."""
+    with pytest.raises(N.InvalidParameterError):
+        gpx.optimizers.Scipy().minimize_stream(_models(4), width=2, engine=BadThetaEngine(2))
+    ms = _models(4)
+    res, _ = gpx.optimizers.Scipy().minimize_stream(ms, width=2, engine=BadThetaEngine(2), on_not_pd="inf")
+    for r, m in zip(res, ms):
+        assert np.isfinite(r.fun) and m.kernel.lengthscales.value <= 2.5
+
+
+def test_screen_theta():
+    from portfoliooptgp_amd.engine import screen_theta
+    th = np.ones((4, N.GPX_THETA_STRIDE))
+    th[1, 0] = 0.0          # softplus underflow
+    th[2, 2] = np.nan       # beyond problem 2's parameters (n_params=1: θ0, σn² at index 1) ...
+    th[3, 1] = np.inf       # ... σn² of problem 3
+    info = np.zeros(4, dtype=np.int32)
+    act = screen_theta(np.arange(4, dtype=np.int32), th, np.array([2, 2, 1, 1]), info)
+    assert list(act) == [0, 2] and list(info) == [0, N.INFO_BAD_THETA, 0, N.INFO_BAD_THETA]

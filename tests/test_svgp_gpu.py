@@ -91,6 +91,8 @@ def test_predict_f_and_predict_y():
     assert np.abs(var.numpy() - vo).max() <= 1e-7 * np.abs(vo).max() + 1e-10
     _, vy = m.predict_y(xs)
     np.testing.assert_allclose(vy.numpy() - var.numpy(), 1e-3, rtol=1e-9)
+    mu0, var0 = m.predict_f(np.zeros((0, 2)))  # empty Xnew: empty outputs
+    assert tuple(mu0.shape) == (0, 1) and tuple(var0.shape) == (0, 1)
 
 
 def test_sharded_partials_equal_single_shard():

@@ -1,0 +1,153 @@
+"""Throughput of the BASELINE.json configurations other than the headline C2 on one GPU, each
+next to the CPU oracle on the same inputs (the oracle is the checker / CPU baseline only).
+
+  C1  the reference's own plumbing: GPR/main.py's 8-kernel sweep (GPR/main.py:105-114, noise
+      1e-5 fixed, maxiter 100, predict_f at the training inputs — GPR/model_trainer.py:14-25)
+      on every daily ticker series of tests/golden/tickers.npz (N=68), all fits streamed
+      through the device slots; the oracle fits every one of them too (so losses are compared
+      fit by fit).
+  C3  20 synthetic series x N=2048 (seeds 0..19, SE, same protocol); CPU: one full oracle fit.
+  C4  Multi-Input_GPR shape: D=5 (4 z-scored random-walk features + z-scored time),
+      Matern52, N=4096, fp64; CPU: oracle evaluations x the GPU's mean nfev.
+
+usage: python tools/config_bench.py [--configs c1,c3,c4] [--c4-fits 32]
+Prints one JSON line per config.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+os.environ.setdefault("GPX_TRACE_ROUNDS", "1")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import portfoliooptgp_amd as gpx  # noqa: E402
+from oracle import gp_oracle as O  # noqa: E402
+
+K = gpx.kernels
+
+
+def sweep_kernels():
+    """GPR/main.py:105-114, fresh GPflow defaults."""
+    return [K.SquaredExponential(), K.Matern12(), K.RationalQuadratic(), K.Exponential(),
+            K.SquaredExponential() + K.Matern12(),
+            K.Exponential() + K.Periodic(K.SquaredExponential()) + K.Linear(),
+            K.Exponential() + K.Periodic(K.SquaredExponential()),
+            K.SquaredExponential() * K.Matern12()]
+
+
+def gpr(x, y, kern, noise=1e-5):
+    m = gpx.models.GPR((x, y), kernel=kern)
+    m.likelihood.variance.assign(noise)
+    gpx.set_trainable(m.likelihood.variance, False)
+    return m
+
+
+def stream(models, width, groups=1):
+    opt = gpx.optimizers.Scipy()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res, _ = opt.minimize_stream(models, width=width, groups=groups, predict_train=True,
+                                 options=dict(maxiter=100), on_not_pd="inf")
+    torch.cuda.synchronize()
+    global _last_rounds
+    _last_rounds = getattr(opt, "last_trace", None) or []
+    return res, time.perf_counter() - t0
+
+
+_last_rounds = []
+
+
+def c1():
+    z = np.load(os.path.join(ROOT, "tests", "golden", "tickers.npz"))
+    names = sorted({k.split("|")[0] for k in z.files})
+    series = [(z[f"{t}|x"], z[f"{t}|y"]) for t in names]
+    models = lambda: [gpr(x, y, k) for x, y in series for k in sweep_kernels()]  # noqa: E731
+    stream(models(), 64)  # warm-up (engine creation, code-object load)
+    res, dt = stream(models(), len(series) * 8)
+    t0 = time.perf_counter()
+    ores = [O.scipy_minimize(_omodel(x, y, k), 100) for x, y in series for k in O.reference_kernel_list()]
+    dt_cpu = time.perf_counter() - t0
+    rel = np.array([abs(r.fun - o.fun) / max(1.0, abs(o.fun)) for r, o in zip(res, ores)])
+    kn = ["SE", "M12", "RQ", "Exp", "SE+M12", "Exp+Per+Lin", "Exp+Per", "SExM12"]
+    off = [{"series": names[i // 8], "kernel": kn[i % 8], "gpu_loss": res[i].fun, "oracle_loss": ores[i].fun,
+            "gpu_nfev": int(res[i].nfev), "oracle_nfev": ores[i].nfev,
+            "gpu_msg": str(getattr(res[i], "message", ""))[:60]}
+           for i in range(len(res)) if not rel[i] <= 1e-5]
+    rounds = _last_rounds
+    return {"rounds": len(rounds), "round_ms_mean": float(np.mean(np.diff([t for t, _ in rounds])) * 1e3)
+            if len(rounds) > 1 else None, "nfev_max": int(max(r.nfev for r in res)), "mismatches": off,
+            "config": "C1", "workload": f"8-kernel sweep x {len(series)} daily ticker series (N=68), "
+            "noise 1e-5 fixed, maxiter 100, predict_f(X_train)", "fits": len(res),
+            "fits_per_s": len(res) / dt, "cpu_fits_per_s": len(ores) / dt_cpu, "cpu_cores": _threads(),
+            "nfev_mean": float(np.mean([r.nfev for r in res])),
+            "loss_rel_diff_median": float(np.nanmedian(rel)), "fits_within_1e-5": int(np.sum(rel <= 1e-5))}
+
+
+def _omodel(x, y, k, noise=1e-5):
+    om = O.OGPR(x, y, k, noise_variance=noise)
+    om.noise.trainable = False
+    return om
+
+
+def _threads():
+    return int(os.environ.get("OPENBLAS_NUM_THREADS") or os.environ.get("OMP_NUM_THREADS") or os.cpu_count())
+
+
+def c3():
+    series = [O.synthetic_series(2048, seed=s) for s in range(20)]
+    stream([gpr(x, y, K.SquaredExponential()) for x, y in series[:4]], 4)  # warm-up
+    res, dt = stream([gpr(x, y, K.SquaredExponential()) for x, y in series], 20, groups=2)
+    t0 = time.perf_counter()
+    o = O.scipy_minimize(_omodel(*series[0], O.OSquaredExponential()), 100)
+    O.OGPR(*series[0], O.OSquaredExponential(), noise_variance=1e-5).predict_f(series[0][0])
+    dt_cpu = time.perf_counter() - t0
+    return {"config": "C3", "workload": "20 synthetic series x N=2048, SE, noise 1e-5 fixed, maxiter 100, "
+            "predict_f(X_train), one GPU (20 slots, 2 device batches)", "fits": len(res),
+            "fits_per_s": len(res) / dt, "nfev_mean": float(np.mean([r.nfev for r in res])),
+            "cpu_fits_per_s": 1.0 / dt_cpu, "cpu_sample": f"one full oracle fit of series 0 (nfev {o.nfev})",
+            "cpu_cores": _threads(), "loss_rel_diff_series0": abs(res[0].fun - o.fun) / abs(o.fun)}
+
+
+def c4_data(n, seed):
+    rng = np.random.default_rng(100 + seed)
+    X = np.hstack([np.cumsum(rng.standard_normal((n, 4)), axis=0), np.linspace(0.0, 1.0, n)[:, None]])
+    X = (X - X.mean(0)) / X.std(0, ddof=1)
+    return X, O.synthetic_series(n, seed)[1]
+
+
+def c4(fits):
+    data = [c4_data(4096, s) for s in range(fits)]
+    stream([gpr(x, y, K.Matern52(), 1e-3) for x, y in data[:2]], 2)
+    res, dt = stream([gpr(x, y, K.Matern52(), 1e-3) for x, y in data], fits, groups=2)
+    nfev = float(np.mean([r.nfev for r in res]))
+    om = _omodel(*data[0], O.OMatern52(), 1e-3)
+    om.loss_and_grad_u()
+    t0 = time.perf_counter()
+    om.loss_and_grad_u()
+    ev = time.perf_counter() - t0
+    return {"config": "C4", "workload": f"Multi-Input shape D=5, Matern52, N=4096, fp64, noise 1e-3 fixed, "
+            f"{fits} fits, predict_f(X_train)", "fits": fits, "fits_per_s": fits / dt, "nfev_mean": nfev,
+            "evals_per_s": sum(r.nfev for r in res) / dt,
+            "eval_alg_tflops": sum(r.nfev for r in res) * (4096 ** 3 + 2 * 3 * 4096 ** 2) / dt / 1e12,
+            "cpu_fits_per_s": 1.0 / (ev * nfev), "cpu_sample": f"1 oracle loss+grad eval ({ev:.2f} s) x GPU nfev",
+            "cpu_cores": _threads()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c1,c3,c4")
+    ap.add_argument("--c4-fits", type=int, default=32)
+    a = ap.parse_args()
+    for c in a.configs.split(","):
+        out = {"c1": c1, "c3": c3, "c4": lambda: c4(a.c4_fits)}[c]()
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
