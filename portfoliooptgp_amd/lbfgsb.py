@@ -1,0 +1,145 @@
+"""scipy's L-BFGS-B, driven by reverse communication instead of a callback.
+
+``scipy.optimize.minimize(fun, x0, jac=True, method="L-BFGS-B", options=...)`` (what
+``gpflow.optimizers.Scipy`` calls, GPR/model_trainer.py:18-19) is a Python loop around the
+compiled L-BFGS-B routine ``setulb``: ``setulb`` asks for f and g at a point, the loop calls
+``fun`` there, and repeats until ``setulb`` reports convergence, or until ``maxiter`` / ``maxfun``
+stops it. ``LbfgsbStepper`` runs that same loop (scipy 1.15's ``_minimize_lbfgsb`` with no
+bounds and no callback) as a generator. The caller reads the requested point, evaluates it
+and passes ``(f, g)`` back. Many fits can then be stepped from ONE host thread, and every
+request of a round is evaluated in one batched device call.
+
+The memoisation follows scipy's ``ScalarFunction`` / ``MemoizeJac``: a point equal to the last
+evaluated one is not evaluated again. ``nfev``, ``nit``, the messages and the returned fields
+are scipy's. Each fit's sequence of ``setulb`` calls is therefore exactly the one
+``scipy.optimize.minimize`` makes, so its trajectory is bit-identical
+(``tests/test_stream_driver.py`` compares against scipy itself with atol=0).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+from scipy.optimize import OptimizeResult
+
+try:  # scipy ≥ 1.15: the C port of L-BFGS-B (task codes as int32 pairs)
+    from scipy.optimize import _lbfgsb
+    from scipy.optimize._lbfgsb_py import LbfgsInvHessProduct, status_messages, task_messages
+    AVAILABLE = hasattr(_lbfgsb, "setulb") and isinstance(status_messages, dict)
+except Exception:  # pragma: no cover - older scipy: callers use the threaded driver
+    AVAILABLE = False
+
+# scipy 1.15 _minimize_lbfgsb defaults
+_DEFAULTS = dict(maxcor=10, ftol=2.2204460492503131e-09, gtol=1e-5, maxfun=15000, maxiter=15000, maxls=20)
+# options accepted by _minimize_lbfgsb that have no effect with jac=True and no bounds
+_INERT = {"disp", "iprint", "eps", "finite_diff_rel_step"}
+
+
+def supports(method: str, scipy_kwargs: dict) -> bool:
+    """True when minimize(..., method, **scipy_kwargs) is a plain unbounded L-BFGS-B run
+    that the stepper reproduces exactly."""
+    if not AVAILABLE or str(method).lower() != "l-bfgs-b":
+        return False
+    if set(scipy_kwargs) - {"options"}:
+        return False  # bounds, callback, tol, ... : leave those to scipy itself
+    opts = scipy_kwargs.get("options") or {}
+    return not (set(opts) - set(_DEFAULTS) - _INERT)
+
+
+class LbfgsbStepper:
+    """One L-BFGS-B minimisation. ``x`` is the point whose (f, g) is wanted next (None once
+    finished); ``tell(f, g)`` supplies it; ``result()`` is scipy's OptimizeResult."""
+
+    def __init__(self, x0, options: Optional[dict] = None):
+        opts = dict(_DEFAULTS)
+        opts.update({k: v for k, v in (options or {}).items() if k in _DEFAULTS})
+        x0 = np.atleast_1d(np.asarray(x0))
+        if x0.ndim != 1:
+            raise ValueError("'x0' must only have one dimension.")
+        if x0.dtype.kind in np.typecodes["AllInteger"]:
+            x0 = np.asarray(x0, dtype=float)
+        if not opts["maxls"] > 0:
+            raise ValueError("maxls must be positive.")
+        self.nfev = 0
+        self._res: Optional[OptimizeResult] = None
+        self._gen = self._run(x0.ravel(), opts)
+        self.x: Optional[np.ndarray] = next(self._gen)
+
+    @property
+    def done(self) -> bool:
+        return self.x is None
+
+    def tell(self, f, g) -> None:
+        try:
+            self.x = self._gen.send((f, g))
+        except StopIteration:
+            self.x = None
+
+    def result(self) -> OptimizeResult:
+        return self._res
+
+    @staticmethod
+    def _scalar(fx):
+        if not np.isscalar(fx):
+            try:
+                fx = np.asarray(fx).item()
+            except (TypeError, ValueError) as e:
+                raise ValueError("The user-provided objective function must return a scalar value.") from e
+        return fx
+
+    def _run(self, x0, o):
+        m, pgtol = o["maxcor"], o["gtol"]
+        factr = o["ftol"] / np.finfo(float).eps
+        n, = x0.shape
+        # ScalarFunction: f and g at x0 up front (one evaluation), then memoised on x
+        sf_x = np.atleast_1d(x0).astype(np.float64)
+        fx, gx = yield sf_x.copy()
+        self.nfev = 1
+        sf_f, sf_g = self._scalar(fx), np.atleast_1d(gx)
+
+        nbd = np.zeros(n, np.int32)
+        low_bnd = np.zeros(n, np.float64)
+        upper_bnd = np.zeros(n, np.float64)
+        x = np.array(x0, dtype=np.float64)
+        f = np.array(0.0, dtype=np.int32)
+        g = np.zeros((n,), dtype=np.int32)
+        wa = np.zeros(2 * m * n + 5 * n + 11 * m * m + 8 * m, np.float64)
+        iwa = np.zeros(3 * n, dtype=np.int32)
+        task = np.zeros(2, dtype=np.int32)
+        ln_task = np.zeros(2, dtype=np.int32)
+        lsave = np.zeros(4, dtype=np.int32)
+        isave = np.zeros(44, dtype=np.int32)
+        dsave = np.zeros(29, dtype=np.float64)
+        n_iterations = 0
+        while True:
+            g = g.astype(np.float64)
+            _lbfgsb.setulb(m, x, low_bnd, upper_bnd, nbd, f, g, factr, pgtol, wa,
+                           iwa, task, lsave, isave, dsave, o["maxls"], ln_task)
+            if task[0] == 3:  # f and g wanted at x
+                if not np.array_equal(x, sf_x):
+                    sf_x = np.atleast_1d(np.asarray(x)).astype(np.float64)
+                    fx, gx = yield sf_x.copy()
+                    self.nfev += 1
+                    sf_f, sf_g = self._scalar(fx), np.atleast_1d(gx)
+                f, g = sf_f, sf_g
+            elif task[0] == 1:  # new iteration
+                n_iterations += 1
+                if n_iterations >= o["maxiter"]:
+                    task[0], task[1] = 5, 504
+                elif self.nfev > o["maxfun"]:
+                    task[0], task[1] = 5, 502
+            else:
+                break
+        if task[0] == 4:
+            warnflag = 0
+        elif self.nfev > o["maxfun"] or n_iterations >= o["maxiter"]:
+            warnflag = 1
+        else:
+            warnflag = 2
+        s = wa[0: m * n].reshape(m, n)
+        y = wa[m * n: 2 * m * n].reshape(m, n)
+        n_corrs = min(isave[30], m)
+        msg = status_messages[task[0]] + ": " + task_messages[task[1]]
+        self._res = OptimizeResult(fun=f, jac=g, nfev=self.nfev, njev=self.nfev, nit=n_iterations,
+                                   status=warnflag, message=msg, x=x, success=(warnflag == 0),
+                                   hess_inv=LbfgsInvHessProduct(s[:n_corrs], y[:n_corrs]))

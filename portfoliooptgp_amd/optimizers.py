@@ -6,11 +6,15 @@ unconstrained variables and writes the result back, returning scipy's OptimizeRe
 (``.fun``, ``.x``, ``.nfev``, ``.nit``; ``opt_logs.fun`` at
 Multi-Input_GPR/models/model_trainer.py:40).
 
-``minimize_batch`` runs one *unmodified* scipy L-BFGS-B per model, each in its own host
-thread; whenever every still-running optimiser is waiting for a function value, the pending
-points are evaluated together in ONE batched device pass (gpx_batch_lml_grad). Each
-optimiser sees exactly the values a solo run would see, so trajectories are per-fit identical
-to sequential fitting while the device works on all fits at once.
+``minimize_batch`` / ``minimize_stream`` run one scipy L-BFGS-B per model and evaluate the
+points the fits are waiting for together, in ONE batched device pass (gpx_batch_lml_grad).
+Each optimiser sees exactly the values a solo run would see, so trajectories are per-fit
+identical to sequential fitting while the device works on all fits at once. For plain
+L-BFGS-B runs (the reference's) the fits are stepped by reverse communication
+(``lbfgsb.LbfgsbStepper``: scipy's own ``setulb`` calls, no callback) from one host thread per
+device batch (``_SteppedDriver``). Other methods or options, or GPX_THREADED_DRIVER=1, run
+each fit's ``scipy.optimize.minimize`` in its own host thread around a barrier
+(``_LockstepEvaluator``).
 """
 from __future__ import annotations
 
@@ -26,8 +30,14 @@ import scipy.optimize
 import torch
 
 from . import _native as N
+from . import lbfgsb
 from .engine import Engine
 from .kernels import compile_spec
+
+
+# GPX_THREADED_DRIVER=1: one host thread per fit/slot around scipy.optimize.minimize (the
+# generic path, always used for methods/options the reverse-communication stepper does not cover)
+_THREADED = os.environ.get("GPX_THREADED_DRIVER", "0") not in ("", "0")
 
 
 def _new_stream(device):
@@ -138,6 +148,15 @@ class Scipy:
                             device=device if device is not None else models[0].device)
         for i, m in enumerate(models):
             m._attach(engine, i)
+        if lbfgsb.supports(method, scipy_kwargs) and not _THREADED:
+            drv = _SteppedDriver(models, [engine], 1, scipy_kwargs.get("options") or {}, as_inf,
+                                 models[0].data[0].shape[1], fixed=True)
+            drv.run()
+            self.last_trace = drv.trace
+            for e in drv.errors:
+                if e is not None:
+                    raise e
+            return drv.results
         step = _LockstepEvaluator(engine, models)
         results: List[Optional[scipy.optimize.OptimizeResult]] = [None] * len(models)
         errors: List[Optional[BaseException]] = [None] * len(models)
@@ -215,6 +234,18 @@ class Scipy:
                                       [compile_spec(m.kernel, D) for m in seed], device=dev))
         else:
             engines = list(engine) if isinstance(engine, (list, tuple)) else [engine]
+        if predict_inputs is not None and len(predict_inputs) != len(models):
+            raise ValueError("predict_inputs needs one Xnew per model")
+        if lbfgsb.supports(method, scipy_kwargs) and not _THREADED:
+            drv = _SteppedDriver(models, engines, groups, scipy_kwargs.get("options") or {}, as_inf, D,
+                                 predict_train=predict_train or predict_inputs is not None,
+                                 predict_inputs=predict_inputs, width=width)
+            drv.run()
+            self.last_trace = drv.trace
+            for e in drv.errors:
+                if e is not None:
+                    raise e
+            return drv.results, drv.preds
         step = _LockstepEvaluator(engines, None, total=len(models), groups=groups)
         results = [None] * len(models)
         if predict_inputs is not None:
@@ -516,3 +547,200 @@ class _LockstepEvaluator:
                 self.cv.notify_all()
             for i in out:
                 self._slot_event(i).set()
+
+
+class _SteppedDriver:
+    """Single-threaded-per-group fitting with reverse-communication L-BFGS-B (lbfgsb.py).
+
+    Device slots are split into groups; each group has (engine, rows, lock) and ONE host
+    thread (group 0: the caller's) that loops: refill idle rows from the shared queue, evaluate
+    every active fit's requested point in one ``lml_grad`` call, pass each fit its (loss, grad),
+    and predict + release the fits that finished. Per-fit trajectories are exactly scipy's
+    (same setulb calls); there are no per-fit threads, events or condition variables, so the
+    host cost of a round is just the fits' L-BFGS-B steps. ``fixed=True`` (minimize_batch):
+    model i stays in row i of the single engine, nothing is rebound."""
+
+    def __init__(self, models, engines, groups: int, options: dict, as_inf: bool, D: int,
+                 predict_train: bool = False, predict_inputs=None, width: Optional[int] = None,
+                 fixed: bool = False):
+        self.models, self.options, self.as_inf, self.D = models, options, as_inf, D
+        self.predict_train, self.predict_inputs, self.fixed = predict_train, predict_inputs, fixed
+        G = max(1, groups)
+        # group g: rows of its engine (one engine per group, or one engine split row-wise)
+        if len(engines) > 1:
+            G = len(engines)
+            per = min(e.B for e in engines)
+            self.groups = [(engines[g], list(range(per)), threading.Lock(), _new_stream(engines[g].device))
+                           for g in range(G)]
+        else:
+            e = engines[0]
+            lock = threading.Lock()
+            self.groups = [(e, list(range(g, e.B, G)), lock, _new_stream(e.device) if G > 1 else None)
+                           for g in range(G)]
+        if width is not None:  # at most `width` slots in total, dealt round-robin over groups
+            keep = [[] for _ in self.groups]
+            flat = [(g, r) for k in range(max(len(x[1]) for x in self.groups))
+                    for g, x in enumerate(self.groups) if k < len(x[1]) for r in [x[1][k]]]
+            for g, r in flat[:width]:
+                keep[g].append(r)
+            self.groups = [(e, keep[g], lk, s) for g, (e, _, lk, s) in enumerate(self.groups)]
+        self.queue = list(range(len(models)))
+        self.qlock = threading.Lock()
+        self.results = [None] * len(models)
+        self.preds = [None] * len(models) if predict_train else None
+        self.errors: List[Optional[BaseException]] = [None] * len(models)
+        self.trace = [] if os.environ.get("GPX_TRACE_ROUNDS") else None
+        self.first_call = threading.Event()
+        self.first_call_s = 0.0
+
+    def _next(self) -> Optional[int]:
+        with self.qlock:
+            return self.queue.pop(0) if self.queue else None
+
+    def run(self):
+        G = len(self.groups)
+        errs = []
+
+        def run_group(g):
+            try:
+                self._serve(g)
+            except BaseException as e:  # pragma: no cover - surfaced below
+                errs.append(e)
+            finally:
+                if g == 0:
+                    self.first_call.set()
+        helpers = [threading.Thread(target=run_group, args=(g,), daemon=True) for g in range(1, G)]
+        for t in helpers:
+            t.start()
+        run_group(0)
+        for t in helpers:
+            t.join()
+        if errs:
+            raise errs[0]
+
+    def _serve(self, g: int):
+        eng, rows, lock, stream = self.groups[g]
+        if stream is None:
+            return self._loop(g, eng, rows, lock)
+        prev = torch.cuda.current_stream()
+        torch.cuda.set_stream(stream)  # this group's device calls use its own stream
+        try:
+            return self._loop(g, eng, rows, lock)
+        finally:
+            torch.cuda.set_stream(prev)
+
+    def _bind(self, i: int, eng, row: int, lock):
+        m = self.models[i]
+        if not self.fixed:
+            with lock:
+                eng.rebind(row, m.data[0], m.data[1], compile_spec(m.kernel, self.D))
+            m._attach(eng, row)
+        variables = m.trainable_variables
+        if not variables:
+            raise ValueError("model has no trainable variables")
+        return {"i": i, "m": m, "v": variables, "st": lbfgsb.LbfgsbStepper(_pack(variables), self.options)}
+
+    def _loop(self, g: int, eng, rows, lock):
+        G = len(self.groups)
+        free = list(rows) if not self.fixed else []
+        active = {}
+        if self.fixed:
+            for r in rows:
+                if r < len(self.models):
+                    active[r] = self._bind(r, eng, r, lock)
+        n_calls = 0
+        while True:
+            while free:
+                i = self._next()
+                if i is None:
+                    break
+                r = free.pop(0)
+                try:
+                    active[r] = self._bind(i, eng, r, lock)
+                except BaseException as e:
+                    self.errors[i] = e
+                    self.models[i]._engine = None
+                    free.insert(0, r)
+            if not active:
+                return
+            if g > 0 and n_calls == 0 and G > 1:
+                # stagger: start g/G of a group-0 call after group 0's first call returns, so the
+                # concurrent batches run out of phase (one's latency-bound recursion levels under
+                # the other's large GEMMs); started in phase they stay in phase
+                self.first_call.wait(timeout=10.0)
+                time.sleep(self.first_call_s * g / G)
+            act = sorted(active)
+            theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+            for r in act:
+                s = active[r]
+                _unpack(s["v"], s["st"].x)
+                theta[r] = s["m"].theta_row()
+            if self.trace is not None:
+                self.trace.append((time.perf_counter(), len(act)))
+            t_call = time.perf_counter()
+            with lock:
+                lml, grad, info = eng.lml_grad(act, theta)
+            if g == 0 and n_calls == 0:
+                self.first_call_s = time.perf_counter() - t_call
+                self.first_call.set()
+            n_calls += 1
+            done = []
+            for r in act:
+                s = active[r]
+                err = None
+                if info[r] == N.INFO_BAD_THETA:
+                    err = N.InvalidParameterError(
+                        f"model {s['i']}: hyperparameters out of (0, inf): {theta[r, :eng.n_params[r] + 1]}")
+                elif info[r] != 0:
+                    err = N.NotPositiveDefiniteError(
+                        f"Cholesky decomposition was not successful (model {s['i']}, pivot "
+                        f"{int(info[r])}): K + noise I is not positive definite", info[r])
+                try:
+                    if err is not None:
+                        if not self.as_inf:
+                            raise err
+                        loss, gr = float("inf"), np.zeros_like(np.asarray(s["st"].x, dtype=np.float64))
+                    else:
+                        loss, gr = s["m"].loss_and_grad_unconstrained(s["v"], lml=lml[r], grad_theta=grad[r])
+                    s["st"].tell(loss, gr)
+                except BaseException as e:
+                    self.errors[s["i"]] = e
+                    done.append((r, False))
+                    continue
+                if s["st"].done:
+                    done.append((r, True))
+            self._finish(eng, lock, active, done)
+            for r, _ in done:
+                del active[r]
+                if not self.fixed:
+                    free.append(r)
+
+    def _finish(self, eng, lock, active, done):
+        pred_rows, xs = [], []
+        for r, ok in done:
+            s = active[r]
+            if ok:
+                res = s["st"].result()
+                _unpack(s["v"], res.x)
+                self.results[s["i"]] = res
+                if self.predict_train:
+                    pred_rows.append(r)
+                    xs.append(s["m"].data[0] if self.predict_inputs is None else self.predict_inputs[s["i"]])
+            elif not self.fixed:
+                s["m"]._engine = None
+        if pred_rows:
+            theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+            for r in pred_rows:
+                theta[r] = active[r]["m"].theta_row()
+            try:
+                with lock:
+                    mu, var, _ = eng.predict(pred_rows, theta, xs, False)
+                for k, r in enumerate(pred_rows):
+                    self.preds[active[r]["i"]] = (mu[k].reshape(-1, 1), var[k].reshape(-1, 1))
+            except BaseException as e:
+                for r in pred_rows:
+                    self.errors[active[r]["i"]] = e
+        if not self.fixed:
+            for r, ok in done:
+                if ok:
+                    active[r]["m"]._engine = None

@@ -145,3 +145,46 @@ def test_screen_theta():
     info = np.zeros(4, dtype=np.int32)
     act = screen_theta(np.arange(4, dtype=np.int32), th, np.array([2, 2, 1, 1]), info)
     assert list(act) == [0, 2] and list(info) == [0, N.INFO_BAD_THETA, 0, N.INFO_BAD_THETA]
+
+
+def test_lbfgsb_stepper_is_scipy():
+    """The reverse-communication driver makes exactly scipy.optimize.minimize's setulb calls:
+    same x, fun, jac, nfev, nit, status and message, including maxiter / maxfun stops and an
+    infinite-loss region (the on_not_pd="inf" back-off)."""
+    from portfoliooptgp_amd.lbfgsb import LbfgsbStepper
+
+    def rosen(x):
+        return scipy.optimize.rosen(x), scipy.optimize.rosen_der(x)
+
+    def walled(x):
+        if x[0] > 2.0:
+            return float("inf"), np.zeros_like(x)
+        return float(-x[0] + (x[1] - 1.0) ** 2), np.array([-1.0, 2.0 * (x[1] - 1.0)])
+
+    cases = [(rosen, [-1.2, 1.0, 0.3, 2.0], {}), (rosen, [0.0] * 7, dict(maxiter=15)),
+             (rosen, [3.0, -2.0], dict(maxfun=20)), (walled, [0.0, 0.0], dict(maxiter=100)),
+             (rosen, [0.5413248546129181] * 2, dict(maxiter=100, ftol=1e-12, gtol=1e-9, maxcor=5, maxls=10))]
+    for fn, x0, opts in cases:
+        r0 = scipy.optimize.minimize(fn, np.array(x0), jac=True, method="L-BFGS-B", options=opts)
+        st = LbfgsbStepper(np.array(x0), opts)
+        while not st.done:
+            st.tell(*fn(st.x.copy()))
+        r1 = st.result()
+        np.testing.assert_array_equal(r1.x, r0.x)
+        np.testing.assert_array_equal(r1.jac, r0.jac)
+        assert (r1.fun, r1.nfev, r1.njev, r1.nit, r1.status, r1.message) == \
+               (r0.fun, r0.nfev, r0.njev, r0.nit, r0.status, r0.message)
+
+
+def test_batch_equals_solo():
+    """minimize_batch (lock-step, model i in row i) gives every fit its solo trajectory."""
+    ms = _models(5)
+    ref = [_solo(m) for m in _models(5)]
+    eng = FakeEngine(5)
+    for b, m in enumerate(ms):
+        eng.rebind(b, m.data[0], m.data[1], None)
+    res = gpx.optimizers.Scipy().minimize_batch(ms, engine=eng)
+    for r, r0 in zip(res, ref):
+        assert r.nfev == r0.nfev and r.message == r0.message
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+    assert eng.calls[0] == 5
