@@ -647,7 +647,10 @@ class _SteppedDriver:
         if self.fixed:
             for r in rows:
                 if r < len(self.models):
-                    active[r] = self._bind(r, eng, r, lock)
+                    try:
+                        active[r] = self._bind(r, eng, r, lock)
+                    except BaseException as e:
+                        self.errors[r] = e
         n_calls = 0
         while True:
             while free:

@@ -188,3 +188,21 @@ def test_batch_equals_solo():
         assert r.nfev == r0.nfev and r.message == r0.message
         np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
     assert eng.calls[0] == 5
+
+
+def test_model_without_trainable_variables_fails_alone():
+    """A fit that cannot start (nothing trainable) raises ValueError after the others finish,
+    in both the lock-step and the streaming driver."""
+    for stream in (False, True):
+        ms = _models(3)
+        gpx.set_trainable(ms[1].kernel.lengthscales, False)
+        gpx.set_trainable(ms[1].kernel.variance, False)
+        eng = FakeEngine(3)
+        for b, m in enumerate(ms):
+            eng.rebind(b, m.data[0], m.data[1], None)
+        with pytest.raises(ValueError, match="no trainable variables"):
+            if stream:
+                gpx.optimizers.Scipy().minimize_stream(ms, width=2, engine=FakeEngine(2))
+            else:
+                gpx.optimizers.Scipy().minimize_batch(ms, engine=eng)
+        assert ms[0].kernel.lengthscales.value != 1.0 and ms[2].kernel.lengthscales.value != 1.0
