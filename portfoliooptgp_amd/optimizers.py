@@ -281,6 +281,8 @@ class Scipy:
                 m._attach(eng, local)
                 step.bind(slot, m)
                 variables = m.trainable_variables
+                if not variables:
+                    raise ValueError("model has no trainable variables")
 
                 def func(x):
                     _unpack(variables, x)
