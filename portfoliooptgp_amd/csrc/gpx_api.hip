@@ -212,10 +212,12 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
         return fail(ctx, GPX_BAD_ARG, "theta must be finite and > 0 (constrained space)");
     }
   }
-  HIPX(ctx, hipMemcpyAsync(bt->d_active, active, sizeof(int) * n_active, hipMemcpyHostToDevice, s));
-  HIPX(ctx, hipMemcpyAsync(bt->d_theta, theta, sizeof(double) * GPX_THETA_STRIDE * bt->B,
-                           hipMemcpyHostToDevice, s));
-  HIPX(ctx, hipMemsetAsync(bt->d_info, 0, sizeof(int) * bt->B, s));
+  // one DMA from the pinned block: [active | info = 0 | theta] (every call ends with a stream
+  // synchronize, so the previous call's transfers out of h_io have completed)
+  std::memcpy(bt->h_io, active, sizeof(int) * n_active);
+  std::memset(bt->h_io + bt->io_info_off, 0, sizeof(int) * bt->B);
+  std::memcpy(bt->h_io + bt->io_theta_off, theta, sizeof(double) * GPX_THETA_STRIDE * bt->B);
+  HIPX(ctx, hipMemcpyAsync(bt->d_io, bt->h_io, bt->io_res_off, hipMemcpyHostToDevice, s));
   return GPX_OK;
 }
 
@@ -317,13 +319,26 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
   if (hipMalloc(&bt->z, vec) != hipSuccess || hipMalloc(&bt->alpha, vec) != hipSuccess ||
       hipMalloc(&bt->ldiag, vec) != hipSuccess ||
       hipMalloc(&bt->partial, (size_t)B * bt->partial_stride * sizeof(double)) != hipSuccess ||
-      hipMalloc(&bt->results, (size_t)B * kResStride * sizeof(double)) != hipSuccess ||
       hipMalloc(&bt->d_n, sizeof(int) * B) != hipSuccess ||
-      hipMalloc(&bt->d_specs, sizeof(DevSpec) * B) != hipSuccess ||
-      hipMalloc(&bt->d_theta, sizeof(double) * GPX_THETA_STRIDE * B) != hipSuccess ||
-      hipMalloc(&bt->d_active, sizeof(int) * B) != hipSuccess ||
-      hipMalloc(&bt->d_info, sizeof(int) * B) != hipSuccess)
+      hipMalloc(&bt->d_specs, sizeof(DevSpec) * B) != hipSuccess)
     return cleanup("out of device memory for batch vectors");
+  {
+    const size_t ints = ((size_t)B * sizeof(int) + 7) / 8 * 8;
+    bt->io_info_off = ints;
+    bt->io_theta_off = 2 * ints;
+    bt->io_res_off = bt->io_theta_off + (size_t)B * GPX_THETA_STRIDE * sizeof(double);
+    bt->io_bytes = bt->io_res_off + (size_t)B * kResStride * sizeof(double);
+    if (hipMalloc(&bt->d_io, bt->io_bytes) != hipSuccess ||
+        hipHostMalloc(&bt->h_io, bt->io_bytes) != hipSuccess)
+      return cleanup("out of memory for the batch I/O block");
+    std::memset(bt->h_io, 0, bt->io_bytes);
+    bt->d_active = reinterpret_cast<int*>(bt->d_io);
+    bt->d_info = reinterpret_cast<int*>(bt->d_io + bt->io_info_off);
+    bt->d_theta = reinterpret_cast<double*>(bt->d_io + bt->io_theta_off);
+    bt->results = reinterpret_cast<double*>(bt->d_io + bt->io_res_off);
+    bt->h_info = reinterpret_cast<int*>(bt->h_io + bt->io_info_off);
+    bt->h_results = reinterpret_cast<double*>(bt->h_io + bt->io_res_off);
+  }
   // W and L upper triangles must read as exact zeros (never written afterwards)
   if (hipMemset(bt->W, 0, mat) != hipSuccess || hipMemset(bt->L, 0, mat) != hipSuccess ||
       hipMemset(bt->K, 0, mat) != hipSuccess)
@@ -342,8 +357,6 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
     return cleanup("upload failed");
   bt->fac_theta.assign((size_t)B * GPX_THETA_STRIDE, 0.0);
   bt->fac_valid.assign(B, 0);
-  bt->h_results.assign((size_t)B * kResStride, 0.0);
-  bt->h_info.assign(B, 0);
   *out = bt;
   return GPX_OK;
 }
@@ -352,10 +365,10 @@ int gpx_batch_destroy(gpx_batch* bt) {
   if (!bt) return GPX_BAD_ARG;
   (void)hipSetDevice(bt->ctx->device);
   for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
-                  (void*)bt->ldiag, (void*)bt->partial, (void*)bt->results, (void*)bt->d_n,
-                  (void*)bt->d_specs, (void*)bt->d_theta, (void*)bt->d_active, (void*)bt->d_info,
-                  (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw})
+                  (void*)bt->ldiag, (void*)bt->partial, (void*)bt->d_io, (void*)bt->d_n,
+                  (void*)bt->d_specs, (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw})
     if (p) (void)hipFree(p);
+  if (bt->h_io) (void)hipHostFree(bt->h_io);
   for (int g = 0; g < kAux; ++g)
     if (bt->aux[g]) (void)hipStreamDestroy(bt->aux[g]);
   if (bt->hp) (void)hipStreamDestroy(bt->hp);
@@ -488,9 +501,9 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   ct.mark();
   total.mark();
   HIPX(ctx, hipGetLastError());
-  HIPX(ctx, hipMemcpyAsync(bt->h_results.data(), bt->results, sizeof(double) * kResStride * bt->B,
-                           hipMemcpyDeviceToHost, s));
-  HIPX(ctx, hipMemcpyAsync(bt->h_info.data(), bt->d_info, sizeof(int) * bt->B, hipMemcpyDeviceToHost, s));
+  // one DMA into the pinned block: [info | theta (unchanged) | results]
+  HIPX(ctx, hipMemcpyAsync(bt->h_io + bt->io_info_off, bt->d_io + bt->io_info_off,
+                           bt->io_bytes - bt->io_info_off, hipMemcpyDeviceToHost, s));
   HIPX(ctx, hipStreamSynchronize(s));
   if (total.on) {
     bt->timing.factor_ms = bt->timing.alpha_ms = 0.0;
@@ -515,7 +528,7 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   int status = GPX_OK;
   for (int i = 0; i < n_active; ++i) {
     const int b = active[i];
-    const double* res = bt->h_results.data() + (size_t)b * kResStride;
+    const double* res = bt->h_results + (size_t)b * kResStride;
     info[b] = bt->h_info[b];
     const int np = bt->specs[b].n_params;
     if (info[b] != 0) {
@@ -659,7 +672,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   }
   pt.mark();
   HIPX(ctx, hipGetLastError());
-  HIPX(ctx, hipMemcpyAsync(bt->h_info.data(), bt->d_info, sizeof(int) * bt->B, hipMemcpyDeviceToHost, s));
+  HIPX(ctx, hipMemcpyAsync(bt->h_info, bt->d_info, sizeof(int) * bt->B, hipMemcpyDeviceToHost, s));
   HIPX(ctx, hipStreamSynchronize(s));
   if (pt.on) {
     bt->timing.factor_ms = pt.ms(0, 1);

@@ -47,8 +47,15 @@ struct gpx_batch {
   // factor cache: theta row of the last factorisation per problem
   std::vector<double> fac_theta;
   std::vector<char> fac_valid;
-  std::vector<double> h_results;
-  std::vector<int> h_info;
+  // per-call I/O in ONE device block mirrored by ONE pinned host block, laid out
+  //   [active: B ints][info: B ints][theta: B×16][results: B×kResStride]   (8-byte aligned)
+  // so an evaluation uploads [active, info=0, theta] in one DMA and downloads [info ..
+  // results] in one DMA (was 2 pageable copies + a memset up, 2 pageable copies down)
+  char* d_io = nullptr;
+  char* h_io = nullptr;       // pinned
+  size_t io_info_off = 0, io_theta_off = 0, io_res_off = 0, io_bytes = 0;
+  double* h_results = nullptr;  // views into h_io
+  int* h_info = nullptr;
   gpx_timing timing{};
   double flops_acc = 0.0;
   // per-batch auxiliary streams and events (the recursion's T-product forks), so that

@@ -53,6 +53,8 @@ def screen_theta(act: np.ndarray, theta: np.ndarray, n_params: np.ndarray, info:
     """Active rows whose constrained θ (kernel parameters + σn²) are all finite and > 0; the
     others get info = INFO_BAD_THETA and stay out of the device call, so one fit whose softplus
     underflowed does not fail its whole batch (gpx_batch_lml_grad rejects the call otherwise)."""
+    if np.isfinite(theta).all() and (theta > 0.0).all():  # the usual case, one pass
+        return act
     ok = np.array([bool(np.all(np.isfinite(theta[b, : n_params[b] + 1]) & (theta[b, : n_params[b] + 1] > 0.0)))
                    for b in act], dtype=bool)
     if ok.all():
