@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--m", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--cpu", action="store_true",
+                    help="also time one ELBO+gradient evaluation of the CPU oracle (oracle/svgp_oracle.py)")
     a = ap.parse_args()
     n, M = a.n, a.m
     rng = np.random.default_rng(0)
@@ -51,8 +53,20 @@ def main():
         eng.predict(theta, Z, q, R, xs, False)
     torch.cuda.synchronize()
     dp = (time.perf_counter() - t1) / a.reps
-    print(json.dumps({"N": n, "M": M, "eval_ms": dt * 1e3, "alg_tflops": (big + small) / dt / 1e12,
-                      "big_gemm_flops": big, "predict_ms_4096": dp * 1e3}))
+    out = {"N": n, "M": M, "eval_ms": dt * 1e3, "alg_tflops": (big + small) / dt / 1e12,
+           "big_gemm_flops": big, "predict_ms_4096": dp * 1e3}
+    if a.cpu:  # CPU baseline: the oracle (test infrastructure) on the same inputs, one evaluation
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from oracle import gp_oracle as O
+        from oracle import svgp_oracle as S
+        osv = S.OSVGP(O.OSquaredExponential(lengthscales=2.0, variance=1.0), Z, num_data=n,
+                      noise_variance=1e-4, q_mu=q, q_sqrt=R)
+        t2 = time.perf_counter()
+        elbo_cpu = osv.elbo_and_grads(X, Y)[0]
+        out["cpu_eval_ms"] = (time.perf_counter() - t2) * 1e3
+        out["cpu_threads"] = int(os.environ.get("OPENBLAS_NUM_THREADS") or os.cpu_count())
+        out["elbo_rel_diff"] = abs(eng.elbo_grad(theta, Z, q, R)[0] - elbo_cpu) / abs(elbo_cpu)
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
