@@ -5,15 +5,23 @@ CSRC := portfoliooptgp_amd/csrc
 LIB := portfoliooptgp_amd/libgpx.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 
-all: $(LIB)
+CSMOKE := tests/c/gpx_c_smoke
+
+all: $(LIB) $(CSMOKE)
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h include/gpx.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-soname,libgpx.so $^ -o $@
+
+# plain-C consumer of the C ABI (gcc, HIP runtime API only), run by tests/test_c_abi_gpu.py
+$(CSMOKE): tests/c/gpx_c_smoke.c include/gpx.h $(LIB)
+	gcc -O2 -std=c11 -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude $< $(LIB) \
+	  -L/opt/rocm/lib -lamdhip64 -lm -Wl,-rpath,'$$ORIGIN/../../portfoliooptgp_amd' \
+	  -Wl,-rpath,/opt/rocm/lib -o $@
 
 clean:
-	rm -f $(CSRC)/*.o $(LIB)
+	rm -f $(CSRC)/*.o $(LIB) $(CSMOKE)
 
 .PHONY: all clean
