@@ -20,7 +20,8 @@ GPX_MAX_DIM = 16
  GPX_LINEAR) = range(1, 9)
 GPX_SUM, GPX_PRODUCT = 0, 1
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgpx.so")
+# GPX_LIB: an alternative build of the library (A/B experiments); default the in-tree one
+LIB_PATH = os.environ.get("GPX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgpx.so")
 
 # every symbol include/gpx.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
