@@ -116,8 +116,9 @@ class LbfgsbStepper:
             _lbfgsb.setulb(m, x, low_bnd, upper_bnd, nbd, f, g, factr, pgtol, wa,
                            iwa, task, lsave, isave, dsave, o["maxls"], ln_task)
             if task[0] == 3:  # f and g wanted at x
-                if not np.array_equal(x, sf_x):
-                    sf_x = np.atleast_1d(np.asarray(x)).astype(np.float64)
+                # np.array_equal(x, sf_x) for two float64 vectors of one shape (NaN unequal)
+                if not (x == sf_x).all():
+                    sf_x = x.copy()
                     fx, gx = yield sf_x.copy()
                     self.nfev += 1
                     sf_f, sf_g = self._scalar(fx), np.atleast_1d(gx)

@@ -147,18 +147,26 @@ class GPR:
         if lml is None:
             lml, grad_theta = self._lml_and_grad_theta()
         variables = self.trainable_variables if variables is None else variables
-        pindex = {id(p): i for i, p in enumerate(self.kernel.parameters)}
-        nk = len(self.kernel.parameters)
-        g = np.empty(len(variables), dtype=np.float64)
-        for k, v in enumerate(variables):
-            p = v._param
-            if p is self.likelihood.variance:
-                gi = grad_theta[nk]
-            elif id(p) in pindex:
-                gi = grad_theta[pindex[id(p)]]
-            else:
-                raise ValueError(f"variable {v.name} is not a parameter of this model")
-            g[k] = -gi * p.dtheta_du()
+        cache = getattr(self, "_grad_map", None)
+        if cache is None or cache[0] is not variables:
+            # θ-row index of each variable (kernel parameters, then σn² at n_params); cached
+            # for the variables object an optimiser passes on every call
+            pindex = {id(p): i for i, p in enumerate(self.kernel.parameters)}
+            nk = len(self.kernel.parameters)
+            rows = []
+            for v in variables:
+                p = v._param
+                if p is self.likelihood.variance:
+                    rows.append(nk)
+                elif id(p) in pindex:
+                    rows.append(pindex[id(p)])
+                else:
+                    raise ValueError(f"variable {v.name} is not a parameter of this model")
+            cache = self._grad_map = (variables, rows, [v._param for v in variables])
+        _, rows, params = cache
+        g = np.empty(len(rows), dtype=np.float64)
+        for k, (r, p) in enumerate(zip(rows, params)):
+            g[k] = -grad_theta[r] * p.dtheta_du()
         return -float(lml), g
 
     # ---------------------------------------------------------------- prediction ------

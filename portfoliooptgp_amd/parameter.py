@@ -17,7 +17,16 @@ _THRESH = math.log(_EPS) + 2.0  # tfp.math.softplus_inverse threshold
 
 
 def softplus(u: float) -> float:
-    return float(np.logaddexp(0.0, u))
+    """np.logaddexp(0, u) bit for bit: numpy's scalar npy_logaddexp with the same libm
+    exp/log1p, without the ufunc dispatch (this runs once per parameter per evaluation)."""
+    u = float(u)
+    if u == 0.0:
+        return math.log(2.0)
+    if u < 0.0:
+        return math.log1p(math.exp(u))
+    if u > 0.0:
+        return u + math.log1p(math.exp(-u))
+    return u  # nan
 
 
 def softplus_inverse(t: float) -> float:
