@@ -542,9 +542,18 @@ void launch_leaf128(const LeafArgs& a, int n_active, hipStream_t s) {
 // v_mfma_f64_16x16x4_f64: lane l holds A[l&15][l>>4], B[l>>4][l&15]; result register r of
 // lane l is C[(l>>4) + 4r][l&15] (verified on gfx950, tools/probe_f64.hip).
 // ======================================================================================
+#ifndef GPX_BK128
+// K-tile depth of the plain-store 128-tile GEMMs (the recursion's TRMM/SYRK products): 8 halves
+// their LDS (36 KiB), so THREE workgroups share a CU instead of two and the third covers the
+// others' barrier/LDS bubbles: factor 101.7 -> 99.6 ms per B=128 evaluation (BK=16: 2 per CU).
+// The contraction instances keep BK=16: their 68 KiB epilogue staging caps them at 2 per CU.
+#define GPX_BK128 8
+#endif
 template <int BM, bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a) {
-  constexpr int BN = BM, BK = 16, S = BM + 16;
+__global__ __launch_bounds__(256, BM == 128 ? (GPX_BK128 == 8 && EPI == EPI_STORE ? 3 : 2) : 1)
+void gemm_kernel(GemmArgs a) {
+  constexpr int BN = BM, BK = (BM == 128 && EPI == EPI_STORE) ? GPX_BK128 : 16, S = BM + 16;
+  constexpr int KC = BK / 2;  // double2 chunks per operand row of a K-tile
   constexpr int WT = BM / 2;
   constexpr int MT = WT / 16;
   constexpr int NLD = BM * BK / 2 / 256;  // double2 chunks per thread per operand
@@ -614,9 +623,9 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
 #pragma unroll
   for (int q = 0; q < NLD; ++q) {
     const int c = tid + 256 * q;
-    if (!TA) offa[q] = (int)(((c >> 3) * lda + (c & 7) * 2) * 8);
+    if (!TA) offa[q] = (int)(((c / KC) * lda + (c % KC) * 2) * 8);
     else offa[q] = (int)(((c / (BM / 2)) * lda + (c % (BM / 2)) * 2) * 8);
-    if (TB) offb[q] = (int)(((c >> 3) * ldb + (c & 7) * 2) * 8);
+    if (TB) offb[q] = (int)(((c / KC) * ldb + (c % KC) * 2) * 8);
     else offb[q] = (int)(((c / (BN / 2)) * ldb + (c % (BN / 2)) * 2) * 8);
   }
   auto gload = [&](int k0) {
@@ -637,7 +646,7 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
     for (int q = 0; q < NLD; ++q) {
       const int c = tid + 256 * q;
       if (!TA) {
-        const int row = c >> 3, kc = (c & 7) * 2;
+        const int row = c / KC, kc = (c % KC) * 2;
         // transposed write: XOR-swizzle the row inside its 16-row group by k (bank spread)
         sA[kc * S + (row ^ (kc & 15))] = ra[q].x;
         sA[(kc + 1) * S + (row ^ ((kc + 1) & 15))] = ra[q].y;
@@ -646,7 +655,7 @@ __global__ __launch_bounds__(256, BM == 128 ? 2 : 1) void gemm_kernel(GemmArgs a
         *reinterpret_cast<d2*>(sA + krow * S + ic) = ra[q];
       }
       if (TB) {
-        const int row = c >> 3, kc = (c & 7) * 2;
+        const int row = c / KC, kc = (c % KC) * 2;
         sB[kc * S + (row ^ (kc & 15))] = rb[q].x;
         sB[(kc + 1) * S + (row ^ ((kc + 1) & 15))] = rb[q].y;
       } else {
