@@ -542,17 +542,21 @@ void launch_leaf128(const LeafArgs& a, int n_active, hipStream_t s) {
 // v_mfma_f64_16x16x4_f64: lane l holds A[l&15][l>>4], B[l>>4][l&15]; result register r of
 // lane l is C[(l>>4) + 4r][l&15] (verified on gfx950, tools/probe_f64.hip).
 // ======================================================================================
+// epilogues light enough for three workgroups per CU (168 VGPRs, no spills): the plain store
+// and predict's column sums of squares. The contraction epilogue spills ~500 VGPRs at that cap
+// (measured), so it keeps BK=16 and two workgroups per CU.
+constexpr bool kLeanEpi(int epi) { return epi == EPI_STORE || epi == EPI_COLSUMSQ; }
 #ifndef GPX_BK128
 // K-tile depth of the plain-store 128-tile GEMMs (the recursion's TRMM/SYRK products): 8 halves
 // their LDS (36 KiB), so THREE workgroups share a CU instead of two and the third covers the
 // others' barrier/LDS bubbles: factor 101.7 -> 99.6 ms per B=128 evaluation (BK=16: 2 per CU).
-// The contraction instances keep BK=16: their 68 KiB epilogue staging caps them at 2 per CU.
+// The contraction instances keep BK=16 (see kLeanEpi).
 #define GPX_BK128 8
 #endif
 template <int BM, bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(256, BM == 128 ? (GPX_BK128 == 8 && EPI == EPI_STORE ? 3 : 2) : 1)
+__global__ __launch_bounds__(256, BM == 128 ? (GPX_BK128 == 8 && kLeanEpi(EPI) ? 3 : 2) : 1)
 void gemm_kernel(GemmArgs a) {
-  constexpr int BN = BM, BK = (BM == 128 && EPI == EPI_STORE) ? GPX_BK128 : 16, S = BM + 16;
+  constexpr int BN = BM, BK = (BM == 128 && kLeanEpi(EPI)) ? GPX_BK128 : 16, S = BM + 16;
   constexpr int KC = BK / 2;  // double2 chunks per operand row of a K-tile
   constexpr int WT = BM / 2;
   constexpr int MT = WT / 16;
