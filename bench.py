@@ -59,28 +59,54 @@ def synthetic_series(n: int, seed: int, lengthscale: float = 64.0, n_features: i
     return x.reshape(-1, 1), y.reshape(-1, 1)
 
 
+def job_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup-v2 CPU quota when
+    one is set (a container's mask can list every CPU of the host while its quota allots a
+    share). Returns (cpus, affinity_count, quota_cpus_or_None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
 def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
     """The oracle (numpy/scipy/OpenBLAS restatement of the GPflow CPU path) timed on this
     host on a bounded sample: `evals` loss+grad evaluations and one predict_f at N, scaled to
-    fits/s with the GPU run's mean nfev per fit."""
+    fits/s with the GPU run's mean nfev per fit. BLAS runs on every CPU available to the job
+    (job_cpus(); `cores`); a second, 1-thread sample (1 evaluation + 1 predict_f) gives the
+    single-core figure SURVEY §8d asks for."""
     from oracle import gp_oracle as O
     import threadpoolctl
 
     x, y = synthetic_series(n, 0)
     m = O.OGPR(x, y, O.OSquaredExponential(), noise_variance=NOISE)
     m.noise.trainable = False
-    info = threadpoolctl.threadpool_info()
-    cores = max([i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"] or [1])
-    m.loss_and_grad_u()  # warm-up (page in, thread pool up)
-    t0 = time.perf_counter()
-    for k in range(evals):
-        m.kernel.lengthscales.value = 1.0 + 4.0 * k
-        m.loss_and_grad_u()
-    t_eval = (time.perf_counter() - t0) / evals
-    t0 = time.perf_counter()
-    m.predict_f(x)
-    t_pred = time.perf_counter() - t0
+    cores, aff, quota = job_cpus()
+
+    def timed(n_evals):
+        m.kernel.lengthscales.value = 1.0
+        m.loss_and_grad_u()  # warm-up (page in, thread pool up)
+        t0 = time.perf_counter()
+        for k in range(n_evals):
+            m.kernel.lengthscales.value = 1.0 + 4.0 * k
+            m.loss_and_grad_u()
+        t_e = (time.perf_counter() - t0) / n_evals
+        t0 = time.perf_counter()
+        m.predict_f(x)
+        return t_e, time.perf_counter() - t0
+
+    with threadpoolctl.threadpool_limits(limits=cores, user_api="blas"):
+        t_eval, t_pred = timed(evals)
+    with threadpoolctl.threadpool_limits(limits=1, user_api="blas"):
+        t_eval1, t_pred1 = timed(1)
     t_fit = nfev_per_fit * t_eval + t_pred
+    t_fit1 = nfev_per_fit * t_eval1 + t_pred1
     cpu_model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -92,13 +118,18 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
         "unit": "fits/s",
         "cores": int(cores),
         "kind": "port",
-        "sample": (f"oracle/gp_oracle.py (numpy {np.__version__} + OpenBLAS, fp64) on this host: "
-                   f"{evals} loss+grad evals ({t_eval:.3f} s each) + 1 predict_f ({t_pred:.3f} s) "
-                   f"at N={n}; fit time = mean GPU nfev/fit ({nfev_per_fit:.1f}) x eval + predict"),
+        "sample": (f"oracle/gp_oracle.py (numpy {np.__version__} + OpenBLAS, fp64) on this host, "
+                   f"BLAS on {cores} threads: {evals} loss+grad evals ({t_eval:.3f} s each) + 1 predict_f "
+                   f"({t_pred:.3f} s) at N={n}; fit time = mean GPU nfev/fit ({nfev_per_fit:.1f}) x eval + "
+                   "predict"),
         "eval_s": t_eval,
         "predict_s": t_pred,
+        "value_1core": 1.0 / t_fit1,
+        "eval_s_1core": t_eval1,
+        "predict_s_1core": t_pred1,
         "cpu_model": cpu_model,
-        "host_cpus_visible": len(os.sched_getaffinity(0)),
+        "host_cpus_visible": aff,
+        "cgroup_cpu_quota": quota,
     }
 
 

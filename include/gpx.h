@@ -32,7 +32,12 @@
  *  - Return codes: GPX_OK, GPX_NOT_PD (some problem's K+σn²I is not positive definite; its
  *    info[b] holds the 1-based index of the first failing pivot, like LAPACK potrf),
  *    GPX_BAD_ARG, GPX_HIP_ERROR. No C++ exception crosses this boundary.
- *  - A context is bound to one device and is NOT thread-safe.
+ *  - A context is bound to one device. Several threads may use one context at the same time
+ *    as long as each thread works on its own batch / svgp object (all per-evaluation streams,
+ *    events and workspace belong to the batch); a single batch is NOT thread-safe.
+ *    gpx_last_error returns the calling thread's most recent failure message (errno-like).
+ *    A NULL stream means the context's own stream, which concurrent threads then share
+ *    (correct, but their evaluations serialise): pass one stream per thread instead.
  */
 #ifndef GPX_H_
 #define GPX_H_

@@ -26,6 +26,11 @@ namespace gpx {
 
 const char* kVersion = "gpx 0.1.0 (gfx950, fp64 MFMA)";
 
+std::string& last_error_slot() {
+  static thread_local std::string msg;
+  return msg;
+}
+
 
 // MFMA flops the GEMM launcher will issue for these args (bench / roofline bookkeeping)
 double gemm_issued_flops(const GemmArgs& a, int na) {
@@ -236,15 +241,7 @@ int gpx_create(int device, gpx_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return GPX_HIP_ERROR;
   gpx_ctx* c = new gpx_ctx();
   c->device = device;
-  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
-  for (int g = 0; g < kGroups && ok; ++g)
-    ok = hipStreamCreateWithFlags(&c->workers[g], hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&c->join[g], hipEventDisableTiming) == hipSuccess;
-  for (int g = 0; g < kAux && ok; ++g)
-    ok = hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking) == hipSuccess;
-  for (int e = 0; e < kEvents && ok; ++e)
-    ok = hipEventCreateWithFlags(&c->ev[e], hipEventDisableTiming) == hipSuccess;
+  const bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
   if (!ok) {
     delete c;
     return GPX_HIP_ERROR;
@@ -256,21 +253,15 @@ int gpx_create(int device, gpx_ctx** out) {
 int gpx_destroy(gpx_ctx* ctx) {
   if (!ctx) return GPX_BAD_ARG;
   (void)hipSetDevice(ctx->device);
-  for (int g = 0; g < kGroups; ++g) {
-    if (ctx->workers[g]) (void)hipStreamDestroy(ctx->workers[g]);
-    if (ctx->join[g]) (void)hipEventDestroy(ctx->join[g]);
-  }
-  for (int g = 0; g < kAux; ++g)
-    if (ctx->aux[g]) (void)hipStreamDestroy(ctx->aux[g]);
-  for (int e = 0; e < kEvents; ++e)
-    if (ctx->ev[e]) (void)hipEventDestroy(ctx->ev[e]);
-  if (ctx->fork) (void)hipEventDestroy(ctx->fork);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return GPX_OK;
 }
 
-const char* gpx_last_error(const gpx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* gpx_last_error(const gpx_ctx* ctx) {
+  (void)ctx;
+  return last_error_slot().c_str();
+}
 
 int gpx_set_profiling(gpx_ctx* ctx, int enabled) {
   if (!ctx) return GPX_BAD_ARG;
@@ -298,6 +289,8 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
         return fail(ctx, GPX_BAD_ARG, "bad kernel term");
     }
   }
+  if (((long long)N_max + kLeaf - 1) / kLeaf * kLeaf > kGemmMaxLd)
+    return fail(ctx, GPX_BAD_ARG, "N_max exceeds the GEMM buffer-load window (kGemmMaxLd)");
   HIPX(ctx, hipSetDevice(ctx->device));
   gpx_batch* bt = new gpx_batch();
   bt->ctx = ctx; bt->B = B; bt->Nmax = N_max; bt->D = D;
@@ -372,6 +365,11 @@ int gpx_batch_destroy(gpx_batch* bt) {
   for (int g = 0; g < kAux; ++g)
     if (bt->aux[g]) (void)hipStreamDestroy(bt->aux[g]);
   if (bt->hp) (void)hipStreamDestroy(bt->hp);
+  for (int g = 0; g < kGroups; ++g) {
+    if (bt->workers[g]) (void)hipStreamDestroy(bt->workers[g]);
+    if (bt->join[g]) (void)hipEventDestroy(bt->join[g]);
+  }
+  if (bt->fork) (void)hipEventDestroy(bt->fork);
   for (int e = 0; e < kEvents; ++e)
     if (bt->ev[e]) (void)hipEventDestroy(bt->ev[e]);
   delete bt;
@@ -422,17 +420,24 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   int ng = 1;
   if (const char* e = getenv("GPX_GROUPS")) ng = atoi(e);
   ng = std::max(1, std::min(std::min(ng, kGroups), n_active));
+  if (ng > 1 && !bt->fork) {
+    HIPX(ctx, hipEventCreateWithFlags(&bt->fork, hipEventDisableTiming));
+    for (int g = 0; g < kGroups; ++g) {
+      HIPX(ctx, hipStreamCreateWithFlags(&bt->workers[g], hipStreamNonBlocking));
+      HIPX(ctx, hipEventCreateWithFlags(&bt->join[g], hipEventDisableTiming));
+    }
+  }
   int next_event = 0;
   Run runs[kGroups];
   int start = 0;
   for (int g = 0; g < ng; ++g) {
     const int cnt = n_active / ng + (g < n_active % ng ? 1 : 0);
-    runs[g] = Run{bt, bt->d_active + start, cnt, ng == 1 ? s : ctx->workers[g], ng == 1, &next_event};
+    runs[g] = Run{bt, bt->d_active + start, cnt, ng == 1 ? s : bt->workers[g], ng == 1, &next_event};
     start += cnt;
   }
   if (ng > 1) {
-    HIPX(ctx, hipEventRecord(ctx->fork, s));
-    for (int g = 0; g < ng; ++g) HIPX(ctx, hipStreamWaitEvent(runs[g].s, ctx->fork, 0));
+    HIPX(ctx, hipEventRecord(bt->fork, s));
+    for (int g = 0; g < ng; ++g) HIPX(ctx, hipStreamWaitEvent(runs[g].s, bt->fork, 0));
   }
   PhaseTimer total(ctx->profiling != 0, s);
   total.mark();
@@ -449,8 +454,8 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   }
   if (ng > 1) {
     for (int g = 0; g < ng; ++g) {
-      HIPX(ctx, hipEventRecord(ctx->join[g], runs[g].s));
-      HIPX(ctx, hipStreamWaitEvent(s, ctx->join[g], 0));
+      HIPX(ctx, hipEventRecord(bt->join[g], runs[g].s));
+      HIPX(ctx, hipStreamWaitEvent(s, bt->join[g], 0));
     }
   }
   // The contraction fills the chip by itself (Np²/2/128² tiles per problem): one launch over
@@ -544,7 +549,7 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
                 sizeof(double) * GPX_THETA_STRIDE);
     bt->fac_valid[b] = 1;
   }
-  if (status == GPX_NOT_PD) ctx->err = "K + noise*I is not positive definite for some problem";
+  if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
   return status;
 }
 
@@ -558,6 +563,8 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   gpx_ctx* ctx = bt->ctx;
   if ((!train && (!Xnew || M <= 0)) || !mean || !(var || cov) || !info)
     return fail(ctx, GPX_BAD_ARG, "bad predict args");
+  if (!train && ((long long)M + 63) / 64 * 64 > kGemmMaxLd)
+    return fail(ctx, GPX_BAD_ARG, "too many prediction points for one call (kGemmMaxLd): split Xnew");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   int rc = upload_common(bt, n_active, active, theta, s);
@@ -697,7 +704,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
       bt->fac_valid[b] = 1;
     }
   }
-  if (status == GPX_NOT_PD) ctx->err = "K + noise*I is not positive definite for some problem";
+  if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
   return status;
 }
 

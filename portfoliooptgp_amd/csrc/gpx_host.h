@@ -11,14 +11,13 @@ constexpr int kGroups = 4;  // max concurrent pipelines per evaluation (HIP stre
 constexpr int kAux = 3;     // auxiliary streams for the T = L21·W11 products of depths 0..2
 constexpr int kEvents = 64;
 
+// A context only names the device and holds its default stream (used when a call passes a
+// NULL stream). Every piece of per-evaluation state (worker / aux streams, fork and join
+// events, workspace) lives in the batch, so threads that evaluate different batches of one
+// context never share mutable state; error messages are per calling thread (gpx::fail).
 struct gpx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t workers[kGroups] = {};
-  hipStream_t aux[kAux] = {};
-  hipEvent_t fork = nullptr, join[kGroups] = {};
-  hipEvent_t ev[kEvents] = {};
-  std::string err;
   int profiling = 0;
 };
 
@@ -65,12 +64,20 @@ struct gpx_batch {
   hipStream_t aux[kAux] = {};
   hipEvent_t ev[kEvents] = {};
   hipStream_t hp = nullptr;   // highest-priority stream for the contraction (GPX_CONTRACT_PRIORITY)
+  // GPX_GROUPS > 1: per-batch pipelines (created on first use)
+  hipStream_t workers[kGroups] = {};
+  hipEvent_t fork = nullptr, join[kGroups] = {};
 };
 
 namespace gpx {
 
+// The last error message of the calling thread (errno-like): a context may be used by
+// several threads at once (one batch each), so the message cannot live in the context.
+std::string& last_error_slot();
+
 inline int fail(gpx_ctx* ctx, int code, const std::string& msg) {
-  if (ctx) ctx->err = msg;
+  (void)ctx;
+  last_error_slot() = msg;
   return code;
 }
 

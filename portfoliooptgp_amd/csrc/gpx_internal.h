@@ -122,6 +122,12 @@ void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s);
 void launch_train_pred(const TrainPredArgs& a, int n_active, int Np, hipStream_t s);
 void launch_predvar(const PredVarArgs& a, int n_active, hipStream_t s);
 int gemm_tile(const GemmArgs& a, int n_active);  // tile edge the launcher will use (64 or 128)
+// The GEMM stages operands with buffer loads: a per-K-tile base plus a 32-bit per-lane byte
+// offset, inside a 0x7fffffff-byte buffer window. The farthest element a tile reads is
+// (128 - 1) rows * ld * 8 B + one 128-wide row, so every leading dimension must satisfy
+// 127 * ld * 8 + 1024 < 2^31 (ld <= 2,113,662 doubles). Out-of-window buffer loads return 0
+// without faulting, so the API rejects larger shapes (GPX_BAD_ARG) and the launcher asserts.
+constexpr long long kGemmMaxLd = (0x7fffffffLL - 1024) / (127LL * 8);
 
 // ---- SVGP (gpx_svgp_kernels.hip) -----------------------------------------------------
 // Row-organised derivative contraction over an M×N (or M×M) index set:

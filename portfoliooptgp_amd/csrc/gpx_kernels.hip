@@ -12,6 +12,8 @@
 // and for predict_f: the cross-covariance build, mean = Kxsᵀα, and W·Kxs with a fused
 // column-sum-of-squares epilogue (EPI_COLSUMSQ) for the variance.
 #include <hip/hip_ext.h>
+#include <cstdio>
+#include <cstdlib>
 #include "gpx_internal.h"
 
 namespace gpx {
@@ -915,6 +917,13 @@ static void launch_gemm_t(const GemmArgs& a0, bool ta, bool tb, int n_active, hi
 }
 
 void launch_gemm(const GemmArgs& a, int epi, bool ta, bool tb, int n_active, hipStream_t s) {
+  // unreachable through the C ABI (shapes are checked against kGemmMaxLd at create/predict);
+  // a silent zero-filled operand would be far worse than stopping here
+  if (a.lda > kGemmMaxLd || a.ldb > kGemmMaxLd) {
+    fprintf(stderr, "gpx: GEMM leading dimension %d/%d exceeds the buffer-load window (%lld)\n",
+            a.lda, a.ldb, kGemmMaxLd);
+    abort();
+  }
   const int bm = gemm_tile(a, n_active);
   if (bm == 128) {
     if (epi == EPI_STORE) launch_gemm_t<128, EPI_STORE>(a, ta, tb, n_active, s);

@@ -151,6 +151,11 @@ int gpx_svgp_create(gpx_ctx* ctx, int N, int M, int D, const double* X, const do
   sv->chunkK = ((n64 + sv->nc - 1) / sv->nc + 63) / 64 * 64;
   sv->Ncols = sv->nc * sv->chunkK;
   sv->rows_chunk = rows_chunk_for(D);
+  if (sv->Ncols > kGemmMaxLd || Mp > kGemmMaxLd) {
+    delete sv;
+    return fail(ctx, GPX_BAD_ARG, "svgp shard too large for the GEMM buffer-load window "
+                                  "(N <= ~2.1M rows per gpx_svgp): shard the data over more objects");
+  }
   auto bail = [&](const std::string& m) {
     gpx_svgp_destroy(sv);
     return fail(ctx, GPX_HIP_ERROR, m);
@@ -448,6 +453,8 @@ int gpx_svgp_predict(gpx_svgp* sv, const double* theta, const double* Z, const d
   if (!sv) return GPX_BAD_ARG;
   gpx_ctx* ctx = sv->ctx;
   if (!Xnew || Mn < 1 || !mean || !var) return fail(ctx, GPX_BAD_ARG, "bad predict args");
+  if (((long long)Mn + 63) / 64 * 64 > kGemmMaxLd)
+    return fail(ctx, GPX_BAD_ARG, "too many prediction points for one call (kGemmMaxLd): split Xnew");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   sv->local_done = false;

@@ -107,13 +107,32 @@ def asset_fingerprint(x, y, horizon) -> str:
     return h.hexdigest()
 
 
-def _load_checkpoint(path: str, H: int, n_theta: int) -> Dict[str, dict]:
-    """{fingerprint: result} of a previous run's rank file (absent or unreadable: empty)."""
+def config_fingerprint(fit_fn: Callable, fit_config=None) -> str:
+    """Hash of what produced a checkpoint's results: the fit function's qualified name (with a
+    functools.partial's bound arguments) and the caller's ``fit_config`` (kernel spec, maxiter,
+    noise, ... — anything whose repr changes when the fit would). A rerun whose configuration
+    differs refits everything instead of reusing results of another fit protocol."""
+    import functools
+    parts = []
+    f = fit_fn
+    while isinstance(f, functools.partial):
+        parts.append(repr((f.args, sorted(f.keywords.items()))))
+        f = f.func
+    parts.append(f"{getattr(f, '__module__', '?')}.{getattr(f, '__qualname__', repr(f))}")
+    parts.append(repr(fit_config))
+    return hashlib.sha1("\x1f".join(parts).encode()).hexdigest()
+
+
+def _load_checkpoint(path: str, H: int, n_theta: int, config: str = "") -> Dict[str, dict]:
+    """{fingerprint: result} of a previous run's rank file (absent, unreadable or written
+    under another fit configuration: empty)."""
     if not os.path.exists(path):
         return {}
     try:
         with np.load(path, allow_pickle=False) as z:
             if int(z["H"]) != H or int(z["n_theta"]) != n_theta:
+                return {}
+            if "config" not in z.files or str(z["config"]) != config:
                 return {}
             rows = unpack_results(torch.as_tensor(z["table"]), H, n_theta)
             fps = [str(f) for f in z["fingerprints"]]
@@ -123,16 +142,17 @@ def _load_checkpoint(path: str, H: int, n_theta: int) -> Dict[str, dict]:
     return {fp: rows[i] for fp, i in zip(fps, index) if i in rows}
 
 
-def _save_checkpoint(path: str, table: torch.Tensor, fingerprints: Sequence[str], H: int, n_theta: int):
+def _save_checkpoint(path: str, table: torch.Tensor, fingerprints: Sequence[str], H: int, n_theta: int,
+                     config: str = ""):
     tmp = path + ".tmp.npz"
     np.savez(tmp, table=table.numpy(), fingerprints=np.asarray(list(fingerprints), dtype="U40"),
-             H=np.int64(H), n_theta=np.int64(n_theta))
+             H=np.int64(H), n_theta=np.int64(n_theta), config=np.asarray(config, dtype="U40"))
     os.replace(tmp, path)
 
 
 def fit_assets(series: Sequence[Tuple[np.ndarray, np.ndarray]], horizons: Sequence[np.ndarray],
                fit_fn: Optional[Callable] = None, n_theta: int = 2, group=None,
-               checkpoint: Optional[str] = None) -> Dict[int, dict]:
+               checkpoint: Optional[str] = None, fit_config=None) -> Dict[int, dict]:
     """Shard the assets over the ranks of `group`, fit the local shard with `fit_fn`
     (default: GPU exact GPR with a SquaredExponential kernel and σn² = 1e-5 fixed, the
     GPR/model_trainer.py:15-19 protocol, continuous-batched), predict each asset at its
@@ -142,7 +162,10 @@ def fit_assets(series: Sequence[Tuple[np.ndarray, np.ndarray]], horizons: Sequen
     nfev and the horizon predictions of each fitted asset, keyed by a content hash of its
     inputs). A rerun with the same prefix (say after a crash of another rank) fits only the
     assets whose results are missing, so a long multi-asset sweep resumes at asset
-    granularity; changed inputs are refitted. The reference has no checkpointing."""
+    granularity; changed inputs are refitted. The file also records a fingerprint of the fit
+    configuration (``fit_fn``'s qualified name and bound arguments plus ``fit_config``, e.g. the
+    kernel spec / maxiter / noise of a custom fitter); a file written under another
+    configuration is discarded. The reference has no checkpointing."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     shards = shard_lpt([fit_cost(len(x)) for x, _ in series], world)
@@ -151,14 +174,15 @@ def fit_assets(series: Sequence[Tuple[np.ndarray, np.ndarray]], horizons: Sequen
     H = max(len(h) for h in horizons)
     fps = {i: asset_fingerprint(series[i][0], series[i][1], horizons[i]) for i in mine} if checkpoint else {}
     path = f"{checkpoint}.rank{rank}.npz" if checkpoint else None
-    done = _load_checkpoint(path, H, n_theta) if checkpoint else {}
+    cfg = config_fingerprint(fit_fn, fit_config) if checkpoint else ""
+    done = _load_checkpoint(path, H, n_theta, cfg) if checkpoint else {}
     todo = [i for i in mine if fps.get(i) not in done]
     fitted = fit_fn([series[i] for i in todo], [horizons[i] for i in todo]) if todo else []
     by_index = dict(zip(todo, fitted))
     local = [by_index[i] if i in by_index else done[fps[i]] for i in mine]
     table = pack_results(mine, local, H, n_theta)
     if checkpoint:
-        _save_checkpoint(path, table, [fps[i] for i in mine], H, n_theta)
+        _save_checkpoint(path, table, [fps[i] for i in mine], H, n_theta, cfg)
     if world > 1:
         table = all_gather_results(table, len(series), group)
     return unpack_results(table, H, n_theta)

@@ -571,9 +571,10 @@ class _SteppedDriver:
         # group g: rows of its engine (one engine per group, or one engine split row-wise)
         if len(engines) > 1:
             G = len(engines)
-            per = min(e.B for e in engines)
-            self.groups = [(engines[g], list(range(per)), threading.Lock(), _new_stream(engines[g].device))
-                           for g in range(G)]
+            # every row of every engine is a slot (the last engine of a ceil split may be
+            # smaller); the width cap below trims the total
+            self.groups = [(engines[g], list(range(engines[g].B)), threading.Lock(),
+                            _new_stream(engines[g].device)) for g in range(G)]
         else:
             e = engines[0]
             lock = threading.Lock()

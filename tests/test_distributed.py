@@ -188,3 +188,33 @@ def test_fit_assets_checkpoint_resumes_at_asset_granularity(tmp_path):
             np.testing.assert_array_equal(res[i]["mean"], fresh[i]["mean"])
     assert changed[2]["loss"] == pytest.approx(float(np.sum((y2 + 1.0) ** 2)))
     assert changed[0]["loss"] == fresh[0]["loss"]
+
+
+def test_fit_assets_checkpoint_discarded_under_another_fit_configuration(tmp_path):
+    """A checkpoint written by one fit protocol is not reused by another (different fit_fn,
+    different bound arguments, or a different fit_config): everything is refitted."""
+    import functools
+    series = [_series(k) for k in range(3)]
+    horizons = [np.arange(len(s[0]), len(s[0]) + 2, dtype=np.float64)[:, None] for s in series]
+    calls = []
+
+    def fit_a(ss, hs, scale=1.0):
+        calls.append(("a", len(ss), scale))
+        return _stand_in_fit(ss, hs)
+
+    def fit_b(ss, hs):
+        calls.append(("b", len(ss)))
+        return _stand_in_fit(ss, hs)
+
+    prefix = str(tmp_path / "cfg")
+    D.fit_assets(series, horizons, fit_fn=fit_a, checkpoint=prefix, fit_config={"maxiter": 100})
+    D.fit_assets(series, horizons, fit_fn=fit_a, checkpoint=prefix, fit_config={"maxiter": 100})
+    assert calls == [("a", 3, 1.0)]          # same configuration: resumed, nothing refitted
+    D.fit_assets(series, horizons, fit_fn=fit_a, checkpoint=prefix, fit_config={"maxiter": 50})
+    assert calls[-1] == ("a", 3, 1.0) and len(calls) == 2   # other fit_config: refitted
+    D.fit_assets(series, horizons, fit_fn=fit_b, checkpoint=prefix, fit_config={"maxiter": 50})
+    assert calls[-1] == ("b", 3) and len(calls) == 3         # other fit function: refitted
+    D.fit_assets(series, horizons, fit_fn=functools.partial(fit_a, scale=2.0), checkpoint=prefix,
+                 fit_config={"maxiter": 50})
+    assert calls[-1] == ("a", 3, 2.0) and len(calls) == 4    # other bound arguments: refitted
+    assert D.config_fingerprint(fit_a, 1) != D.config_fingerprint(fit_b, 1)

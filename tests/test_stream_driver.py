@@ -206,3 +206,21 @@ def test_model_without_trainable_variables_fails_alone():
             else:
                 gpx.optimizers.Scipy().minimize_batch(ms, engine=eng)
         assert ms[0].kernel.lengthscales.value != 1.0 and ms[2].kernel.lengthscales.value != 1.0
+
+
+@pytest.mark.parametrize("width,engines_b,expect", [(5, (3, 2), [3, 2]), (3, (2, 1), [2, 1]),
+                                                    (4, (3, 2), [2, 2]), (2, (3, 2), [1, 1])])
+def test_stream_uses_every_engine_row(width, engines_b, expect):
+    """Unequal engines (the last of a ceil split is smaller) contribute all their rows, and the
+    width cap deals the slots round-robin over the groups: `width` slots in total, not
+    groups x the smallest engine."""
+    from portfoliooptgp_amd.optimizers import _SteppedDriver
+    ms = _models(9)
+    eng = [FakeEngine(b) for b in engines_b]
+    drv = _SteppedDriver(ms, eng, len(eng), {}, False, 1, width=width)
+    assert [len(rows) for _, rows, _, _ in drv.groups] == expect
+    ref = [_solo(m) for m in _models(9)]
+    res, _ = gpx.optimizers.Scipy().minimize_stream(ms, width=width, engine=eng, groups=len(eng))
+    for r, r0 in zip(res, ref):
+        assert r.nfev == r0.nfev
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
