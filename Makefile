@@ -12,7 +12,11 @@ all: $(LIB) $(CSMOKE)
 $(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h include/gpx.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o
+# host helpers of the L-BFGS-B driver: plain gcc, libm calls as Python's math module makes them
+$(CSRC)/gpx_host_math.o: $(CSRC)/gpx_host_math.c include/gpx.h
+	gcc -O2 -fno-builtin -fno-fast-math -fPIC -std=c11 -Wall -c $< -o $@
+
+$(LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-soname,libgpx.so $^ -o $@
 
 # plain-C consumer of the C ABI (gcc, HIP runtime API only), run by tests/test_c_abi_gpu.py

@@ -266,7 +266,8 @@ def main():
     class _Tm:  # timing summed over the device batches
         pass
     tm = _Tm()
-    for f in ("contract_ms_total", "contract_launches", "contract_alg_flops", "eval_ms_total", "evals"):
+    for f in ("contract_ms_total", "contract_launches", "contract_alg_flops", "eval_ms_total", "evals",
+              "band_ms_total", "band_calls", "band_evals", "band_p_sum"):
         setattr(tm, f, sum(getattr(t, f) for t in tms))
     if world > 1:
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
@@ -298,7 +299,7 @@ def main():
         iso = ti.contract_alg_flops / (ti.contract_ms_total * 1e-3) / 1e12 if ti.contract_ms_total else None
     contract_ms = tm.contract_ms_total / max(tm.contract_launches, 1.0)
     contract_flops = tm.contract_alg_flops / max(tm.contract_launches, 1.0)
-    achieved = contract_flops / (contract_ms * 1e-3) / 1e12
+    achieved = contract_flops / (contract_ms * 1e-3) / 1e12 if contract_ms > 0 else 0.0
     traffic, traffic_src = contract_traffic(n, contract_flops)
     eval_alg = (n ** 3 + 2 * 3 * n ** 2) * evals_all  # SURVEY §8d F_eval(N), P=2, all ranks
     out = {
@@ -320,6 +321,10 @@ def main():
                    "kernel": "SquaredExponential",
                    "parallelism": f"independent fits, {world} process(es) x 1 GPU, RCCL all_gather of results"},
         "nfev_mean": nfev_mean,
+        "band_path": {"evals": tm.band_evals, "dense_evals": tm.evals - tm.band_evals,
+                      "mean_p_blocks": tm.band_p_sum / max(tm.band_evals, 1.0),
+                      "ms_per_call": tm.band_ms_total / max(tm.band_calls, 1.0),
+                      "problems_per_call": tm.band_evals / max(tm.band_calls, 1.0)},
         "evals_per_s": evals_all / elapsed,
         # whole-job algorithmic rate: F_eval(N) x evaluations / wall time of the timed steps
         "eval_alg_tflops": eval_alg / elapsed / 1e12,

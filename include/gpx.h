@@ -15,6 +15,13 @@
  *   gpx_kernel_spec     <- the kernel objects of GPR/main.py:105-114 and the composite
  *                          Exponential*Exponential of Multi-Input_GPR/main.py:118-135
  *
+ * Evaluation paths (chosen per problem and per call, results agree to rounding): the dense
+ * recursive Cholesky-and-inverse, or — when K and every ∂K/∂θ are exactly zero in fp64 beyond a
+ * band of 64-blocks (SE / Matern / Exponential with a lengthscale small against the spacing of
+ * sorted inputs, e.g. GPflow's default ℓ = 1 on the reference's integer day offsets) — a
+ * block-banded Cholesky, banded solves and selected inversion of K⁻¹ on the band, O(N·bw²).
+ * GPX_BAND=0 in the environment forces the dense path.
+ *
  * Conventions
  *  - All arithmetic is fp64. X, Y, Xnew and the predict outputs are caller-owned DEVICE
  *    pointers (e.g. torch tensors' data_ptr()); the library never frees them.
@@ -170,6 +177,13 @@ typedef struct {
   double contract_alg_flops;  /* algorithmic flops of those launches: n_active * sum_i 2(i+1)(Np-i) */
   double eval_ms_total;       /* whole gpx_batch_lml_grad device time */
   double evals;               /* problem-evaluations (sum of n_active) */
+  /* block-banded path (cumulative, profiling enabled only): device time of its part of the
+   * calls, calls that had banded problems, banded problem-evaluations, Σ band width p (64-blocks)
+   * over those evaluations */
+  double band_ms_total;
+  double band_calls;
+  double band_evals;
+  double band_p_sum;
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);
@@ -215,6 +229,22 @@ int gpx_svgp_elbo_grad(gpx_svgp* svgp, const double* theta, const double* Z, con
 int gpx_svgp_predict(gpx_svgp* svgp, const double* theta, const double* Z, const double* q_mu,
                      const double* q_sqrt, const double* Xnew, int Mn, int add_noise, double* mean,
                      double* var, int32_t* info, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Host helpers of the batched L-BFGS-B driver (no device work): for the n_fits fits of one
+ * round, u [n_fits, n_vars] are the unconstrained variables (gpflow.optimizers.Scipy's x,
+ * GPR/model_trainer.py:18-19), rows [n_fits] their batch slots, cols [n_vars] the θ index of each
+ * variable, lower [n_vars] its Shift (1e-6 for the Gaussian likelihood variance, else 0).
+ *   gpx_host_theta_rows   theta[rows[k]][cols[v]] = lower[v] + softplus(u[k][v])
+ *   gpx_host_loss_grad_u  loss[k] = −lml[rows[k]];
+ *                         grad_u[k][v] = −grad[rows[k]][cols[v]] · sigmoid(u[k][v])
+ * theta / grad rows have GPX_THETA_STRIDE entries (gpx_batch_lml_grad's layout).
+ */
+int gpx_host_theta_rows(int n_fits, int n_vars, const double* u, const int32_t* rows,
+                        const int32_t* cols, const double* lower, double* theta);
+int gpx_host_loss_grad_u(int n_fits, int n_vars, const double* u, const int32_t* rows,
+                         const int32_t* cols, const double* lml, const double* grad, double* loss,
+                         double* grad_u);
 
 #ifdef __cplusplus
 }

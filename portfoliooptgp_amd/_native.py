@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "gpx_set_profiling", "gpx_batch_reset_timing", "gpx_batch_rebind",
     "gpx_svgp_create", "gpx_svgp_destroy", "gpx_svgp_partials", "gpx_svgp_bind_partials",
     "gpx_svgp_eval_local", "gpx_svgp_eval_finish", "gpx_svgp_elbo_grad", "gpx_svgp_predict",
+    "gpx_host_theta_rows", "gpx_host_loss_grad_u",
 )
 
 
@@ -51,7 +52,9 @@ class GpxTiming(ctypes.Structure):
                 ("total_ms", ctypes.c_double), ("gemm_flops", ctypes.c_double),
                 ("contract_ms_total", ctypes.c_double), ("contract_launches", ctypes.c_double),
                 ("contract_alg_flops", ctypes.c_double), ("eval_ms_total", ctypes.c_double),
-                ("evals", ctypes.c_double)]
+                ("evals", ctypes.c_double), ("band_ms_total", ctypes.c_double),
+                ("band_calls", ctypes.c_double), ("band_evals", ctypes.c_double),
+                ("band_p_sum", ctypes.c_double)]
 
 
 class GPXError(RuntimeError):
@@ -150,6 +153,11 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_svgp_predict.restype = c_int
         lib.gpx_svgp_predict.argtypes = [c_void_p, c_double_p, c_double_p, c_double_p, c_double_p,
                                          c_void_p, c_int, c_int, c_void_p, c_void_p, c_int_p, c_void_p]
+        lib.gpx_host_theta_rows.restype = c_int
+        lib.gpx_host_theta_rows.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.gpx_host_loss_grad_u.restype = c_int
+        lib.gpx_host_loss_grad_u.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_void_p]
         if path is None:
             _lib = lib
         return lib

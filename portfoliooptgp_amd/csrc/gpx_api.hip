@@ -184,6 +184,196 @@ void reduce(const Run& r) {
 }
 
 
+// ---------------------------------------------------------------------------------------
+// Block-banded path (kernels in gpx_band.hip)
+// ---------------------------------------------------------------------------------------
+// Exactness: for the monotone stationary kernels (SE, Matern12/32/52, Exponential) every value
+// and θ-derivative carries the factor exp(−a(s)), s = r/ℓ, with a(s) = s²/2, s, s/2, √3 s or
+// √5 s. When a(s) ≥ 746 that factor is exactly 0 in fp64 (exp underflows below 2^-1075 at
+// 745.13) and so is the whole entry (0 times a finite polynomial). band_rmin bounds r from
+// below for every pair of points in blocks (k, k − d) (bounding boxes of the blocks' valid
+// rows, per term's active dims); the margin 746 − 745.13 covers the rounding of r²/ℓ² on the
+// device many times over. A sum vanishes when all its terms do, a product when any does.
+namespace {
+bool band_kind(int kind) { return kind >= GPX_SE && kind <= GPX_EXPONENTIAL; }
+
+double band_arg(int kind, double s) {
+  switch (kind) {
+    case GPX_SE: return 0.5 * s * s;
+    case GPX_MATERN12: return s;
+    case GPX_EXPONENTIAL: return 0.5 * s;
+    case GPX_MATERN32: return 1.7320508075688772 * s;
+    default: return 2.23606797749979 * s;  // GPX_MATERN52
+  }
+}
+}  // namespace
+
+void band_tables(gpx_batch* bt, int b, const double* hostX) {
+  const int nb = bt->Np / kLeaf, D = bt->D, n = bt->n[b];
+  double* out = bt->band_rmin.data() + (size_t)b * GPX_MAX_TERMS * nb;
+  std::fill(out, out + (size_t)GPX_MAX_TERMS * nb, INFINITY);
+  const gpx_kernel_spec& sp = bt->specs[b];
+  const int nvb = (n + kLeaf - 1) / kLeaf;  // blocks holding valid rows
+  std::vector<double> lo((size_t)nvb * D), hi((size_t)nvb * D);
+  for (int k = 0; k < nvb; ++k)
+    for (int d = 0; d < D; ++d) {
+      double a = INFINITY, z = -INFINITY;
+      for (int r = k * kLeaf; r < std::min(n, (k + 1) * kLeaf); ++r) {
+        a = std::min(a, hostX[(size_t)r * D + d]);
+        z = std::max(z, hostX[(size_t)r * D + d]);
+      }
+      lo[(size_t)k * D + d] = a;
+      hi[(size_t)k * D + d] = z;
+    }
+  for (int t = 0; t < sp.n_terms; ++t) {
+    const int d0 = sp.terms[t].dim_start, dn = sp.terms[t].dim_count;
+    double* rt = out + (size_t)t * nb;
+    for (int dd = 1; dd < nvb; ++dd) {
+      double m = INFINITY;
+      for (int k = dd; k < nvb; ++k) {
+        double g2 = 0.0;
+        for (int d = d0; d < d0 + dn; ++d) {
+          const double g = std::max(0.0, std::max(lo[(size_t)k * D + d] - hi[(size_t)(k - dd) * D + d],
+                                                  lo[(size_t)(k - dd) * D + d] - hi[(size_t)k * D + d]));
+          g2 += g * g;
+        }
+        m = std::min(m, g2);
+      }
+      // the box gap is exact in real arithmetic; shave a relative 1e-12 off for the rounding
+      // of the sums above
+      rt[dd] = std::sqrt(m) * (1.0 - 1e-12);
+    }
+  }
+}
+
+int band_width(const gpx_batch* bt, int b, const double* th) {
+  const gpx_kernel_spec& sp = bt->specs[b];
+  for (int t = 0; t < sp.n_terms; ++t)
+    if (!band_kind(sp.terms[t].kind)) return -1;
+  const int nb = bt->Np / kLeaf;
+  const double* tab = bt->band_rmin.data() + (size_t)b * GPX_MAX_TERMS * nb;
+  const bool prod = sp.n_terms > 1 && sp.combine == GPX_PRODUCT;
+  for (int d = nb - 1; d >= 1; --d) {
+    bool nz = prod;
+    for (int t = 0; t < sp.n_terms; ++t) {
+      const double ell = th[sp.terms[t].param_offset];
+      const double r = tab[(size_t)t * nb + d];
+      const bool term_nz = !(r == INFINITY || band_arg(sp.terms[t].kind, r / ell) >= 746.0);
+      nz = prod ? (nz && term_nz) : (nz || term_nz);
+    }
+    if (nz) return d;
+  }
+  return 0;
+}
+
+// shapes the banded path handles: ≥ 8 blocks (smaller problems are a few leaves densely) and
+// z in LDS for the solve. Band tables are kept for every such batch, whatever GPX_BAND says.
+bool band_shape(const gpx_batch* bt) { return bt->Np / kLeaf >= 8 && bt->Np <= 8192; }
+
+int band_limit(const gpx_batch* bt) {
+  // read per call (cheap), so a process can compare the paths on the same problems
+  const char* em = getenv("GPX_BAND");
+  const char* ep = getenv("GPX_BAND_PMAX");
+  const int mode = em ? atoi(em) : 1;
+  const int pmax_env = ep ? atoi(ep) : -1;
+  if (mode == 0 || !band_shape(bt)) return -1;
+  return pmax_env >= 0 ? pmax_env : bt->Np / kLeaf / 4;
+}
+
+void band_eval(const Run& r, int p, int max_terms) {
+  gpx_batch* bt = r.bt;
+  const int Np = bt->Np, nb = Np / kLeaf;
+  const long long st = mat_stride(bt);
+  const long long rowb = (long long)kLeaf * Np;  // one block row
+  BuildArgs ba{};
+  ba.active = r.d_act; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
+  ba.X = bt->X; ba.sX = (long long)bt->Nmax * bt->D; ba.X2 = bt->X; ba.sX2 = ba.sX; ba.D = bt->D;
+  ba.m2 = 0; ba.out = bt->K; ba.sOut = st; ba.ldo = Np; ba.rows = ba.cols = Np;
+  ba.symmetric = 1; ba.band1 = p + 1;
+  launch_build(ba, r.na, r.s);
+  // forward: right-looking block Cholesky over the band; W_kk = L_kk⁻¹ from the leaf
+  LeafArgs la{};
+  la.active = r.d_act; la.K = bt->K; la.W = bt->W; la.sMat = st; la.ld = Np;
+  la.ldiag = bt->ldiag; la.sVec = Np; la.info = bt->d_info;
+  for (int k = 0; k < nb; ++k) {
+    la.off = k * kLeaf;
+    launch_leaf(la, r.na, r.s);
+    const int q = std::min(p, nb - 1 - k);
+    if (q == 0) continue;
+    const long long okk = k * rowb + k * kLeaf, opan = (k + 1) * rowb + k * kLeaf,
+                    owin = (k + 1) * rowb + (k + 1) * kLeaf;
+    // L_panel = A_panel · W_kkᵀ
+    gemm(r, gemm_args(bt->K + opan, Np, bt->W + okk, Np, bt->L + opan, Np, st, q * kLeaf, kLeaf, kLeaf,
+                      TRI_KMAX_J, 0, 1.0, 0.0), EPI_STORE, false, true);
+    // A_window −= L_panel L_panelᵀ (lower tiles)
+    gemm(r, gemm_args(bt->L + opan, Np, bt->L + opan, Np, bt->K + owin, Np, st, q * kLeaf, q * kLeaf,
+                      kLeaf, 0, 1, -1.0, 1.0), EPI_STORE, false, true);
+  }
+  BandSolveArgs sa{};
+  sa.active = r.d_act; sa.W = bt->W; sa.L = bt->L; sa.sMat = st; sa.ld = Np;
+  sa.Y = bt->Y; sa.sY = bt->Nmax; sa.nvalid = bt->d_n; sa.z = bt->z; sa.alpha = bt->alpha; sa.sVec = Np;
+  sa.Np = Np; sa.p = p;
+  launch_band_solve(sa, r.na, r.s);
+  // backward: selected inversion into K's band blocks (K is dead after the leaves read it)
+  //   G = L_panel W_kk (in place over the panel), Z_panel = −Z_window G,
+  //   Z_kk = W_kkᵀ W_kk − Gᵀ Z_panel, and the panel mirrored above the diagonal
+  BandTransposeArgs ta{};
+  ta.active = r.d_act; ta.Z = bt->K; ta.sMat = st; ta.ld = Np;
+  for (int k = nb - 1; k >= 0; --k) {
+    const int q = std::min(p, nb - 1 - k);
+    const long long okk = k * rowb + k * kLeaf, opan = (k + 1) * rowb + k * kLeaf,
+                    owin = (k + 1) * rowb + (k + 1) * kLeaf;
+    gemm(r, gemm_args(bt->W + okk, Np, bt->W + okk, Np, bt->K + okk, Np, st, kLeaf, kLeaf, kLeaf, 0, 0,
+                      1.0, 0.0), EPI_STORE, true, false);
+    if (q == 0) continue;
+    gemm(r, gemm_args(bt->L + opan, Np, bt->W + okk, Np, bt->L + opan, Np, st, q * kLeaf, kLeaf, kLeaf,
+                      TRI_KMIN_J, 0, 1.0, 0.0), EPI_STORE, false, false);
+    gemm(r, gemm_args(bt->K + owin, Np, bt->L + opan, Np, bt->K + opan, Np, st, q * kLeaf, kLeaf,
+                      q * kLeaf, 0, 0, -1.0, 0.0), EPI_STORE, false, false);
+    ta.k = k;
+    launch_band_transpose(ta, q, r.na, r.s);
+    gemm(r, gemm_args(bt->L + opan, Np, bt->K + opan, Np, bt->K + okk, Np, st, kLeaf, kLeaf, q * kLeaf,
+                      0, 0, -1.0, 1.0), EPI_STORE, true, false);
+  }
+  BandContractArgs ca{};
+  ca.active = r.d_act; ca.Z = bt->K; ca.sMat = st; ca.ld = Np; ca.alpha = bt->alpha; ca.sVec = Np;
+  ca.X = bt->X; ca.sX = (long long)bt->Nmax * bt->D; ca.D = bt->D; ca.specs = bt->d_specs;
+  ca.theta = bt->d_theta; ca.nvalid = bt->d_n; ca.partial = bt->partial; ca.sPartial = bt->partial_stride;
+  ca.Np = Np; ca.p = p;
+  launch_band_contract(ca, max_terms, r.na, r.s);
+  ReduceArgs ra{};
+  ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
+  ra.ntiles = (p + 1) * nb; ra.z = bt->z; ra.sVec = Np; ra.ldiag = bt->ldiag;
+  ra.nvalid = bt->d_n; ra.specs = bt->d_specs; ra.results = bt->results; ra.Np = Np;
+  launch_reduce(ra, r.na, r.s);
+}
+
+// Band width <= 2 blocks: the whole sweep per problem in two fused kernels (gpx_band.hip),
+// each problem with its own p (d_bandp); K's band is built for the widest.
+void band_fused_eval(const Run& r, int p, int max_terms) {
+  gpx_batch* bt = r.bt;
+  const int Np = bt->Np;
+  const long long st = mat_stride(bt);
+  BuildArgs ba{};
+  ba.active = r.d_act; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
+  ba.X = bt->X; ba.sX = (long long)bt->Nmax * bt->D; ba.X2 = bt->X; ba.sX2 = ba.sX; ba.D = bt->D;
+  ba.m2 = 0; ba.out = bt->K; ba.sOut = st; ba.ldo = Np; ba.rows = ba.cols = Np;
+  ba.symmetric = 1; ba.band1 = p + 1;
+  launch_build(ba, r.na, r.s);
+  BandFusedArgs fa{};
+  fa.active = r.d_act; fa.bandp = bt->d_bandp; fa.K = bt->K; fa.L = bt->L; fa.W = bt->W; fa.sMat = st;
+  fa.Y = bt->Y; fa.sY = bt->Nmax; fa.nvalid = bt->d_n; fa.z = bt->z; fa.alpha = bt->alpha;
+  fa.ldiag = bt->ldiag; fa.sVec = Np; fa.X = bt->X; fa.sX = (long long)bt->Nmax * bt->D; fa.D = bt->D;
+  fa.specs = bt->d_specs; fa.theta = bt->d_theta; fa.partial = bt->partial; fa.sPartial = bt->partial_stride;
+  fa.info = bt->d_info; fa.Np = Np;
+  launch_band_fused(fa, max_terms, r.na, r.s);
+  ReduceArgs ra{};
+  ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
+  ra.ntiles = 1; ra.z = bt->z; ra.sVec = Np; ra.ldiag = bt->ldiag;
+  ra.nvalid = bt->d_n; ra.specs = bt->d_specs; ra.results = bt->results; ra.Np = Np;
+  launch_reduce(ra, r.na, r.s);
+}
+
 // The batch's auxiliary streams (the forked T products of the recursion) take the priority of
 // the stream the caller evaluates on, so a batch submitted on a high-priority stream is high
 // priority throughout. Called at the start of an evaluation, when the aux streams are idle (the
@@ -217,8 +407,9 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
         return fail(ctx, GPX_BAD_ARG, "theta must be finite and > 0 (constrained space)");
     }
   }
-  // one DMA from the pinned block: [active | info = 0 | theta] (every call ends with a stream
-  // synchronize, so the previous call's transfers out of h_io have completed)
+  // one DMA from the pinned block: [active | info = 0 | bandp | theta] (every call ends with a
+  // stream synchronize, so the previous call's transfers out of h_io have completed; bandp is
+  // written into h_bandp by gpx_batch_lml_grad before this)
   std::memcpy(bt->h_io, active, sizeof(int) * n_active);
   std::memset(bt->h_io + bt->io_info_off, 0, sizeof(int) * bt->B);
   std::memcpy(bt->h_io + bt->io_theta_off, theta, sizeof(double) * GPX_THETA_STRIDE * bt->B);
@@ -318,7 +509,8 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
   {
     const size_t ints = ((size_t)B * sizeof(int) + 7) / 8 * 8;
     bt->io_info_off = ints;
-    bt->io_theta_off = 2 * ints;
+    bt->io_bandp_off = 2 * ints;
+    bt->io_theta_off = 3 * ints;
     bt->io_res_off = bt->io_theta_off + (size_t)B * GPX_THETA_STRIDE * sizeof(double);
     bt->io_bytes = bt->io_res_off + (size_t)B * kResStride * sizeof(double);
     if (hipMalloc(&bt->d_io, bt->io_bytes) != hipSuccess ||
@@ -327,6 +519,8 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
     std::memset(bt->h_io, 0, bt->io_bytes);
     bt->d_active = reinterpret_cast<int*>(bt->d_io);
     bt->d_info = reinterpret_cast<int*>(bt->d_io + bt->io_info_off);
+    bt->d_bandp = reinterpret_cast<int*>(bt->d_io + bt->io_bandp_off);
+    bt->h_bandp = reinterpret_cast<int*>(bt->h_io + bt->io_bandp_off);
     bt->d_theta = reinterpret_cast<double*>(bt->d_io + bt->io_theta_off);
     bt->results = reinterpret_cast<double*>(bt->d_io + bt->io_res_off);
     bt->h_info = reinterpret_cast<int*>(bt->h_io + bt->io_info_off);
@@ -350,6 +544,14 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
     return cleanup("upload failed");
   bt->fac_theta.assign((size_t)B * GPX_THETA_STRIDE, 0.0);
   bt->fac_valid.assign(B, 0);
+  bt->fac_band.assign(B, 0);
+  bt->band_rmin.assign((size_t)B * GPX_MAX_TERMS * (bt->Np / kLeaf), INFINITY);
+  if (band_shape(bt)) {
+    std::vector<double> hx((size_t)B * N_max * D);
+    if (hipMemcpy(hx.data(), X, sizeof(double) * hx.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      return cleanup("upload failed");
+    for (int b = 0; b < B; ++b) band_tables(bt, b, hx.data() + (size_t)b * N_max * D);
+  }
   *out = bt;
   return GPX_OK;
 }
@@ -395,8 +597,15 @@ int gpx_batch_rebind(gpx_batch* bt, int b, int n, const gpx_kernel_spec* spec) {
   bt->n[b] = n;
   bt->specs[b] = sp;
   bt->fac_valid[b] = 0;
+  bt->fac_band[b] = 0;
   HIPX(ctx, hipMemcpy(bt->d_n + b, &n, sizeof(int), hipMemcpyHostToDevice));
   HIPX(ctx, hipMemcpy(bt->d_specs + b, &sp, sizeof(DevSpec), hipMemcpyHostToDevice));
+  if (band_shape(bt)) {
+    std::vector<double> hx((size_t)n * bt->D);
+    HIPX(ctx, hipMemcpy(hx.data(), bt->X + (size_t)b * bt->Nmax * bt->D, sizeof(double) * hx.size(),
+                        hipMemcpyDeviceToHost));
+    band_tables(bt, b, hx.data());
+  }
   return GPX_OK;
 }
 
@@ -405,67 +614,48 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   if (!bt) return GPX_BAD_ARG;
   gpx_ctx* ctx = bt->ctx;
   if (!lml || !grad || !info) return fail(ctx, GPX_BAD_ARG, "null output");
+  if (n_active <= 0 || n_active > bt->B || !active || !theta)
+    return fail(ctx, GPX_BAD_ARG, "bad active set / theta");
+  for (int i = 0; i < n_active; ++i)
+    if (active[i] < 0 || active[i] >= bt->B) return fail(ctx, GPX_BAD_ARG, "active index out of range");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-  int rc = upload_common(bt, n_active, active, theta, s);
+  // Route each problem: the block-banded path when K and every ∂K/∂θ vanish exactly beyond a
+  // band of p <= band_limit 64-blocks at this θ (gpx_band.hip), the dense recursion otherwise.
+  // The device active list is [dense problems | banded problems].
+  std::vector<int32_t> order;
+  order.reserve(n_active);
+  std::vector<int32_t> band_ids, fused_ids;
+  int pband = 0, pfused = 0;
+  const int plim = band_limit(bt);
+  const char* ef = getenv("GPX_BAND_FUSED");  // 0: p <= 2 problems take the per-block launches too
+  const bool fused_on = !(ef && atoi(ef) == 0);
+  for (int i = 0; i < n_active; ++i) {
+    const int b = active[i];
+    const int p = plim >= 0 ? band_width(bt, b, theta + (size_t)b * GPX_THETA_STRIDE) : -1;
+    if (p >= 0 && p <= plim) {
+      bt->h_bandp[b] = p;
+      if (fused_on && p <= 2) {
+        fused_ids.push_back(b);
+        pfused = std::max(pfused, p);
+      } else {
+        band_ids.push_back(b);
+        pband = std::max(pband, p);
+      }
+    } else {
+      order.push_back(b);
+    }
+  }
+  const int n_dense = (int)order.size(), n_band = (int)band_ids.size(), n_fused = (int)fused_ids.size();
+  order.insert(order.end(), band_ids.begin(), band_ids.end());
+  order.insert(order.end(), fused_ids.begin(), fused_ids.end());
+  int rc = upload_common(bt, n_active, order.data(), theta, s);
   if (rc != GPX_OK) return rc;
   rc = match_aux_priority(bt, s);
   if (rc != GPX_OK) return rc;
   bt->flops_acc = 0.0;
-  // Split the active problems into up to kGroups ranges, each running the whole pipeline on
-  // its own stream: one group's latency-bound phases (64x64 leaves, small recursion levels)
-  // overlap another group's large MFMA GEMMs.
-  // Default: one pipeline whose recursion forks the top-level T products onto aux streams
-  // (concurrency inside the DAG). GPX_GROUPS=g instead splits the problems into g pipelines.
-  int ng = 1;
-  if (const char* e = getenv("GPX_GROUPS")) ng = atoi(e);
-  ng = std::max(1, std::min(std::min(ng, kGroups), n_active));
-  if (ng > 1 && !bt->fork) {
-    HIPX(ctx, hipEventCreateWithFlags(&bt->fork, hipEventDisableTiming));
-    for (int g = 0; g < kGroups; ++g) {
-      HIPX(ctx, hipStreamCreateWithFlags(&bt->workers[g], hipStreamNonBlocking));
-      HIPX(ctx, hipEventCreateWithFlags(&bt->join[g], hipEventDisableTiming));
-    }
-  }
-  int next_event = 0;
-  Run runs[kGroups];
-  int start = 0;
-  for (int g = 0; g < ng; ++g) {
-    const int cnt = n_active / ng + (g < n_active % ng ? 1 : 0);
-    runs[g] = Run{bt, bt->d_active + start, cnt, ng == 1 ? s : bt->workers[g], ng == 1, &next_event};
-    start += cnt;
-  }
-  if (ng > 1) {
-    HIPX(ctx, hipEventRecord(bt->fork, s));
-    for (int g = 0; g < ng; ++g) HIPX(ctx, hipStreamWaitEvent(runs[g].s, bt->fork, 0));
-  }
   PhaseTimer total(ctx->profiling != 0, s);
   total.mark();
-  std::vector<PhaseTimer> pts;
-  pts.reserve(ng);
-  for (int g = 0; g < ng; ++g) pts.emplace_back(ctx->profiling != 0, runs[g].s);
-  for (int g = 0; g < ng; ++g) {
-    const Run& r = runs[g];
-    pts[g].mark();
-    factor(r);
-    pts[g].mark();
-    alpha_solve(r);
-    pts[g].mark();
-  }
-  if (ng > 1) {
-    for (int g = 0; g < ng; ++g) {
-      HIPX(ctx, hipEventRecord(bt->join[g], runs[g].s));
-      HIPX(ctx, hipStreamWaitEvent(s, bt->join[g], 0));
-    }
-  }
-  // The contraction fills the chip by itself (Np²/2/128² tiles per problem): one launch over
-  // every active problem, alone on the stream.
-  const Run all{bt, bt->d_active, n_active, s};
-  int max_terms = 1;
-  for (int i = 0; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[active[i]].n_terms);
-  PhaseTimer ct(ctx->profiling != 0, s);
-  // the contraction kernel is timestamped at its actual start/end (hipExtLaunchKernel), so
-  // its duration excludes any wait behind kernels of other streams (concurrent batches)
   struct EvPair {
     hipEvent_t e[2] = {nullptr, nullptr};
     ~EvPair() {
@@ -474,36 +664,104 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     }
   } kp;
   hipEvent_t* kev = kp.e;
-  if (ctx->profiling) {
-    HIPX(ctx, hipEventCreate(&kev[0]));
-    HIPX(ctx, hipEventCreate(&kev[1]));
-  }
-  // optional: run the contraction on a highest-priority stream so that, with several batches
-  // evaluating concurrently, its workgroups are dispatched ahead of the other batches' kernels
-  static const bool prio = [] {
-    const char* e = getenv("GPX_CONTRACT_PRIORITY");
-    return e && atoi(e) != 0;
-  }();
-  Run cr = all;
-  if (prio) {
-    if (!bt->hp) {
-      int lo = 0, hi = 0;
-      HIPX(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
-      HIPX(ctx, hipStreamCreateWithPriority(&bt->hp, hipStreamNonBlocking, hi));
+  int ng = 0;
+  std::vector<PhaseTimer> pts;
+  PhaseTimer ct(ctx->profiling != 0 && n_dense > 0, s);
+  if (n_dense > 0) {
+    // Split the dense problems into up to kGroups ranges, each running the whole pipeline on
+    // its own stream: one group's latency-bound phases (64x64 leaves, small recursion levels)
+    // overlap another group's large MFMA GEMMs.
+    // Default: one pipeline whose recursion forks the top-level T products onto aux streams
+    // (concurrency inside the DAG). GPX_GROUPS=g instead splits the problems into g pipelines.
+    ng = 1;
+    if (const char* e = getenv("GPX_GROUPS")) ng = atoi(e);
+    ng = std::max(1, std::min(std::min(ng, kGroups), n_dense));
+    if (ng > 1 && !bt->fork) {
+      HIPX(ctx, hipEventCreateWithFlags(&bt->fork, hipEventDisableTiming));
+      for (int g = 0; g < kGroups; ++g) {
+        HIPX(ctx, hipStreamCreateWithFlags(&bt->workers[g], hipStreamNonBlocking));
+        HIPX(ctx, hipEventCreateWithFlags(&bt->join[g], hipEventDisableTiming));
+      }
     }
-    HIPX(ctx, hipEventRecord(bt->ev[kEvents - 4], s));
-    HIPX(ctx, hipStreamWaitEvent(bt->hp, bt->ev[kEvents - 4], 0));
-    cr.s = bt->hp;
+    int next_event = 0;
+    Run runs[kGroups];
+    int start = 0;
+    for (int g = 0; g < ng; ++g) {
+      const int cnt = n_dense / ng + (g < n_dense % ng ? 1 : 0);
+      runs[g] = Run{bt, bt->d_active + start, cnt, ng == 1 ? s : bt->workers[g], ng == 1, &next_event};
+      start += cnt;
+    }
+    if (ng > 1) {
+      HIPX(ctx, hipEventRecord(bt->fork, s));
+      for (int g = 0; g < ng; ++g) HIPX(ctx, hipStreamWaitEvent(runs[g].s, bt->fork, 0));
+    }
+    pts.reserve(ng);
+    for (int g = 0; g < ng; ++g) pts.emplace_back(ctx->profiling != 0, runs[g].s);
+    for (int g = 0; g < ng; ++g) {
+      const Run& r = runs[g];
+      pts[g].mark();
+      factor(r);
+      pts[g].mark();
+      alpha_solve(r);
+      pts[g].mark();
+    }
+    if (ng > 1) {
+      for (int g = 0; g < ng; ++g) {
+        HIPX(ctx, hipEventRecord(bt->join[g], runs[g].s));
+        HIPX(ctx, hipStreamWaitEvent(s, bt->join[g], 0));
+      }
+    }
+    // The contraction fills the chip by itself (Np²/2/128² tiles per problem): one launch over
+    // every dense problem, alone on the stream.
+    const Run all{bt, bt->d_active, n_dense, s};
+    int max_terms = 1;
+    for (int i = 0; i < n_dense; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
+    // the contraction kernel is timestamped at its actual start/end (hipExtLaunchKernel), so
+    // its duration excludes any wait behind kernels of other streams (concurrent batches)
+    if (ctx->profiling) {
+      HIPX(ctx, hipEventCreate(&kev[0]));
+      HIPX(ctx, hipEventCreate(&kev[1]));
+    }
+    // optional: run the contraction on a highest-priority stream so that, with several batches
+    // evaluating concurrently, its workgroups are dispatched ahead of the other batches' kernels
+    static const bool prio = [] {
+      const char* e = getenv("GPX_CONTRACT_PRIORITY");
+      return e && atoi(e) != 0;
+    }();
+    Run cr = all;
+    if (prio) {
+      if (!bt->hp) {
+        int lo = 0, hi = 0;
+        HIPX(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPX(ctx, hipStreamCreateWithPriority(&bt->hp, hipStreamNonBlocking, hi));
+      }
+      HIPX(ctx, hipEventRecord(bt->ev[kEvents - 4], s));
+      HIPX(ctx, hipStreamWaitEvent(bt->hp, bt->ev[kEvents - 4], 0));
+      cr.s = bt->hp;
+    }
+    ct.mark();
+    contract(cr, max_terms, kev[0], kev[1]);
+    ct.mark();
+    reduce(cr);
+    if (prio) {
+      HIPX(ctx, hipEventRecord(bt->ev[kEvents - 3], bt->hp));
+      HIPX(ctx, hipStreamWaitEvent(s, bt->ev[kEvents - 3], 0));
+    }
+    ct.mark();
   }
-  ct.mark();
-  contract(cr, max_terms, kev[0], kev[1]);
-  ct.mark();
-  reduce(cr);
-  if (prio) {
-    HIPX(ctx, hipEventRecord(bt->ev[kEvents - 3], bt->hp));
-    HIPX(ctx, hipStreamWaitEvent(s, bt->ev[kEvents - 3], 0));
+  PhaseTimer bp(ctx->profiling != 0, s);
+  bp.mark();
+  if (n_band > 0) {
+    int max_terms = 1;
+    for (int i = n_dense; i < n_dense + n_band; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
+    band_eval(Run{bt, bt->d_active + n_dense, n_band, s}, pband, max_terms);
   }
-  ct.mark();
+  if (n_fused > 0) {
+    int max_terms = 1;
+    for (int i = n_dense + n_band; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
+    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, pfused, max_terms);
+  }
+  bp.mark();
   total.mark();
   HIPX(ctx, hipGetLastError());
   // one DMA into the pinned block: [info | theta (unchanged) | results]
@@ -516,14 +774,22 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
       bt->timing.factor_ms += pts[g].ms(0, 1) / ng;
       bt->timing.alpha_ms += pts[g].ms(1, 2) / ng;
     }
-    bt->timing.grad_ms = ct.ms(0, 2);
-    float kms = 0.f;
-    (void)hipEventElapsedTime(&kms, kev[0], kev[1]);
-    bt->timing.contract_ms_total += kms;
-    bt->timing.contract_launches += 1.0;
-    double f = 0.0;
-    for (int i = 0; i < bt->Np; ++i) f += 2.0 * (i + 1) * (double)(bt->Np - i);
-    bt->timing.contract_alg_flops += n_active * f;
+    bt->timing.grad_ms = n_dense > 0 ? ct.ms(0, 2) : 0.0;
+    if (n_dense > 0) {
+      float kms = 0.f;
+      (void)hipEventElapsedTime(&kms, kev[0], kev[1]);
+      bt->timing.contract_ms_total += kms;
+      bt->timing.contract_launches += 1.0;
+      double f = 0.0;
+      for (int i = 0; i < bt->Np; ++i) f += 2.0 * (i + 1) * (double)(bt->Np - i);
+      bt->timing.contract_alg_flops += n_dense * f;
+    }
+    if (n_band + n_fused > 0) {
+      bt->timing.band_ms_total += bp.ms(0, 1);
+      bt->timing.band_calls += 1.0;
+      bt->timing.band_evals += n_band + n_fused;
+      for (int i = n_dense; i < n_active; ++i) bt->timing.band_p_sum += bt->h_bandp[order[i]];
+    }
     bt->timing.predict_ms = 0.0;
     bt->timing.total_ms = total.ms(0, 1);
     bt->timing.gemm_flops = bt->flops_acc;
@@ -532,7 +798,7 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   }
   int status = GPX_OK;
   for (int i = 0; i < n_active; ++i) {
-    const int b = active[i];
+    const int b = order[i];
     const double* res = bt->h_results + (size_t)b * kResStride;
     info[b] = bt->h_info[b];
     const int np = bt->specs[b].n_params;
@@ -548,6 +814,7 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     std::memcpy(&bt->fac_theta[(size_t)b * GPX_THETA_STRIDE], theta + (size_t)b * GPX_THETA_STRIDE,
                 sizeof(double) * GPX_THETA_STRIDE);
     bt->fac_valid[b] = 1;
+    bt->fac_band[b] = i >= n_dense;
   }
   if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
   return status;
@@ -572,24 +839,36 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   PhaseTimer pt(ctx->profiling != 0, s);
   bt->flops_acc = 0.0;
   pt.mark();
-  // re-factorise the problems whose cached factor is not at exactly this theta
-  std::vector<int> refac;
+  // re-factorise the problems whose cached factor is not at exactly this theta. A cached
+  // block-banded factorisation (gpx_band.hip) serves predict at the training inputs (it holds
+  // α and the diagonal of K⁻¹); any other predict re-factorises densely.
+  std::vector<int> refac, band_cached;
   for (int i = 0; i < n_active; ++i) {
     const int b = active[i];
     const bool same = bt->fac_valid[b] &&
                       std::memcmp(&bt->fac_theta[(size_t)b * GPX_THETA_STRIDE],
                                   theta + (size_t)b * GPX_THETA_STRIDE,
                                   sizeof(double) * GPX_THETA_STRIDE) == 0;
-    if (!same) refac.push_back(b);
+    if (!same || (bt->fac_band[b] && !train)) refac.push_back(b);
+    else if (bt->fac_band[b]) band_cached.push_back(b);
   }
+  // device active list: [dense-factored problems | band-cached problems]
+  std::vector<int32_t> order;
+  order.reserve(n_active);
+  for (int i = 0; i < n_active; ++i)
+    if (std::find(band_cached.begin(), band_cached.end(), active[i]) == band_cached.end())
+      order.push_back(active[i]);
+  const int n_dense = (int)order.size();
+  order.insert(order.end(), band_cached.begin(), band_cached.end());
   if (!refac.empty()) {
     HIPX(ctx, hipMemcpyAsync(bt->d_active, refac.data(), sizeof(int) * refac.size(),
                              hipMemcpyHostToDevice, s));
     const Run rr{bt, bt->d_active, (int)refac.size(), s};
     factor(rr);
     alpha_solve(rr);
-    HIPX(ctx, hipMemcpyAsync(bt->d_active, active, sizeof(int) * n_active, hipMemcpyHostToDevice, s));
   }
+  if (!refac.empty() || n_dense < n_active)
+    HIPX(ctx, hipMemcpyAsync(bt->d_active, order.data(), sizeof(int) * n_active, hipMemcpyHostToDevice, s));
   pt.mark();
   const int Np = bt->Np;
   if (train) {
@@ -598,7 +877,13 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
     ta.alpha = bt->alpha; ta.sVec = Np; ta.Y = bt->Y; ta.sY = bt->Nmax; ta.nvalid = bt->d_n;
     ta.specs = bt->d_specs; ta.theta = bt->d_theta; ta.add_noise = add_noise;
     ta.mean = mean; ta.var = var; ta.sOut = bt->Nmax;
-    launch_train_pred(ta, n_active, Np, s);
+    if (n_dense > 0) launch_train_pred(ta, n_dense, Np, s);
+    if (n_dense < n_active) {
+      // banded: diag(K⁻¹) from the selected inverse in K's diagonal blocks
+      TrainPredArgs tb = ta;
+      tb.active = bt->d_active + n_dense; tb.W = bt->K;
+      launch_band_train_pred(tb, n_active - n_dense, Np, s);
+    }
   } else {
   const int Mp = ((M + 63) / 64) * 64;
   // cross-covariance workspace [B][Np][Mp]
@@ -702,6 +987,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
       std::memcpy(&bt->fac_theta[(size_t)b * GPX_THETA_STRIDE], theta + (size_t)b * GPX_THETA_STRIDE,
                   sizeof(double) * GPX_THETA_STRIDE);
       bt->fac_valid[b] = 1;
+      bt->fac_band[b] = 0;
     }
   }
   if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";

@@ -46,13 +46,20 @@ struct gpx_batch {
   // factor cache: theta row of the last factorisation per problem
   std::vector<double> fac_theta;
   std::vector<char> fac_valid;
+  std::vector<char> fac_band;      // the cached factorisation is the block-banded one (gpx_band.hip)
+  // block-band eligibility (see band_width): per problem, per kernel term, per block offset d,
+  // a lower bound on the distance between any point of block k and any point of block k − d
+  // over the term's active dims, [B][GPX_MAX_TERMS][Np/64]; computed when a problem is bound
+  std::vector<double> band_rmin;
   // per-call I/O in ONE device block mirrored by ONE pinned host block, laid out
-  //   [active: B ints][info: B ints][theta: B×16][results: B×kResStride]   (8-byte aligned)
+  //   [active: B ints][info: B ints][bandp: B ints][theta: B×16][results: B×kResStride]
   // so an evaluation uploads [active, info=0, theta] in one DMA and downloads [info ..
   // results] in one DMA (was 2 pageable copies + a memset up, 2 pageable copies down)
   char* d_io = nullptr;
   char* h_io = nullptr;       // pinned
-  size_t io_info_off = 0, io_theta_off = 0, io_res_off = 0, io_bytes = 0;
+  size_t io_info_off = 0, io_bandp_off = 0, io_theta_off = 0, io_res_off = 0, io_bytes = 0;
+  int* d_bandp = nullptr;     // [B] band width (64-blocks) of the banded problems of the call
+  int* h_bandp = nullptr;
   double* h_results = nullptr;  // views into h_io
   int* h_info = nullptr;
   gpx_timing timing{};
@@ -138,6 +145,12 @@ GemmArgs gemm_args(const double* A, int lda, const double* B, int ldb, double* C
                    long long stride, int M, int N, int K, int tri, int lower, double alpha,
                    double beta);
 void chol_inv(const Run& r, int off, int n, int depth = 0);
+void band_tables(gpx_batch* bt, int b, const double* hostX);  // fills band_rmin for problem b
+int band_width(const gpx_batch* bt, int b, const double* theta_row);  // p in 64-blocks, or -1
+bool band_shape(const gpx_batch* bt);  // the banded path handles this batch's padded size
+int band_limit(const gpx_batch* bt);  // largest p the banded path takes (-1: path disabled)
+void band_eval(const Run& r, int p, int max_terms);  // build .. reduce for a banded active set
+void band_fused_eval(const Run& r, int p, int max_terms);  // same for p <= 2, two fused kernels
 void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W = L⁻¹)
 void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,

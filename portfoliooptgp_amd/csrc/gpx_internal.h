@@ -24,6 +24,7 @@ struct BuildArgs {
   int rows, cols;          // padded, multiples of 64
   int symmetric;           // 1: lower tiles of K(X,X)+σn²I with identity padding
   int rows_valid;          // >0: valid rows for every problem (K(X*,X*)), else nvalid[b]
+  int band1;               // symmetric only: >0 builds just the 64-blocks (k, k−d), d < band1
 };
 
 // ---- leaf: 64x64 Cholesky + triangular inverse in LDS --------------------------------
@@ -111,6 +112,46 @@ struct PredVarArgs {
   int M; int add_noise;
   double* var; long long sVar;
 };
+
+// ---- block-banded path (gpx_band.hip) --------------------------------------------------
+struct BandSolveArgs {
+  const int* active;
+  const double* W; const double* L; long long sMat; int ld;   // diagonal W_kk blocks, L panels
+  const double* Y; long long sY; const int* nvalid;
+  double* z; double* alpha; long long sVec;
+  int Np, p;                       // p: band width in 64-blocks
+};
+struct BandTransposeArgs {
+  const int* active;
+  double* Z; long long sMat; int ld;
+  int k;                           // mirror blocks (k+d, k) -> (k, k+d), d = 1..q
+};
+struct BandContractArgs {
+  const int* active;
+  const double* Z; long long sMat; int ld;       // selected inverse (band blocks of K⁻¹)
+  const double* alpha; long long sVec;
+  const double* X; long long sX; int D;
+  const DevSpec* specs; const double* theta; const int* nvalid;
+  double* partial; long long sPartial;           // [B][(p+1)·nb][16], tile = d·nb + k
+  int Np, p;
+};
+// fused per-problem sweep for band width p <= 2 (gpx_band.hip: band_fwd_kernel, band_bwd_kernel)
+struct BandFusedArgs {
+  const int* active; const int* bandp;           // per-problem band width p (64-blocks), <= 2
+  double* K; double* L; double* W; long long sMat;
+  const double* Y; long long sY; const int* nvalid;
+  double* z; double* alpha; double* ldiag; long long sVec;
+  const double* X; long long sX; int D;
+  const DevSpec* specs; const double* theta;
+  double* partial; long long sPartial;           // one [16] row per problem (tile 0)
+  int* info;
+  int Np;
+};
+void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s);
+void launch_band_solve(const BandSolveArgs& a, int n_active, hipStream_t s);
+void launch_band_transpose(const BandTransposeArgs& a, int q, int n_active, hipStream_t s);
+void launch_band_contract(const BandContractArgs& a, int max_terms, int n_active, hipStream_t s);
+void launch_band_train_pred(const TrainPredArgs& a, int n_active, int Np, hipStream_t s);
 
 void launch_build(const BuildArgs& a, int n_active, hipStream_t s);
 void launch_leaf(const LeafArgs& a, int n_active, hipStream_t s);

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include "gpx_internal.h"
+#include "gpx_leaf.h"
 
 namespace gpx {
 
@@ -65,36 +66,6 @@ __device__ __forceinline__ double stationary_value(double r2, double var) {
   return 0.0;
 }
 
-// value derivatives (∂K/∂ℓ, ∂K/∂σ²) of a single-term isotropic stationary kernel at r2 = d²/ℓ²,
-// with 1/ℓ precomputed by the caller (same formulas and clamp as eval_term<true>)
-__device__ __forceinline__ void stationary_grad(int kind, double r2, double var, double inv_ell,
-                                                double (&dk)[3]) {
-  dk[2] = 0.0;
-  if (kind == GPX_SE) {
-    const double g = exp(-0.5 * r2);
-    dk[0] = var * g * r2 * inv_ell;
-    dk[1] = g;
-    return;
-  }
-  const bool clamped = !(r2 > 1e-36);
-  const double r = sqrt(clamped ? 1e-36 : r2);
-  double g, dgdr;
-  if (kind == GPX_MATERN12) {
-    g = exp(-r); dgdr = -g;
-  } else if (kind == GPX_EXPONENTIAL) {
-    g = exp(-0.5 * r); dgdr = -0.5 * g;
-  } else if (kind == GPX_MATERN32) {
-    const double sq3 = 1.7320508075688772, e = exp(-sq3 * r);
-    g = (1.0 + sq3 * r) * e; dgdr = -3.0 * r * e;
-  } else {
-    const double sq5 = 2.23606797749979, e = exp(-sq5 * r);
-    g = (1.0 + sq5 * r + (5.0 / 3.0) * r * r) * e;
-    dgdr = -(5.0 / 3.0) * r * (1.0 + sq5 * r) * e;
-  }
-  dk[0] = clamped ? 0.0 : var * dgdr * (-r * inv_ell);
-  dk[1] = g;
-}
-
 template <int KIND>
 __device__ __forceinline__ void build_stationary(const BuildArgs& a, const DevSpec& spec,
                                                  const double* sth, const double* sxi,
@@ -130,7 +101,13 @@ __device__ __forceinline__ void build_stationary(const BuildArgs& a, const DevSp
 __global__ __launch_bounds__(256) void build_kernel(BuildArgs a) {
   const int b = a.active[blockIdx.y];
   int ti, tj;
-  if (a.symmetric) {
+  if (a.symmetric && a.band1 > 0) {
+    // block band: tile x = d·nb + k -> (k, k − d), d < band1 (tiles with k < d are empty)
+    const int nb = a.rows / 64, d = blockIdx.x / nb;
+    ti = blockIdx.x - d * nb;
+    tj = ti - d;
+    if (tj < 0) return;
+  } else if (a.symmetric) {
     lower_tile(blockIdx.x, ti, tj);
   } else {
     const int ntj = a.cols / 64;
@@ -192,7 +169,7 @@ __global__ __launch_bounds__(256) void build_kernel(BuildArgs a) {
 
 void launch_build(const BuildArgs& a, int n_active, hipStream_t s) {
   const int ti = a.rows / 64, tj = a.cols / 64;
-  const int ntiles = a.symmetric ? ti * (ti + 1) / 2 : ti * tj;
+  const int ntiles = a.symmetric ? (a.band1 > 0 ? a.band1 * ti : ti * (ti + 1) / 2) : ti * tj;
   hipLaunchKernelGGL(build_kernel, dim3(ntiles, n_active), dim3(256), 0, s, a);
 }
 
@@ -207,25 +184,8 @@ void launch_build(const BuildArgs& a, int n_active, hipStream_t s) {
 // the first product is the B operand of the second without an LDS round trip).
 // 15 barriers in all. Writes W11 (zeros above the diagonal) and log L_ii.
 // ======================================================================================
-__device__ __forceinline__ double readlane_d(double v, int l) {
-  const unsigned long long u = __double_as_longlong(v);
-  const unsigned lo = __builtin_amdgcn_readlane((unsigned)(u & 0xffffffffu), l);
-  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
-  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
-
-// 1/sqrt(x) from the hardware estimate and two Newton steps (each doubles the ~22 correct bits):
-// within an ulp or two of 1/sqrt, and one multiply gives sqrt(x) = x/sqrt(x). Replaces a
-// correctly rounded sqrt and a division on the leaves' serial 16-step diagonal chain.
-__device__ __forceinline__ double rsqrt_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  y = y * fma(-0.5 * x, y * y, 1.5);
-  y = y * fma(-0.5 * x, y * y, 1.5);
-  return y;
-}
-
 __global__ __launch_bounds__(256) void leaf_kernel(LeafArgs a) {
-  constexpr int S = 66;  // row stride (doubles): 16 rows x 1 col fragment reads are conflict-free
+  constexpr int S = kLeafS;
   __shared__ __attribute__((aligned(16))) double sA[64 * S];
   __shared__ __attribute__((aligned(16))) double sW[64 * S];
   __shared__ int sfail;
@@ -233,8 +193,6 @@ __global__ __launch_bounds__(256) void leaf_kernel(LeafArgs a) {
   const double* K = a.K + (long long)b * a.sMat;
   double* W = a.W + (long long)b * a.sMat;
   const int ld = a.ld, off = a.off, tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int l15 = lane & 15, l4 = lane >> 4;
   // 8 independent loads in flight per thread (a load-then-store loop serialises on latency)
 #pragma unroll 1
   for (int e0 = tid; e0 < 4096; e0 += 256 * 8) {
@@ -254,102 +212,7 @@ __global__ __launch_bounds__(256) void leaf_kernel(LeafArgs a) {
   if (tid == 0) sfail = -1;
   __syncthreads();
 
-  for (int jb = 0; jb < 4; ++jb) {
-    const int c0 = jb * 16;
-    if (wave == 0) {
-      double r[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) r[k] = sA[(c0 + l15) * S + c0 + k];
-      int fail = -1;
-      double invd[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const double piv = readlane_d(r[j], j);
-        if (!(piv > 0.0) && fail < 0) fail = j;
-        const double inv = rsqrt_nr(piv);
-        const double ljj = piv * inv;
-        invd[j] = inv;
-        r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
-#pragma unroll
-        for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], readlane_d(r[j], k), r[k]);
-      }
-      // lane l15 holds row l15 of L_jj (r[0..l15]); column l15 of D = L_jj⁻¹ by substitution
-      double w[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        double sacc = (i == l15) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < i; ++k) sacc = fma(-readlane_d(r[k], i), w[k], sacc);
-        w[i] = sacc * invd[i];
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sW[(c0 + i) * S + c0 + lane] = w[i];
-        a.ldiag[(long long)b * a.sVec + off + c0 + lane] = log(r[lane & 15]);
-      }
-      if (lane == 0 && fail >= 0 && sfail < 0) sfail = c0 + fail;
-    }
-    __syncthreads();
-    // panel: L_(ib,jb) = A_(ib,jb) · Dᵀ for ib = jb+1 .. 3, one wave per block
-    const int nblk = 3 - jb;
-    if (wave < nblk) {
-      const int r0 = (jb + 1 + wave) * 16;
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const double av = sA[(r0 + l15) * S + c0 + 4 * kk + l4];
-        const double bv = sW[(c0 + l15) * S + c0 + 4 * kk + l4];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sA[(r0 + l4 + 4 * q) * S + c0 + l15] = acc[q];
-    }
-    __syncthreads();
-    // trailing update of the lower blocks (ib, kb), jb < kb <= ib
-    const int ntr = nblk * (nblk + 1) / 2;
-    for (int t = wave; t < ntr; t += 4) {
-      int p = 0;
-      while ((p + 1) * (p + 2) / 2 <= t) ++p;
-      const int q = t - p * (p + 1) / 2;
-      const int ri = (jb + 1 + p) * 16, rk = (jb + 1 + q) * 16;
-      d4 acc;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = sA[(ri + l4 + 4 * u) * S + rk + l15];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const double av = sA[(ri + l15) * S + c0 + 4 * kk + l4];
-        const double bv = sA[(rk + l15) * S + c0 + 4 * kk + l4];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) sA[(ri + l4 + 4 * u) * S + rk + l15] = acc[u];
-    }
-    __syncthreads();
-  }
-  // W = L⁻¹: block rows 1..3, blocks j < i in parallel (wave j)
-  for (int i = 1; i < 4; ++i) {
-    if (wave < i) {
-      const int j = wave;
-      d4 t = {0.0, 0.0, 0.0, 0.0};
-      for (int k = j; k < i; ++k) {
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const double av = sA[(i * 16 + l15) * S + k * 16 + 4 * kk + l4];   // L_ik[row][k']
-          const double bv = sW[(k * 16 + 4 * kk + l4) * S + j * 16 + l15];   // W_kj[k'][col]
-          t = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, t, 0, 0, 0);
-        }
-      }
-      d4 wv = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const double av = sW[(i * 16 + l15) * S + i * 16 + 4 * kk + l4];     // D_i[row][k']
-        wv = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, t[kk], wv, 0, 0, 0);  // T[k'][col]
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sW[(i * 16 + l4 + 4 * q) * S + j * 16 + l15] = wv[q];
-    }
-    __syncthreads();
-  }
+  leaf64_lds(sA, sW, a.ldiag + (long long)b * a.sVec + off, &sfail);
   for (int e = tid; e < 4096; e += 256) {
     const int r = e >> 6, c = e & 63;
     W[(long long)(off + r) * ld + off + c] = sW[r * S + c];

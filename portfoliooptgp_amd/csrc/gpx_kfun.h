@@ -120,6 +120,36 @@ __device__ __forceinline__ double eval_term(const gpx_term& t, const double* __r
   return var * g;
 }
 
+// value derivatives (∂K/∂ℓ, ∂K/∂σ²) of a single-term isotropic stationary kernel at r2 = d²/ℓ²,
+// with 1/ℓ precomputed by the caller (same formulas and clamp as eval_term<true>)
+__device__ __forceinline__ void stationary_grad(int kind, double r2, double var, double inv_ell,
+                                                double (&dk)[3]) {
+  dk[2] = 0.0;
+  if (kind == GPX_SE) {
+    const double g = exp(-0.5 * r2);
+    dk[0] = var * g * r2 * inv_ell;
+    dk[1] = g;
+    return;
+  }
+  const bool clamped = !(r2 > 1e-36);
+  const double r = sqrt(clamped ? 1e-36 : r2);
+  double g, dgdr;
+  if (kind == GPX_MATERN12) {
+    g = exp(-r); dgdr = -g;
+  } else if (kind == GPX_EXPONENTIAL) {
+    g = exp(-0.5 * r); dgdr = -0.5 * g;
+  } else if (kind == GPX_MATERN32) {
+    const double sq3 = 1.7320508075688772, e = exp(-sq3 * r);
+    g = (1.0 + sq3 * r) * e; dgdr = -3.0 * r * e;
+  } else {
+    const double sq5 = 2.23606797749979, e = exp(-sq5 * r);
+    g = (1.0 + sq5 * r + (5.0 / 3.0) * r * r) * e;
+    dgdr = -(5.0 / 3.0) * r * (1.0 + sq5 * r) * e;
+  }
+  dk[0] = clamped ? 0.0 : var * dgdr * (-r * inv_ell);
+  dk[1] = g;
+}
+
 // K(xi, xj) for a full spec.
 __device__ __forceinline__ double eval_k(const DevSpec& s, const double* __restrict__ th,
                                          const double* __restrict__ xi,

@@ -80,6 +80,8 @@ class LbfgsbStepper:
 
     @staticmethod
     def _scalar(fx):
+        if type(fx) is float:
+            return fx
         if not np.isscalar(fx):
             try:
                 fx = np.asarray(fx).item()
@@ -111,23 +113,31 @@ class LbfgsbStepper:
         isave = np.zeros(44, dtype=np.int32)
         dsave = np.zeros(29, dtype=np.float64)
         n_iterations = 0
+        maxiter, maxfun, maxls = o["maxiter"], o["maxfun"], o["maxls"]
+        setulb = _lbfgsb.setulb
+        sf_key = sf_x.tolist()
         while True:
-            g = g.astype(np.float64)
-            _lbfgsb.setulb(m, x, low_bnd, upper_bnd, nbd, f, g, factr, pgtol, wa,
-                           iwa, task, lsave, isave, dsave, o["maxls"], ln_task)
-            if task[0] == 3:  # f and g wanted at x
-                # np.array_equal(x, sf_x) for two float64 vectors of one shape (NaN unequal)
-                if not (x == sf_x).all():
+            if g.dtype != np.float64:  # scipy re-casts g every pass; only the first is not f64
+                g = g.astype(np.float64)
+            setulb(m, x, low_bnd, upper_bnd, nbd, f, g, factr, pgtol, wa,
+                   iwa, task, lsave, isave, dsave, maxls, ln_task)
+            t0 = task[0]
+            if t0 == 3:  # f and g wanted at x
+                # np.array_equal(x, sf_x) for two float64 vectors of one shape: Python float
+                # equality of the elements (0.0 == -0.0; NaN unequal: tolist() makes new objects)
+                key = x.tolist()
+                if key != sf_key:
                     sf_x = x.copy()
-                    fx, gx = yield sf_x.copy()
+                    sf_key = key
+                    fx, gx = yield sf_x
                     self.nfev += 1
                     sf_f, sf_g = self._scalar(fx), np.atleast_1d(gx)
-                f, g = sf_f, sf_g
-            elif task[0] == 1:  # new iteration
+                f, g = sf_f, sf_g.copy()  # setulb gets its own g, as scipy's per-pass astype copy
+            elif t0 == 1:  # new iteration
                 n_iterations += 1
-                if n_iterations >= o["maxiter"]:
+                if n_iterations >= maxiter:
                     task[0], task[1] = 5, 504
-                elif self.nfev > o["maxfun"]:
+                elif self.nfev > maxfun:
                     task[0], task[1] = 5, 502
             else:
                 break

@@ -142,15 +142,11 @@ class GPR:
         closure._gpx_model = self
         return closure
 
-    def loss_and_grad_unconstrained(self, variables=None, lml=None, grad_theta=None):
-        """(−logML, ∂(−logML)/∂u) for ``variables`` (default: trainable_variables)."""
-        if lml is None:
-            lml, grad_theta = self._lml_and_grad_theta()
-        variables = self.trainable_variables if variables is None else variables
+    def _variable_map(self, variables):
+        """(variables, θ-row index of each variable, its Parameter), cached for the variables
+        object an optimiser passes on every call (kernel parameters, then σn² at n_params)."""
         cache = getattr(self, "_grad_map", None)
         if cache is None or cache[0] is not variables:
-            # θ-row index of each variable (kernel parameters, then σn² at n_params); cached
-            # for the variables object an optimiser passes on every call
             pindex = {id(p): i for i, p in enumerate(self.kernel.parameters)}
             nk = len(self.kernel.parameters)
             rows = []
@@ -163,7 +159,20 @@ class GPR:
                 else:
                     raise ValueError(f"variable {v.name} is not a parameter of this model")
             cache = self._grad_map = (variables, rows, [v._param for v in variables])
-        _, rows, params = cache
+        return cache
+
+    def theta_layout(self, variables):
+        """(cols int32 [P], lower float64 [P]): θ-row index and Shift of each variable, for the
+        batched driver's native θ / chain-rule helpers (gpx_host_theta_rows / _loss_grad_u)."""
+        _, rows, params = self._variable_map(variables)
+        return (np.asarray(rows, dtype=np.int32), np.asarray([p.lower for p in params], dtype=np.float64))
+
+    def loss_and_grad_unconstrained(self, variables=None, lml=None, grad_theta=None):
+        """(−logML, ∂(−logML)/∂u) for ``variables`` (default: trainable_variables)."""
+        if lml is None:
+            lml, grad_theta = self._lml_and_grad_theta()
+        variables = self.trainable_variables if variables is None else variables
+        _, rows, params = self._variable_map(variables)
         g = np.empty(len(rows), dtype=np.float64)
         for k, (r, p) in enumerate(zip(rows, params)):
             g[k] = -grad_theta[r] * p.dtheta_du()

@@ -595,6 +595,7 @@ class _SteppedDriver:
         self.trace = [] if os.environ.get("GPX_TRACE_ROUNDS") else None
         self.first_call = threading.Event()
         self.first_call_s = 0.0
+        self._theta = {}  # id(engine) -> [B, 16] θ rows (one array per engine, slots disjoint)
 
     def _next(self) -> Optional[int]:
         with self.qlock:
@@ -641,7 +642,17 @@ class _SteppedDriver:
         variables = m.trainable_variables
         if not variables:
             raise ValueError("model has no trainable variables")
-        return {"i": i, "m": m, "v": variables, "st": lbfgsb.LbfgsbStepper(_pack(variables), self.options)}
+        cols, lower = m.theta_layout(variables)
+        # the slot's θ row: fixed parameters now, the trainable columns rewritten every round
+        self._theta_of(eng)[row] = m.theta_row()
+        return {"i": i, "m": m, "v": variables, "st": lbfgsb.LbfgsbStepper(_pack(variables), self.options),
+                "cols": cols, "lower": lower, "key": (len(cols), cols.tobytes(), lower.tobytes())}
+
+    def _theta_of(self, eng) -> np.ndarray:
+        th = self._theta.get(id(eng))
+        if th is None:
+            th = self._theta[id(eng)] = np.ones((eng.B, N.GPX_THETA_STRIDE))
+        return th
 
     def _loop(self, g: int, eng, rows, lock):
         G = len(self.groups)
@@ -654,6 +665,8 @@ class _SteppedDriver:
                         active[r] = self._bind(r, eng, r, lock)
                     except BaseException as e:
                         self.errors[r] = e
+        lib = N.load_library()
+        theta = self._theta_of(eng)
         n_calls = 0
         while True:
             while free:
@@ -676,11 +689,20 @@ class _SteppedDriver:
                 self.first_call.wait(timeout=10.0)
                 time.sleep(self.first_call_s * g / G)
             act = sorted(active)
-            theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+            # θ rows of every requested point in one native call per variable layout (the same
+            # libm softplus as Parameter.value, so the values are those of the per-model path)
+            layouts = {}
             for r in act:
-                s = active[r]
-                _unpack(s["v"], s["st"].x)
-                theta[r] = s["m"].theta_row()
+                layouts.setdefault(active[r]["key"], []).append(r)
+            packs = []
+            for key, rs in layouts.items():
+                s0 = active[rs[0]]
+                P = key[0]
+                U = np.array([active[r]["st"].x for r in rs], dtype=np.float64).reshape(len(rs), P)
+                R = np.asarray(rs, dtype=np.int32)
+                lib.gpx_host_theta_rows(len(rs), P, U.ctypes.data, R.ctypes.data, s0["cols"].ctypes.data,
+                                        s0["lower"].ctypes.data, theta.ctypes.data)
+                packs.append((rs, P, U, R, s0["cols"]))
             if self.trace is not None:
                 self.trace.append((time.perf_counter(), len(act)))
             t_call = time.perf_counter()
@@ -691,30 +713,33 @@ class _SteppedDriver:
                 self.first_call.set()
             n_calls += 1
             done = []
-            for r in act:
-                s = active[r]
-                err = None
-                if info[r] == N.INFO_BAD_THETA:
-                    err = N.InvalidParameterError(
-                        f"model {s['i']}: hyperparameters out of (0, inf): {theta[r, :eng.n_params[r] + 1]}")
-                elif info[r] != 0:
-                    err = N.NotPositiveDefiniteError(
-                        f"Cholesky decomposition was not successful (model {s['i']}, pivot "
-                        f"{int(info[r])}): K + noise I is not positive definite", info[r])
-                try:
-                    if err is not None:
-                        if not self.as_inf:
-                            raise err
-                        loss, gr = float("inf"), np.zeros_like(np.asarray(s["st"].x, dtype=np.float64))
-                    else:
-                        loss, gr = s["m"].loss_and_grad_unconstrained(s["v"], lml=lml[r], grad_theta=grad[r])
-                    s["st"].tell(loss, gr)
-                except BaseException as e:
-                    self.errors[s["i"]] = e
-                    done.append((r, False))
-                    continue
-                if s["st"].done:
-                    done.append((r, True))
+            for rs, P, U, R, cols in packs:
+                loss = np.empty(len(rs))
+                gu = np.empty((len(rs), P))
+                lib.gpx_host_loss_grad_u(len(rs), P, U.ctypes.data, R.ctypes.data, cols.ctypes.data,
+                                         lml.ctypes.data, grad.ctypes.data, loss.ctypes.data, gu.ctypes.data)
+                for k, r in enumerate(rs):
+                    s = active[r]
+                    try:
+                        if info[r] != 0:
+                            if info[r] == N.INFO_BAD_THETA:
+                                err = N.InvalidParameterError(
+                                    f"model {s['i']}: hyperparameters out of (0, inf): {theta[r, :eng.n_params[r] + 1]}")
+                            else:
+                                err = N.NotPositiveDefiniteError(
+                                    f"Cholesky decomposition was not successful (model {s['i']}, pivot "
+                                    f"{int(info[r])}): K + noise I is not positive definite", info[r])
+                            if not self.as_inf:
+                                raise err
+                            s["st"].tell(float("inf"), np.zeros(P))
+                        else:
+                            s["st"].tell(float(loss[k]), gu[k])
+                    except BaseException as e:
+                        self.errors[s["i"]] = e
+                        done.append((r, False))
+                        continue
+                    if s["st"].done:
+                        done.append((r, True))
             self._finish(eng, lock, active, done)
             for r, _ in done:
                 del active[r]

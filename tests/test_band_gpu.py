@@ -1,0 +1,238 @@
+"""GPU parity of the block-banded evaluation path (csrc/gpx_band.hip) against the oracle and
+against the dense path on the same inputs.
+
+The banded path is taken when K and every ∂K/∂θ are exactly zero in fp64 beyond a band of
+64-blocks (the kernel's exp underflows): SE / Matern / Exponential with a lengthscale small
+against the spacing of sorted inputs — the C2 bench regime (X = day offsets 0..N-1, GPflow's
+default ℓ = 1; every evaluation of a C2 fit stays at ℓ ∈ [1, 1.72]) and the reference's own
+(GPR/data_handler.py:42-44 leaves day offsets unnormalised). Tolerances as test_gpu_parity.py
+(κ-scaled logML / gradient bars); the dense path of the same build is a second
+reference at full size (N=4096), where the oracle is too slow to call per case.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import portfoliooptgp_amd as gpx  # noqa: E402
+from portfoliooptgp_amd import _native as N  # noqa: E402
+from portfoliooptgp_amd.engine import Engine  # noqa: E402
+from portfoliooptgp_amd.kernels import compile_spec  # noqa: E402
+from oracle import gp_oracle as O  # noqa: E402
+from tests.test_gpu_parity import check_grad, check_loss, check_mean, check_var, gpx_kernel, oracle_kernel  # noqa: E402
+
+K = gpx.kernels
+
+
+class _Env:
+    """Set an environment switch of the library inside the block (read per call)."""
+
+    def __init__(self, key, value):
+        self.key, self.value = key, value
+
+    def __enter__(self):
+        self.prev = os.environ.get(self.key)
+        os.environ[self.key] = self.value
+
+    def __exit__(self, *a):
+        if self.prev is None:
+            os.environ.pop(self.key, None)
+        else:
+            os.environ[self.key] = self.prev
+
+
+def _Dense():
+    """Force the dense path inside the block."""
+    return _Env("GPX_BAND", "0")
+
+
+def _engine(xs, ys, kern):
+    D = xs[0].shape[1]
+    eng = Engine(xs, ys, [compile_spec(kern, D)] * len(xs))
+    eng.ctx.set_profiling(True)
+    return eng
+
+
+def _theta(eng, rows):
+    th = np.ones((eng.B, N.GPX_THETA_STRIDE))
+    for b, r in enumerate(rows):
+        th[b, :len(r)] = r
+    return th
+
+
+def _band_evals(eng):
+    return eng.last_timing().band_evals
+
+
+def _cond(x, kern_o, noise):
+    Kx = kern_o.K(x) + noise * np.eye(len(x))
+    return np.linalg.cond(Kx)
+
+
+@pytest.mark.parametrize("fam,ell", [("se", 1.0), ("se", 1.1795), ("se", 1.7146), ("se", 3.0), ("se", 4.5),
+                                     ("m12", 0.02), ("m32", 0.05), ("m52", 0.06), ("exp", 0.01),
+                                     ("se+m12", 0.05), ("se*m12", 0.9)])
+def test_band_against_oracle_n1024(fam, ell):
+    """logML and ∂loss/∂u through the banded path vs the oracle (N=1024, C2 data)."""
+    x, y = O.synthetic_series(1024, seed=3)
+    m = gpx.models.GPR((x, y), kernel=gpx_kernel(fam), noise_variance=1e-5)
+    ko = oracle_kernel(fam)
+    vals = []
+    for p, po in zip(m.kernel.parameters, ko.params()):
+        v = ell if "lengthscale" in p.name else 0.8
+        p.assign(v)
+        po.value = v
+        vals.append(v)
+    om = O.OGPR(x, y, ko, noise_variance=1e-5)
+    N.Context.get(0).set_profiling(True)
+    from portfoliooptgp_amd.engine import solo_engine
+    eng = solo_engine(m)
+    eng.reset_timing()
+    loss, g = m.loss_and_grad_unconstrained()
+    assert eng.last_timing().band_evals == 1, "expected the banded path"
+    lo, go = om.loss_and_grad_u()
+    cond = _cond(x, ko, 1e-5)
+    check_loss(loss, lo, cond)
+    check_grad(g, go, cond)
+    # predict at the training inputs from the banded factor (diag of K⁻¹ from the selected
+    # inverse) and at new inputs (re-factorised densely)
+    mu, var = m.predict_f(x)
+    mo, vo = om.predict_f(x)
+    check_mean(mu.numpy(), mo, cond, float(np.abs(y).max()))
+    check_var(var.numpy(), vo, 1.0)
+    xs = np.linspace(-3.5, 1030.5, 37)[:, None]
+    mu2, var2 = m.predict_f(xs)
+    mo2, vo2 = om.predict_f(xs)
+    check_mean(mu2.numpy(), mo2, cond, float(np.abs(y).max()))
+    check_var(var2.numpy(), vo2, 1.0)
+
+
+def test_band_equals_dense_n4096_and_composition():
+    """Full size (C2, N=4096): banded vs dense on the same batch across the C2 lengthscale range
+    (p = 1..3 blocks) and a ragged member; a problem's banded result does not depend on the
+    batch's widest band (the extra blocks are exact zeros)."""
+    n = 4096
+    data = [O.synthetic_series(n, seed=s) for s in range(4)]
+    xs = [d[0] for d in data]
+    ys = [d[1] for d in data]
+    xs[3], ys[3] = xs[3][:3001], ys[3][:3001]
+    eng = _engine(xs, ys, K.SquaredExponential())
+    rows = [(1.0, 1.0, 1e-5), (1.7146, 0.8649, 1e-5), (2.6, 0.6, 1e-5), (1.1795, 0.5632, 1e-5)]
+    th = _theta(eng, rows)
+    eng.reset_timing()
+    lb, gb, ib = eng.lml_grad([0, 1, 2, 3], th)
+    assert not ib.any() and _band_evals(eng) == 4
+    with _Dense():
+        eng.reset_timing()
+        ld, gd, idn = eng.lml_grad([0, 1, 2, 3], th)
+        assert not idn.any() and _band_evals(eng) == 0
+    for b in range(4):
+        assert abs(lb[b] - ld[b]) <= 1e-9 * abs(ld[b]), (b, lb[b], ld[b])
+        tol = 1e-7 * (1.0 + np.abs(gd[b, :3]).max())
+        assert np.all(np.abs(gb[b, :3] - gd[b, :3]) <= tol), (b, gb[b, :3], gd[b, :3])
+    # the fused per-problem kernels (p <= 2) against the per-block launches of the same algorithm
+    with _Env("GPX_BAND_FUSED", "0"):
+        eng.reset_timing()
+        lu, gu, _ = eng.lml_grad([0, 1, 2, 3], th)
+        assert _band_evals(eng) == 4
+    for b in range(4):
+        assert abs(lb[b] - lu[b]) <= 1e-9 * abs(lu[b])
+        assert np.all(np.abs(gb[b, :3] - gu[b, :3]) <= 1e-7 * (1.0 + np.abs(gu[b, :3]).max()))
+    # composition: problem 0 (p = 1) alone, then with problem 2 (p = 2) in the same call
+    l0, g0, _ = eng.lml_grad([0], th)
+    l02, g02, _ = eng.lml_grad([0, 2], th)
+    assert l0[0] == l02[0] and np.array_equal(g0[0, :3], g02[0, :3])
+    assert l0[0] == lb[0] and np.array_equal(g0[0, :3], gb[0, :3])
+
+
+def test_band_mixed_with_dense_in_one_call():
+    """One call routes some problems to the banded path and others (large ℓ, unsorted inputs,
+    Periodic) to the dense one; every problem matches its dense-only evaluation."""
+    n = 1536
+    x, y = O.synthetic_series(n, seed=9)
+    perm = np.random.default_rng(1).permutation(n)
+    xs = [x, x, x[perm]]
+    ys = [y, y, y[perm]]
+    eng = _engine(xs, ys, K.SquaredExponential())
+    th = _theta(eng, [(1.3, 0.9, 1e-5), (40.0, 0.9, 1e-5), (1.3, 0.9, 1e-5)])
+    eng.reset_timing()
+    lb, gb, _ = eng.lml_grad([0, 1, 2], th)
+    assert _band_evals(eng) == 1          # only the sorted small-ℓ problem
+    with _Dense():
+        ld, gd, _ = eng.lml_grad([0, 1, 2], th)
+    for b in range(3):
+        assert abs(lb[b] - ld[b]) <= 1e-9 * abs(ld[b])
+        assert np.all(np.abs(gb[b, :3] - gd[b, :3]) <= 1e-7 * (1.0 + np.abs(gd[b, :3]).max()))
+    # the permuted problem is the same GP: same logML as the sorted one
+    assert lb[2] == pytest.approx(lb[0], rel=1e-9)
+    # Periodic never takes the banded path
+    engp = _engine([x], [y], K.Periodic(K.SquaredExponential()))
+    engp.reset_timing()
+    engp.lml_grad([0], _theta(engp, [(1.0, 1.0, 3.0, 1e-2)]))
+    assert _band_evals(engp) == 0
+
+
+def test_band_two_dimensional_inputs():
+    """D = 2 (time + a feature column), Matern32 over both dims: block boxes bound the distance
+    in the term's active dims."""
+    n = 1024
+    rng = np.random.default_rng(5)
+    t = np.arange(n, dtype=np.float64)
+    f = np.cumsum(rng.standard_normal(n)) * 0.01
+    x = np.stack([t, f], 1)
+    y = rng.standard_normal((n, 1))
+    m = gpx.models.GPR((x, y), kernel=K.Matern32(lengthscales=0.05, variance=1.1), noise_variance=1e-4)
+    om = O.OGPR(x, y, O.OMatern32(lengthscales=0.05, variance=1.1), noise_variance=1e-4)
+    N.Context.get(0).set_profiling(True)
+    from portfoliooptgp_amd.engine import solo_engine
+    eng = solo_engine(m)
+    eng.reset_timing()
+    loss, g = m.loss_and_grad_unconstrained()
+    assert eng.last_timing().band_evals == 1
+    lo, go = om.loss_and_grad_u()
+    cond = _cond(x, O.OMatern32(lengthscales=0.05, variance=1.1), 1e-4)
+    check_loss(loss, lo, cond)
+    check_grad(g, go, cond)
+
+
+def test_band_not_positive_definite_reports_pivot():
+    """A NaN input row makes pivot 701 fail: the banded path reports NOT_PD with the same
+    LAPACK-style pivot as the dense one (and NaN outputs for that problem)."""
+    n = 1024
+    x = np.arange(n, dtype=np.float64)[:, None]
+    x[700] = np.nan
+    y = np.random.default_rng(2).standard_normal((n, 1))
+    eng = _engine([x], [y], K.SquaredExponential())
+    th = _theta(eng, [(1.0, 1.0, 1e-5)])
+    eng.reset_timing()
+    lml, grad, info = eng.lml_grad([0], th)
+    assert _band_evals(eng) == 1
+    assert info[0] == 701 and np.isnan(lml[0])
+    with _Dense():
+        _, _, info_d = eng.lml_grad([0], th)
+    assert info_d[0] == 701
+
+
+def test_band_fits_match_dense_fits():
+    """End to end (C2 protocol at N=2048): streamed fits through the banded path reach the same
+    optimum as dense fits (|Δloss*| <= 1e-5 rel) and the same predictions."""
+    data = [O.synthetic_series(2048, seed=s) for s in range(3)]
+
+    def make(x, y):
+        mm = gpx.models.GPR((x, y), kernel=K.SquaredExponential())
+        mm.likelihood.variance.assign(1e-5)
+        gpx.set_trainable(mm.likelihood.variance, False)
+        return mm
+
+    res_b, pred_b = gpx.optimizers.Scipy().minimize_stream([make(x, y) for x, y in data], width=3,
+                                                           predict_train=True, options=dict(maxiter=100))
+    with _Dense():
+        res_d, pred_d = gpx.optimizers.Scipy().minimize_stream([make(x, y) for x, y in data], width=3,
+                                                               predict_train=True, options=dict(maxiter=100))
+    for rb, rd, (mb, vb), (md, vd) in zip(res_b, res_d, pred_b, pred_d):
+        assert rb.fun == pytest.approx(rd.fun, rel=1e-5)
+        np.testing.assert_allclose(mb.cpu().numpy(), md.cpu().numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(vb.cpu().numpy(), vd.cpu().numpy(), rtol=1e-4, atol=1e-9)

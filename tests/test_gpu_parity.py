@@ -586,3 +586,39 @@ def test_pooled_solo_engines_interleaved_models():
     ob = O.OGPR(xb, yb, O.OMatern32(lengthscales=4.0), noise_variance=1e-2)
     assert lb1 == pytest.approx(ob.loss_and_grad_u()[0], rel=1e-10)
     check_mean(mb1.numpy(), ob.predict_f(xb)[0])
+
+
+def test_shared_context_two_threads_with_split_pipelines():
+    """Two device batches of one context driven from two host threads, each batch splitting its
+    evaluations into two concurrent pipelines (GPX_GROUPS=2: per-batch worker streams and
+    fork/join events). Every fit equals its solo fit: nothing per-evaluation is shared through
+    the context (the fork/join events and the error slot used to be)."""
+    data = [O.synthetic_series(300 + 41 * i, seed=90 + i) for i in range(6)]
+
+    def make(x, y):
+        m = gpx.models.GPR((x, y), kernel=K.SquaredExponential(lengthscales=20.0))
+        m.likelihood.variance.assign(1e-4)
+        gpx.set_trainable(m.likelihood.variance, False)
+        return m
+
+    solo = []
+    for x, y in data:
+        m = make(x, y)
+        solo.append(gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables,
+                                                    options=dict(maxiter=100)))
+    prev = {k: os.environ.get(k) for k in ("GPX_GROUPS", "GPX_BAND")}
+    os.environ["GPX_GROUPS"] = "2"
+    os.environ["GPX_BAND"] = "0"
+    try:
+        res, _ = gpx.optimizers.Scipy().minimize_stream([make(x, y) for x, y in data], width=6, groups=2,
+                                                        options=dict(maxiter=100))
+    finally:
+        for k, v in prev.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    for r0, r1 in zip(solo, res):
+        assert r0.nfev == r1.nfev
+        assert r1.fun == pytest.approx(r0.fun, rel=1e-9)
+        np.testing.assert_allclose(r1.x, r0.x, rtol=1e-7)
