@@ -267,7 +267,8 @@ def main():
         pass
     tm = _Tm()
     for f in ("contract_ms_total", "contract_launches", "contract_alg_flops", "eval_ms_total", "evals",
-              "band_ms_total", "band_calls", "band_evals", "band_p_sum"):
+              "band_ms_total", "band_calls", "band_evals", "band_p_sum", "band_fwd_ms_total",
+              "band_bwd_ms_total", "band_fused_launches", "band_fwd_flops", "band_bwd_flops"):
         setattr(tm, f, sum(getattr(t, f) for t in tms))
     if world > 1:
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
@@ -301,7 +302,54 @@ def main():
     contract_flops = tm.contract_alg_flops / max(tm.contract_launches, 1.0)
     achieved = contract_flops / (contract_ms * 1e-3) / 1e12 if contract_ms > 0 else 0.0
     traffic, traffic_src = contract_traffic(n, contract_flops)
-    eval_alg = (n ** 3 + 2 * 3 * n ** 2) * evals_all  # SURVEY §8d F_eval(N), P=2, all ranks
+    eval_alg = (n ** 3 + 2 * 3 * n ** 2) * evals_all  # SURVEY §8d F_eval(N), P=2, all ranks (dense count)
+    # the kernel with the most device time in the timed region: the fused banded sweep kernels
+    # when the fits' evaluations take the banded path (C2: every evaluation), else the dense
+    # fused K⁻¹ + gradient contraction
+    band_kernels = {
+        "band_fwd_kernel (banded Cholesky + z solve, one workgroup per problem)":
+            (tm.band_fwd_ms_total, tm.band_fwd_flops),
+        "band_bwd_kernel<1> (selected inversion + alpha solve + gradient contraction)":
+            (tm.band_bwd_ms_total, tm.band_bwd_flops),
+    }
+    kname, (kms, kflops) = max(band_kernels.items(), key=lambda kv: kv[1][0])
+    if kms > tm.contract_ms_total:
+        launches = tm.band_fused_launches
+        b_ms = kms / max(launches, 1.0)
+        b_flops = kflops / max(launches, 1.0)
+        b_ach = b_flops / (b_ms * 1e-3) / 1e12 if b_ms > 0 else 0.0
+        roofline = {
+            "kernel": kname, "bound": "mfma", "achieved": b_ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": b_ach / FP64_PEAK_TFLOPS, "traffic": None, "traffic_unit": "bytes/launch",
+            "avg_launch_ms": b_ms, "launches": launches, "alg_flops_per_launch": b_flops,
+            "note": ("banded path: each launch walks its problems' 64 block steps in sequence, one "
+                     "workgroup (one CU) per problem; achieved = the 64^3 block products issued "
+                     "(2*64^3 flops each, leaf 2/3 of one) / launch duration. The chain of "
+                     "dependent block steps, not MFMA or HBM throughput, sets the duration "
+                     "(DESIGN.md §3c); traffic: profiles/<round>_band_traffic.json"),
+            "dense_contraction_isolated": iso, "dense_contraction_frac_isolated": iso / FP64_PEAK_TFLOPS if iso else None,
+        }
+    else:
+        roofline = {
+            "kernel": "gemm_kernel<128,T,N,EPI_CONTRACT1> (K^-1 = W^T W fused with the gradient contraction)",
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS,
+            "traffic": traffic,
+            "traffic_unit": "bytes/launch",
+            "traffic_source": traffic_src,
+            "avg_launch_ms": contract_ms,
+            "launches": tm.contract_launches,
+            "alg_flops_per_launch": contract_flops,
+            "note": (f"timed region runs {G} device batches concurrently on separate streams, so the "
+                     "kernel's launches share the GPU with the other batch's kernels; "
+                     "achieved_isolated = the same kernel alone (one full batch, after the timed region)"
+                     if G > 1 else "one device batch"),
+            "achieved_isolated": iso,
+            "frac_isolated": iso / FP64_PEAK_TFLOPS if iso else None,
+        }
     out = {
         "metric": "GP fits/sec (N=4096, 1-D RBF)",
         "value": value,
@@ -326,32 +374,10 @@ def main():
                       "ms_per_call": tm.band_ms_total / max(tm.band_calls, 1.0),
                       "problems_per_call": tm.band_evals / max(tm.band_calls, 1.0)},
         "evals_per_s": evals_all / elapsed,
-        # whole-job algorithmic rate: F_eval(N) x evaluations / wall time of the timed steps
-        "eval_alg_tflops": eval_alg / elapsed / 1e12,
-        "roofline": {
-            "kernel": "gemm_kernel<128,T,N,EPI_CONTRACT1> (K^-1 = W^T W fused with the gradient contraction)",
-            "bound": "mfma",
-            "achieved": achieved,
-            "peak": FP64_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved / FP64_PEAK_TFLOPS,
-            "traffic": traffic,
-            "traffic_unit": "bytes/launch",
-            "traffic_source": traffic_src,
-            "avg_launch_ms": contract_ms,
-            "launches": tm.contract_launches,
-            "alg_flops_per_launch": contract_flops,
-            "note": (f"timed region runs {G} device batches concurrently on separate streams, so the "
-                     "kernel's launches share the GPU with the other batch's kernels; "
-                     "achieved_isolated = the same kernel alone (one full batch, after the timed region)"
-                     if G > 1 else "one device batch"),
-            "achieved_isolated": iso,
-            "frac_isolated": iso / FP64_PEAK_TFLOPS if iso else None,
-            # the whole path: F_eval(N) x evaluations / wall time of the timed steps
-            # per GPU: the whole-job algorithmic rate over all ranks ÷ the number of GPUs
-            "achieved_job": eval_alg / elapsed / 1e12 / world,
-            "frac_job": eval_alg / elapsed / 1e12 / world / FP64_PEAK_TFLOPS,
-        },
+        # the dense algorithm's count F_eval(N) x evaluations / wall time: what the same job
+        # would have to sustain on the dense path (the banded path does far fewer flops)
+        "eval_dense_equiv_tflops": eval_alg / elapsed / 1e12,
+        "roofline": roofline,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, nfev_mean)

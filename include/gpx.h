@@ -20,6 +20,9 @@
  * band of 64-blocks (SE / Matern / Exponential with a lengthscale small against the spacing of
  * sorted inputs, e.g. GPflow's default ℓ = 1 on the reference's integer day offsets) — a
  * block-banded Cholesky, banded solves and selected inversion of K⁻¹ on the band, O(N·bw²).
+ * Every banded evaluation checks itself: max_j |Σ_i K_ji Z_ij − 1| over the band (Z the selected
+ * inverse) must be <= GPX_BAND_TOL (default 1e-6), else that problem is re-evaluated densely in
+ * the same call (selected inversion loses accuracy for very smooth kernels with wide bands).
  * GPX_BAND=0 in the environment forces the dense path.
  *
  * Conventions
@@ -184,6 +187,15 @@ typedef struct {
   double band_calls;
   double band_evals;
   double band_p_sum;
+  /* fused banded kernels (p <= 2), each launch timestamped at its actual start and end:
+   * summed durations, launches, and block-product flops issued (2·64³ per 64³ product, the
+   * leaf counted as 2/3 of one) */
+  double band_fwd_ms_total;
+  double band_bwd_ms_total;
+  double band_fused_launches;
+  double band_fwd_flops;
+  double band_bwd_flops;
+  double band_fallbacks;      /* banded evaluations whose check failed, redone densely */
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);

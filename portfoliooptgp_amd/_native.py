@@ -54,7 +54,10 @@ class GpxTiming(ctypes.Structure):
                 ("contract_alg_flops", ctypes.c_double), ("eval_ms_total", ctypes.c_double),
                 ("evals", ctypes.c_double), ("band_ms_total", ctypes.c_double),
                 ("band_calls", ctypes.c_double), ("band_evals", ctypes.c_double),
-                ("band_p_sum", ctypes.c_double)]
+                ("band_p_sum", ctypes.c_double), ("band_fwd_ms_total", ctypes.c_double),
+                ("band_bwd_ms_total", ctypes.c_double), ("band_fused_launches", ctypes.c_double),
+                ("band_fwd_flops", ctypes.c_double), ("band_bwd_flops", ctypes.c_double),
+                ("band_fallbacks", ctypes.c_double)]
 
 
 class GPXError(RuntimeError):

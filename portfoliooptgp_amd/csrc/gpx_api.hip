@@ -276,7 +276,7 @@ int band_limit(const gpx_batch* bt) {
   const char* ep = getenv("GPX_BAND_PMAX");
   const int mode = em ? atoi(em) : 1;
   const int pmax_env = ep ? atoi(ep) : -1;
-  if (mode == 0 || !band_shape(bt)) return -1;
+  if (mode == 0 || bt->force_dense || !band_shape(bt)) return -1;
   return pmax_env >= 0 ? pmax_env : bt->Np / kLeaf / 4;
 }
 
@@ -340,7 +340,12 @@ void band_eval(const Run& r, int p, int max_terms) {
   ca.X = bt->X; ca.sX = (long long)bt->Nmax * bt->D; ca.D = bt->D; ca.specs = bt->d_specs;
   ca.theta = bt->d_theta; ca.nvalid = bt->d_n; ca.partial = bt->partial; ca.sPartial = bt->partial_stride;
   ca.Np = Np; ca.p = p;
+  // column sums of K∘Z for the band check (the batch-wide buffer is grown on first use;
+  // gpx_batch_lml_grad checked the allocation before launching anything)
+  (void)hipMemsetAsync(bt->bres, 0, sizeof(double) * (size_t)bt->B * Np, r.s);
+  ca.colsum = bt->bres; ca.sCol = Np;
   launch_band_contract(ca, max_terms, r.na, r.s);
+  launch_band_check(r.d_act, bt->bres, Np, bt->d_n, bt->results, r.na, Np, r.s);
   ReduceArgs ra{};
   ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
   ra.ntiles = (p + 1) * nb; ra.z = bt->z; ra.sVec = Np; ra.ldiag = bt->ldiag;
@@ -350,7 +355,19 @@ void band_eval(const Run& r, int p, int max_terms) {
 
 // Band width <= 2 blocks: the whole sweep per problem in two fused kernels (gpx_band.hip),
 // each problem with its own p (d_bandp); K's band is built for the widest.
-void band_fused_eval(const Run& r, int p, int max_terms) {
+double band_fused_flops(int Np, int p, bool fwd) {
+  const double U = 2.0 * kLeaf * kLeaf * kLeaf;  // one 64³ block product
+  const int nb = Np / kLeaf;
+  double f = 0.0;
+  for (int k = 0; k < nb; ++k) {
+    const double q = std::min(p, nb - 1 - k);
+    f += fwd ? (2.0 / 3.0 + q + q * (q + 1) / 2.0) * U   // leaf, panels, window update
+             : (1.0 + q + q * q + q) * U;               // WᵀW, G, Z panel, Gᵀ Z
+  }
+  return f;
+}
+
+void band_fused_eval(const Run& r, int p, int max_terms, hipEvent_t* ev) {
   gpx_batch* bt = r.bt;
   const int Np = bt->Np;
   const long long st = mat_stride(bt);
@@ -365,8 +382,8 @@ void band_fused_eval(const Run& r, int p, int max_terms) {
   fa.Y = bt->Y; fa.sY = bt->Nmax; fa.nvalid = bt->d_n; fa.z = bt->z; fa.alpha = bt->alpha;
   fa.ldiag = bt->ldiag; fa.sVec = Np; fa.X = bt->X; fa.sX = (long long)bt->Nmax * bt->D; fa.D = bt->D;
   fa.specs = bt->d_specs; fa.theta = bt->d_theta; fa.partial = bt->partial; fa.sPartial = bt->partial_stride;
-  fa.info = bt->d_info; fa.Np = Np;
-  launch_band_fused(fa, max_terms, r.na, r.s);
+  fa.info = bt->d_info; fa.results = bt->results; fa.Np = Np;
+  launch_band_fused(fa, max_terms, r.na, r.s, ev);
   ReduceArgs ra{};
   ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
   ra.ntiles = 1; ra.z = bt->z; ra.sVec = Np; ra.ldiag = bt->ldiag;
@@ -561,7 +578,8 @@ int gpx_batch_destroy(gpx_batch* bt) {
   (void)hipSetDevice(bt->ctx->device);
   for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
                   (void*)bt->ldiag, (void*)bt->partial, (void*)bt->d_io, (void*)bt->d_n,
-                  (void*)bt->d_specs, (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw})
+                  (void*)bt->d_specs, (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw,
+                  (void*)bt->bres})
     if (p) (void)hipFree(p);
   if (bt->h_io) (void)hipHostFree(bt->h_io);
   for (int g = 0; g < kAux; ++g)
@@ -649,6 +667,10 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   const int n_dense = (int)order.size(), n_band = (int)band_ids.size(), n_fused = (int)fused_ids.size();
   order.insert(order.end(), band_ids.begin(), band_ids.end());
   order.insert(order.end(), fused_ids.begin(), fused_ids.end());
+  if (n_band > 0) {
+    const int e = ensure(ctx, bt->bres, bt->bres_cap, (size_t)bt->B * bt->Np);
+    if (e != GPX_OK) return e;
+  }
   int rc = upload_common(bt, n_active, order.data(), theta, s);
   if (rc != GPX_OK) return rc;
   rc = match_aux_priority(bt, s);
@@ -756,10 +778,20 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     for (int i = n_dense; i < n_dense + n_band; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
     band_eval(Run{bt, bt->d_active + n_dense, n_band, s}, pband, max_terms);
   }
+  struct EvQuad {
+    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+    ~EvQuad() {
+      for (auto x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } fq;
   if (n_fused > 0) {
     int max_terms = 1;
     for (int i = n_dense + n_band; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
-    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, pfused, max_terms);
+    if (ctx->profiling)
+      for (auto& x : fq.e) HIPX(ctx, hipEventCreate(&x));
+    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, pfused, max_terms,
+                    ctx->profiling ? fq.e : nullptr);
   }
   bp.mark();
   total.mark();
@@ -790,6 +822,19 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
       bt->timing.band_evals += n_band + n_fused;
       for (int i = n_dense; i < n_active; ++i) bt->timing.band_p_sum += bt->h_bandp[order[i]];
     }
+    if (n_fused > 0) {
+      float f0 = 0.f, f1 = 0.f;
+      (void)hipEventElapsedTime(&f0, fq.e[0], fq.e[1]);
+      (void)hipEventElapsedTime(&f1, fq.e[2], fq.e[3]);
+      bt->timing.band_fwd_ms_total += f0;
+      bt->timing.band_bwd_ms_total += f1;
+      bt->timing.band_fused_launches += 1.0;
+      for (int i = n_dense + n_band; i < n_active; ++i) {
+        const int pb = bt->h_bandp[order[i]];
+        bt->timing.band_fwd_flops += band_fused_flops(bt->Np, pb, true);
+        bt->timing.band_bwd_flops += band_fused_flops(bt->Np, pb, false);
+      }
+    }
     bt->timing.predict_ms = 0.0;
     bt->timing.total_ms = total.ms(0, 1);
     bt->timing.gemm_flops = bt->flops_acc;
@@ -797,11 +842,19 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     bt->timing.evals += n_active;
   }
   int status = GPX_OK;
+  // banded evaluations whose check failed are redone on the dense path below
+  const char* et = getenv("GPX_BAND_TOL");
+  const double band_tol = et ? atof(et) : 1e-6;
+  std::vector<int32_t> redo;
   for (int i = 0; i < n_active; ++i) {
     const int b = order[i];
     const double* res = bt->h_results + (size_t)b * kResStride;
     info[b] = bt->h_info[b];
     const int np = bt->specs[b].n_params;
+    if (i >= n_dense && info[b] == 0 && !(res[kResBandCheck] <= band_tol)) {
+      redo.push_back(b);
+      continue;
+    }
     if (info[b] != 0) {
       status = GPX_NOT_PD;
       lml[b] = NAN;
@@ -817,6 +870,14 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     bt->fac_band[b] = i >= n_dense;
   }
   if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
+  if (!redo.empty()) {
+    if (total.on) bt->timing.band_fallbacks += (double)redo.size();
+    bt->force_dense = 1;
+    const int rc2 = gpx_batch_lml_grad(bt, (int)redo.size(), redo.data(), theta, lml, grad, info, stream);
+    bt->force_dense = 0;
+    if (rc2 != GPX_OK && rc2 != GPX_NOT_PD) return rc2;
+    if (rc2 == GPX_NOT_PD) status = GPX_NOT_PD;
+  }
   return status;
 }
 

@@ -18,6 +18,7 @@
 //   band_contract_kernel   ½Σ w(α_iα_j − Z_ij)∂K_ij/∂θ over the band's lower blocks
 //   band_train_pred_kernel predict at the training inputs from α and diag(Z)
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include "gpx_internal.h"
 #include "gpx_leaf.h"
 
@@ -159,8 +160,10 @@ __global__ __launch_bounds__(256) void band_contract_kernel(BandContractArgs a) 
       const int i = i0 + il;
       if (i >= n || (d == 0 && il < jl)) continue;
       const double w = (d == 0 && il == jl) ? 1.0 : 2.0;
-      const double v = w * fma(sai[il], aj, -Z[(long long)i * a.ld + j]);
+      const double zij = Z[(long long)i * a.ld + j];
+      const double v = w * fma(sai[il], aj, -zij);
       double dk[NT][3];
+      double kij;
       if (fast) {
         double d2 = 0.0;
         for (int q = 0; q < fdn; ++q) {
@@ -168,9 +171,15 @@ __global__ __launch_bounds__(256) void band_contract_kernel(BandContractArgs a) 
           d2 = fma(diff, diff, d2);
         }
         stationary_grad(fkind, d2 * finv_l2, fvar, finv_ell, dk[0]);
+        kij = fvar * dk[0][1];
       } else {
-        eval_k_grad<NT>(spec, sth, sxi + il * D, sxj + jl * D, dk);
+        kij = eval_k_grad<NT>(spec, sth, sxi + il * D, sxj + jl * D, dk);
       }
+      // band check: Σ_i K_ji Z_ij for column j (and, by symmetry, column i)
+      if (i == j) kij += sth[spec.n_params];
+      const double kz = kij * zij;
+      atomicAdd(a.colsum + (long long)b * a.sCol + j, kz);
+      if (i != j) atomicAdd(a.colsum + (long long)b * a.sCol + i, kz);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         sums[t][0] = fma(v, dk[t][0], sums[t][0]);
@@ -207,6 +216,29 @@ __global__ __launch_bounds__(256) void band_contract_kernel(BandContractArgs a) 
     if (slot >= 0) s = (sred[0][slot] + sred[1][slot]) + (sred[2][slot] + sred[3][slot]);
     out[tid] = s;
   }
+}
+
+__global__ __launch_bounds__(256) void band_check_kernel(const int* active, const double* colsum, long long sCol,
+                                                        const int* nvalid, double* results) {
+  __shared__ double sm[4];
+  const int b = active[blockIdx.x];
+  const int n = nvalid[b], tid = threadIdx.x;
+  double m = 0.0;
+  for (int j = tid; j < n; j += 256) {
+    const double r = fabs(colsum[(long long)b * sCol + j] - 1.0);
+    m = (r == r) ? fmax(m, r) : INFINITY;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+  if ((tid & 63) == 0) sm[tid >> 6] = m;
+  __syncthreads();
+  if (tid == 0) results[(long long)b * kResStride + kResBandCheck] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
+}
+
+void launch_band_check(const int* active, const double* colsum, long long sCol, const int* nvalid,
+                       double* results, int n_active, int Np, hipStream_t s) {
+  (void)Np;
+  hipLaunchKernelGGL(band_check_kernel, dim3(n_active), dim3(256), 0, s, active, colsum, sCol, nvalid, results);
 }
 
 void launch_band_contract(const BandContractArgs& a, int max_terms, int n_active, hipStream_t s) {
@@ -477,6 +509,7 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
   __shared__ double spart[2][4][64];
   __shared__ double sth[GPX_THETA_STRIDE];
   __shared__ double sred[4][16];
+  __shared__ double sres[3][64];      // Σ_i K_ji Z_ij for the columns of blocks k, k+1, k+2
   const int b = a.active[blockIdx.x];
   const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
   const long long ld = Np;
@@ -488,10 +521,12 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
   const double* X = a.X + (long long)b * a.sX;
   const int n = a.nvalid[b], D = a.D;
   const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
-  if (tid < 64) { sal[1][tid] = 0.0; sal[2][tid] = 0.0; }
+  if (tid < 64) { sal[1][tid] = 0.0; sal[2][tid] = 0.0; sres[0][tid] = sres[1][tid] = sres[2][tid] = 0.0; }
   if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
   __syncthreads();
   const DevSpec spec = a.specs[b];
+  const double noise = sth[spec.n_params];
+  double resmax = 0.0;  // max |Σ_i K_ji Z_ij − 1| over the completed columns (this thread's share)
   const int fkind = spec.terms[0].kind;
   const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
   const int fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
@@ -502,7 +537,9 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
   for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
   double snoise = 0.0;
   // w (α_i α_j − Z_ij) ∂K_ij/∂θ for the elements of one Z block held in a fragment
-  auto contract = [&](const Frag& f, int i0, int j0, const double* ai, const double* aj, bool diag) {
+  // ... and the products K_ij Z_ij into the column sums of the band check (column j, and by
+  // symmetry column i): srow = the rolling slot of the row block
+  auto contract = [&](const Frag& f, int i0, int j0, const double* ai, const double* aj, bool diag, int srow) {
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -517,6 +554,7 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
             const double* xi = X + (long long)i * D;
             const double* xj = X + (long long)j * D;
             double dk[NT][3];
+            double kij;
             if (fast) {
               double d2 = 0.0;
               for (int q = 0; q < fdn; ++q) {
@@ -524,9 +562,14 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
                 d2 = fma(diff, diff, d2);
               }
               stationary_grad(fkind, d2 * finv_l2, fvar, finv_ell, dk[0]);
+              kij = fvar * dk[0][1];  // ∂K/∂σ² = K/σ² for a single stationary term
             } else {
-              eval_k_grad<NT>(spec, sth, xi, xj, dk);
+              kij = eval_k_grad<NT>(spec, sth, xi, xj, dk);
             }
+            if (i == j) kij += noise;
+            const double kz = kij * f.c[m][nn][r];
+            atomicAdd(&sres[0][jl], kz);
+            if (i != j) atomicAdd(&sres[srow][il], kz);
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
               sums[t][0] = fma(v, dk[t][0], sums[t][0]);
@@ -622,14 +665,36 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
     }
     frag_store_global(zk, K + (long long)k64 * ld + k64, ld);
     // gradient contraction of the three new blocks (band blocks (k,k), (k+1,k), (k+2,k))
-    contract(zk, k64, k64, sal[0], sal[0], true);
-    if (q >= 1) contract(z1, k64 + 64, k64, sal[1], sal[0], false);
-    if (q >= 2) contract(z2, k64 + 128, k64, sal[2], sal[0], false);
+    contract(zk, k64, k64, sal[0], sal[0], true, 0);
+    if (q >= 1) contract(z1, k64 + 64, k64, sal[1], sal[0], false, 1);
+    if (q >= 2) contract(z2, k64 + 128, k64, sal[2], sal[0], false, 2);
     __syncthreads();
+    // block k + p has all its band contributions now (later steps touch blocks < k + p only)
     if (tid < 64) {
+      const int cb = k + p;
+      if (cb < nb && cb * 64 + tid < n) resmax = fmax(resmax, fabs(sres[p][tid] - 1.0));
       sal[2][tid] = sal[1][tid];
       sal[1][tid] = sal[0][tid];
+      sres[2][tid] = sres[1][tid];
+      sres[1][tid] = sres[0][tid];
+      sres[0][tid] = 0.0;
     }
+    __syncthreads();
+  }
+  // blocks 0 .. p−1 complete at the end (rolled into slots 1 .. p)
+  if (tid < 64)
+    for (int cb = 0; cb < p && cb < nb; ++cb)
+      if (cb * 64 + tid < n) resmax = fmax(resmax, fabs(sres[cb + 1][tid] - 1.0));
+  // the band check: max over the workgroup (NaN propagates as a failure)
+  {
+    double rm = (resmax == resmax) ? resmax : INFINITY;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) rm = fmax(rm, __shfl_xor(rm, o, 64));
+    if (lane == 0) sred[part][15] = rm;
+    __syncthreads();
+    if (tid == 0)
+      a.results[(long long)b * kResStride + kResBandCheck] =
+          fmax(fmax(sred[0][15], sred[1][15]), fmax(sred[2][15], sred[3][15]));
     __syncthreads();
   }
   // block reduction of the θ sums into the problem's single partial row
@@ -663,11 +728,17 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
   }
 }
 
-void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s) {
+void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s,
+                       hipEvent_t* ev) {
+  auto bwd = max_terms <= 1 ? band_bwd_kernel<1> : max_terms == 2 ? band_bwd_kernel<2>
+                                                                   : band_bwd_kernel<GPX_MAX_TERMS>;
+  if (ev) {  // timestamped at the kernels' actual start and end (profiling)
+    hipExtLaunchKernelGGL(band_fwd_kernel, dim3(n_active), dim3(256), 0, s, ev[0], ev[1], 0, a);
+    hipExtLaunchKernelGGL(bwd, dim3(n_active), dim3(256), 0, s, ev[2], ev[3], 0, a);
+    return;
+  }
   hipLaunchKernelGGL(band_fwd_kernel, dim3(n_active), dim3(256), 0, s, a);
-  if (max_terms <= 1) hipLaunchKernelGGL(band_bwd_kernel<1>, dim3(n_active), dim3(256), 0, s, a);
-  else if (max_terms == 2) hipLaunchKernelGGL(band_bwd_kernel<2>, dim3(n_active), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(band_bwd_kernel<GPX_MAX_TERMS>, dim3(n_active), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(bwd, dim3(n_active), dim3(256), 0, s, a);
 }
 
 }  // namespace gpx

@@ -51,6 +51,8 @@ struct gpx_batch {
   // a lower bound on the distance between any point of block k and any point of block k − d
   // over the term's active dims, [B][GPX_MAX_TERMS][Np/64]; computed when a problem is bound
   std::vector<double> band_rmin;
+  double* bres = nullptr; size_t bres_cap = 0;  // [B][Np] band-check column sums (per-block path)
+  int force_dense = 0;         // re-evaluation of problems whose band check failed
   // per-call I/O in ONE device block mirrored by ONE pinned host block, laid out
   //   [active: B ints][info: B ints][bandp: B ints][theta: B×16][results: B×kResStride]
   // so an evaluation uploads [active, info=0, theta] in one DMA and downloads [info ..
@@ -150,7 +152,8 @@ int band_width(const gpx_batch* bt, int b, const double* theta_row);  // p in 64
 bool band_shape(const gpx_batch* bt);  // the banded path handles this batch's padded size
 int band_limit(const gpx_batch* bt);  // largest p the banded path takes (-1: path disabled)
 void band_eval(const Run& r, int p, int max_terms);  // build .. reduce for a banded active set
-void band_fused_eval(const Run& r, int p, int max_terms);  // same for p <= 2, two fused kernels
+void band_fused_eval(const Run& r, int p, int max_terms, hipEvent_t* ev = nullptr);  // p <= 2, two fused kernels
+double band_fused_flops(int Np, int p, bool fwd);  // block-product flops of one problem's sweep
 void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W = L⁻¹)
 void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,

@@ -8,7 +8,9 @@
 namespace gpx {
 
 constexpr int kLeaf = 64;      // diagonal-block size of the recursive Cholesky-and-inverse
-constexpr int kResStride = 32; // results row: [0]=lml, [1..16]=grad, [17]=yᵀK⁻¹y, [18]=Σlog L_ii
+constexpr int kResStride = 32; // results row: [0]=lml, [1..16]=grad, [17]=yᵀK⁻¹y, [18]=Σlog L_ii,
+                               // [19]=banded path check: max_j |Σ_i K_ji Z_ij − 1| (Z = K⁻¹ on the band)
+constexpr int kResBandCheck = 19;
 
 // ---- K / cross-covariance build -------------------------------------------------------
 struct BuildArgs {
@@ -133,6 +135,7 @@ struct BandContractArgs {
   const double* X; long long sX; int D;
   const DevSpec* specs; const double* theta; const int* nvalid;
   double* partial; long long sPartial;           // [B][(p+1)·nb][16], tile = d·nb + k
+  double* colsum; long long sCol;                // [B][Np]: Σ_i K_ji Z_ij accumulated (atomics)
   int Np, p;
 };
 // fused per-problem sweep for band width p <= 2 (gpx_band.hip: band_fwd_kernel, band_bwd_kernel)
@@ -145,12 +148,17 @@ struct BandFusedArgs {
   const DevSpec* specs; const double* theta;
   double* partial; long long sPartial;           // one [16] row per problem (tile 0)
   int* info;
+  double* results;                               // [B][kResStride]: writes [kResBandCheck]
   int Np;
 };
-void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s);
+void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s,
+                       hipEvent_t* ev = nullptr);  // ev[4]: fwd start/stop, bwd start/stop
 void launch_band_solve(const BandSolveArgs& a, int n_active, hipStream_t s);
 void launch_band_transpose(const BandTransposeArgs& a, int q, int n_active, hipStream_t s);
 void launch_band_contract(const BandContractArgs& a, int max_terms, int n_active, hipStream_t s);
+// results[b][kResBandCheck] = max_{j<n} |colsum[b][j] − 1|
+void launch_band_check(const int* active, const double* colsum, long long sCol, const int* nvalid,
+                       double* results, int n_active, int Np, hipStream_t s);
 void launch_band_train_pred(const TrainPredArgs& a, int n_active, int Np, hipStream_t s);
 
 void launch_build(const BuildArgs& a, int n_active, hipStream_t s);

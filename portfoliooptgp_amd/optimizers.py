@@ -765,7 +765,12 @@ class _SteppedDriver:
                 theta[r] = active[r]["m"].theta_row()
             try:
                 with lock:
-                    mu, var, _ = eng.predict(pred_rows, theta, xs, False)
+                    if self.predict_inputs is None and hasattr(eng, "_predict_train"):
+                        # predict_f at each fit's own training inputs (GPR/model_trainer.py:20):
+                        # known here, so the engine's input comparison is skipped
+                        mu, var, _ = eng._predict_train(np.asarray(pred_rows, dtype=np.int32), theta, False)
+                    else:
+                        mu, var, _ = eng.predict(pred_rows, theta, xs, False)
                 for k, r in enumerate(pred_rows):
                     self.preds[active[r]["i"]] = (mu[k].reshape(-1, 1), var[k].reshape(-1, 1))
             except BaseException as e:

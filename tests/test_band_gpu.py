@@ -236,3 +236,24 @@ def test_band_fits_match_dense_fits():
         assert rb.fun == pytest.approx(rd.fun, rel=1e-5)
         np.testing.assert_allclose(mb.cpu().numpy(), md.cpu().numpy(), rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(vb.cpu().numpy(), vd.cpu().numpy(), rtol=1e-4, atol=1e-9)
+
+
+def test_band_check_falls_back_to_dense():
+    """Selected inversion loses accuracy for very smooth kernels with wide bands (SE, ℓ=26,
+    σn² = 1e-5 on N=4096: p = 16 blocks; the numpy restatement of the same recurrences is off
+    by 1e23 there). The banded evaluation's check max_j |Σ_i K_ji Z_ij − 1| catches it and the
+    problem is re-evaluated densely in the same call; the C2 regime passes the check."""
+    n = 4096
+    x, y = O.synthetic_series(n, seed=9)
+    eng = _engine([x, x], [y, y], K.SquaredExponential())
+    th = _theta(eng, [(26.0, 1.1, 1e-5), (1.2, 0.6, 1e-5)])
+    eng.reset_timing()
+    lb, gb, ib = eng.lml_grad([0, 1], th)
+    t = eng.last_timing()
+    assert not ib.any()
+    assert t.band_fallbacks == 1 and t.band_evals == 2
+    with _Dense():
+        ld, gd, _ = eng.lml_grad([0, 1], th)
+    assert lb[0] == ld[0] and np.array_equal(gb[0, :3], gd[0, :3])   # problem 0 WAS the dense path
+    assert abs(lb[1] - ld[1]) <= 1e-9 * abs(ld[1])
+    assert np.all(np.abs(gb[1, :3] - gd[1, :3]) <= 1e-7 * (1.0 + np.abs(gd[1, :3]).max()))
