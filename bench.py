@@ -212,8 +212,9 @@ def main():
     G = max(1, args.groups)
     per = W // G
     proto = make_models()
-    engines = [Engine(Xd[g * per:(g + 1) * per], Yd[g * per:(g + 1) * per],
-                      [compile_spec(m.kernel, 1) for m in proto[g * per:(g + 1) * per]], device=gpu)
+    # slot shapes only: every slot is rebound to its fit's series when the fit starts
+    engines = [Engine([Xd[(g * per + i) % F] for i in range(per)], [Yd[(g * per + i) % F] for i in range(per)],
+                      [compile_spec(proto[(g * per + i) % F].kernel, 1) for i in range(per)], device=gpu)
                for g in range(G)]
     engines[0].ctx.set_profiling(True)
     opt = gpx.optimizers.Scipy()
