@@ -159,7 +159,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 256)),
                     help="independent series fitted per GPU per step")
-    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 256)),
+    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 512)),
                     help="resident device slots (continuous-batching width)")
     ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 2)),
                     help="alternating device batches (host/device overlap)")
@@ -220,6 +220,7 @@ def main():
     opt = gpx.optimizers.Scipy()
 
     traces = []
+    stats = []
 
     def run_steps(k):
         """k steps (k × F fits, each from GPflow defaults) streamed back to back through the
@@ -230,6 +231,8 @@ def main():
                                          options=dict(maxiter=MAXITER))
         if getattr(opt, "last_trace", None):
             traces.append(opt.last_trace)
+        if getattr(opt, "last_stats", None):
+            stats.append(dict(opt.last_stats))
         summary = torch.stack([
             torch.stack([
                 torch.tensor(m.kernel.lengthscales.value, device=dev, dtype=torch.float64),
@@ -383,6 +386,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, nfev_mean)
         out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if stats and rank == 0:
+        out["driver_stats_last_call"] = stats[-1]
     if traces and rank == 0:
         with open(os.environ.get("GPX_TRACE_OUT", "rounds_trace.json"), "w") as f:
             json.dump([[[t, b] for t, b in tr] for tr in traces], f)

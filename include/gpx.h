@@ -126,6 +126,22 @@ int gpx_batch_destroy(gpx_batch* batch);
 int gpx_batch_rebind(gpx_batch* batch, int b, int n, const gpx_kernel_spec* spec);
 
 /*
+ * gpx_batch_rebind with the problem's inputs given on the HOST (X [n, D], Y [n], fp64): they are
+ * staged through pinned memory and copied into slot b of the batch's X / Y arrays by DMA on
+ * `stream` (NULL: the context's stream), so a rebind never waits for compute units held by
+ * other streams' kernels (device-to-device copies are blit kernels). Rows n .. N_max-1 of the
+ * slot are zeroed. Returns once the host buffers may be reused; the copies are ordered before
+ * later work on `stream`.
+ */
+int gpx_batch_rebind_host(gpx_batch* batch, int b, int n, const double* X, const double* Y,
+                          const gpx_kernel_spec* spec, void* stream);
+/* The same with the inputs in DEVICE memory (X [n, D], Y [n], e.g. a model's resident tensors):
+ * brought down into the slot's pinned staging by DMA (the band tables need them on the host),
+ * then up into the slot by DMA; waits for the device-to-host copy on `stream`. */
+int gpx_batch_rebind_device(gpx_batch* batch, int b, int n, const double* X, const double* Y,
+                            const gpx_kernel_spec* spec, void* stream);
+
+/*
  * logML and ∂logML/∂θ at theta for the n_active problems listed in active (host int32).
  * Outputs are written at each active problem's row: lml[b], grad[b*GPX_THETA_STRIDE + p],
  * info[b]. stream may be NULL (library stream). Returns after the outputs are on the host.

@@ -25,7 +25,8 @@ LIB_PATH = os.environ.get("GPX_LIB") or os.path.join(os.path.dirname(os.path.abs
 
 # every symbol include/gpx.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
-    "gpx_version", "gpx_create", "gpx_destroy", "gpx_last_error", "gpx_batch_create",
+    "gpx_version", "gpx_create", "gpx_destroy", "gpx_last_error", "gpx_batch_create", "gpx_batch_rebind_host",
+    "gpx_batch_rebind_device",
     "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_predict", "gpx_batch_predict_full_cov", "gpx_batch_predict_train",
     "gpx_batch_last_timing",
     "gpx_set_profiling", "gpx_batch_reset_timing", "gpx_batch_rebind",
@@ -131,6 +132,12 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_last_timing.argtypes = [c_void_p, ctypes.POINTER(GpxTiming)]
         lib.gpx_batch_rebind.restype = c_int
         lib.gpx_batch_rebind.argtypes = [c_void_p, c_int, c_int, ctypes.POINTER(GpxKernelSpec)]
+        lib.gpx_batch_rebind_host.restype = c_int
+        lib.gpx_batch_rebind_host.argtypes = [c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                              ctypes.POINTER(GpxKernelSpec), c_void_p]
+        lib.gpx_batch_rebind_device.restype = c_int
+        lib.gpx_batch_rebind_device.argtypes = [c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                                ctypes.POINTER(GpxKernelSpec), c_void_p]
         lib.gpx_batch_reset_timing.restype = c_int
         lib.gpx_batch_reset_timing.argtypes = [c_void_p]
         spec_p = ctypes.POINTER(GpxKernelSpec)

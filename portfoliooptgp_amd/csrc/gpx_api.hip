@@ -408,6 +408,29 @@ int match_aux_priority(gpx_batch* bt, hipStream_t s) {
   return GPX_OK;
 }
 
+int flush_rebinds(gpx_batch* bt, hipStream_t s) {
+  if (bt->n_dirty == 0) return GPX_OK;
+  gpx_ctx* ctx = bt->ctx;
+  const size_t nx = (size_t)bt->Nmax * bt->D, ny = bt->Nmax;
+  for (int b = 0; b < bt->B; ++b) {
+    if (!bt->dirty[b]) continue;
+    const double* hx = bt->h_stage + (size_t)b * bt->stage_stride;
+    HIPX(ctx, hipMemcpyAsync(const_cast<double*>(bt->X) + (size_t)b * nx, hx, sizeof(double) * nx,
+                             hipMemcpyHostToDevice, s));
+    HIPX(ctx, hipMemcpyAsync(const_cast<double*>(bt->Y) + (size_t)b * ny, hx + nx, sizeof(double) * ny,
+                             hipMemcpyHostToDevice, s));
+    bt->dirty[b] = 0;
+  }
+  bt->n_dirty = 0;
+  for (int b = 0; b < bt->B; ++b) {
+    bt->h_nmeta[b] = bt->n[b];
+    std::memcpy(&bt->h_specs[b], &bt->specs[b], sizeof(DevSpec));
+  }
+  HIPX(ctx, hipMemcpyAsync(bt->d_n, bt->h_nmeta, sizeof(int) * bt->B, hipMemcpyHostToDevice, s));
+  HIPX(ctx, hipMemcpyAsync(bt->d_specs, bt->h_specs, sizeof(DevSpec) * bt->B, hipMemcpyHostToDevice, s));
+  return GPX_OK;
+}
+
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                   hipStream_t s) {
   gpx_ctx* ctx = bt->ctx;
@@ -424,8 +447,13 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
         return fail(ctx, GPX_BAD_ARG, "theta must be finite and > 0 (constrained space)");
     }
   }
-  // one DMA from the pinned block: [active | info = 0 | bandp | theta] (every call ends with a
-  // stream synchronize, so the previous call's transfers out of h_io have completed; bandp is
+  {
+    const int e = flush_rebinds(bt, s);
+    if (e != GPX_OK) return e;
+  }
+  // one DMA from the pinned block (allocated non-coherent: the host reads and writes it as
+  // ordinary cached memory, the DMAs at the call boundaries see it whole):
+  // [active | info = 0 | bandp | theta] (every call ends with a stream synchronize, so the previous call's transfers out of h_io have completed; bandp is
   // written into h_bandp by gpx_batch_lml_grad before this)
   std::memcpy(bt->h_io, active, sizeof(int) * n_active);
   std::memset(bt->h_io + bt->io_info_off, 0, sizeof(int) * bt->B);
@@ -531,7 +559,7 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
     bt->io_res_off = bt->io_theta_off + (size_t)B * GPX_THETA_STRIDE * sizeof(double);
     bt->io_bytes = bt->io_res_off + (size_t)B * kResStride * sizeof(double);
     if (hipMalloc(&bt->d_io, bt->io_bytes) != hipSuccess ||
-        hipHostMalloc(&bt->h_io, bt->io_bytes) != hipSuccess)
+        hipHostMalloc(&bt->h_io, bt->io_bytes, hipHostMallocNonCoherent) != hipSuccess)
       return cleanup("out of memory for the batch I/O block");
     std::memset(bt->h_io, 0, bt->io_bytes);
     bt->d_active = reinterpret_cast<int*>(bt->d_io);
@@ -582,6 +610,9 @@ int gpx_batch_destroy(gpx_batch* bt) {
                   (void*)bt->bres})
     if (p) (void)hipFree(p);
   if (bt->h_io) (void)hipHostFree(bt->h_io);
+  if (bt->h_stage) (void)hipHostFree(bt->h_stage);
+  if (bt->h_nmeta) (void)hipHostFree(bt->h_nmeta);
+  if (bt->h_specs) (void)hipHostFree(bt->h_specs);
   for (int g = 0; g < kAux; ++g)
     if (bt->aux[g]) (void)hipStreamDestroy(bt->aux[g]);
   if (bt->hp) (void)hipStreamDestroy(bt->hp);
@@ -596,8 +627,7 @@ int gpx_batch_destroy(gpx_batch* bt) {
   return GPX_OK;
 }
 
-int gpx_batch_rebind(gpx_batch* bt, int b, int n, const gpx_kernel_spec* spec) {
-  if (!bt) return GPX_BAD_ARG;
+static int check_rebind(gpx_batch* bt, int b, int n, const gpx_kernel_spec* spec) {
   gpx_ctx* ctx = bt->ctx;
   if (b < 0 || b >= bt->B || n < 1 || n > bt->Nmax || !spec)
     return fail(ctx, GPX_BAD_ARG, "bad rebind arguments");
@@ -611,11 +641,24 @@ int gpx_batch_rebind(gpx_batch* bt, int b, int n, const gpx_kernel_spec* spec) {
         tm.dim_start + tm.dim_count > bt->D || tm.param_offset < 0 || tm.param_offset + np > sp.n_params)
       return fail(ctx, GPX_BAD_ARG, "bad kernel term");
   }
+  return GPX_OK;
+}
+
+int gpx_batch_rebind(gpx_batch* bt, int b, int n, const gpx_kernel_spec* spec) {
+  if (!bt) return GPX_BAD_ARG;
+  gpx_ctx* ctx = bt->ctx;
+  int rc = check_rebind(bt, b, n, spec);
+  if (rc != GPX_OK) return rc;
+  const gpx_kernel_spec& sp = *spec;
   HIPX(ctx, hipSetDevice(ctx->device));
   bt->n[b] = n;
   bt->specs[b] = sp;
   bt->fac_valid[b] = 0;
   bt->fac_band[b] = 0;
+  if (!bt->dirty.empty() && bt->dirty[b]) {  // the caller's own device data supersedes a staged one
+    bt->dirty[b] = 0;
+    --bt->n_dirty;
+  }
   HIPX(ctx, hipMemcpy(bt->d_n + b, &n, sizeof(int), hipMemcpyHostToDevice));
   HIPX(ctx, hipMemcpy(bt->d_specs + b, &sp, sizeof(DevSpec), hipMemcpyHostToDevice));
   if (band_shape(bt)) {
@@ -624,6 +667,74 @@ int gpx_batch_rebind(gpx_batch* bt, int b, int n, const gpx_kernel_spec* spec) {
                         hipMemcpyDeviceToHost));
     band_tables(bt, b, hx.data());
   }
+  return GPX_OK;
+}
+
+static int stage_slot(gpx_batch* bt, int b, double** hx, double** hy) {
+  gpx_ctx* ctx = bt->ctx;
+  const size_t nx = (size_t)bt->Nmax * bt->D, ny = bt->Nmax;
+  constexpr size_t kSpecDoubles = (sizeof(DevSpec) + sizeof(double) - 1) / sizeof(double);
+  if (!bt->h_stage) {
+    bt->stage_stride = nx + ny + 1 + kSpecDoubles;
+    HIPX(ctx, hipHostMalloc(&bt->h_stage, sizeof(double) * bt->stage_stride * bt->B, hipHostMallocNonCoherent));
+    HIPX(ctx, hipHostMalloc(&bt->h_nmeta, sizeof(int) * bt->B, hipHostMallocNonCoherent));
+    HIPX(ctx, hipHostMalloc(&bt->h_specs, sizeof(DevSpec) * bt->B, hipHostMallocNonCoherent));
+    bt->dirty.assign(bt->B, 0);
+    bt->n_dirty = 0;
+  }
+  *hx = bt->h_stage + (size_t)b * bt->stage_stride;
+  *hy = *hx + nx;
+  return GPX_OK;
+}
+
+int gpx_batch_rebind_device(gpx_batch* bt, int b, int n, const double* X, const double* Y,
+                            const gpx_kernel_spec* spec, void* stream) {
+  if (!bt) return GPX_BAD_ARG;
+  gpx_ctx* ctx = bt->ctx;
+  if (!X || !Y) return fail(ctx, GPX_BAD_ARG, "null device inputs");
+  int rc = check_rebind(bt, b, n, spec);
+  if (rc != GPX_OK) return rc;
+  HIPX(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  double *hx, *hy;
+  rc = stage_slot(bt, b, &hx, &hy);
+  if (rc != GPX_OK) return rc;
+  // down by DMA into the slot's pinned region, then the host path (which copies in place)
+  HIPX(ctx, hipMemcpyAsync(hx, X, sizeof(double) * (size_t)n * bt->D, hipMemcpyDeviceToHost, s));
+  HIPX(ctx, hipMemcpyAsync(hy, Y, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  HIPX(ctx, hipStreamSynchronize(s));
+  return gpx_batch_rebind_host(bt, b, n, hx, hy, spec, stream);
+}
+
+int gpx_batch_rebind_host(gpx_batch* bt, int b, int n, const double* X, const double* Y,
+                          const gpx_kernel_spec* spec, void* stream) {
+  if (!bt) return GPX_BAD_ARG;
+  gpx_ctx* ctx = bt->ctx;
+  if (!X || !Y) return fail(ctx, GPX_BAD_ARG, "null host inputs");
+  int rc = check_rebind(bt, b, n, spec);
+  if (rc != GPX_OK) return rc;
+  HIPX(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  const size_t nx = (size_t)bt->Nmax * bt->D, ny = bt->Nmax;
+  double *hx, *hy;
+  rc = stage_slot(bt, b, &hx, &hy);
+  if (rc != GPX_OK) return rc;
+  // (gpx_batch_rebind_device already brought the inputs down into this region)
+  if (hx != X) std::memcpy(hx, X, sizeof(double) * (size_t)n * bt->D);
+  std::memset(hx + (size_t)n * bt->D, 0, sizeof(double) * (nx - (size_t)n * bt->D));
+  if (hy != Y) std::memcpy(hy, Y, sizeof(double) * n);
+  std::memset(hy + n, 0, sizeof(double) * (ny - n));
+  // the copies go out with the next device call (flush_rebinds)
+  bt->n[b] = n;
+  bt->specs[b] = *spec;
+  bt->fac_valid[b] = 0;
+  bt->fac_band[b] = 0;
+  if (!bt->dirty[b]) {
+    bt->dirty[b] = 1;
+    ++bt->n_dirty;
+  }
+  (void)s;
+  if (band_shape(bt)) band_tables(bt, b, hx);
   return GPX_OK;
 }
 

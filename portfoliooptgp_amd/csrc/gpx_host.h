@@ -53,6 +53,17 @@ struct gpx_batch {
   std::vector<double> band_rmin;
   double* bres = nullptr; size_t bres_cap = 0;  // [B][Np] band-check column sums (per-block path)
   int force_dense = 0;         // re-evaluation of problems whose band check failed
+  // pinned staging for gpx_batch_rebind_host, one region per slot ([Nmax*D] X, [Nmax] Y, n and
+  // the spec): a slot's previous copies have completed before it is rebound (every evaluation
+  // synchronises its stream), so no region is reused while a DMA may still read it
+  double* h_stage = nullptr;
+  size_t stage_stride = 0;      // doubles per slot
+  // gpx_batch_rebind_host only stages; the copies of every slot rebound since the last device
+  // call go out at the start of the next one (flush_rebinds), ordered before its kernels
+  std::vector<char> dirty;
+  int n_dirty = 0;
+  int* h_nmeta = nullptr;       // pinned copies of n[] and specs[] for those uploads
+  gpx::DevSpec* h_specs = nullptr;
   // per-call I/O in ONE device block mirrored by ONE pinned host block, laid out
   //   [active: B ints][info: B ints][bandp: B ints][theta: B×16][results: B×kResStride]
   // so an evaluation uploads [active, info=0, theta] in one DMA and downloads [info ..
@@ -158,5 +169,6 @@ void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W 
 void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                   hipStream_t s);
+int flush_rebinds(gpx_batch* bt, hipStream_t s);  // staged rebinds -> device (DMA, on s)
 
 }  // namespace gpx

@@ -188,8 +188,8 @@ int gpx_svgp_create(gpx_ctx* ctx, int N, int M, int D, const double* X, const do
   for (double** p : vecs)
     if (hipMalloc(p, sizeof(double) * Mp) != hipSuccess || hipMemset(*p, 0, sizeof(double) * Mp) != hipSuccess)
       return bail("out of device memory for M vectors");
-  if (hipHostMalloc(&sv->h_R, sizeof(double) * mm) != hipSuccess ||
-      hipHostMalloc(&sv->h_Rbar, sizeof(double) * mm) != hipSuccess)
+  if (hipHostMalloc(&sv->h_R, sizeof(double) * mm, hipHostMallocNonCoherent) != hipSuccess ||
+      hipHostMalloc(&sv->h_Rbar, sizeof(double) * mm, hipHostMallocNonCoherent) != hipSuccess)
     return bail("out of pinned host memory");
   std::memset(sv->h_R, 0, sizeof(double) * mm);
   const size_t mn = (size_t)Mp * sv->Ncols;

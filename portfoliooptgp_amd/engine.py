@@ -42,6 +42,13 @@ def to_device_f64(a, device: int) -> torch.Tensor:
     return t.to(device=f"cuda:{device}", dtype=torch.float64).contiguous()
 
 
+def _host_f64(a) -> np.ndarray:
+    """fp64 host array of a (a device tensor is copied down)."""
+    if isinstance(a, torch.Tensor):
+        return a.detach().to(device="cpu", dtype=torch.float64).numpy()
+    return np.asarray(a, dtype=np.float64)
+
+
 def _rows(x: torch.Tensor, D: int) -> torch.Tensor:
     """[M, D] view of prediction inputs (a 1-D input is one column; an empty one has D columns)."""
     if x.numel() == 0:
@@ -223,22 +230,32 @@ class Engine:
         return ([mean[b, : self.n[b]] for b in act], [var[b, : self.n[b]] for b in act], info)
 
     def rebind(self, b: int, X, Y, spec: N.GpxKernelSpec) -> None:
-        """Load a new problem into slot b (continuous batching)."""
-        x = to_device_f64(X, self.device)
-        x = x.reshape(x.shape[0], -1)
-        y = to_device_f64(Y, self.device).reshape(-1)
-        n = x.shape[0]
-        if x.shape[1] != self.D or n > self.Nmax or y.shape[0] != n:
+        """Load a new problem into slot b (continuous batching). The inputs go through the host
+        (gpx_batch_rebind_host: DMA copies ordered on the current stream), so a rebind does not
+        wait for compute units held by other streams' kernels the way device-to-device copies
+        (blit kernels) do."""
+        ok_dev = (isinstance(X, torch.Tensor) and isinstance(Y, torch.Tensor) and X.is_cuda and Y.is_cuda
+                  and X.device.index == self.device and Y.device.index == self.device
+                  and X.dtype == torch.float64 and Y.dtype == torch.float64)
+        if ok_dev:
+            x = X.detach().contiguous()
+            y = Y.detach().contiguous()
+            x2 = x.reshape(x.shape[0], -1)
+            n, D, ny = x2.shape[0], x2.shape[1], y.numel()
+            fn = self.lib.gpx_batch_rebind_device
+        else:
+            x = np.ascontiguousarray(_host_f64(X))
+            y = np.ascontiguousarray(_host_f64(Y)).reshape(-1)
+            x2 = x.reshape(x.shape[0], -1)
+            n, D, ny = x2.shape[0], x2.shape[1], y.shape[0]
+            fn = self.lib.gpx_batch_rebind_host
+        if D != self.D or n > self.Nmax or ny != n:
             raise ValueError(f"problem does not fit slot shape (N <= {self.Nmax}, D = {self.D})")
-        self.X[b].zero_()
-        self.Y[b].zero_()
-        self.X[b, :n] = x
-        self.Y[b, :n] = y
-        torch.cuda.current_stream(self.device).synchronize()
         self.specs[b] = spec
         self.n_params[b] = spec.n_params
         self.n[b] = n
-        rc = self.lib.gpx_batch_rebind(self.handle, int(b), int(n), ctypes.byref(spec))
+        rc = fn(self.handle, int(b), int(n), ctypes.c_void_p(x.data_ptr() if ok_dev else x.ctypes.data),
+                ctypes.c_void_p(y.data_ptr() if ok_dev else y.ctypes.data), ctypes.byref(spec), self._stream())
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_rebind failed ({rc}): {self.ctx.last_error()}")
 

@@ -153,6 +153,7 @@ class Scipy:
                                  models[0].data[0].shape[1], fixed=True)
             drv.run()
             self.last_trace = drv.trace
+            self.last_stats = drv.stats
             for e in drv.errors:
                 if e is not None:
                     raise e
@@ -242,6 +243,7 @@ class Scipy:
                                  predict_inputs=predict_inputs, width=width)
             drv.run()
             self.last_trace = drv.trace
+            self.last_stats = drv.stats
             for e in drv.errors:
                 if e is not None:
                     raise e
@@ -596,6 +598,9 @@ class _SteppedDriver:
         self.first_call = threading.Event()
         self.first_call_s = 0.0
         self._theta = {}  # id(engine) -> [B, 16] θ rows (one array per engine, slots disjoint)
+        # GPX_DRIVER_STATS=1: wall time per phase (bind, theta, device call, steps, finish) summed
+        # over the groups' threads, in Scipy().last_stats
+        self.stats = {} if os.environ.get("GPX_DRIVER_STATS") else None
 
     def _next(self) -> Optional[int]:
         with self.qlock:
@@ -636,8 +641,11 @@ class _SteppedDriver:
     def _bind(self, i: int, eng, row: int, lock):
         m = self.models[i]
         if not self.fixed:
+            t0 = time.perf_counter()
             with lock:
                 eng.rebind(row, m.data[0], m.data[1], compile_spec(m.kernel, self.D))
+            if self.stats is not None:
+                self.stats["bind_rebind"] = self.stats.get("bind_rebind", 0.0) + (time.perf_counter() - t0)
             m._attach(eng, row)
         variables = m.trainable_variables
         if not variables:
@@ -668,7 +676,14 @@ class _SteppedDriver:
         lib = N.load_library()
         theta = self._theta_of(eng)
         n_calls = 0
+        st = self.stats
+        clk = time.perf_counter
+
+        def tick(key, t0):
+            if st is not None:
+                st[key] = st.get(key, 0.0) + (clk() - t0)
         while True:
+            t0 = clk()
             while free:
                 i = self._next()
                 if i is None:
@@ -688,6 +703,8 @@ class _SteppedDriver:
                 # the other's large GEMMs); started in phase they stay in phase
                 self.first_call.wait(timeout=10.0)
                 time.sleep(self.first_call_s * g / G)
+            tick("bind", t0)
+            t0 = clk()
             act = sorted(active)
             # θ rows of every requested point in one native call per variable layout (the same
             # libm softplus as Parameter.value, so the values are those of the per-model path)
@@ -705,9 +722,12 @@ class _SteppedDriver:
                 packs.append((rs, P, U, R, s0["cols"]))
             if self.trace is not None:
                 self.trace.append((time.perf_counter(), len(act)))
+            tick("theta", t0)
             t_call = time.perf_counter()
             with lock:
                 lml, grad, info = eng.lml_grad(act, theta)
+            tick("device_call", t_call)
+            t0 = clk()
             if g == 0 and n_calls == 0:
                 self.first_call_s = time.perf_counter() - t_call
                 self.first_call.set()
@@ -740,7 +760,13 @@ class _SteppedDriver:
                         continue
                     if s["st"].done:
                         done.append((r, True))
+            tick("steps", t0)
+            t0 = clk()
             self._finish(eng, lock, active, done)
+            tick("finish", t0)
+            if st is not None:
+                st["rounds"] = st.get("rounds", 0) + 1
+                st["fit_evals"] = st.get("fit_evals", 0) + len(act)
             for r, _ in done:
                 del active[r]
                 if not self.fixed:
