@@ -133,6 +133,19 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
     }
 
 
+def band_traffic(problems_per_launch):
+    """HBM bytes per launch of the banded roofline kernel from the committed PMC summary
+    (profiles/<round>_band_traffic.json, tools/pmc_summary.py ... band_bwd1_kernel): bytes per
+    problem x the launch's problem count. None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "*_band_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d["hbm_bytes_per_problem"] * problems_per_launch, os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+
+
 def contract_traffic(n, flops_per_launch):
     """HBM bytes per contraction launch from the committed PMC summary of this bench command
     (profiles/<round>_contract_traffic.json, written by tools/pmc_summary.py from separate
@@ -311,9 +324,9 @@ def main():
     # when the fits' evaluations take the banded path (C2: every evaluation), else the dense
     # fused K⁻¹ + gradient contraction
     band_kernels = {
-        "band_fwd_kernel (banded Cholesky + z solve, one workgroup per problem)":
+        "band_fwd1_kernel (p<=1 class: banded Cholesky + z solve, one workgroup per problem)":
             (tm.band_fwd_ms_total, tm.band_fwd_flops),
-        "band_bwd_kernel<1> (selected inversion + alpha solve + gradient contraction)":
+        "band_bwd1_kernel<1> (p<=1 class: selected inversion + alpha solve + gradient contraction)":
             (tm.band_bwd_ms_total, tm.band_bwd_flops),
     }
     kname, (kms, kflops) = max(band_kernels.items(), key=lambda kv: kv[1][0])
@@ -322,9 +335,13 @@ def main():
         b_ms = kms / max(launches, 1.0)
         b_flops = kflops / max(launches, 1.0)
         b_ach = b_flops / (b_ms * 1e-3) / 1e12 if b_ms > 0 else 0.0
+        # problems per timed launch: its flops / one p-weighted problem's (mean p of the class)
+        from_p = tm.band_p_sum / max(tm.band_evals, 1.0)
+        b_traffic, b_src = band_traffic(tm.band_evals / max(tm.band_calls, 1.0))
         roofline = {
             "kernel": kname, "bound": "mfma", "achieved": b_ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": b_ach / FP64_PEAK_TFLOPS, "traffic": None, "traffic_unit": "bytes/launch",
+            "frac": b_ach / FP64_PEAK_TFLOPS, "traffic": b_traffic, "traffic_source": b_src,
+            "traffic_unit": "bytes/launch", "mean_p_blocks": from_p,
             "avg_launch_ms": b_ms, "launches": launches, "alg_flops_per_launch": b_flops,
             "note": ("banded path: each launch walks its problems' 64 block steps in sequence, one "
                      "workgroup (one CU) per problem; achieved = the 64^3 block products issued "

@@ -367,10 +367,13 @@ double band_fused_flops(int Np, int p, bool fwd) {
   return f;
 }
 
-void band_fused_eval(const Run& r, int p, int max_terms, hipEvent_t* ev) {
+void band_fused_eval(const Run& r, int n1, int max_terms, hipEvent_t* ev) {
+  // r's active range is [p <= 1 problems (n1 of them) | p = 2 problems]; the two classes run
+  // as separate launch pairs, the p = 2 one on an auxiliary stream concurrently
   gpx_batch* bt = r.bt;
   const int Np = bt->Np;
   const long long st = mat_stride(bt);
+  const int p = n1 < r.na ? 2 : 1;
   BuildArgs ba{};
   ba.active = r.d_act; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
   ba.X = bt->X; ba.sX = (long long)bt->Nmax * bt->D; ba.X2 = bt->X; ba.sX2 = ba.sX; ba.D = bt->D;
@@ -383,7 +386,22 @@ void band_fused_eval(const Run& r, int p, int max_terms, hipEvent_t* ev) {
   fa.ldiag = bt->ldiag; fa.sVec = Np; fa.X = bt->X; fa.sX = (long long)bt->Nmax * bt->D; fa.D = bt->D;
   fa.specs = bt->d_specs; fa.theta = bt->d_theta; fa.partial = bt->partial; fa.sPartial = bt->partial_stride;
   fa.info = bt->d_info; fa.results = bt->results; fa.Np = Np;
-  launch_band_fused(fa, max_terms, r.na, r.s, ev);
+  hipStream_t sa = bt->aux[0];
+  const bool fork = n1 > 0 && n1 < r.na;
+  if (fork) {
+    (void)hipEventRecord(bt->ev[kEvents - 2], r.s);   // K's band is built
+    (void)hipStreamWaitEvent(sa, bt->ev[kEvents - 2], 0);
+  }
+  if (n1 < r.na) {
+    BandFusedArgs f2 = fa;
+    f2.active = r.d_act + n1;
+    launch_band_fused(f2, max_terms, r.na - n1, fork ? sa : r.s, n1 == 0 ? ev : nullptr);
+  }
+  if (n1 > 0) launch_band_fused1(fa, max_terms, n1, r.s, ev);
+  if (fork) {
+    (void)hipEventRecord(bt->ev[kEvents - 1], sa);
+    (void)hipStreamWaitEvent(r.s, bt->ev[kEvents - 1], 0);
+  }
   ReduceArgs ra{};
   ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
   ra.ntiles = 1; ra.z = bt->z; ra.sVec = Np; ra.ldiag = bt->ldiag;
@@ -777,7 +795,12 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   }
   const int n_dense = (int)order.size(), n_band = (int)band_ids.size(), n_fused = (int)fused_ids.size();
   order.insert(order.end(), band_ids.begin(), band_ids.end());
-  order.insert(order.end(), fused_ids.begin(), fused_ids.end());
+  // fused problems: the p <= 1 class first (its own two-blocks-per-CU kernels), then p = 2
+  int n_fused1 = 0;
+  for (int b : fused_ids)
+    if (bt->h_bandp[b] <= 1) order.push_back(b), ++n_fused1;
+  for (int b : fused_ids)
+    if (bt->h_bandp[b] > 1) order.push_back(b);
   if (n_band > 0) {
     const int e = ensure(ctx, bt->bres, bt->bres_cap, (size_t)bt->B * bt->Np);
     if (e != GPX_OK) return e;
@@ -901,7 +924,7 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     for (int i = n_dense + n_band; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
     if (ctx->profiling)
       for (auto& x : fq.e) HIPX(ctx, hipEventCreate(&x));
-    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, pfused, max_terms,
+    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, n_fused1, max_terms,
                     ctx->profiling ? fq.e : nullptr);
   }
   bp.mark();
@@ -940,7 +963,9 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
       bt->timing.band_fwd_ms_total += f0;
       bt->timing.band_bwd_ms_total += f1;
       bt->timing.band_fused_launches += 1.0;
-      for (int i = n_dense + n_band; i < n_active; ++i) {
+      // the timed launch pair is the p <= 1 class's when there is one, else the p = 2 class's
+      const int t0 = n_dense + n_band, t1 = n_fused1 > 0 ? t0 + n_fused1 : n_active;
+      for (int i = t0; i < t1; ++i) {
         const int pb = bt->h_bandp[order[i]];
         bt->timing.band_fwd_flops += band_fused_flops(bt->Np, pb, true);
         bt->timing.band_bwd_flops += band_fused_flops(bt->Np, pb, false);

@@ -742,3 +742,299 @@ void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipS
 }
 
 }  // namespace gpx
+
+// =======================================================================================
+// p <= 1 (91 % of the C2 evaluations): the same sweeps with two 64x64 LDS blocks (68 KiB), so
+// two problems share a CU and interleave their latency chains (the leaf's serial diagonal, the
+// barriers, the global round trips); the p = 2 kernels above hold four blocks (one per CU).
+// =======================================================================================
+namespace gpx {
+
+__global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
+  __shared__ __attribute__((aligned(16))) double sA[64 * BS];   // A_kk -> (leaf) -> A_{k+1,k} -> P
+  __shared__ __attribute__((aligned(16))) double sW[64 * BS];   // W_kk
+  __shared__ double sv[2][64];        // t / z_k, u_{k+1}
+  __shared__ double spart[4][64];
+  __shared__ int sfail;
+  const int b = a.active[blockIdx.x];
+  const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
+  const long long ld = Np;
+  double* K = a.K + (long long)b * a.sMat;
+  double* L = a.L + (long long)b * a.sMat;
+  double* W = a.W + (long long)b * a.sMat;
+  double* z = a.z + (long long)b * a.sVec;
+  double* ldiag = a.ldiag + (long long)b * a.sVec;
+  const double* y = a.Y + (long long)b * a.sY;
+  const int n = a.nvalid[b];
+  const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
+  if (tid < 64) sv[1][tid] = 0.0;
+  if (tid == 0) sfail = -1;
+  int gfail = 0;
+  for (int k = 0; k < nb; ++k) {
+    const int q = min(p, nb - 1 - k), k64 = k * 64;
+#pragma unroll 1
+    for (int e0 = tid; e0 < 4096; e0 += 256 * 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + 256 * u, r = e >> 6, c = e & 63;
+        v[u] = (c <= r) ? K[(long long)(k64 + r) * ld + k64 + c] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + 256 * u, r = e >> 6, c = e & 63;
+        sA[r * BS + c] = v[u];
+        sW[r * BS + c] = 0.0;
+      }
+    }
+    __syncthreads();
+    leaf64_lds(sA, sW, ldiag + k64, &sfail);
+    if (tid == 0 && sfail >= 0) {
+      if (gfail == 0) gfail = k64 + sfail + 1;
+      sfail = -1;
+    }
+    for (int e = tid; e < 4096; e += 256) W[(long long)(k64 + (e >> 6)) * ld + k64 + (e & 63)] = sW[(e >> 6) * BS + (e & 63)];
+    if (tid < 64) sv[0][tid] = (k64 + tid < n ? y[k64 + tid] : 0.0) + sv[1][tid];
+    __syncthreads();
+    {
+      double s = 0.0;
+      for (int c = part; c <= lane; c += 4) s = fma(sW[lane * BS + c], sv[0][c], s);
+      spart[part][lane] = s;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const double zk = (spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]);
+      sv[0][tid] = zk;
+      z[k64 + tid] = zk;
+    }
+    if (q >= 1) {
+      Frag f;
+      block_load(sA, K + (long long)(k64 + 64) * ld + k64, ld);
+      __syncthreads();
+      frag_zero(f);
+      frag_mma<false, true>(f, sA, sW, false);
+      __syncthreads();
+      frag_store_lds(f, sA);
+      frag_store_global(f, L + (long long)(k64 + 64) * ld + k64, ld);
+      __syncthreads();
+      // u_{k+1} = −P z_k
+      {
+        double s1 = 0.0;
+        for (int c = part; c < 64; c += 4) s1 = fma(sA[lane * BS + c], sv[0][c], s1);
+        spart[part][lane] = s1;
+      }
+      __syncthreads();
+      if (tid < 64) sv[1][tid] = -((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]));
+      // A_{k+1,k+1} −= P Pᵀ
+      double* C = K + (long long)(k64 + 64) * ld + k64 + 64;
+      frag_load_global(f, C, ld);
+      frag_mma<false, true>(f, sA, sA, true);
+      frag_store_global(f, C, ld);
+    } else if (tid < 64) {
+      sv[1][tid] = 0.0;
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && gfail > 0 && a.info[b] == 0) a.info[b] = gfail;
+}
+
+template <int NT>
+__global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
+  __shared__ __attribute__((aligned(16))) double sA[64 * BS];   // P -> G
+  __shared__ __attribute__((aligned(16))) double sW[64 * BS];   // W_kk -> Z_{k+1,k+1} -> Z panel
+  __shared__ double sal[2][64];       // α_k, α_{k+1}
+  __shared__ double st[64];
+  __shared__ double spart[4][64];
+  __shared__ double sth[GPX_THETA_STRIDE];
+  __shared__ double sred[4][16];
+  __shared__ double sres[2][64];      // Σ_i K_ji Z_ij for the columns of blocks k, k+1
+  const int b = a.active[blockIdx.x];
+  const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
+  const long long ld = Np;
+  double* K = a.K + (long long)b * a.sMat;
+  const double* L = a.L + (long long)b * a.sMat;
+  const double* W = a.W + (long long)b * a.sMat;
+  const double* z = a.z + (long long)b * a.sVec;
+  double* alpha = a.alpha + (long long)b * a.sVec;
+  const double* X = a.X + (long long)b * a.sX;
+  const int n = a.nvalid[b], D = a.D;
+  const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
+  if (tid < 64) { sal[1][tid] = 0.0; sres[0][tid] = sres[1][tid] = 0.0; }
+  if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
+  __syncthreads();
+  const DevSpec spec = a.specs[b];
+  const double noise = sth[spec.n_params];
+  const int fkind = spec.terms[0].kind;
+  const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
+  const int fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
+  const double fvar = sth[spec.terms[0].param_offset + 1];
+  const double finv_ell = 1.0 / sth[spec.terms[0].param_offset], finv_l2 = finv_ell * finv_ell;
+  double sums[NT][3];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
+  double snoise = 0.0, resmax = 0.0;
+  // w (α_i α_j − Z_ij) ∂K_ij/∂θ over one Z block staged in LDS (lanes over columns, rows over
+  // the waves: a rolled loop, so the sweep's registers stay within two workgroups per CU), and
+  // K_ij Z_ij into the band-check column sums (column j, and column i by symmetry)
+  auto contract = [&](const double* sZ, int i0, int j0, const double* ai, const double* aj, bool diag, int srow) {
+    const int jl = lane, j = j0 + jl;
+    double colacc = 0.0;
+#pragma unroll 1
+    for (int il = part; il < 64; il += 4) {
+      const int i = i0 + il;
+      double kz = 0.0;
+      if (i < n && j < n && !(diag && il < jl)) {
+        const double zij = sZ[il * BS + jl];
+        const double w = (diag && il == jl) ? 1.0 : 2.0;
+        const double v = w * fma(ai[il], aj[jl], -zij);
+        const double* xi = X + (long long)i * D;
+        const double* xj = X + (long long)j * D;
+        double dk[NT][3];
+        double kij;
+        if (fast) {
+          double d2 = 0.0;
+          for (int q = 0; q < fdn; ++q) {
+            const double diff = xi[fd0 + q] - xj[fd0 + q];
+            d2 = fma(diff, diff, d2);
+          }
+          stationary_grad(fkind, d2 * finv_l2, fvar, finv_ell, dk[0]);
+          kij = fvar * dk[0][1];
+        } else {
+          kij = eval_k_grad<NT>(spec, sth, xi, xj, dk);
+        }
+        if (i == j) kij += noise;
+        kz = kij * zij;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          sums[t][0] = fma(v, dk[t][0], sums[t][0]);
+          sums[t][1] = fma(v, dk[t][1], sums[t][1]);
+          sums[t][2] = fma(v, dk[t][2], sums[t][2]);
+        }
+        if (i == j) snoise += v;
+      }
+      colacc += kz;
+      const double rs = wsum(i != j ? kz : 0.0);
+      if (lane == 0) atomicAdd(&sres[srow][il], rs);
+    }
+    atomicAdd(&sres[0][jl], colacc);
+  };
+  for (int k = nb - 1; k >= 0; --k) {
+    const int q = min(p, nb - 1 - k), k64 = k * 64;
+    block_load(sW, W + (long long)k64 * ld + k64, ld);
+    if (q >= 1) block_load(sA, L + (long long)(k64 + 64) * ld + k64, ld);
+    __syncthreads();
+    // α_k = W_kkᵀ (z_k − Pᵀ α_{k+1})
+    {
+      double s = 0.0;
+      if (q >= 1)
+        for (int r = part; r < 64; r += 4) s = fma(sA[r * BS + lane], sal[1][r], s);
+      spart[part][lane] = s;
+    }
+    __syncthreads();
+    if (tid < 64) st[tid] = z[k64 + tid] - ((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]));
+    __syncthreads();
+    {
+      double s = 0.0;
+      for (int r = part; r < 64; r += 4) s = (r >= lane) ? fma(sW[r * BS + lane], st[r], s) : s;
+      spart[part][lane] = s;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const double ak = (spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]);
+      sal[0][tid] = ak;
+      alpha[k64 + tid] = ak;
+    }
+    // Z_kk = W_kkᵀW_kk (− Gᵀ Z_{k+1,k}); G = P W_kk
+    Frag zk, g, z1;
+    frag_zero(zk);
+    frag_mma<true, false>(zk, sW, sW, false);
+    if (q >= 1) {
+      frag_zero(g);
+      frag_mma<false, false>(g, sA, sW, false);
+      __syncthreads();
+      frag_store_lds(g, sA);                                               // G
+      block_load(sW, K + (long long)(k64 + 64) * ld + k64 + 64, ld);        // Z_{k+1,k+1}
+      __syncthreads();
+      frag_zero(z1);
+      frag_mma<false, false>(z1, sW, sA, true);                            // Z_{k+1,k} = −Z11 G
+      __syncthreads();
+      frag_store_lds(z1, sW);
+      __syncthreads();
+      frag_mma<true, false>(zk, sA, sW, true);                             // − Gᵀ Z_{k+1,k}
+      frag_store_global(z1, K + (long long)(k64 + 64) * ld + k64, ld);
+      for (int e = tid; e < 4096; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        K[(long long)(k64 + r) * ld + k64 + 64 + c] = sW[c * BS + r];
+      }
+    }
+    frag_store_global(zk, K + (long long)k64 * ld + k64, ld);
+    __syncthreads();                     // every wave is done reading G (sA)
+    frag_store_lds(zk, sA);
+    __syncthreads();
+    contract(sA, k64, k64, sal[0], sal[0], true, 0);
+    if (q >= 1) contract(sW, k64 + 64, k64, sal[1], sal[0], false, 1);
+    __syncthreads();
+    if (tid < 64) {
+      const int cb = k + p;
+      if (cb < nb && cb * 64 + tid < n) resmax = fmax(resmax, fabs(sres[p][tid] - 1.0));
+      sal[1][tid] = sal[0][tid];
+      sres[1][tid] = sres[0][tid];
+      sres[0][tid] = 0.0;
+    }
+    __syncthreads();
+  }
+  if (tid < 64 && p >= 1 && tid < n) resmax = fmax(resmax, fabs(sres[1][tid] - 1.0));  // block 0
+  {
+    double rm = (resmax == resmax) ? resmax : INFINITY;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) rm = fmax(rm, __shfl_xor(rm, o, 64));
+    if (lane == 0) sred[part][15] = rm;
+    __syncthreads();
+    if (tid == 0)
+      a.results[(long long)b * kResStride + kResBandCheck] =
+          fmax(fmax(sred[0][15], sred[1][15]), fmax(sred[2][15], sred[3][15]));
+    __syncthreads();
+  }
+  double vals[GPX_MAX_TERMS * 3 + 1];
+#pragma unroll
+  for (int t = 0; t < GPX_MAX_TERMS; ++t)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wsum(sums[t][q]) : 0.0;
+  vals[GPX_MAX_TERMS * 3] = wsum(snoise);
+  if (lane == 0) {
+#pragma unroll
+    for (int v = 0; v < GPX_MAX_TERMS * 3 + 1; ++v) sred[part][v] = vals[v];
+  }
+  __syncthreads();
+  if (tid < GPX_THETA_STRIDE) {
+    double* out = a.partial + (long long)b * a.sPartial;
+    double s = 0.0;
+    int slot = -1;
+    if (tid == spec.n_params) {
+      slot = GPX_MAX_TERMS * 3;
+    } else {
+      const DevSpec* gs = a.specs + b;
+      for (int t = 0; t < gs->n_terms; ++t) {
+        const int o = gs->terms[t].param_offset, kind = gs->terms[t].kind;
+        const int np = (kind == GPX_RQ || kind == GPX_PERIODIC_SE) ? 3 : (kind == GPX_LINEAR ? 1 : 2);
+        if (tid >= o && tid < o + np) slot = t * 3 + (tid - o);
+      }
+    }
+    if (slot >= 0) s = (sred[0][slot] + sred[1][slot]) + (sred[2][slot] + sred[3][slot]);
+    out[tid] = s;
+  }
+}
+
+void launch_band_fused1(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s, hipEvent_t* ev) {
+  auto bwd = max_terms <= 1 ? band_bwd1_kernel<1> : max_terms == 2 ? band_bwd1_kernel<2>
+                                                                    : band_bwd1_kernel<GPX_MAX_TERMS>;
+  if (ev) {
+    hipExtLaunchKernelGGL(band_fwd1_kernel, dim3(n_active), dim3(256), 0, s, ev[0], ev[1], 0, a);
+    hipExtLaunchKernelGGL(bwd, dim3(n_active), dim3(256), 0, s, ev[2], ev[3], 0, a);
+    return;
+  }
+  hipLaunchKernelGGL(band_fwd1_kernel, dim3(n_active), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(bwd, dim3(n_active), dim3(256), 0, s, a);
+}
+
+}  // namespace gpx

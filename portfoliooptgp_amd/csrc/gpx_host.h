@@ -163,7 +163,7 @@ int band_width(const gpx_batch* bt, int b, const double* theta_row);  // p in 64
 bool band_shape(const gpx_batch* bt);  // the banded path handles this batch's padded size
 int band_limit(const gpx_batch* bt);  // largest p the banded path takes (-1: path disabled)
 void band_eval(const Run& r, int p, int max_terms);  // build .. reduce for a banded active set
-void band_fused_eval(const Run& r, int p, int max_terms, hipEvent_t* ev = nullptr);  // p <= 2, two fused kernels
+void band_fused_eval(const Run& r, int n1, int max_terms, hipEvent_t* ev = nullptr);  // p <= 2: [p<=1 (n1) | p=2]
 double band_fused_flops(int Np, int p, bool fwd);  // block-product flops of one problem's sweep
 void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W = L⁻¹)
 void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z

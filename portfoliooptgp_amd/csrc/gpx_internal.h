@@ -153,6 +153,9 @@ struct BandFusedArgs {
 };
 void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s,
                        hipEvent_t* ev = nullptr);  // ev[4]: fwd start/stop, bwd start/stop
+// the same for problems with p <= 1 (two LDS blocks per workgroup: two problems per CU)
+void launch_band_fused1(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s,
+                        hipEvent_t* ev = nullptr);
 void launch_band_solve(const BandSolveArgs& a, int n_active, hipStream_t s);
 void launch_band_transpose(const BandTransposeArgs& a, int q, int n_active, hipStream_t s);
 void launch_band_contract(const BandContractArgs& a, int max_terms, int n_active, hipStream_t s);

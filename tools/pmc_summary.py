@@ -7,7 +7,10 @@ WRITE_SIZE is taken as is. Each dispatch's problem count is its workgroup count 
 the lower-tile count of one problem (exact when the active count is a multiple of 8, the
 XCD-hybrid grid adds < 8 idle-tail workgroups otherwise).
 
-usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR NP OUT.json
+usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR NP OUT.json [KERNEL_TAG]
+
+With KERNEL_TAG (e.g. band_bwd1_kernel) the fused banded kernel of that name is summarised
+instead: one workgroup per problem, so a dispatch's problem count is its workgroup count.
 """
 import csv
 import json
@@ -19,10 +22,11 @@ def is_contract(name: str) -> bool:
     return "gemm_kernel<" in name and ("true, false, 1>" in name or "true, false, 3>" in name)
 
 
-def collect(d, counter):
+def collect(d, counter, match=None):
+    match = match or is_contract
     tot, wgs, n, names = 0.0, 0, 0, set()
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-        if r["Counter_Name"] != counter or not is_contract(r["Kernel_Name"]):
+        if r["Counter_Name"] != counter or not match(r["Kernel_Name"]):
             continue
         tot += float(r["Counter_Value"])
         wgs += int(r["Grid_Size"]) // int(r["Workgroup_Size"])
@@ -33,10 +37,16 @@ def collect(d, counter):
 
 def main():
     fdir, wdir, np_, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    nt = np_ // 128
-    ntl = nt * (nt + 1) // 2
-    f_kb, f_wgs, f_n, names = collect(fdir, "FETCH_SIZE")
-    w_kb, w_wgs, w_n, _ = collect(wdir, "WRITE_SIZE")
+    tag = sys.argv[5] if len(sys.argv) > 5 else None
+    if tag:
+        match = lambda name: tag + "<" in name or tag + "(" in name  # noqa: E731
+        ntl = 1  # one workgroup per problem
+    else:
+        match = None
+        nt = np_ // 128
+        ntl = nt * (nt + 1) // 2
+    f_kb, f_wgs, f_n, names = collect(fdir, "FETCH_SIZE", match)
+    w_kb, w_wgs, w_n, _ = collect(wdir, "WRITE_SIZE", match)
     fb = f_kb * 1024 * 2
     wb = w_kb * 1024
     res = {

@@ -1,7 +1,8 @@
-"""Cross-check of bench.py's live contraction timing against a rocprofv3 kernel trace of the
-same command: the contraction dispatches between the bench's two timed-region markers (the
+"""Cross-check of bench.py's live timing of its roofline kernel against a rocprofv3 kernel trace
+of the same command: that kernel's dispatches between the bench's two timed-region markers (the
 spin kernel of torch.cuda._sleep) are averaged and compared with the bench line's
-roofline.avg_launch_ms / launches.
+roofline.avg_launch_ms / launches. The kernel is the one the bench line names: the fused
+banded sweep (band_bwd1_kernel / band_fwd1_kernel) or the dense fused contraction.
 
 usage: python tools/trace_check.py TRACE_CSV[.gz] BENCH_LOG OUT.json
 """
@@ -15,6 +16,14 @@ def is_contract(name: str) -> bool:
     return "gemm_kernel<" in name and ("true, false, 1>" in name or "true, false, 3>" in name)
 
 
+def matcher(bench_kernel: str):
+    """Trace-name predicate for the kernel a bench line's roofline names."""
+    for tag in ("band_bwd1_kernel", "band_fwd1_kernel", "band_bwd_kernel", "band_fwd_kernel"):
+        if bench_kernel.startswith(tag):
+            return lambda name, tag=tag: tag + "<" in name or tag + "(" in name
+    return is_contract
+
+
 def main():
     tpath, blog, out = sys.argv[1], sys.argv[2], sys.argv[3]
     op = gzip.open if tpath.endswith(".gz") else open
@@ -23,14 +32,15 @@ def main():
     if len(marks) < 2:
         sys.exit(f"expected 2 timed-region markers, found {len(marks)}")
     t0, t1 = marks[-2], marks[-1]
-    ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
-          if is_contract(r["Kernel_Name"]) and t0 <= int(r["Start_Timestamp"]) <= t1]
     line = [l for l in open(blog) if '"metric"' in l][-1]
     bench = json.loads(line[line.index("{"):])
     rf = bench["roofline"]
+    match = matcher(rf["kernel"])
+    ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
+          if match(r["Kernel_Name"]) and t0 <= int(r["Start_Timestamp"]) <= t1]
     avg = sum(e - s for s, e in ks) / len(ks) / 1e6
     res = {
-        "kernel": "gemm_kernel<128,true,false,EPI_CONTRACT1> (fused K^-1 = W^T W + gradient contraction)",
+        "kernel": rf["kernel"],
         "timed_region_ms_trace": (t1 - t0) / 1e6,
         "trace_launches": len(ks),
         "trace_avg_launch_ms": avg,
