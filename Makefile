@@ -9,7 +9,7 @@ CSMOKE := tests/c/gpx_c_smoke
 
 all: $(LIB) $(CSMOKE)
 
-$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h include/gpx.h
+$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h $(CSRC)/gpx_leaf.h include/gpx.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 # host helpers of the L-BFGS-B driver: plain gcc, libm calls as Python's math module makes them
@@ -25,7 +25,16 @@ $(CSMOKE): tests/c/gpx_c_smoke.c include/gpx.h $(LIB)
 	  -L/opt/rocm/lib -lamdhip64 -lm -Wl,-rpath,'$$ORIGIN/../../portfoliooptgp_amd' \
 	  -Wl,-rpath,/opt/rocm/lib -o $@
 
-clean:
-	rm -f $(CSRC)/*.o $(LIB) $(CSMOKE)
+# diagnostic variant: the fused band sweeps record per-phase shader-clock cycles
+# (tools/band_phases.py loads it through GPX_LIB); never the product library
+PHASES_LIB := portfoliooptgp_amd/libgpx_phases.so
+$(CSRC)/gpx_band_phases.o: $(CSRC)/gpx_band.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_leaf.h $(CSRC)/gpx_kfun.h
+	$(HIPCC) $(HIPFLAGS) -DGPX_BAND_PHASES -c $< -o $@
+$(PHASES_LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band_phases.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-soname,libgpx_phases.so $^ -o $@
+phases: $(PHASES_LIB)
 
-.PHONY: all clean
+clean:
+	rm -f $(CSRC)/*.o $(LIB) $(PHASES_LIB) $(CSMOKE)
+
+.PHONY: all clean phases

@@ -782,7 +782,8 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     const int p = plim >= 0 ? band_width(bt, b, theta + (size_t)b * GPX_THETA_STRIDE) : -1;
     if (p >= 0 && p <= plim) {
       bt->h_bandp[b] = p;
-      if (fused_on && p <= 2) {
+      // the p = 2 sweep holds four 64x64 LDS blocks plus three 64·D X-row slots (<= 160 KiB)
+      if (fused_on && (p <= 1 || (p == 2 && bt->D <= 12))) {
         fused_ids.push_back(b);
         pfused = std::max(pfused, p);
       } else {

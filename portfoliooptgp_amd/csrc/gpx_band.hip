@@ -24,6 +24,35 @@
 
 namespace gpx {
 
+// Phase timing of the fused sweeps (diagnostic build only: tools/band_phases.py links a
+// libgpx_phases.so compiled with -DGPX_BAND_PHASES). Thread 0 of each workgroup adds the
+// shader-clock cycles of each phase of its block steps into g_band_phase[kernel][phase].
+#ifdef GPX_BAND_PHASES
+__device__ unsigned long long g_band_phase[4][16];
+#define PH_BEGIN unsigned long long ph_t = __builtin_amdgcn_s_memtime(), ph_acc[12] = {};
+#define PH(i)                                                              \
+  do {                                                                     \
+    const unsigned long long ph_n = __builtin_amdgcn_s_memtime();          \
+    ph_acc[i] += ph_n - ph_t;                                              \
+    ph_t = ph_n;                                                           \
+  } while (0)
+#define PH_END(kid)                                                               \
+  do {                                                                            \
+    if (threadIdx.x == 0) {                                                       \
+      for (int ph_i = 0; ph_i < 12; ++ph_i) atomicAdd(&g_band_phase[kid][ph_i], ph_acc[ph_i]); \
+      atomicAdd(&g_band_phase[kid][15], 1ull);                                    \
+    }                                                                             \
+  } while (0)
+#else
+#define PH_BEGIN
+#define PH(i) \
+  do {        \
+  } while (0)
+#define PH_END(kid) \
+  do {              \
+  } while (0)
+#endif
+
 namespace {
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
@@ -295,11 +324,21 @@ __device__ __forceinline__ void frag_zero(Frag& f) {
     for (int n = 0; n < 2; ++n) f.c[m][n] = (bd4){0.0, 0.0, 0.0, 0.0};
 }
 
+// threadIdx.x through an empty asm: address arithmetic built on it is recomputed where it is
+// used instead of being hoisted out of the block-step loops (where the 64-bit row offsets of
+// every 64x64 block access would otherwise pin ~30 registers and spill)
+__device__ __forceinline__ int tid_fresh() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 // f += ±opA·opB over 64 k; A and B 64x64 in LDS. TA: opA(i,k) = A[k][i]; TB: opB(k,j) = B[j][k].
 template <bool TA, bool TB>
 __device__ __forceinline__ void frag_mma(Frag& f, const double* __restrict__ sA, const double* __restrict__ sB,
                                          bool neg) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t = tid_fresh();
+  const int lane = t & 63, wave = t >> 6;
   const int wr = wave >> 1, wc = wave & 1, l15 = lane & 15, l4 = lane >> 4;
   const double sg = neg ? -1.0 : 1.0;
 #pragma unroll 4
@@ -331,41 +370,47 @@ __device__ __forceinline__ int frag_col(int n) {
   return ((threadIdx.x >> 6) & 1) * 32 + n * 16 + (threadIdx.x & 15);
 }
 
-__device__ __forceinline__ void frag_load_global(Frag& f, const double* __restrict__ g, long long ld) {
+__device__ __forceinline__ void frag_load_global(Frag& f, const double* __restrict__ g, int ld) {
+  const int t = tid_fresh();
+  g += ((t >> 7) * 32 + ((t & 63) >> 4)) * ld + ((t >> 6) & 1) * 32 + (t & 15);
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) f.c[m][n][r] = g[(long long)frag_row(m, r) * ld + frag_col(n)];
+      for (int r = 0; r < 4; ++r) f.c[m][n][r] = g[(m * 16 + 4 * r) * ld + n * 16];
 }
-__device__ __forceinline__ void frag_store_global(const Frag& f, double* __restrict__ g, long long ld) {
+__device__ __forceinline__ void frag_store_global(const Frag& f, double* __restrict__ g, int ld) {
+  const int t = tid_fresh();
+  g += ((t >> 7) * 32 + ((t & 63) >> 4)) * ld + ((t >> 6) & 1) * 32 + (t & 15);
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) g[(long long)frag_row(m, r) * ld + frag_col(n)] = f.c[m][n][r];
+      for (int r = 0; r < 4; ++r) g[(m * 16 + 4 * r) * ld + n * 16] = f.c[m][n][r];
 }
 __device__ __forceinline__ void frag_store_lds(const Frag& f, double* __restrict__ s) {
+  const int t = tid_fresh();
+  s += ((t >> 7) * 32 + ((t & 63) >> 4)) * BS + ((t >> 6) & 1) * 32 + (t & 15);
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) s[frag_row(m, r) * BS + frag_col(n)] = f.c[m][n][r];
+      for (int r = 0; r < 4; ++r) s[(m * 16 + 4 * r) * BS + n * 16] = f.c[m][n][r];
 }
 
 // 64x64 block global -> LDS (coalesced rows, 8 loads in flight per thread)
-__device__ __forceinline__ void block_load(double* __restrict__ s, const double* __restrict__ g, long long ld) {
-  const int tid = threadIdx.x;
+__device__ __forceinline__ void block_load(double* __restrict__ s, const double* __restrict__ g, int ld) {
+  const int tid = tid_fresh();
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     double v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = tid + 256 * (h * 8 + u);
-      v[u] = g[(long long)(e >> 6) * ld + (e & 63)];
+      v[u] = g[(e >> 6) * ld + (e & 63)];
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -374,20 +419,196 @@ __device__ __forceinline__ void block_load(double* __restrict__ s, const double*
     }
   }
 }
+
+// 64x64 block global -> registers in block_load's layout (element e = tid + 256u: row e>>6,
+// column e&63), so the loads can be issued a phase ahead and stored to LDS later
+__device__ __forceinline__ void block_fetch(double (&v)[16], const double* __restrict__ g, int ld) {
+  const int tid = tid_fresh();
+  g += (tid >> 6) * ld + (tid & 63);
+#pragma unroll
+  for (int u = 0; u < 16; ++u) v[u] = g[4 * u * ld];
+}
+__device__ __forceinline__ void block_store_lds(const double (&v)[16], double* __restrict__ s) {
+  const int tid = tid_fresh();
+  s += (tid >> 6) * BS + (tid & 63);
+#pragma unroll
+  for (int u = 0; u < 16; ++u) s[4 * u * BS] = v[u];
+}
+__device__ __forceinline__ void frag_load_lds(Frag& f, const double* __restrict__ s) {
+  const int t = tid_fresh();
+  s += ((t >> 7) * 32 + ((t & 63) >> 4)) * BS + ((t >> 6) & 1) * 32 + (t & 15);
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) f.c[m][n][r] = s[(m * 16 + 4 * r) * BS + n * 16];
+}
+// the diagonal of a fragment-held block -> global (the selected inverse's diag(K⁻¹), read by
+// band_train_pred_kernel)
+__device__ __forceinline__ void frag_store_diag(const Frag& f, double* __restrict__ g, int ld) {
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = frag_row(m, r), j = frag_col(n);
+        if (i == j) g[i * ld + j] = f.c[m][n][r];
+      }
+}
+
+// X rows of one 64-row block -> LDS in two parts: xrows_fetch loads the first 256 elements
+// (all of it for D <= 4) into a register a phase ahead, from a clamped (always valid) address
+// and without a branch, so the load stays in flight; xrows_store writes it and loads any rest
+__device__ __forceinline__ double xrows_fetch(const double* __restrict__ X, int r0, int n, int D) {
+  const int e = tid_fresh();
+  const int idx = min(r0 * D + e, n * D - 1);
+  const double v = X[idx];
+  return (e < 64 * D && r0 + e / D < n) ? v : 0.0;
+}
+__device__ __forceinline__ void xrows_store(double xr, double* __restrict__ s, const double* __restrict__ X,
+                                            int r0, int n, int D) {
+  const int nx = 64 * D, tid = threadIdx.x;
+  if (tid < nx) s[tid] = xr;
+  for (int e = tid + 256; e < nx; e += 256) s[e] = (r0 + e / D < n) ? X[r0 * D + e] : 0.0;
+}
+
+// Kernel-function context of one problem's gradient contraction
+template <int NT>
+struct ContractCtx {
+  const DevSpec* spec;
+  const double* sth;
+  int D, n, fkind, fd0, fdn;
+  bool fast;  // one stationary term (SE / Matern / Exponential): closed form below
+  double fvar, finv_ell, finv_l2, noise;
+  double sums[NT][3];
+  double snoise;
+};
+
+// Gradient contraction of one 64x64 Z block staged in LDS (rows i0.., columns j0..; lanes over
+// the columns, each wave over 16 rows): Σ w (α_i α_j − Z_ij) ∂K_ij/∂θ into cx.sums, and the
+// products K_ij Z_ij into colacc (this thread's column). A diagonal block is taken whole (both
+// triangles, w = 1: Z_kk and K_kk are symmetric); an off-diagonal block stands for itself and
+// its mirror (w = 2), and its K_ij Z_ij overwrite Z in place for the row sums (block_rowsum).
+// Inputs come from LDS: Z, the α slices and the X rows of both blocks (sxi, sxj).
+// The same for the reference's kernel (one SquaredExponential term on one input column), as
+// straight-line code: g = exp(−r²/2), ∂K/∂ℓ = σ² g r²/ℓ, ∂K/∂σ² = g (stationary_grad's SE case,
+// operation for operation)
+template <int NT>
+__device__ __forceinline__ void contract_block_se1(ContractCtx<NT>& cx, double* __restrict__ sZ,
+                                                   const double* __restrict__ sxi, const double* __restrict__ sxj,
+                                                   int i0, int j0, const double* __restrict__ ai,
+                                                   const double* __restrict__ aj, bool diag, double& colacc) {
+  const int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int jl = lane, j = j0 + jl, D = cx.D, d0 = cx.fd0;
+  const double ajl = aj[jl], w = diag ? 1.0 : 2.0, xj = sxj[jl * D + d0];
+  const double var = cx.fvar, inv_ell = cx.finv_ell, inv_l2 = cx.finv_l2;
+  const bool jok = j < cx.n;
+  double s0 = 0.0, s1 = 0.0, sn = 0.0, ca = 0.0;
+#pragma unroll 4
+  for (int t = 0; t < 16; ++t) {
+    const int il = part * 16 + t, i = i0 + il;
+    const double zij = sZ[il * BS + jl];
+    const double diff = sxi[il * D + d0] - xj;
+    const double r2 = fma(diff, diff, 0.0) * inv_l2;
+    const double g = exp(-0.5 * r2);
+    const double v = w * fma(ai[il], ajl, -zij);
+    const bool ok = jok && i < cx.n;
+    const double kij = var * g + (i == j ? cx.noise : 0.0);
+    const double kz = ok ? kij * zij : 0.0;
+    s0 = ok ? fma(v, var * g * r2 * inv_ell, s0) : s0;
+    s1 = ok ? fma(v, g, s1) : s1;
+    sn = (ok && i == j) ? sn + v : sn;
+    ca += kz;
+    if (!diag) sZ[il * BS + jl] = kz;
+  }
+  cx.sums[0][0] += s0;
+  cx.sums[0][1] += s1;
+  cx.snoise += sn;
+  colacc += ca;
+}
+
+template <int NT>
+__device__ __forceinline__ void contract_block(ContractCtx<NT>& cx, double* __restrict__ sZ,
+                                               const double* __restrict__ sxi, const double* __restrict__ sxj,
+                                               int i0, int j0, const double* __restrict__ ai,
+                                               const double* __restrict__ aj, bool diag, double& colacc) {
+  if (cx.fast && cx.fkind == GPX_SE && cx.fdn == 1) {
+    contract_block_se1<NT>(cx, sZ, sxi, sxj, i0, j0, ai, aj, diag, colacc);
+    return;
+  }
+  const int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int jl = lane, j = j0 + jl, D = cx.D;
+  const double ajl = aj[jl], w = diag ? 1.0 : 2.0;
+  const double* xj = sxj + jl * D;
+  const bool jok = j < cx.n;
+#pragma unroll 2
+  for (int t = 0; t < 16; ++t) {
+    const int il = part * 16 + t, i = i0 + il;
+    const double zij = sZ[il * BS + jl];
+    double kz = 0.0;
+    if (jok && i < cx.n) {
+      const double v = w * fma(ai[il], ajl, -zij);
+      const double* xi = sxi + il * D;
+      double dk[NT][3];
+      double kij;
+      if (cx.fast) {
+        double d2 = 0.0;
+        for (int q = 0; q < cx.fdn; ++q) {
+          const double diff = xi[cx.fd0 + q] - xj[cx.fd0 + q];
+          d2 = fma(diff, diff, d2);
+        }
+        stationary_grad(cx.fkind, d2 * cx.finv_l2, cx.fvar, cx.finv_ell, dk[0]);
+        kij = cx.fvar * dk[0][1];  // ∂K/∂σ² = K/σ² for a single stationary term
+      } else {
+        kij = eval_k_grad<NT>(*cx.spec, cx.sth, xi, xj, dk);
+      }
+      if (i == j) {
+        kij += cx.noise;
+        cx.snoise += v;
+      }
+      kz = kij * zij;
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        cx.sums[q][0] = fma(v, dk[q][0], cx.sums[q][0]);
+        cx.sums[q][1] = fma(v, dk[q][1], cx.sums[q][1]);
+        cx.sums[q][2] = fma(v, dk[q][2], cx.sums[q][2]);
+      }
+    }
+    colacc += kz;
+    if (!diag) sZ[il * BS + jl] = kz;
+  }
+}
+
+// Row sums of a K∘Z block left in LDS by contract_block: row r by threads 4r..4r+3 (16 columns
+// each); returns the sum on the thread with (tid & 3) == 0, row tid >> 2
+__device__ __forceinline__ double block_rowsum(const double* __restrict__ sKZ) {
+  const int r = threadIdx.x >> 2, seg = threadIdx.x & 3;
+  double s = 0.0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) s += sKZ[r * BS + seg * 16 + c];
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  return s;
+}
 }  // namespace
 
+// The window's trailing-updated blocks stay in registers between steps (fragments D1 = A_kk,
+// E1 = A_{k+1,k}, D2 = A_{k+1,k+1}); the original blocks entering the window at step k
+// (A_{k+2,k}, A_{k+2,k+1}, A_{k+2,k+2}) are fetched before the leaf.
 __global__ __launch_bounds__(256, 1) void band_fwd_kernel(BandFusedArgs a) {
   __shared__ __attribute__((aligned(16))) double sA[64 * BS];
   __shared__ __attribute__((aligned(16))) double sW[64 * BS];
   __shared__ __attribute__((aligned(16))) double sX[64 * BS];
   __shared__ __attribute__((aligned(16))) double sY[64 * BS];
-  __shared__ double sv[3][64];        // t / z_k, u_{k+1}, u_{k+2}
+  __shared__ double sv[3][64];        // y_k + u_k -> z_k, u_{k+1}, u_{k+2}
   __shared__ double spart[2][4][64];
   __shared__ int sfail;
   const int b = a.active[blockIdx.x];
   const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
   const long long ld = Np;
-  double* K = a.K + (long long)b * a.sMat;
+  const double* K = a.K + (long long)b * a.sMat;
   double* L = a.L + (long long)b * a.sMat;
   double* W = a.W + (long long)b * a.sMat;
   double* z = a.z + (long long)b * a.sVec;
@@ -397,68 +618,72 @@ __global__ __launch_bounds__(256, 1) void band_fwd_kernel(BandFusedArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
   if (tid < 64) { sv[1][tid] = 0.0; sv[2][tid] = 0.0; }
   if (tid == 0) sfail = -1;
-  int gfail = 0;  // thread 0: first failing global pivot (1-based)
+  int gfail = 0;
+  Frag d1, e1, d2, f21, f22;
+  double a20[16];
+  frag_load_global(d1, K, ld);                                         // A_00
+  if (nb > 1) {
+    frag_load_global(d2, K + (long long)64 * ld + 64, ld);             // A_11
+    if (p >= 1) frag_load_global(e1, K + (long long)64 * ld, ld);      // A_10
+  }
+  PH_BEGIN
   for (int k = 0; k < nb; ++k) {
     const int q = min(p, nb - 1 - k), k64 = k * 64;
-    // A_kk (lower) -> sA, sW = 0
-#pragma unroll 1
-    for (int e0 = tid; e0 < 4096; e0 += 256 * 8) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + 256 * u, r = e >> 6, c = e & 63;
-        v[u] = (c <= r) ? K[(long long)(k64 + r) * ld + k64 + c] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + 256 * u, r = e >> 6, c = e & 63;
-        sA[r * BS + c] = v[u];
-        sW[r * BS + c] = 0.0;
-      }
+    // originals entering the window at this step
+    if (k + 2 < nb) {
+      frag_load_global(f22, K + (long long)(k64 + 128) * ld + k64 + 128, ld);
+      if (p >= 1) frag_load_global(f21, K + (long long)(k64 + 128) * ld + k64 + 64, ld);
+      if (q >= 2) block_fetch(a20, K + (long long)(k64 + 128) * ld + k64, ld);
     }
+    const double yk = (tid < 64 && k64 + tid < n) ? y[k64 + tid] : 0.0;
+    frag_store_lds(d1, sA);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = tid + 256 * u;
+      sW[(e >> 6) * BS + (e & 63)] = 0.0;
+    }
+    if (q >= 1) frag_store_lds(e1, sX);
+    if (tid < 64) sv[0][tid] = yk + sv[1][tid];
     __syncthreads();
+    PH(0);
     leaf64_lds(sA, sW, ldiag + k64, &sfail);
+    PH(1);
     if (tid == 0 && sfail >= 0) {
       if (gfail == 0) gfail = k64 + sfail + 1;
       sfail = -1;
     }
-    // W_kk -> global (the backward sweep reads it)
-    for (int e = tid; e < 4096; e += 256) W[(long long)(k64 + (e >> 6)) * ld + k64 + (e & 63)] = sW[(e >> 6) * BS + (e & 63)];
-    // z_k = W_kk (y_k + u_k)
-    if (tid < 64) sv[0][tid] = (k64 + tid < n ? y[k64 + tid] : 0.0) + sv[1][tid];
-    __syncthreads();
     {
+      double* Wk = W + (long long)k64 * ld + k64;
+      for (int e = tid; e < 4096; e += 256) Wk[(e >> 6) * Np + (e & 63)] = sW[(e >> 6) * BS + (e & 63)];
+    }
+    {  // z_k = W_kk (y_k + u_k)
       double s = 0.0;
       for (int c = part; c <= lane; c += 4) s = fma(sW[lane * BS + c], sv[0][c], s);
       spart[0][part][lane] = s;
     }
+    if (q >= 2) block_store_lds(a20, sY);
     __syncthreads();
     if (tid < 64) {
       const double zk = (spart[0][0][tid] + spart[0][1][tid]) + (spart[0][2][tid] + spart[0][3][tid]);
       sv[0][tid] = zk;
       z[k64 + tid] = zk;
     }
+    PH(2);
     // panels P_i = A_{k+i,k} W_kkᵀ -> L (global) and sX / sY
-    Frag f;
+    Frag f1, f2;
+    if (q >= 1) { frag_zero(f1); frag_mma<false, true>(f1, sX, sW, false); }
+    if (q >= 2) { frag_zero(f2); frag_mma<false, true>(f2, sY, sW, false); }
+    __syncthreads();
     if (q >= 1) {
-      block_load(sX, K + (long long)(k64 + 64) * ld + k64, ld);
-      __syncthreads();
-      frag_zero(f);
-      frag_mma<false, true>(f, sX, sW, false);
-      __syncthreads();
-      frag_store_lds(f, sX);
-      frag_store_global(f, L + (long long)(k64 + 64) * ld + k64, ld);
+      frag_store_lds(f1, sX);
+      frag_store_global(f1, L + (long long)(k64 + 64) * ld + k64, ld);
     }
     if (q >= 2) {
-      block_load(sY, K + (long long)(k64 + 128) * ld + k64, ld);
-      __syncthreads();
-      frag_zero(f);
-      frag_mma<false, true>(f, sY, sW, false);
-      __syncthreads();
-      frag_store_lds(f, sY);
-      frag_store_global(f, L + (long long)(k64 + 128) * ld + k64, ld);
+      frag_store_lds(f2, sY);
+      frag_store_global(f2, L + (long long)(k64 + 128) * ld + k64, ld);
     }
     __syncthreads();
+    PH(3);
     // right-looking solve: u_{k+1} = u_{k+2} − P_1 z_k, u_{k+2} = −P_2 z_k
     if (q >= 1) {
       double s1 = 0.0, s2 = 0.0;
@@ -469,6 +694,12 @@ __global__ __launch_bounds__(256, 1) void band_fwd_kernel(BandFusedArgs a) {
       spart[0][part][lane] = s1;
       spart[1][part][lane] = s2;
     }
+    // window update in registers: D2 −= P1 P1ᵀ, A_{k+2,k+1} −= P2 P1ᵀ, A_{k+2,k+2} −= P2 P2ᵀ
+    if (q >= 1) frag_mma<false, true>(d2, sX, sX, true);
+    if (q >= 2) {
+      frag_mma<false, true>(f21, sY, sX, true);
+      frag_mma<false, true>(f22, sY, sY, true);
+    }
     __syncthreads();
     if (tid < 64) {
       const double s1 = (spart[0][0][tid] + spart[0][1][tid]) + (spart[0][2][tid] + spart[0][3][tid]);
@@ -476,25 +707,14 @@ __global__ __launch_bounds__(256, 1) void band_fwd_kernel(BandFusedArgs a) {
       sv[1][tid] = q >= 1 ? sv[2][tid] - s1 : 0.0;
       sv[2][tid] = q >= 2 ? -s2 : 0.0;
     }
-    // trailing update of the window: A_{k+i,k+j} −= P_i P_jᵀ
-    if (q >= 1) {
-      double* C = K + (long long)(k64 + 64) * ld + k64 + 64;
-      frag_load_global(f, C, ld);
-      frag_mma<false, true>(f, sX, sX, true);
-      frag_store_global(f, C, ld);
-    }
-    if (q >= 2) {
-      double* C = K + (long long)(k64 + 128) * ld + k64 + 64;
-      frag_load_global(f, C, ld);
-      frag_mma<false, true>(f, sY, sX, true);
-      frag_store_global(f, C, ld);
-      C = K + (long long)(k64 + 128) * ld + k64 + 128;
-      frag_load_global(f, C, ld);
-      frag_mma<false, true>(f, sY, sY, true);
-      frag_store_global(f, C, ld);
-    }
+    // roll the window: (D1, E1, D2) <- (D2, A_{k+2,k+1}, A_{k+2,k+2})
+    d1 = d2;
+    e1 = f21;
+    d2 = f22;
     __syncthreads();
+    PH(4);
   }
+  PH_END(2);
   if (tid == 0 && gfail > 0 && a.info[b] == 0) a.info[b] = gfail;
 }
 
@@ -510,6 +730,7 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
   __shared__ double sth[GPX_THETA_STRIDE];
   __shared__ double sred[4][16];
   __shared__ double sres[3][64];      // Σ_i K_ji Z_ij for the columns of blocks k, k+1, k+2
+  extern __shared__ double sxr[];     // [3][64·D] X rows, block k in slot k % 3
   const int b = a.active[blockIdx.x];
   const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
   const long long ld = Np;
@@ -525,82 +746,60 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
   if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
   __syncthreads();
   const DevSpec spec = a.specs[b];
-  const double noise = sth[spec.n_params];
+  const int nx = 64 * D;
   double resmax = 0.0;  // max |Σ_i K_ji Z_ij − 1| over the completed columns (this thread's share)
-  const int fkind = spec.terms[0].kind;
-  const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
-  const int fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
-  const double fvar = sth[spec.terms[0].param_offset + 1];
-  const double finv_ell = 1.0 / sth[spec.terms[0].param_offset], finv_l2 = finv_ell * finv_ell;
-  double sums[NT][3];
+  ContractCtx<NT> cx;
+  cx.spec = &spec; cx.sth = sth; cx.D = D; cx.n = n;
+  cx.fkind = spec.terms[0].kind;
+  cx.fast = (NT == 1) && spec.n_terms == 1 && cx.fkind >= GPX_SE && cx.fkind <= GPX_EXPONENTIAL;
+  cx.fd0 = spec.terms[0].dim_start; cx.fdn = spec.terms[0].dim_count;
+  cx.fvar = sth[spec.terms[0].param_offset + 1];
+  cx.finv_ell = 1.0 / sth[spec.terms[0].param_offset]; cx.finv_l2 = cx.finv_ell * cx.finv_ell;
+  cx.noise = sth[spec.n_params];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
-  double snoise = 0.0;
-  // w (α_i α_j − Z_ij) ∂K_ij/∂θ for the elements of one Z block held in a fragment
-  // ... and the products K_ij Z_ij into the column sums of the band check (column j, and by
-  // symmetry column i): srow = the rolling slot of the row block
-  auto contract = [&](const Frag& f, int i0, int j0, const double* ai, const double* aj, bool diag, int srow) {
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int nn = 0; nn < 2; ++nn)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int il = frag_row(m, r), jl = frag_col(nn);
-          const int i = i0 + il, j = j0 + jl;
-          if (i < n && j < n && !(diag && il < jl)) {
-            const double w = (diag && il == jl) ? 1.0 : 2.0;
-            const double v = w * fma(ai[il], aj[jl], -f.c[m][nn][r]);
-            const double* xi = X + (long long)i * D;
-            const double* xj = X + (long long)j * D;
-            double dk[NT][3];
-            double kij;
-            if (fast) {
-              double d2 = 0.0;
-              for (int q = 0; q < fdn; ++q) {
-                const double diff = xi[fd0 + q] - xj[fd0 + q];
-                d2 = fma(diff, diff, d2);
-              }
-              stationary_grad(fkind, d2 * finv_l2, fvar, finv_ell, dk[0]);
-              kij = fvar * dk[0][1];  // ∂K/∂σ² = K/σ² for a single stationary term
-            } else {
-              kij = eval_k_grad<NT>(spec, sth, xi, xj, dk);
-            }
-            if (i == j) kij += noise;
-            const double kz = kij * f.c[m][nn][r];
-            atomicAdd(&sres[0][jl], kz);
-            if (i != j) atomicAdd(&sres[srow][il], kz);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-              sums[t][0] = fma(v, dk[t][0], sums[t][0]);
-              sums[t][1] = fma(v, dk[t][1], sums[t][1]);
-              sums[t][2] = fma(v, dk[t][2], sums[t][2]);
-            }
-            if (i == j) snoise += v;
-          }
-        }
-  };
+  for (int t = 0; t < NT; ++t) cx.sums[t][0] = cx.sums[t][1] = cx.sums[t][2] = 0.0;
+  cx.snoise = 0.0;
+  // the first step's inputs (k = nb − 1 has no panels); the Z window (Z_{k+1,k+1},
+  // Z_{k+2,k+1}, Z_{k+2,k+2}) rides in registers from step to step
+  double pw[16], p1[16], p2[16];
+  block_fetch(pw, W + (long long)(nb - 1) * 64 * ld + (nb - 1) * 64, ld);
+  double zpre = z[(nb - 1) * 64 + lane];
+  double xr = xrows_fetch(X, (nb - 1) * 64, n, D);
+  Frag zA, zB, zC;
+  frag_zero(zA);
+  frag_zero(zB);
+  frag_zero(zC);
+  PH_BEGIN
   for (int k = nb - 1; k >= 0; --k) {
     const int q = min(p, nb - 1 - k), k64 = k * 64;
-    block_load(sW, W + (long long)k64 * ld + k64, ld);
-    if (q >= 1) block_load(sX, L + (long long)(k64 + 64) * ld + k64, ld);
-    if (q >= 2) block_load(sY, L + (long long)(k64 + 128) * ld + k64, ld);
-    __syncthreads();
-    // α_k = W_kkᵀ (z_k − P_1ᵀ α_{k+1} − P_2ᵀ α_{k+2})   (lanes over columns)
+    const int s0 = k % 3, s1 = (k + 1) % 3, s2 = (k + 2) % 3;
+    // α_k = W_kkᵀ (z_k − P_1ᵀ α_{k+1} − P_2ᵀ α_{k+2}): partials from the fetched registers
     {
       double s = 0.0;
-      if (q >= 1)
-        for (int r = part; r < 64; r += 4) s = fma(sX[r * BS + lane], sal[1][r], s);
-      if (q >= 2)
-        for (int r = part; r < 64; r += 4) s = fma(sY[r * BS + lane], sal[2][r], s);
+      if (q >= 1) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s = fma(p1[u], sal[1][part + 4 * u], s);
+      }
+      if (q >= 2) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s = fma(p2[u], sal[2][part + 4 * u], s);
+      }
       spart[0][part][lane] = s;
     }
+    block_store_lds(pw, sW);
+    if (q >= 1) block_store_lds(p1, sX);
+    if (q >= 2) block_store_lds(p2, sY);
+    xrows_store(xr, sxr + s0 * nx, X, k64, n, D);
     __syncthreads();
-    if (tid < 64) st[tid] = z[k64 + tid] - ((spart[0][0][tid] + spart[0][1][tid]) + (spart[0][2][tid] + spart[0][3][tid]));
+    if (tid < 64) st[tid] = zpre - ((spart[0][0][tid] + spart[0][1][tid]) + (spart[0][2][tid] + spart[0][3][tid]));
     __syncthreads();
     {
       double s = 0.0;
-      for (int r = part; r < 64; r += 4) s = (r >= lane) ? fma(sW[r * BS + lane], st[r], s) : s;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int r = part + 4 * u;
+        s = (r >= lane) ? fma(pw[u], st[r], s) : s;
+      }
       spart[1][part][lane] = s;
     }
     __syncthreads();
@@ -609,65 +808,83 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
       sal[0][tid] = ak;
       alpha[k64 + tid] = ak;
     }
-    // G_i = P_i W_kk (into sX / sY)
-    Frag g1, g2;
+    PH(0);
+    // G_i = P_i W_kk;  Z_{k+i,k} = −Σ_j Z_{k+i,k+j} G_j  (Z_{k+1,k+2} = Z_{k+2,k+1}ᵀ);
+    // Z_kk = W_kkᵀ W_kk − Σ_i G_iᵀ Z_{k+i,k}
+    Frag g1, g2, z1, z2, zk;
+    frag_zero(zk);
+    frag_mma<true, false>(zk, sW, sW, false);
     if (q >= 1) { frag_zero(g1); frag_mma<false, false>(g1, sX, sW, false); }
     if (q >= 2) { frag_zero(g2); frag_mma<false, false>(g2, sY, sW, false); }
     __syncthreads();
-    if (q >= 1) frag_store_lds(g1, sX);
-    if (q >= 2) frag_store_lds(g2, sY);
-    // Z_{k+i,k} = −Σ_j Z_{k+i,k+j} G_j   (Z_{k+1,k+2} = Z_{k+2,k+1}ᵀ)
-    Frag z1, z2, zk;
+    PH(1);
     frag_zero(z1);
     frag_zero(z2);
-    if (q >= 2) {
-      block_load(sA, K + (long long)(k64 + 128) * ld + k64 + 64, ld);
-      __syncthreads();
-      frag_mma<true, false>(z1, sA, sY, true);
-      frag_mma<false, false>(z2, sA, sX, true);
-      __syncthreads();
-      block_load(sA, K + (long long)(k64 + 128) * ld + k64 + 128, ld);
-      __syncthreads();
-      frag_mma<false, false>(z2, sA, sY, true);
-      __syncthreads();
-    }
     if (q >= 1) {
-      block_load(sA, K + (long long)(k64 + 64) * ld + k64 + 64, ld);
+      frag_store_lds(g1, sX);
+      if (q >= 2) {
+        frag_store_lds(g2, sY);
+        frag_store_lds(zB, sA);
+        frag_store_lds(zC, sW);
+      }
+      __syncthreads();
+      if (q >= 2) {
+        frag_mma<true, false>(z1, sA, sY, true);
+        frag_mma<false, false>(z2, sA, sX, true);
+        frag_mma<false, false>(z2, sW, sY, true);
+        __syncthreads();
+      }
+      frag_store_lds(zA, sA);
       __syncthreads();
       frag_mma<false, false>(z1, sA, sX, true);
       __syncthreads();
-    }
-    // Z_kk = W_kkᵀ W_kk − G_1ᵀ Z_{k+1,k} − G_2ᵀ Z_{k+2,k}; the new blocks go to K (lower, and
-    // mirrored above the diagonal for the next windows)
-    frag_zero(zk);
-    frag_mma<true, false>(zk, sW, sW, false);
-    if (q >= 1) {
       frag_store_lds(z1, sA);
+      if (q >= 2) frag_store_lds(z2, sW);
       __syncthreads();
       frag_mma<true, false>(zk, sX, sA, true);
-      frag_store_global(z1, K + (long long)(k64 + 64) * ld + k64, ld);
-      for (int e = tid; e < 4096; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        K[(long long)(k64 + r) * ld + k64 + 64 + c] = sA[c * BS + r];
-      }
-      __syncthreads();
+      if (q >= 2) frag_mma<true, false>(zk, sY, sW, true);
+      __syncthreads();                   // every wave is done reading G_1 (sX)
+      frag_store_lds(zk, sX);            // contraction: Z_kk in sX, Z_{k+1,k} in sA, Z_{k+2,k} in sW
+    } else {
+      frag_store_lds(zk, sX);
+    }
+    PH(2);
+    frag_store_diag(zk, K + (long long)k64 * ld + k64, ld);
+    // the next step's inputs, in flight during the contraction
+    if (k > 0) {
+      const int k1 = k64 - 64;
+      block_fetch(pw, W + (long long)k1 * ld + k1, ld);
+      block_fetch(p1, L + (long long)k64 * ld + k1, ld);
+      if (k + 1 < nb) block_fetch(p2, L + (long long)(k64 + 64) * ld + k1, ld);
+    }
+    __syncthreads();
+    PH(3);
+    double colacc = 0.0;
+    contract_block<NT>(cx, sX, sxr + s0 * nx, sxr + s0 * nx, k64, k64, sal[0], sal[0], true, colacc);
+    if (q >= 1)
+      contract_block<NT>(cx, sA, sxr + s1 * nx, sxr + s0 * nx, k64 + 64, k64, sal[1], sal[0], false, colacc);
+    if (q >= 2)
+      contract_block<NT>(cx, sW, sxr + s2 * nx, sxr + s0 * nx, k64 + 128, k64, sal[2], sal[0], false, colacc);
+    PH(4);
+    spart[0][part][lane] = colacc;
+    if (k > 0) {
+      zpre = z[k64 - 64 + lane];
+      xr = xrows_fetch(X, k64 - 64, n, D);
+    }
+    __syncthreads();
+    if (tid < 64) sres[0][tid] += (spart[0][0][tid] + spart[0][1][tid]) + (spart[0][2][tid] + spart[0][3][tid]);
+    if (q >= 1) {
+      const double rs = block_rowsum(sA);
+      if ((tid & 3) == 0) sres[1][tid >> 2] += rs;
     }
     if (q >= 2) {
-      frag_store_lds(z2, sA);
-      __syncthreads();
-      frag_mma<true, false>(zk, sY, sA, true);
-      frag_store_global(z2, K + (long long)(k64 + 128) * ld + k64, ld);
-      for (int e = tid; e < 4096; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        K[(long long)(k64 + r) * ld + k64 + 128 + c] = sA[c * BS + r];
-      }
-      __syncthreads();
+      const double rs = block_rowsum(sW);
+      if ((tid & 3) == 0) sres[2][tid >> 2] += rs;
     }
-    frag_store_global(zk, K + (long long)k64 * ld + k64, ld);
-    // gradient contraction of the three new blocks (band blocks (k,k), (k+1,k), (k+2,k))
-    contract(zk, k64, k64, sal[0], sal[0], true, 0);
-    if (q >= 1) contract(z1, k64 + 64, k64, sal[1], sal[0], false, 1);
-    if (q >= 2) contract(z2, k64 + 128, k64, sal[2], sal[0], false, 2);
+    // roll the Z window: (Z_{k,k}, Z_{k+1,k}, Z_{k+1,k+1}) are the next step's (A, B, C)
+    zC = zA;
+    zB = z1;
+    zA = zk;
     __syncthreads();
     // block k + p has all its band contributions now (later steps touch blocks < k + p only)
     if (tid < 64) {
@@ -680,7 +897,9 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
       sres[0][tid] = 0.0;
     }
     __syncthreads();
+    PH(5);
   }
+  PH_END(3);
   // blocks 0 .. p−1 complete at the end (rolled into slots 1 .. p)
   if (tid < 64)
     for (int cb = 0; cb < p && cb < nb; ++cb)
@@ -702,8 +921,8 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
 #pragma unroll
   for (int t = 0; t < GPX_MAX_TERMS; ++t)
 #pragma unroll
-    for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wsum(sums[t][q]) : 0.0;
-  vals[GPX_MAX_TERMS * 3] = wsum(snoise);
+    for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wsum(cx.sums[t][q]) : 0.0;
+  vals[GPX_MAX_TERMS * 3] = wsum(cx.snoise);
   if (lane == 0) {
 #pragma unroll
     for (int v = 0; v < GPX_MAX_TERMS * 3 + 1; ++v) sred[part][v] = vals[v];
@@ -732,13 +951,14 @@ void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipS
                        hipEvent_t* ev) {
   auto bwd = max_terms <= 1 ? band_bwd_kernel<1> : max_terms == 2 ? band_bwd_kernel<2>
                                                                    : band_bwd_kernel<GPX_MAX_TERMS>;
+  const size_t xs = 3 * 64 * (size_t)a.D * sizeof(double);  // X-row slots of the backward sweep
   if (ev) {  // timestamped at the kernels' actual start and end (profiling)
     hipExtLaunchKernelGGL(band_fwd_kernel, dim3(n_active), dim3(256), 0, s, ev[0], ev[1], 0, a);
-    hipExtLaunchKernelGGL(bwd, dim3(n_active), dim3(256), 0, s, ev[2], ev[3], 0, a);
+    hipExtLaunchKernelGGL(bwd, dim3(n_active), dim3(256), xs, s, ev[2], ev[3], 0, a);
     return;
   }
   hipLaunchKernelGGL(band_fwd_kernel, dim3(n_active), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(bwd, dim3(n_active), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(bwd, dim3(n_active), dim3(256), xs, s, a);
 }
 
 }  // namespace gpx
@@ -750,16 +970,19 @@ void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipS
 // =======================================================================================
 namespace gpx {
 
+// The trailing-updated diagonal block A_{k+1,k+1} stays in the SYRK's fragment and is the next
+// leaf's input (no global round trip); the original blocks A_{k+1,k} and A_{k+1,k+1} are
+// fetched as soon as the leaf is done (the leaf needs every register it can get).
 __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
   __shared__ __attribute__((aligned(16))) double sA[64 * BS];   // A_kk -> (leaf) -> A_{k+1,k} -> P
   __shared__ __attribute__((aligned(16))) double sW[64 * BS];   // W_kk
-  __shared__ double sv[2][64];        // t / z_k, u_{k+1}
+  __shared__ double sv[2][64];        // y_k + u_k -> z_k, u_{k+1}
   __shared__ double spart[4][64];
   __shared__ int sfail;
   const int b = a.active[blockIdx.x];
   const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
   const long long ld = Np;
-  double* K = a.K + (long long)b * a.sMat;
+  const double* K = a.K + (long long)b * a.sMat;
   double* L = a.L + (long long)b * a.sMat;
   double* W = a.W + (long long)b * a.sMat;
   double* z = a.z + (long long)b * a.sVec;
@@ -770,84 +993,92 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
   if (tid < 64) sv[1][tid] = 0.0;
   if (tid == 0) sfail = -1;
   int gfail = 0;
+  Frag cur, nxt;
+  double pa[16];
+  frag_load_global(cur, K, ld);  // A_00
+  PH_BEGIN
   for (int k = 0; k < nb; ++k) {
     const int q = min(p, nb - 1 - k), k64 = k * 64;
-#pragma unroll 1
-    for (int e0 = tid; e0 < 4096; e0 += 256 * 8) {
-      double v[8];
+    const double yk = (tid < 64 && k64 + tid < n) ? y[k64 + tid] : 0.0;
+    frag_store_lds(cur, sA);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + 256 * u, r = e >> 6, c = e & 63;
-        v[u] = (c <= r) ? K[(long long)(k64 + r) * ld + k64 + c] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + 256 * u, r = e >> 6, c = e & 63;
-        sA[r * BS + c] = v[u];
-        sW[r * BS + c] = 0.0;
-      }
+    for (int u = 0; u < 16; ++u) {
+      const int e = tid + 256 * u;
+      sW[(e >> 6) * BS + (e & 63)] = 0.0;
     }
+    if (tid < 64) sv[0][tid] = yk + sv[1][tid];
     __syncthreads();
+    PH(0);
     leaf64_lds(sA, sW, ldiag + k64, &sfail);
+    PH(1);
+    if (q >= 1) block_fetch(pa, K + (long long)(k64 + 64) * ld + k64, ld);
+    if (k + 1 < nb) frag_load_global(nxt, K + (long long)(k64 + 64) * ld + k64 + 64, ld);
     if (tid == 0 && sfail >= 0) {
       if (gfail == 0) gfail = k64 + sfail + 1;
       sfail = -1;
     }
-    for (int e = tid; e < 4096; e += 256) W[(long long)(k64 + (e >> 6)) * ld + k64 + (e & 63)] = sW[(e >> 6) * BS + (e & 63)];
-    if (tid < 64) sv[0][tid] = (k64 + tid < n ? y[k64 + tid] : 0.0) + sv[1][tid];
-    __syncthreads();
+    // W_kk -> global (the backward sweep reads it); z_k partials; the panel block -> sA
+    {
+      double* Wk = W + (long long)k64 * ld + k64;
+      for (int e = tid; e < 4096; e += 256) Wk[(e >> 6) * Np + (e & 63)] = sW[(e >> 6) * BS + (e & 63)];
+    }
     {
       double s = 0.0;
       for (int c = part; c <= lane; c += 4) s = fma(sW[lane * BS + c], sv[0][c], s);
       spart[part][lane] = s;
     }
+    if (q >= 1) block_store_lds(pa, sA);
     __syncthreads();
     if (tid < 64) {
       const double zk = (spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]);
       sv[0][tid] = zk;
       z[k64 + tid] = zk;
     }
+    PH(2);
     if (q >= 1) {
       Frag f;
-      block_load(sA, K + (long long)(k64 + 64) * ld + k64, ld);
-      __syncthreads();
       frag_zero(f);
-      frag_mma<false, true>(f, sA, sW, false);
+      frag_mma<false, true>(f, sA, sW, false);      // P = A_{k+1,k} W_kkᵀ
       __syncthreads();
+      PH(3);
       frag_store_lds(f, sA);
       frag_store_global(f, L + (long long)(k64 + 64) * ld + k64, ld);
       __syncthreads();
-      // u_{k+1} = −P z_k
-      {
+      PH(4);
+      {  // u_{k+1} = −P z_k
         double s1 = 0.0;
         for (int c = part; c < 64; c += 4) s1 = fma(sA[lane * BS + c], sv[0][c], s1);
         spart[part][lane] = s1;
       }
+      frag_mma<false, true>(nxt, sA, sA, true);     // A_{k+1,k+1} −= P Pᵀ (the next leaf's input)
       __syncthreads();
       if (tid < 64) sv[1][tid] = -((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]));
-      // A_{k+1,k+1} −= P Pᵀ
-      double* C = K + (long long)(k64 + 64) * ld + k64 + 64;
-      frag_load_global(f, C, ld);
-      frag_mma<false, true>(f, sA, sA, true);
-      frag_store_global(f, C, ld);
+      PH(5);
     } else if (tid < 64) {
       sv[1][tid] = 0.0;
     }
+    cur = nxt;
     __syncthreads();
+    PH(6);
   }
+  PH_END(0);
   if (tid == 0 && gfail > 0 && a.info[b] == 0) a.info[b] = gfail;
 }
 
+// The backward sweep takes Z_{k+1,k+1} (the previous step's Z_kk) from LDS, fetches the next
+// step's W_kk, P and X rows into registers during the contraction, and contracts from LDS with the X
+// rows staged there (dynamic LDS: two 64·D slots, block k in slot k & 1).
 template <int NT>
 __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
-  __shared__ __attribute__((aligned(16))) double sA[64 * BS];   // P -> G
-  __shared__ __attribute__((aligned(16))) double sW[64 * BS];   // W_kk -> Z_{k+1,k+1} -> Z panel
-  __shared__ double sal[2][64];       // α_k, α_{k+1}
+  __shared__ __attribute__((aligned(16))) double sA[64 * BS];   // P -> G -> Z_kk
+  __shared__ __attribute__((aligned(16))) double sW[64 * BS];   // W_kk -> Z_{k+1,k+1} -> Z_{k+1,k} -> K∘Z
+  extern __shared__ double sxr[];     // [2][64·D] X rows, block k in slot k & 1
+  __shared__ double sal[2][64];       // α ring: α_k in slot k & 1
   __shared__ double st[64];
   __shared__ double spart[4][64];
   __shared__ double sth[GPX_THETA_STRIDE];
   __shared__ double sred[4][16];
-  __shared__ double sres[2][64];      // Σ_i K_ji Z_ij for the columns of blocks k, k+1
+  __shared__ double sres[2][64];      // Σ_i K_ji Z_ij ring: the columns of block k in slot k & 1
   const int b = a.active[blockIdx.x];
   const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
   const long long ld = Np;
@@ -857,94 +1088,67 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
   const double* z = a.z + (long long)b * a.sVec;
   double* alpha = a.alpha + (long long)b * a.sVec;
   const double* X = a.X + (long long)b * a.sX;
-  const int n = a.nvalid[b], D = a.D;
+  const int n = a.nvalid[b], D = a.D, nx = 64 * D;
   const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
-  if (tid < 64) { sal[1][tid] = 0.0; sres[0][tid] = sres[1][tid] = 0.0; }
+  if (tid < 64) { sal[0][tid] = sal[1][tid] = 0.0; sres[0][tid] = sres[1][tid] = 0.0; }
   if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
+  // the first step's inputs (k = nb − 1 has no panel)
+  double pw[16], pp[16];
+  block_fetch(pw, W + (long long)(nb - 1) * 64 * ld + (nb - 1) * 64, ld);
+  double zpre = z[(nb - 1) * 64 + lane];
+  double xr = xrows_fetch(X, (nb - 1) * 64, n, D);
   __syncthreads();
   const DevSpec spec = a.specs[b];
-  const double noise = sth[spec.n_params];
-  const int fkind = spec.terms[0].kind;
-  const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
-  const int fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
-  const double fvar = sth[spec.terms[0].param_offset + 1];
-  const double finv_ell = 1.0 / sth[spec.terms[0].param_offset], finv_l2 = finv_ell * finv_ell;
-  double sums[NT][3];
+  ContractCtx<NT> cx;
+  cx.spec = &spec; cx.sth = sth; cx.D = D; cx.n = n;
+  cx.fkind = spec.terms[0].kind;
+  cx.fast = (NT == 1) && spec.n_terms == 1 && cx.fkind >= GPX_SE && cx.fkind <= GPX_EXPONENTIAL;
+  cx.fd0 = spec.terms[0].dim_start; cx.fdn = spec.terms[0].dim_count;
+  cx.fvar = sth[spec.terms[0].param_offset + 1];
+  cx.finv_ell = 1.0 / sth[spec.terms[0].param_offset]; cx.finv_l2 = cx.finv_ell * cx.finv_ell;
+  cx.noise = sth[spec.n_params];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
-  double snoise = 0.0, resmax = 0.0;
-  // w (α_i α_j − Z_ij) ∂K_ij/∂θ over one Z block staged in LDS (lanes over columns, rows over
-  // the waves: a rolled loop, so the sweep's registers stay within two workgroups per CU), and
-  // K_ij Z_ij into the band-check column sums (column j, and column i by symmetry)
-  auto contract = [&](const double* sZ, int i0, int j0, const double* ai, const double* aj, bool diag, int srow) {
-    const int jl = lane, j = j0 + jl;
-    double colacc = 0.0;
-#pragma unroll 1
-    for (int il = part; il < 64; il += 4) {
-      const int i = i0 + il;
-      double kz = 0.0;
-      if (i < n && j < n && !(diag && il < jl)) {
-        const double zij = sZ[il * BS + jl];
-        const double w = (diag && il == jl) ? 1.0 : 2.0;
-        const double v = w * fma(ai[il], aj[jl], -zij);
-        const double* xi = X + (long long)i * D;
-        const double* xj = X + (long long)j * D;
-        double dk[NT][3];
-        double kij;
-        if (fast) {
-          double d2 = 0.0;
-          for (int q = 0; q < fdn; ++q) {
-            const double diff = xi[fd0 + q] - xj[fd0 + q];
-            d2 = fma(diff, diff, d2);
-          }
-          stationary_grad(fkind, d2 * finv_l2, fvar, finv_ell, dk[0]);
-          kij = fvar * dk[0][1];
-        } else {
-          kij = eval_k_grad<NT>(spec, sth, xi, xj, dk);
-        }
-        if (i == j) kij += noise;
-        kz = kij * zij;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          sums[t][0] = fma(v, dk[t][0], sums[t][0]);
-          sums[t][1] = fma(v, dk[t][1], sums[t][1]);
-          sums[t][2] = fma(v, dk[t][2], sums[t][2]);
-        }
-        if (i == j) snoise += v;
-      }
-      colacc += kz;
-      const double rs = wsum(i != j ? kz : 0.0);
-      if (lane == 0) atomicAdd(&sres[srow][il], rs);
-    }
-    atomicAdd(&sres[0][jl], colacc);
-  };
+  for (int t = 0; t < NT; ++t) cx.sums[t][0] = cx.sums[t][1] = cx.sums[t][2] = 0.0;
+  cx.snoise = 0.0;
+  double resmax = 0.0;
+  Frag zprev;  // Z_{k+1,k+1}
+  frag_zero(zprev);
+  PH_BEGIN
   for (int k = nb - 1; k >= 0; --k) {
-    const int q = min(p, nb - 1 - k), k64 = k * 64;
-    block_load(sW, W + (long long)k64 * ld + k64, ld);
-    if (q >= 1) block_load(sA, L + (long long)(k64 + 64) * ld + k64, ld);
-    __syncthreads();
-    // α_k = W_kkᵀ (z_k − Pᵀ α_{k+1})
+    const int q = min(p, nb - 1 - k), k64 = k * 64, cs = k & 1, ns = cs ^ 1;
+    // α_k = W_kkᵀ (z_k − Pᵀ α_{k+1}): partials straight from the fetched registers (thread
+    // (part, lane) holds rows part + 4u of column lane)
     {
       double s = 0.0;
-      if (q >= 1)
-        for (int r = part; r < 64; r += 4) s = fma(sA[r * BS + lane], sal[1][r], s);
+      if (q >= 1) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s = fma(pp[u], sal[ns][part + 4 * u], s);
+      }
       spart[part][lane] = s;
     }
+    block_store_lds(pw, sW);
+    if (q >= 1) block_store_lds(pp, sA);
+    xrows_store(xr, sxr + cs * nx, X, k64, n, D);
     __syncthreads();
-    if (tid < 64) st[tid] = z[k64 + tid] - ((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]));
+    if (tid < 64) st[tid] = zpre - ((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]));
     __syncthreads();
     {
       double s = 0.0;
-      for (int r = part; r < 64; r += 4) s = (r >= lane) ? fma(sW[r * BS + lane], st[r], s) : s;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int r = part + 4 * u;
+        s = (r >= lane) ? fma(pw[u], st[r], s) : s;
+      }
       spart[part][lane] = s;
     }
     __syncthreads();
     if (tid < 64) {
       const double ak = (spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]);
-      sal[0][tid] = ak;
+      sal[cs][tid] = ak;
       alpha[k64 + tid] = ak;
     }
-    // Z_kk = W_kkᵀW_kk (− Gᵀ Z_{k+1,k}); G = P W_kk
+    PH(0);
+    // Z_kk = W_kkᵀW_kk − Gᵀ Z_{k+1,k}, Z_{k+1,k} = −Z_{k+1,k+1} G, G = P W_kk
     Frag zk, g, z1;
     frag_zero(zk);
     frag_mma<true, false>(zk, sW, sW, false);
@@ -952,38 +1156,58 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
       frag_zero(g);
       frag_mma<false, false>(g, sA, sW, false);
       __syncthreads();
-      frag_store_lds(g, sA);                                               // G
-      block_load(sW, K + (long long)(k64 + 64) * ld + k64 + 64, ld);        // Z_{k+1,k+1}
+      frag_store_lds(g, sA);
+      frag_store_lds(zprev, sW);
       __syncthreads();
+      PH(1);
       frag_zero(z1);
-      frag_mma<false, false>(z1, sW, sA, true);                            // Z_{k+1,k} = −Z11 G
+      frag_mma<false, false>(z1, sW, sA, true);
       __syncthreads();
       frag_store_lds(z1, sW);
       __syncthreads();
-      frag_mma<true, false>(zk, sA, sW, true);                             // − Gᵀ Z_{k+1,k}
-      frag_store_global(z1, K + (long long)(k64 + 64) * ld + k64, ld);
-      for (int e = tid; e < 4096; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        K[(long long)(k64 + r) * ld + k64 + 64 + c] = sW[c * BS + r];
-      }
+      frag_mma<true, false>(zk, sA, sW, true);
     }
-    frag_store_global(zk, K + (long long)k64 * ld + k64, ld);
     __syncthreads();                     // every wave is done reading G (sA)
+    PH(2);
     frag_store_lds(zk, sA);
+    frag_store_diag(zk, K + (long long)k64 * ld + k64, ld);
+    // the next step's inputs, in flight during the contraction
+    if (k > 0) {
+      const int k1 = k64 - 64;
+      block_fetch(pw, W + (long long)k1 * ld + k1, ld);
+      if (p >= 1) block_fetch(pp, L + (long long)k64 * ld + k1, ld);
+    }
     __syncthreads();
-    contract(sA, k64, k64, sal[0], sal[0], true, 0);
-    if (q >= 1) contract(sW, k64 + 64, k64, sal[1], sal[0], false, 1);
+    PH(3);
+    double colacc = 0.0;
+    contract_block<NT>(cx, sA, sxr + cs * nx, sxr + cs * nx, k64, k64, sal[cs], sal[cs], true, colacc);
+    PH(4);
+    if (q >= 1)
+      contract_block<NT>(cx, sW, sxr + ns * nx, sxr + cs * nx, k64 + 64, k64, sal[ns], sal[cs], false, colacc);
+    spart[part][lane] = colacc;
+    if (k > 0) {  // (after the contraction: fewer registers live)
+      zpre = z[k64 - 64 + lane];
+      xr = xrows_fetch(X, k64 - 64, n, D);
+    }
     __syncthreads();
+    PH(5);
+    if (tid < 64) sres[cs][tid] += (spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]);
+    if (q >= 1) {
+      const double rs = block_rowsum(sW);
+      if ((tid & 3) == 0) sres[ns][tid >> 2] += rs;
+    }
+    frag_load_lds(zprev, sA);            // Z_kk, the next step's Z_{k+1,k+1} (not held through the contraction)
+    __syncthreads();
+    // block k + p has all its band contributions now; slot ns is block k − 1's next
     if (tid < 64) {
       const int cb = k + p;
-      if (cb < nb && cb * 64 + tid < n) resmax = fmax(resmax, fabs(sres[p][tid] - 1.0));
-      sal[1][tid] = sal[0][tid];
-      sres[1][tid] = sres[0][tid];
-      sres[0][tid] = 0.0;
+      if (cb < nb && cb * 64 + tid < n) resmax = fmax(resmax, fabs(sres[cb & 1][tid] - 1.0));
+      sres[ns][tid] = 0.0;
     }
-    __syncthreads();
+    PH(6);
   }
-  if (tid < 64 && p >= 1 && tid < n) resmax = fmax(resmax, fabs(sres[1][tid] - 1.0));  // block 0
+  PH_END(1);
+  if (tid < 64 && p >= 1 && tid < n) resmax = fmax(resmax, fabs(sres[0][tid] - 1.0));  // block 0
   {
     double rm = (resmax == resmax) ? resmax : INFINITY;
 #pragma unroll
@@ -999,8 +1223,8 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
 #pragma unroll
   for (int t = 0; t < GPX_MAX_TERMS; ++t)
 #pragma unroll
-    for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wsum(sums[t][q]) : 0.0;
-  vals[GPX_MAX_TERMS * 3] = wsum(snoise);
+    for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wsum(cx.sums[t][q]) : 0.0;
+  vals[GPX_MAX_TERMS * 3] = wsum(cx.snoise);
   if (lane == 0) {
 #pragma unroll
     for (int v = 0; v < GPX_MAX_TERMS * 3 + 1; ++v) sred[part][v] = vals[v];
@@ -1028,13 +1252,30 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
 void launch_band_fused1(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s, hipEvent_t* ev) {
   auto bwd = max_terms <= 1 ? band_bwd1_kernel<1> : max_terms == 2 ? band_bwd1_kernel<2>
                                                                     : band_bwd1_kernel<GPX_MAX_TERMS>;
+  const size_t xs = 2 * 64 * (size_t)a.D * sizeof(double);  // X-row slots of the backward sweep
   if (ev) {
     hipExtLaunchKernelGGL(band_fwd1_kernel, dim3(n_active), dim3(256), 0, s, ev[0], ev[1], 0, a);
-    hipExtLaunchKernelGGL(bwd, dim3(n_active), dim3(256), 0, s, ev[2], ev[3], 0, a);
+    hipExtLaunchKernelGGL(bwd, dim3(n_active), dim3(256), xs, s, ev[2], ev[3], 0, a);
     return;
   }
   hipLaunchKernelGGL(band_fwd1_kernel, dim3(n_active), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(bwd, dim3(n_active), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(bwd, dim3(n_active), dim3(256), xs, s, a);
 }
 
 }  // namespace gpx
+
+#ifdef GPX_BAND_PHASES
+// out[72] <- g_band_phase (kernel-major, 16 slots each: phases 0..11, [15] = workgroups) and
+// g_leaf_phase (diag chain, panel, trailing, inverse, ..., [7] = leaves); reset != 0 zeroes
+// both afterwards. Diagnostic build only (not in include/gpx.h).
+extern "C" int gpx_debug_band_phases(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gpx::g_band_phase), sizeof(gpx::g_band_phase)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(gpx::g_leaf_phase), sizeof(gpx::g_leaf_phase)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long zero[4][16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gpx::g_band_phase), zero, sizeof(zero)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gpx::g_leaf_phase), zero, 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

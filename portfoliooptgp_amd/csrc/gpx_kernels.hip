@@ -282,22 +282,26 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
       double invd[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const double piv = readlane_d(r[j], j);
+        const double piv = bc16(r[j], j);
         if (!(piv > 0.0) && fail < 0) fail = j;
         const double inv = rsqrt_nr(piv);
         const double ljj = piv * inv;
         invd[j] = inv;
         r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
 #pragma unroll
-        for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], readlane_d(r[j], k), r[k]);
+        for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], bc16(r[j], k), r[k]);
       }
       double w[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        double sacc = (i == l15) ? 1.0 : 0.0;
+      for (int i = 0; i < 16; ++i) w[i] = (i == l15) ? 1.0 : 0.0;
 #pragma unroll
-        for (int k = 0; k < i; ++k) sacc = fma(-readlane_d(r[k], i), w[k], sacc);
-        w[i] = sacc * invd[i];
+      for (int k = 0; k < 16; ++k) {
+        w[k] *= invd[k];
+        // column k's broadcasts wait for w_k (else all 120 are hoisted: ~240 registers)
+        double rk = r[k];
+        asm volatile("" : "+v"(rk) : "v"(w[k]));
+#pragma unroll
+        for (int i = k + 1; i < 16; ++i) w[i] = fma(-bc16(rk, i), w[k], w[i]);
       }
       // D_j over A_jj (this wave read the whole block into registers above)
       if (lane < 16) {

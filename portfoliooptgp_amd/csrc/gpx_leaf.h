@@ -6,11 +6,53 @@
 
 namespace gpx {
 
+// sub-phase timing of the leaf (diagnostic build of gpx_band.hip only, see GPX_BAND_PHASES)
+#ifdef GPX_BAND_PHASES
+__device__ unsigned long long g_leaf_phase[8];
+#define LEAF_PH_BEGIN unsigned long long lph_t = __builtin_amdgcn_s_memtime(), lph_acc[4] = {};
+#define LEAF_PH(i)                                                \
+  do {                                                            \
+    const unsigned long long lph_n = __builtin_amdgcn_s_memtime(); \
+    lph_acc[i] += lph_n - lph_t;                                  \
+    lph_t = lph_n;                                                \
+  } while (0)
+#define LEAF_PH_END                                                                          \
+  do {                                                                                       \
+    if (threadIdx.x == 0) {                                                                  \
+      for (int lph_i = 0; lph_i < 4; ++lph_i) atomicAdd(&g_leaf_phase[lph_i], lph_acc[lph_i]); \
+      atomicAdd(&g_leaf_phase[7], 1ull);                                                     \
+    }                                                                                        \
+  } while (0)
+#else
+#define LEAF_PH_BEGIN
+#define LEAF_PH(i) \
+  do {             \
+  } while (0)
+#define LEAF_PH_END \
+  do {              \
+  } while (0)
+#endif
+
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const unsigned long long u = __double_as_longlong(v);
   const unsigned lo = __builtin_amdgcn_readlane((unsigned)(u & 0xffffffffu), l);
   const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
   return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// v of lane k of this lane's 16-lane row (DPP row_newbcast: one v_mov_b64_dpp, no SGPR round
+// trip as readlane_d needs). k must fold to a constant (unrolled loops); rows of 16 lanes that
+// hold the same 16 values (lane & 15) all see lane k's.
+__device__ __forceinline__ double bc16(double v, int k) {
+#define GPX_BC16(K) \
+  case K:           \
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + K, 0xf, 0xf, false);
+  switch (k) {
+    GPX_BC16(0) GPX_BC16(1) GPX_BC16(2) GPX_BC16(3) GPX_BC16(4) GPX_BC16(5) GPX_BC16(6) GPX_BC16(7)
+    GPX_BC16(8) GPX_BC16(9) GPX_BC16(10) GPX_BC16(11) GPX_BC16(12) GPX_BC16(13) GPX_BC16(14)
+    default: return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + 15, 0xf, 0xf, false);
+  }
+#undef GPX_BC16
 }
 
 // 1/sqrt(x) from the hardware estimate and two Newton steps (each doubles the ~22 correct bits):
@@ -35,6 +77,7 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, l4 = lane >> 4;
+  LEAF_PH_BEGIN
   for (int jb = 0; jb < 4; ++jb) {
     const int c0 = jb * 16;
     if (wave == 0) {
@@ -45,32 +88,38 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
       double invd[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const double piv = readlane_d(r[j], j);
+        const double piv = bc16(r[j], j);
         if (!(piv > 0.0) && fail < 0) fail = j;
         const double inv = rsqrt_nr(piv);
         const double ljj = piv * inv;
         invd[j] = inv;
         r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
 #pragma unroll
-        for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], readlane_d(r[j], k), r[k]);
+        for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], bc16(r[j], k), r[k]);
       }
-      // lane l15 holds row l15 of L_jj (r[0..l15]); column l15 of D = L_jj⁻¹ by substitution
+      // lane l15 holds row l15 of L_jj (r[0..l15]); column l15 of D = L_jj⁻¹ by substitution,
+      // right-looking so the 16 steps' FMAs are independent across i
       double w[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        double sacc = (i == l15) ? 1.0 : 0.0;
+      for (int i = 0; i < 16; ++i) w[i] = (i == l15) ? 1.0 : 0.0;
 #pragma unroll
-        for (int k = 0; k < i; ++k) sacc = fma(-readlane_d(r[k], i), w[k], sacc);
-        w[i] = sacc * invd[i];
+      for (int k = 0; k < 16; ++k) {
+        w[k] *= invd[k];
+        // column k's broadcasts wait for w_k (else all 120 are hoisted: ~240 registers)
+        double rk = r[k];
+        asm volatile("" : "+v"(rk) : "v"(w[k]));
+#pragma unroll
+        for (int i = k + 1; i < 16; ++i) w[i] = fma(-bc16(rk, i), w[k], w[i]);
       }
       if (lane < 16) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sW[(c0 + i) * S + c0 + lane] = w[i];
-        ldiag[c0 + lane] = log(r[lane & 15]);
+        sA[(c0 + lane) * S + c0 + lane] = r[lane & 15];   // L_ii, for log det at the end
       }
       if (lane == 0 && fail >= 0 && *sfail < 0) *sfail = c0 + fail;
     }
     __syncthreads();
+    LEAF_PH(0);
     // panel: L_(ib,jb) = A_(ib,jb) · Dᵀ for ib = jb+1 .. 3, one wave per block
     const int nblk = 3 - jb;
     if (wave < nblk) {
@@ -86,6 +135,7 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
       for (int q = 0; q < 4; ++q) sA[(r0 + l4 + 4 * q) * S + c0 + l15] = acc[q];
     }
     __syncthreads();
+    LEAF_PH(1);
     // trailing update of the lower blocks (ib, kb), jb < kb <= ib
     const int ntr = nblk * (nblk + 1) / 2;
     for (int t = wave; t < ntr; t += 4) {
@@ -106,9 +156,12 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
       for (int u = 0; u < 4; ++u) sA[(ri + l4 + 4 * u) * S + rk + l15] = acc[u];
     }
     __syncthreads();
+    LEAF_PH(2);
   }
-  // W = L⁻¹: block rows 1..3, blocks j < i in parallel (wave j)
+  // W = L⁻¹: block rows 1..3, blocks j < i in parallel (wave j); the idle wave 3 takes the
+  // logs of L's diagonal (left on sA's diagonal by the diagonal steps)
   for (int i = 1; i < 4; ++i) {
+    if (i == 3 && wave == 3) ldiag[lane] = log(sA[lane * S + lane]);
     if (wave < i) {
       const int j = wave;
       d4 t = {0.0, 0.0, 0.0, 0.0};
@@ -131,6 +184,8 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
     }
     __syncthreads();
   }
+  LEAF_PH(3);
+  LEAF_PH_END;
 }
 
 }  // namespace gpx
