@@ -407,7 +407,7 @@ def main():
         out["driver_stats_last_call"] = stats[-1]
     if traces and rank == 0:
         with open(os.environ.get("GPX_TRACE_OUT", "rounds_trace.json"), "w") as f:
-            json.dump([[[t, b] for t, b in tr] for tr in traces], f)
+            json.dump([[list(e) for e in tr] for tr in traces], f)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

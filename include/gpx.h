@@ -127,17 +127,18 @@ int gpx_batch_rebind(gpx_batch* batch, int b, int n, const gpx_kernel_spec* spec
 
 /*
  * gpx_batch_rebind with the problem's inputs given on the HOST (X [n, D], Y [n], fp64): they are
- * staged through pinned memory and copied into slot b of the batch's X / Y arrays by DMA on
- * `stream` (NULL: the context's stream), so a rebind never waits for compute units held by
- * other streams' kernels (device-to-device copies are blit kernels). Rows n .. N_max-1 of the
- * slot are zeroed. Returns once the host buffers may be reused; the copies are ordered before
- * later work on `stream`.
+ * copied into the slot's pinned staging region at once (the host buffers may be reused on
+ * return) and reach slot b of the batch's X / Y arrays by DMA at the start of the next device
+ * call on the batch, on that call's stream. Rows n .. N_max-1 of the slot are zeroed.
+ * `stream` is unused (kept for the ABI).
  */
 int gpx_batch_rebind_host(gpx_batch* batch, int b, int n, const double* X, const double* Y,
                           const gpx_kernel_spec* spec, void* stream);
 /* The same with the inputs in DEVICE memory (X [n, D], Y [n], e.g. a model's resident tensors):
- * brought down into the slot's pinned staging by DMA (the band tables need them on the host),
- * then up into the slot by DMA; waits for the device-to-host copy on `stream`. */
+ * only recorded; the next device call on the batch gathers every pending slot in one kernel on
+ * its stream (which also returns the per-64-block boxes of X for the band tables), so X and Y
+ * must stay valid and unchanged until that call has been issued and completed. No HIP call is
+ * made here. `stream` is unused (kept for the ABI). */
 int gpx_batch_rebind_device(gpx_batch* batch, int b, int n, const double* X, const double* Y,
                             const gpx_kernel_spec* spec, void* stream);
 
@@ -148,6 +149,19 @@ int gpx_batch_rebind_device(gpx_batch* batch, int b, int n, const double* X, con
  */
 int gpx_batch_lml_grad(gpx_batch* batch, int n_active, const int32_t* active, const double* theta,
                        double* lml, double* grad, int32_t* info, void* stream);
+
+/*
+ * gpx_batch_lml_grad in two halves, so one host thread can keep several batches in flight:
+ * _submit validates, routes and enqueues the whole evaluation (uploads, kernels and the
+ * download of the results into pinned memory) on `stream` and returns without waiting;
+ * _complete waits for it, writes lml / grad / info exactly as gpx_batch_lml_grad does (and
+ * re-evaluates densely, synchronously, any banded problem whose check failed). One submitted
+ * evaluation per batch at a time; the batch must not be used in between (other batches may).
+ * theta is copied by _submit. gpx_batch_lml_grad = _submit + _complete.
+ */
+int gpx_batch_lml_grad_submit(gpx_batch* batch, int n_active, const int32_t* active, const double* theta,
+                              void* stream);
+int gpx_batch_lml_grad_complete(gpx_batch* batch, double* lml, double* grad, int32_t* info);
 
 /*
  * Posterior marginals at Xnew for the active problems: GPflow GPR.predict_f(full_cov=False)

@@ -208,23 +208,13 @@ double band_arg(int kind, double s) {
 }
 }  // namespace
 
-void band_tables(gpx_batch* bt, int b, const double* hostX) {
+// band_rmin of problem b from the per-block boxes lo/hi [nvb][D] of its valid rows
+static void band_tables_lohi(gpx_batch* bt, int b, const std::vector<double>& lo, const std::vector<double>& hi) {
   const int nb = bt->Np / kLeaf, D = bt->D, n = bt->n[b];
   double* out = bt->band_rmin.data() + (size_t)b * GPX_MAX_TERMS * nb;
   std::fill(out, out + (size_t)GPX_MAX_TERMS * nb, INFINITY);
   const gpx_kernel_spec& sp = bt->specs[b];
   const int nvb = (n + kLeaf - 1) / kLeaf;  // blocks holding valid rows
-  std::vector<double> lo((size_t)nvb * D), hi((size_t)nvb * D);
-  for (int k = 0; k < nvb; ++k)
-    for (int d = 0; d < D; ++d) {
-      double a = INFINITY, z = -INFINITY;
-      for (int r = k * kLeaf; r < std::min(n, (k + 1) * kLeaf); ++r) {
-        a = std::min(a, hostX[(size_t)r * D + d]);
-        z = std::max(z, hostX[(size_t)r * D + d]);
-      }
-      lo[(size_t)k * D + d] = a;
-      hi[(size_t)k * D + d] = z;
-    }
   for (int t = 0; t < sp.n_terms; ++t) {
     const int d0 = sp.terms[t].dim_start, dn = sp.terms[t].dim_count;
     double* rt = out + (size_t)t * nb;
@@ -244,6 +234,33 @@ void band_tables(gpx_batch* bt, int b, const double* hostX) {
       rt[dd] = std::sqrt(m) * (1.0 - 1e-12);
     }
   }
+}
+
+void band_tables(gpx_batch* bt, int b, const double* hostX) {
+  const int D = bt->D, n = bt->n[b];
+  const int nvb = (n + kLeaf - 1) / kLeaf;
+  std::vector<double> lo((size_t)nvb * D), hi((size_t)nvb * D);
+  for (int k = 0; k < nvb; ++k)
+    for (int d = 0; d < D; ++d) {
+      double a = INFINITY, z = -INFINITY;
+      for (int r = k * kLeaf; r < std::min(n, (k + 1) * kLeaf); ++r) {
+        a = std::min(a, hostX[(size_t)r * D + d]);
+        z = std::max(z, hostX[(size_t)r * D + d]);
+      }
+      lo[(size_t)k * D + d] = a;
+      hi[(size_t)k * D + d] = z;
+    }
+  band_tables_lohi(bt, b, lo, hi);
+}
+
+void band_tables_boxes(gpx_batch* bt, int b, const double* box) {
+  const int D = bt->D, nvb = (bt->n[b] + kLeaf - 1) / kLeaf;
+  std::vector<double> lo((size_t)nvb * D), hi((size_t)nvb * D);
+  for (size_t e = 0; e < (size_t)nvb * D; ++e) {
+    lo[e] = box[2 * e];
+    hi[e] = box[2 * e + 1];
+  }
+  band_tables_lohi(bt, b, lo, hi);
 }
 
 int band_width(const gpx_batch* bt, int b, const double* th) {
@@ -426,11 +443,37 @@ int match_aux_priority(gpx_batch* bt, hipStream_t s) {
   return GPX_OK;
 }
 
-int flush_rebinds(gpx_batch* bt, hipStream_t s) {
-  if (bt->n_dirty == 0) return GPX_OK;
+// pinned n[] / specs[] mirrors and the dirty flags of the deferred rebinds (first rebind)
+int ensure_rebind_meta(gpx_batch* bt) {
   gpx_ctx* ctx = bt->ctx;
+  if (!bt->h_nmeta) {
+    HIPX(ctx, hipHostMalloc(&bt->h_nmeta, sizeof(int) * bt->B, hipHostMallocNonCoherent));
+    HIPX(ctx, hipHostMalloc(&bt->h_specs, sizeof(DevSpec) * bt->B, hipHostMallocNonCoherent));
+  }
+  if (bt->dirty.empty()) {
+    bt->dirty.assign(bt->B, 0);
+    bt->n_dirty = 0;
+  }
+  return GPX_OK;
+}
+
+int flush_rebinds(gpx_batch* bt, hipStream_t s) {
+  if (bt->n_dirty == 0 && bt->pend.empty()) return GPX_OK;
+  gpx_ctx* ctx = bt->ctx;
+  {
+    const int rc = ensure_rebind_meta(bt);
+    if (rc != GPX_OK) return rc;
+  }
   const size_t nx = (size_t)bt->Nmax * bt->D, ny = bt->Nmax;
-  for (int b = 0; b < bt->B; ++b) {
+  const int nbx = (bt->Nmax + kLeaf - 1) / kLeaf;
+  if (!bt->h_rdesc) {
+    HIPX(ctx, hipHostMalloc(&bt->h_rdesc, sizeof(RebindDesc) * bt->B, hipHostMallocCoherent));
+    HIPX(ctx, hipMalloc(&bt->d_box, sizeof(double) * (size_t)bt->B * nbx * bt->D * 2));
+    HIPX(ctx, hipHostMalloc(&bt->h_box, sizeof(double) * (size_t)bt->B * nbx * bt->D * 2, hipHostMallocNonCoherent));
+  }
+  // host-staged slots: DMA from their pinned regions (non-coherent host memory: DMA, not
+  // kernel reads, is what sees the CPU's writes whole)
+  for (int b = 0; b < bt->B && bt->n_dirty > 0; ++b) {
     if (!bt->dirty[b]) continue;
     const double* hx = bt->h_stage + (size_t)b * bt->stage_stride;
     HIPX(ctx, hipMemcpyAsync(const_cast<double*>(bt->X) + (size_t)b * nx, hx, sizeof(double) * nx,
@@ -438,8 +481,29 @@ int flush_rebinds(gpx_batch* bt, hipStream_t s) {
     HIPX(ctx, hipMemcpyAsync(const_cast<double*>(bt->Y) + (size_t)b * ny, hx + nx, sizeof(double) * ny,
                              hipMemcpyHostToDevice, s));
     bt->dirty[b] = 0;
+    --bt->n_dirty;
   }
   bt->n_dirty = 0;
+  // device sources: one gather kernel for all of them (descriptors in coherent pinned memory),
+  // which also returns their X boxes for the band tables
+  int m = 0;
+  const bool tables = band_shape(bt);
+  int nbox = 0;
+  for (const auto& e : bt->pend)
+    bt->h_rdesc[m++] = RebindDesc{e.x, e.y, const_cast<double*>(bt->X) + (size_t)e.b * nx,
+                                  const_cast<double*>(bt->Y) + (size_t)e.b * ny, e.n, tables ? nbox++ : -1};
+  if (m > 0) {
+    launch_rebind_gather(bt->h_rdesc, m, bt->Nmax, bt->D, bt->d_box, s);
+    HIPX(ctx, hipGetLastError());
+  }
+  if (nbox > 0) {
+    const size_t row = (size_t)nbx * bt->D * 2;
+    HIPX(ctx, hipMemcpyAsync(bt->h_box, bt->d_box, sizeof(double) * row * nbox, hipMemcpyDeviceToHost, s));
+    HIPX(ctx, hipStreamSynchronize(s));
+    int i = 0;
+    for (const auto& e : bt->pend) band_tables_boxes(bt, e.b, bt->h_box + row * i++);
+  }
+  bt->pend.clear();
   for (int b = 0; b < bt->B; ++b) {
     bt->h_nmeta[b] = bt->n[b];
     std::memcpy(&bt->h_specs[b], &bt->specs[b], sizeof(DevSpec));
@@ -622,6 +686,10 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
 int gpx_batch_destroy(gpx_batch* bt) {
   if (!bt) return GPX_BAD_ARG;
   (void)hipSetDevice(bt->ctx->device);
+  if (bt->pending_eval) {  // a submitted evaluation still reads and writes the buffers below
+    (void)hipStreamSynchronize(bt->pending_eval->s);
+    bt->pending_eval.reset();
+  }
   for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
                   (void*)bt->ldiag, (void*)bt->partial, (void*)bt->d_io, (void*)bt->d_n,
                   (void*)bt->d_specs, (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw,
@@ -629,6 +697,9 @@ int gpx_batch_destroy(gpx_batch* bt) {
     if (p) (void)hipFree(p);
   if (bt->h_io) (void)hipHostFree(bt->h_io);
   if (bt->h_stage) (void)hipHostFree(bt->h_stage);
+  if (bt->h_rdesc) (void)hipHostFree(bt->h_rdesc);
+  if (bt->h_box) (void)hipHostFree(bt->h_box);
+  if (bt->d_box) (void)hipFree(bt->d_box);
   if (bt->h_nmeta) (void)hipHostFree(bt->h_nmeta);
   if (bt->h_specs) (void)hipHostFree(bt->h_specs);
   for (int g = 0; g < kAux; ++g)
@@ -677,6 +748,11 @@ int gpx_batch_rebind(gpx_batch* bt, int b, int n, const gpx_kernel_spec* spec) {
     bt->dirty[b] = 0;
     --bt->n_dirty;
   }
+  for (size_t i = 0; i < bt->pend.size(); ++i)
+    if (bt->pend[i].b == b) {
+      bt->pend.erase(bt->pend.begin() + i);
+      break;
+    }
   HIPX(ctx, hipMemcpy(bt->d_n + b, &n, sizeof(int), hipMemcpyHostToDevice));
   HIPX(ctx, hipMemcpy(bt->d_specs + b, &sp, sizeof(DevSpec), hipMemcpyHostToDevice));
   if (band_shape(bt)) {
@@ -695,11 +771,9 @@ static int stage_slot(gpx_batch* bt, int b, double** hx, double** hy) {
   if (!bt->h_stage) {
     bt->stage_stride = nx + ny + 1 + kSpecDoubles;
     HIPX(ctx, hipHostMalloc(&bt->h_stage, sizeof(double) * bt->stage_stride * bt->B, hipHostMallocNonCoherent));
-    HIPX(ctx, hipHostMalloc(&bt->h_nmeta, sizeof(int) * bt->B, hipHostMallocNonCoherent));
-    HIPX(ctx, hipHostMalloc(&bt->h_specs, sizeof(DevSpec) * bt->B, hipHostMallocNonCoherent));
-    bt->dirty.assign(bt->B, 0);
-    bt->n_dirty = 0;
   }
+  const int rc = ensure_rebind_meta(bt);
+  if (rc != GPX_OK) return rc;
   *hx = bt->h_stage + (size_t)b * bt->stage_stride;
   *hy = *hx + nx;
   return GPX_OK;
@@ -712,16 +786,24 @@ int gpx_batch_rebind_device(gpx_batch* bt, int b, int n, const double* X, const 
   if (!X || !Y) return fail(ctx, GPX_BAD_ARG, "null device inputs");
   int rc = check_rebind(bt, b, n, spec);
   if (rc != GPX_OK) return rc;
-  HIPX(ctx, hipSetDevice(ctx->device));
-  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-  double *hx, *hy;
-  rc = stage_slot(bt, b, &hx, &hy);
-  if (rc != GPX_OK) return rc;
-  // down by DMA into the slot's pinned region, then the host path (which copies in place)
-  HIPX(ctx, hipMemcpyAsync(hx, X, sizeof(double) * (size_t)n * bt->D, hipMemcpyDeviceToHost, s));
-  HIPX(ctx, hipMemcpyAsync(hy, Y, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-  HIPX(ctx, hipStreamSynchronize(s));
-  return gpx_batch_rebind_host(bt, b, n, hx, hy, spec, stream);
+  (void)stream;
+  // recorded only: the next device call's flush_rebinds gathers every pending slot in one
+  // kernel on that call's stream (X and Y must stay valid until then)
+  bt->n[b] = n;
+  bt->specs[b] = *spec;
+  bt->fac_valid[b] = 0;
+  bt->fac_band[b] = 0;
+  if (!bt->dirty.empty() && bt->dirty[b]) {  // supersedes a host-staged rebind of the slot
+    bt->dirty[b] = 0;
+    --bt->n_dirty;
+  }
+  for (auto& e : bt->pend)
+    if (e.b == b) {
+      e = gpx_batch::PendingRebind{b, n, X, Y};
+      return GPX_OK;
+    }
+  bt->pend.push_back(gpx_batch::PendingRebind{b, n, X, Y});
+  return GPX_OK;
 }
 
 int gpx_batch_rebind_host(gpx_batch* bt, int b, int n, const double* X, const double* Y,
@@ -737,7 +819,11 @@ int gpx_batch_rebind_host(gpx_batch* bt, int b, int n, const double* X, const do
   double *hx, *hy;
   rc = stage_slot(bt, b, &hx, &hy);
   if (rc != GPX_OK) return rc;
-  // (gpx_batch_rebind_device already brought the inputs down into this region)
+  for (size_t i = 0; i < bt->pend.size(); ++i)
+    if (bt->pend[i].b == b) {
+      bt->pend.erase(bt->pend.begin() + i);
+      break;
+    }
   if (hx != X) std::memcpy(hx, X, sizeof(double) * (size_t)n * bt->D);
   std::memset(hx + (size_t)n * bt->D, 0, sizeof(double) * (nx - (size_t)n * bt->D));
   if (hy != Y) std::memcpy(hy, Y, sizeof(double) * n);
@@ -756,11 +842,11 @@ int gpx_batch_rebind_host(gpx_batch* bt, int b, int n, const double* X, const do
   return GPX_OK;
 }
 
-int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
-                       double* lml, double* grad, int32_t* info, void* stream) {
+int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                              void* stream) {
   if (!bt) return GPX_BAD_ARG;
   gpx_ctx* ctx = bt->ctx;
-  if (!lml || !grad || !info) return fail(ctx, GPX_BAD_ARG, "null output");
+  if (bt->pending_eval) return fail(ctx, GPX_BAD_ARG, "an evaluation is already submitted on this batch");
   if (n_active <= 0 || n_active > bt->B || !active || !theta)
     return fail(ctx, GPX_BAD_ARG, "bad active set / theta");
   for (int i = 0; i < n_active; ++i)
@@ -811,19 +897,18 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   rc = match_aux_priority(bt, s);
   if (rc != GPX_OK) return rc;
   bt->flops_acc = 0.0;
-  PhaseTimer total(ctx->profiling != 0, s);
+  std::unique_ptr<gpx_batch::PendingEval> pe(new gpx_batch::PendingEval());
+  pe->s = s;
+  pe->n_active = n_active;
+  pe->theta.assign(theta, theta + (size_t)bt->B * GPX_THETA_STRIDE);
+  pe->total.reset(new PhaseTimer(ctx->profiling != 0, s));
+  PhaseTimer& total = *pe->total;
   total.mark();
-  struct EvPair {
-    hipEvent_t e[2] = {nullptr, nullptr};
-    ~EvPair() {
-      for (auto x : e)
-        if (x) (void)hipEventDestroy(x);
-    }
-  } kp;
-  hipEvent_t* kev = kp.e;
-  int ng = 0;
-  std::vector<PhaseTimer> pts;
-  PhaseTimer ct(ctx->profiling != 0 && n_dense > 0, s);
+  hipEvent_t* kev = pe->kev;
+  int& ng = pe->ng;
+  std::vector<PhaseTimer>& pts = pe->pts;
+  pe->ct.reset(new PhaseTimer(ctx->profiling != 0 && n_dense > 0, s));
+  PhaseTimer& ct = *pe->ct;
   if (n_dense > 0) {
     // Split the dense problems into up to kGroups ranges, each running the whole pipeline on
     // its own stream: one group's latency-bound phases (64x64 leaves, small recursion levels)
@@ -906,27 +991,22 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     }
     ct.mark();
   }
-  PhaseTimer bp(ctx->profiling != 0, s);
+  pe->bp.reset(new PhaseTimer(ctx->profiling != 0, s));
+  PhaseTimer& bp = *pe->bp;
   bp.mark();
   if (n_band > 0) {
     int max_terms = 1;
     for (int i = n_dense; i < n_dense + n_band; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
     band_eval(Run{bt, bt->d_active + n_dense, n_band, s}, pband, max_terms);
   }
-  struct EvQuad {
-    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
-    ~EvQuad() {
-      for (auto x : e)
-        if (x) (void)hipEventDestroy(x);
-    }
-  } fq;
+  hipEvent_t* fqe = pe->fq;
   if (n_fused > 0) {
     int max_terms = 1;
     for (int i = n_dense + n_band; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
     if (ctx->profiling)
-      for (auto& x : fq.e) HIPX(ctx, hipEventCreate(&x));
+      for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&fqe[e]));
     band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, n_fused1, max_terms,
-                    ctx->profiling ? fq.e : nullptr);
+                    ctx->profiling ? fqe : nullptr);
   }
   bp.mark();
   total.mark();
@@ -934,7 +1014,34 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   // one DMA into the pinned block: [info | theta (unchanged) | results]
   HIPX(ctx, hipMemcpyAsync(bt->h_io + bt->io_info_off, bt->d_io + bt->io_info_off,
                            bt->io_bytes - bt->io_info_off, hipMemcpyDeviceToHost, s));
+  pe->order = std::move(order);
+  pe->n_dense = n_dense;
+  pe->n_band = n_band;
+  pe->n_fused = n_fused;
+  pe->n_fused1 = n_fused1;
+  bt->pending_eval = std::move(pe);
+  return GPX_OK;
+}
+
+int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_t* info) {
+  if (!bt) return GPX_BAD_ARG;
+  gpx_ctx* ctx = bt->ctx;
+  if (!bt->pending_eval) return fail(ctx, GPX_BAD_ARG, "no evaluation submitted on this batch");
+  std::unique_ptr<gpx_batch::PendingEval> pe = std::move(bt->pending_eval);
+  if (!lml || !grad || !info) return fail(ctx, GPX_BAD_ARG, "null output");
+  HIPX(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = pe->s;
   HIPX(ctx, hipStreamSynchronize(s));
+  const int n_active = pe->n_active, n_dense = pe->n_dense, n_band = pe->n_band, n_fused = pe->n_fused;
+  const int n_fused1 = pe->n_fused1, ng = pe->ng;
+  const std::vector<int32_t>& order = pe->order;
+  const double* theta = pe->theta.data();
+  PhaseTimer& total = *pe->total;
+  PhaseTimer& ct = *pe->ct;
+  PhaseTimer& bp = *pe->bp;
+  std::vector<PhaseTimer>& pts = pe->pts;
+  hipEvent_t* kev = pe->kev;
+  hipEvent_t* fqe = pe->fq;
   if (total.on) {
     bt->timing.factor_ms = bt->timing.alpha_ms = 0.0;
     for (int g = 0; g < ng; ++g) {
@@ -959,8 +1066,8 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
     }
     if (n_fused > 0) {
       float f0 = 0.f, f1 = 0.f;
-      (void)hipEventElapsedTime(&f0, fq.e[0], fq.e[1]);
-      (void)hipEventElapsedTime(&f1, fq.e[2], fq.e[3]);
+      (void)hipEventElapsedTime(&f0, fqe[0], fqe[1]);
+      (void)hipEventElapsedTime(&f1, fqe[2], fqe[3]);
       bt->timing.band_fwd_ms_total += f0;
       bt->timing.band_bwd_ms_total += f1;
       bt->timing.band_fused_launches += 1.0;
@@ -1010,7 +1117,7 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   if (!redo.empty()) {
     if (total.on) bt->timing.band_fallbacks += (double)redo.size();
     bt->force_dense = 1;
-    const int rc2 = gpx_batch_lml_grad(bt, (int)redo.size(), redo.data(), theta, lml, grad, info, stream);
+    const int rc2 = gpx_batch_lml_grad(bt, (int)redo.size(), redo.data(), theta, lml, grad, info, s);
     bt->force_dense = 0;
     if (rc2 != GPX_OK && rc2 != GPX_NOT_PD) return rc2;
     if (rc2 == GPX_NOT_PD) status = GPX_NOT_PD;
@@ -1018,6 +1125,15 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
   return status;
 }
 
+
+int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                       double* lml, double* grad, int32_t* info, void* stream) {
+  if (!bt) return GPX_BAD_ARG;
+  if (!lml || !grad || !info) return fail(bt->ctx, GPX_BAD_ARG, "null output");
+  const int rc = gpx_batch_lml_grad_submit(bt, n_active, active, theta, stream);
+  if (rc != GPX_OK) return rc;
+  return gpx_batch_lml_grad_complete(bt, lml, grad, info);
+}
 
 // Shared body of gpx_batch_predict (var != nullptr) and gpx_batch_predict_full_cov
 // (cov != nullptr).

@@ -401,27 +401,7 @@ __device__ __forceinline__ void frag_store_lds(const Frag& f, double* __restrict
       for (int r = 0; r < 4; ++r) s[(m * 16 + 4 * r) * BS + n * 16] = f.c[m][n][r];
 }
 
-// 64x64 block global -> LDS (coalesced rows, 8 loads in flight per thread)
-__device__ __forceinline__ void block_load(double* __restrict__ s, const double* __restrict__ g, int ld) {
-  const int tid = tid_fresh();
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    double v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * (h * 8 + u);
-      v[u] = g[(e >> 6) * ld + (e & 63)];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * (h * 8 + u);
-      s[(e >> 6) * BS + (e & 63)] = v[u];
-    }
-  }
-}
-
-// 64x64 block global -> registers in block_load's layout (element e = tid + 256u: row e>>6,
-// column e&63), so the loads can be issued a phase ahead and stored to LDS later
+// 64x64 block global -> registers (element e = tid + 256u: row e>>6, column e&63), so the loads can be issued a phase ahead and stored to LDS later
 __device__ __forceinline__ void block_fetch(double (&v)[16], const double* __restrict__ g, int ld) {
   const int tid = tid_fresh();
   g += (tid >> 6) * ld + (tid & 63);
@@ -1262,6 +1242,34 @@ void launch_band_fused1(const BandFusedArgs& a, int max_terms, int n_active, hip
   hipLaunchKernelGGL(bwd, dim3(n_active), dim3(256), xs, s, a);
 }
 
+}  // namespace gpx
+
+namespace gpx {
+// flush_rebinds' gather: one workgroup per rebound slot
+__global__ __launch_bounds__(256) void rebind_gather_kernel(const RebindDesc* desc, int Nmax, int D, double* box) {
+  const RebindDesc d = desc[blockIdx.x];
+  const int tid = threadIdx.x, n = d.n, nx = Nmax * D, nv = n * D;
+  for (int e = tid; e < nx; e += 256) d.dx[e] = e < nv ? d.x[e] : 0.0;
+  for (int e = tid; e < Nmax; e += 256) d.dy[e] = e < n ? d.y[e] : 0.0;
+  if (d.box < 0) return;
+  const int nb = (Nmax + 63) / 64;
+  double* out = box + (size_t)d.box * nb * D * 2;
+  for (int t = tid; t < nb * D; t += 256) {
+    const int k = t / D, q = t - k * D;
+    double lo = INFINITY, hi = -INFINITY;
+    for (int r = k * 64; r < min(n, k * 64 + 64); ++r) {
+      const double v = d.x[(size_t)r * D + q];
+      lo = fmin(lo, v);
+      hi = fmax(hi, v);
+    }
+    out[(size_t)t * 2] = lo;
+    out[(size_t)t * 2 + 1] = hi;
+  }
+}
+
+void launch_rebind_gather(const RebindDesc* desc, int m, int Nmax, int D, double* box, hipStream_t s) {
+  hipLaunchKernelGGL(rebind_gather_kernel, dim3(m), dim3(256), 0, s, desc, Nmax, D, box);
+}
 }  // namespace gpx
 
 #ifdef GPX_BAND_PHASES

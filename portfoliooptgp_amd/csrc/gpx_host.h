@@ -3,6 +3,7 @@
 // building blocks (K build + recursive Cholesky-and-inverse, batched MFMA GEMM).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <memory>
 #include <string>
 #include <vector>
 #include "gpx_internal.h"
@@ -64,6 +65,17 @@ struct gpx_batch {
   int n_dirty = 0;
   int* h_nmeta = nullptr;       // pinned copies of n[] and specs[] for those uploads
   gpx::DevSpec* h_specs = nullptr;
+  // gpx_batch_rebind_device only records the source pointers; flush_rebinds copies every
+  // pending slot (device sources and host-staged ones) with ONE gather kernel that also takes
+  // the per-64-block bounding boxes of X for the band tables (one small download per call)
+  struct PendingRebind { int b, n; const double* x; const double* y; };
+  // the evaluation submitted by gpx_batch_lml_grad_submit, completed by _complete (gpx_api.hip)
+  struct PendingEval;
+  std::unique_ptr<PendingEval> pending_eval;
+  std::vector<PendingRebind> pend;
+  gpx::RebindDesc* h_rdesc = nullptr;   // pinned (coherent), one per slot
+  double* d_box = nullptr;               // [B][nb][D][2] per-block lo/hi of X
+  double* h_box = nullptr;               // pinned mirror of the rows of one flush
   // per-call I/O in ONE device block mirrored by ONE pinned host block, laid out
   //   [active: B ints][info: B ints][bandp: B ints][theta: B×16][results: B×kResStride]
   // so an evaluation uploads [active, info=0, theta] in one DMA and downloads [info ..
@@ -159,6 +171,8 @@ GemmArgs gemm_args(const double* A, int lda, const double* B, int ldb, double* C
                    double beta);
 void chol_inv(const Run& r, int off, int n, int depth = 0);
 void band_tables(gpx_batch* bt, int b, const double* hostX);  // fills band_rmin for problem b
+// the same from per-64-block boxes of X ([nb][D][2]: lo, hi over the block's valid rows)
+void band_tables_boxes(gpx_batch* bt, int b, const double* box);
 int band_width(const gpx_batch* bt, int b, const double* theta_row);  // p in 64-blocks, or -1
 bool band_shape(const gpx_batch* bt);  // the banded path handles this batch's padded size
 int band_limit(const gpx_batch* bt);  // largest p the banded path takes (-1: path disabled)
@@ -169,6 +183,27 @@ void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W 
 void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                   hipStream_t s);
-int flush_rebinds(gpx_batch* bt, hipStream_t s);  // staged rebinds -> device (DMA, on s)
+int flush_rebinds(gpx_batch* bt, hipStream_t s);  // pending rebinds -> device (one gather on s)
+int ensure_rebind_meta(gpx_batch* bt);             // pinned n/spec mirrors + dirty flags
 
 }  // namespace gpx
+
+// State of a submitted evaluation between gpx_batch_lml_grad_submit and _complete: the
+// routing, a copy of θ (the factor cache records it), and the timing events
+struct gpx_batch::PendingEval {
+  hipStream_t s = nullptr;
+  int n_active = 0, n_dense = 0, n_band = 0, n_fused = 0, n_fused1 = 0, ng = 0;
+  std::vector<int32_t> order;
+  std::vector<double> theta;
+  std::unique_ptr<gpx::PhaseTimer> total, ct, bp;
+  std::vector<gpx::PhaseTimer> pts;
+  hipEvent_t kev[2] = {nullptr, nullptr};
+  hipEvent_t fq[4] = {nullptr, nullptr, nullptr, nullptr};
+  ~PendingEval() {
+    for (auto x : kev)
+      if (x) (void)hipEventDestroy(x);
+    for (auto x : fq)
+      if (x) (void)hipEventDestroy(x);
+  }
+};
+

@@ -139,6 +139,15 @@ struct BandContractArgs {
   int Np, p;
 };
 // fused per-problem sweep for band width p <= 2 (gpx_band.hip: band_fwd_kernel, band_bwd_kernel)
+// one slot rebind of flush_rebinds' gather: n rows of X [n][D] and Y [n] from x / y (device
+// memory or pinned host staging) into the slot's dx [Nmax][D] / dy [Nmax] (zero padded); with
+// box >= 0 also the per-64-block lo/hi of X into box row `box` of the batch's box table
+struct RebindDesc {
+  const double* x; const double* y; double* dx; double* dy;
+  int n; int box;
+};
+void launch_rebind_gather(const RebindDesc* desc, int m, int Nmax, int D, double* box, hipStream_t s);
+
 struct BandFusedArgs {
   const int* active; const int* bandp;           // per-problem band width p (64-blocks), <= 2
   double* K; double* L; double* W; long long sMat;

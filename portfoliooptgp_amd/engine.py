@@ -110,6 +110,7 @@ class Engine:
         self.handle = h
         self.n_params = np.asarray([s.n_params for s in specs], dtype=np.int64)
         self.eval_count = 0
+        self._rebound = {}  # slot -> device tensors of its last rebind (kept alive for the gather)
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -148,6 +149,41 @@ class Engine:
                                          self._stream())
         if rc not in (N.GPX_OK, N.GPX_NOT_PD):
             raise N.GPXError(f"gpx_batch_lml_grad failed ({rc}): {self.ctx.last_error()}")
+        self.eval_count += len(act)
+        return lml, grad, info
+
+    def lml_grad_submit(self, active: Sequence[int], theta: np.ndarray):
+        """First half of lml_grad: enqueue the evaluation on the current stream and return at
+        once (gpx_batch_lml_grad_submit); lml_grad_complete() waits and returns what lml_grad
+        would. Lets one host thread keep several engines' evaluations in flight."""
+        act = self._active(active)
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        assert theta.shape == (self.B, N.GPX_THETA_STRIDE)
+        lml = np.full(self.B, np.nan)
+        grad = np.full((self.B, N.GPX_THETA_STRIDE), np.nan)
+        info = np.zeros(self.B, dtype=np.int32)
+        act = screen_theta(act, theta, self.n_params, info)
+        self._submitted = (act, lml, grad, info)
+        if len(act) == 0:
+            return
+        ip = ctypes.POINTER(ctypes.c_int32)
+        rc = self.lib.gpx_batch_lml_grad_submit(self.handle, len(act), act.ctypes.data_as(ip),
+                                                theta.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                                self._stream())
+        if rc != N.GPX_OK:
+            self._submitted = None
+            raise N.GPXError(f"gpx_batch_lml_grad_submit failed ({rc}): {self.ctx.last_error()}")
+
+    def lml_grad_complete(self):
+        act, lml, grad, info = self._submitted
+        self._submitted = None
+        if len(act) == 0:
+            return lml, grad, info
+        dp = ctypes.POINTER(ctypes.c_double)
+        rc = self.lib.gpx_batch_lml_grad_complete(self.handle, lml.ctypes.data_as(dp), grad.ctypes.data_as(dp),
+                                                  info.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        if rc not in (N.GPX_OK, N.GPX_NOT_PD):
+            raise N.GPXError(f"gpx_batch_lml_grad_complete failed ({rc}): {self.ctx.last_error()}")
         self.eval_count += len(act)
         return lml, grad, info
 
@@ -230,10 +266,11 @@ class Engine:
         return ([mean[b, : self.n[b]] for b in act], [var[b, : self.n[b]] for b in act], info)
 
     def rebind(self, b: int, X, Y, spec: N.GpxKernelSpec) -> None:
-        """Load a new problem into slot b (continuous batching). The inputs go through the host
-        (gpx_batch_rebind_host: DMA copies ordered on the current stream), so a rebind does not
-        wait for compute units held by other streams' kernels the way device-to-device copies
-        (blit kernels) do."""
+        """Load a new problem into slot b (continuous batching). Host inputs are staged in
+        pinned memory at once (gpx_batch_rebind_host); device tensors are only recorded
+        (gpx_batch_rebind_device) and gathered, with every other slot rebound since, by one
+        kernel at the start of the next device call — so the slot keeps a reference to them
+        until it is rebound again."""
         ok_dev = (isinstance(X, torch.Tensor) and isinstance(Y, torch.Tensor) and X.is_cuda and Y.is_cuda
                   and X.device.index == self.device and Y.device.index == self.device
                   and X.dtype == torch.float64 and Y.dtype == torch.float64)
@@ -258,6 +295,10 @@ class Engine:
                 ctypes.c_void_p(y.data_ptr() if ok_dev else y.ctypes.data), ctypes.byref(spec), self._stream())
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_rebind failed ({rc}): {self.ctx.last_error()}")
+        if ok_dev:
+            self._rebound[b] = (x, y)  # read by the deferred gather
+        else:
+            self._rebound.pop(b, None)
 
     def reset_timing(self) -> None:
         self.lib.gpx_batch_reset_timing(self.handle)

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import sys
 import queue
 import threading
 import time
@@ -609,6 +610,22 @@ class _SteppedDriver:
     def run(self):
         G = len(self.groups)
         errs = []
+        # the groups' host work shares the GIL: a thread whose device call has returned must not
+        # wait out another group's whole 5 ms switch interval before stepping its fits
+        # several device batches: one host thread submits and completes their evaluations in
+        # turn (GPX_PIPELINE=0: one thread per batch instead)
+        if (G > 1 and os.environ.get("GPX_PIPELINE", "1") != "0"
+                and all(hasattr(e, "lml_grad_submit") for e, _, _, _ in self.groups)):
+            try:
+                self._pipeline()
+            finally:
+                self.first_call.set()
+            return
+        self._run_groups(G, errs)
+        if errs:
+            raise errs[0]
+
+    def _run_groups(self, G, errs):
 
         def run_group(g):
             try:
@@ -624,8 +641,6 @@ class _SteppedDriver:
         run_group(0)
         for t in helpers:
             t.join()
-        if errs:
-            raise errs[0]
 
     def _serve(self, g: int):
         eng, rows, lock, stream = self.groups[g]
@@ -662,115 +677,168 @@ class _SteppedDriver:
             th = self._theta[id(eng)] = np.ones((eng.B, N.GPX_THETA_STRIDE))
         return th
 
+    class _Group:
+        """One device batch's host-side state: its slots, active fits and current request."""
+
+        def __init__(self, drv, g, eng, rows, lock, stream):
+            self.g, self.eng, self.lock, self.stream = g, eng, lock, stream
+            self.free = list(rows) if not drv.fixed else []
+            self.active = {}
+            if drv.fixed:
+                for r in rows:
+                    if r < len(drv.models):
+                        try:
+                            self.active[r] = drv._bind(r, eng, r, lock)
+                        except BaseException as e:
+                            drv.errors[r] = e
+            self.theta = drv._theta_of(eng)
+            self.n_calls = 0
+            self.act = self.packs = None
+            self.t_call = 0.0
+
+    def _tick(self, key, t0):
+        if self.stats is not None:
+            self.stats[key] = self.stats.get(key, 0.0) + (time.perf_counter() - t0)
+
+    def _prepare(self, gs) -> bool:
+        """Fill free slots from the queue, then the θ rows of every active fit's requested
+        point. False when the group has nothing left to evaluate."""
+        clk = time.perf_counter
+        t0 = clk()
+        while gs.free:
+            i = self._next()
+            if i is None:
+                break
+            r = gs.free.pop(0)
+            try:
+                gs.active[r] = self._bind(i, gs.eng, r, gs.lock)
+            except BaseException as e:
+                self.errors[i] = e
+                self.models[i]._engine = None
+                gs.free.insert(0, r)
+        if not gs.active:
+            return False
+        self._tick("bind", t0)
+        t0 = clk()
+        lib = N.load_library()
+        active = gs.active
+        gs.act = sorted(active)
+        # θ rows of every requested point in one native call per variable layout (the same
+        # libm softplus as Parameter.value, so the values are those of the per-model path)
+        layouts = {}
+        for r in gs.act:
+            layouts.setdefault(active[r]["key"], []).append(r)
+        gs.packs = []
+        for key, rs in layouts.items():
+            s0 = active[rs[0]]
+            P = key[0]
+            U = np.array([active[r]["st"].x for r in rs], dtype=np.float64).reshape(len(rs), P)
+            R = np.asarray(rs, dtype=np.int32)
+            lib.gpx_host_theta_rows(len(rs), P, U.ctypes.data, R.ctypes.data, s0["cols"].ctypes.data,
+                                    s0["lower"].ctypes.data, gs.theta.ctypes.data)
+            gs.packs.append((rs, P, U, R, s0["cols"]))
+        self._tick("theta", t0)
+        return True
+
+    def _consume(self, gs, lml, grad, info, t_call_end):
+        """Hand every fit its (loss, grad), predict + release the finished ones."""
+        clk = time.perf_counter
+        lib = N.load_library()
+        eng, active = gs.eng, gs.active
+        t0 = clk()
+        gs.n_calls += 1
+        done = []
+        for rs, P, U, R, cols in gs.packs:
+            loss = np.empty(len(rs))
+            gu = np.empty((len(rs), P))
+            lib.gpx_host_loss_grad_u(len(rs), P, U.ctypes.data, R.ctypes.data, cols.ctypes.data,
+                                     lml.ctypes.data, grad.ctypes.data, loss.ctypes.data, gu.ctypes.data)
+            for k, r in enumerate(rs):
+                s = active[r]
+                try:
+                    if info[r] != 0:
+                        if info[r] == N.INFO_BAD_THETA:
+                            err = N.InvalidParameterError(
+                                f"model {s['i']}: hyperparameters out of (0, inf): {gs.theta[r, :eng.n_params[r] + 1]}")
+                        else:
+                            err = N.NotPositiveDefiniteError(
+                                f"Cholesky decomposition was not successful (model {s['i']}, pivot "
+                                f"{int(info[r])}): K + noise I is not positive definite", info[r])
+                        if not self.as_inf:
+                            raise err
+                        s["st"].tell(float("inf"), np.zeros(P))
+                    else:
+                        s["st"].tell(float(loss[k]), gu[k])
+                except BaseException as e:
+                    self.errors[s["i"]] = e
+                    done.append((r, False))
+                    continue
+                if s["st"].done:
+                    done.append((r, True))
+        self._tick("steps", t0)
+        t_steps = clk()
+        self._finish(eng, gs.lock, active, done)
+        self._tick("finish", t_steps)
+        if self.trace is not None:  # GPX_TRACE_ROUNDS: (group, call start, call end, steps end, finish end, n)
+            self.trace.append((gs.g, gs.t_call, t_call_end, t_steps, clk(), len(gs.act)))
+        if self.stats is not None:
+            self.stats["rounds"] = self.stats.get("rounds", 0) + 1
+            self.stats["fit_evals"] = self.stats.get("fit_evals", 0) + len(gs.act)
+        for r, _ in done:
+            del active[r]
+            if not self.fixed:
+                gs.free.append(r)
+
     def _loop(self, g: int, eng, rows, lock):
         G = len(self.groups)
-        free = list(rows) if not self.fixed else []
-        active = {}
-        if self.fixed:
-            for r in rows:
-                if r < len(self.models):
-                    try:
-                        active[r] = self._bind(r, eng, r, lock)
-                    except BaseException as e:
-                        self.errors[r] = e
-        lib = N.load_library()
-        theta = self._theta_of(eng)
-        n_calls = 0
-        st = self.stats
-        clk = time.perf_counter
-
-        def tick(key, t0):
-            if st is not None:
-                st[key] = st.get(key, 0.0) + (clk() - t0)
+        gs = self._Group(self, g, eng, rows, lock, None)
         while True:
-            t0 = clk()
-            while free:
-                i = self._next()
-                if i is None:
-                    break
-                r = free.pop(0)
-                try:
-                    active[r] = self._bind(i, eng, r, lock)
-                except BaseException as e:
-                    self.errors[i] = e
-                    self.models[i]._engine = None
-                    free.insert(0, r)
-            if not active:
+            if not self._prepare(gs):
                 return
-            if g > 0 and n_calls == 0 and G > 1:
+            if g > 0 and gs.n_calls == 0 and G > 1:
                 # stagger: start g/G of a group-0 call after group 0's first call returns, so the
                 # concurrent batches run out of phase (one's latency-bound recursion levels under
                 # the other's large GEMMs); started in phase they stay in phase
                 self.first_call.wait(timeout=10.0)
                 time.sleep(self.first_call_s * g / G)
-            tick("bind", t0)
-            t0 = clk()
-            act = sorted(active)
-            # θ rows of every requested point in one native call per variable layout (the same
-            # libm softplus as Parameter.value, so the values are those of the per-model path)
-            layouts = {}
-            for r in act:
-                layouts.setdefault(active[r]["key"], []).append(r)
-            packs = []
-            for key, rs in layouts.items():
-                s0 = active[rs[0]]
-                P = key[0]
-                U = np.array([active[r]["st"].x for r in rs], dtype=np.float64).reshape(len(rs), P)
-                R = np.asarray(rs, dtype=np.int32)
-                lib.gpx_host_theta_rows(len(rs), P, U.ctypes.data, R.ctypes.data, s0["cols"].ctypes.data,
-                                        s0["lower"].ctypes.data, theta.ctypes.data)
-                packs.append((rs, P, U, R, s0["cols"]))
-            if self.trace is not None:
-                self.trace.append((time.perf_counter(), len(act)))
-            tick("theta", t0)
-            t_call = time.perf_counter()
+            gs.t_call = time.perf_counter()
             with lock:
-                lml, grad, info = eng.lml_grad(act, theta)
-            tick("device_call", t_call)
-            t0 = clk()
-            if g == 0 and n_calls == 0:
-                self.first_call_s = time.perf_counter() - t_call
+                lml, grad, info = eng.lml_grad(gs.act, gs.theta)
+            self._tick("device_call", gs.t_call)
+            t_end = time.perf_counter()
+            if g == 0 and gs.n_calls == 0:
+                self.first_call_s = t_end - gs.t_call
                 self.first_call.set()
-            n_calls += 1
-            done = []
-            for rs, P, U, R, cols in packs:
-                loss = np.empty(len(rs))
-                gu = np.empty((len(rs), P))
-                lib.gpx_host_loss_grad_u(len(rs), P, U.ctypes.data, R.ctypes.data, cols.ctypes.data,
-                                         lml.ctypes.data, grad.ctypes.data, loss.ctypes.data, gu.ctypes.data)
-                for k, r in enumerate(rs):
-                    s = active[r]
-                    try:
-                        if info[r] != 0:
-                            if info[r] == N.INFO_BAD_THETA:
-                                err = N.InvalidParameterError(
-                                    f"model {s['i']}: hyperparameters out of (0, inf): {theta[r, :eng.n_params[r] + 1]}")
-                            else:
-                                err = N.NotPositiveDefiniteError(
-                                    f"Cholesky decomposition was not successful (model {s['i']}, pivot "
-                                    f"{int(info[r])}): K + noise I is not positive definite", info[r])
-                            if not self.as_inf:
-                                raise err
-                            s["st"].tell(float("inf"), np.zeros(P))
-                        else:
-                            s["st"].tell(float(loss[k]), gu[k])
-                    except BaseException as e:
-                        self.errors[s["i"]] = e
-                        done.append((r, False))
-                        continue
-                    if s["st"].done:
-                        done.append((r, True))
-            tick("steps", t0)
-            t0 = clk()
-            self._finish(eng, lock, active, done)
-            tick("finish", t0)
-            if st is not None:
-                st["rounds"] = st.get("rounds", 0) + 1
-                st["fit_evals"] = st.get("fit_evals", 0) + len(act)
-            for r, _ in done:
-                del active[r]
-                if not self.fixed:
-                    free.append(r)
+            self._consume(gs, lml, grad, info, t_end)
+
+    def _pipeline(self):
+        """All groups from ONE host thread: each group's evaluation is submitted
+        (Engine.lml_grad_submit, on the group's stream) and completed in turn, so a group's
+        host work (steps, predicts, rebinds) overlaps the other groups' device work without
+        the threads' GIL hand-offs."""
+        gss = [self._Group(self, g, e, rows, lk, stm) for g, (e, rows, lk, stm) in enumerate(self.groups)]
+        inflight = []
+
+        def submit(gs):
+            if not self._prepare(gs):
+                return False
+            gs.t_call = time.perf_counter()
+            with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():
+                gs.eng.lml_grad_submit(gs.act, gs.theta)
+            return True
+        for gs in gss:
+            if submit(gs):
+                inflight.append(gs)
+        while inflight:
+            gs = inflight.pop(0)
+            t0 = time.perf_counter()
+            lml, grad, info = gs.eng.lml_grad_complete()
+            t_end = time.perf_counter()
+            self._tick("device_wait", t0)
+            with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():
+                self._consume(gs, lml, grad, info, t_end)
+                if submit(gs):
+                    inflight.append(gs)
 
     def _finish(self, eng, lock, active, done):
         pred_rows, xs = [], []

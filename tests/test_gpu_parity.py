@@ -622,3 +622,40 @@ def test_shared_context_two_threads_with_split_pipelines():
         assert r0.nfev == r1.nfev
         assert r1.fun == pytest.approx(r0.fun, rel=1e-9)
         np.testing.assert_allclose(r1.x, r0.x, rtol=1e-7)
+
+
+def test_deferred_device_rebinds_match_fresh_engines():
+    """gpx_batch_rebind_device only records the sources; the next device call gathers every
+    pending slot in one kernel and takes the band tables from device-side block boxes. Mixed
+    device / host rebinds of the same slot, a non-contiguous source (a temporary the engine
+    keeps alive) and several rebinds before one call all give the fresh engines' results —
+    banded (ℓ small on day-offset inputs) and dense alike."""
+    from portfoliooptgp_amd.kernels import compile_spec
+    dev = torch.device("cuda:0")
+    n = 1024
+    series = [O.synthetic_series(n - 64 * i, seed=200 + i) for i in range(5)]
+    spec = compile_spec(K.SquaredExponential(), 1)
+    base = [(np.arange(n, dtype=np.float64), np.zeros(n))] * 3
+    eng = Engine([b[0] for b in base], [b[1] for b in base], [spec] * 3)
+    # slot 0: host then device (device wins); slot 1: device then host (host wins);
+    # slot 2: a non-contiguous device view, rebound twice before the call
+    x0, y0 = series[0]
+    eng.rebind(0, x0, y0, spec)
+    eng.rebind(0, torch.as_tensor(series[1][0], device=dev), torch.as_tensor(series[1][1], device=dev), spec)
+    eng.rebind(1, torch.as_tensor(series[2][0], device=dev), torch.as_tensor(series[2][1], device=dev), spec)
+    eng.rebind(1, series[3][0], series[3][1], spec)
+    wide = torch.as_tensor(np.stack([series[4][0], series[4][0]], 1), device=dev)
+    eng.rebind(2, torch.as_tensor(series[0][0], device=dev), torch.as_tensor(series[0][1], device=dev), spec)
+    eng.rebind(2, wide[:, 0], torch.as_tensor(series[4][1], device=dev), spec)
+    del wide
+    expect = [series[1], series[3], series[4]]
+    for ell in (1.0, 40.0):          # banded (p = 1) and dense
+        th = np.zeros((3, N.GPX_THETA_STRIDE))
+        th[:, :3] = [ell, 1.3, 1e-3]
+        lml, g, info = eng.lml_grad([0, 1, 2], th)
+        assert (info == 0).all()
+        for b, (x, y) in enumerate(expect):
+            ref = Engine([x], [y], [spec])
+            l0, g0, _ = ref.lml_grad([0], th[b:b + 1])
+            assert lml[b] == pytest.approx(l0[0], rel=1e-11)
+            np.testing.assert_allclose(g[b, :3], g0[0, :3], rtol=1e-9, atol=1e-9)

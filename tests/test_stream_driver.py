@@ -224,3 +224,30 @@ def test_stream_uses_every_engine_row(width, engines_b, expect):
     for r, r0 in zip(res, ref):
         assert r.nfev == r0.nfev
         np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+
+
+class AsyncFakeEngine(FakeEngine):
+    """FakeEngine with the submit / complete halves: the driver then steps every group from
+    one host thread (optimizers._SteppedDriver._pipeline)."""
+
+    def lml_grad_submit(self, rows, theta):
+        self._sub = self.lml_grad(rows, theta.copy())
+
+    def lml_grad_complete(self):
+        out, self._sub = self._sub, None
+        return out
+
+
+@pytest.mark.parametrize("width,engines", [(4, 2), (6, 3), (5, 2)])
+def test_pipelined_groups_equal_solo(width, engines):
+    ms = _models(13)
+    ref = [_solo(m) for m in _models(13)]
+    per = -(-width // engines)
+    eng = [AsyncFakeEngine(per) for _ in range(engines)]
+    res, preds = gpx.optimizers.Scipy().minimize_stream(ms, width=width, engine=eng, groups=engines,
+                                                        predict_train=True)
+    for r, r0, m, p in zip(res, ref, ms, preds):
+        assert r.nfev == r0.nfev
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+        assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
+    assert sum(sum(e.calls) for e in eng) == sum(r.nfev for r in res)
