@@ -133,17 +133,33 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
     }
 
 
-def band_traffic(problems_per_launch):
-    """HBM bytes per launch of the banded roofline kernel from the committed PMC summary
-    (profiles/<round>_band_traffic.json, tools/pmc_summary.py ... band_bwd1_kernel): bytes per
-    problem x the launch's problem count. None when absent."""
+def band_traffic(kernel_key, problems_per_launch):
+    """HBM bytes per launch of the banded roofline kernel from the committed PMC summary of
+    THAT kernel (profiles/<round>_band*_traffic.json whose "kernel" names kernel_key, written by
+    tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE passes): bytes per problem x
+    the launch's problem count. None when absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                          "*_band_traffic.json")))
+    root = os.path.dirname(os.path.abspath(__file__))
+    files = []
+    for f in sorted(glob.glob(os.path.join(root, "profiles", "*_band*traffic.json"))):
+        d = json.load(open(f))
+        if any(kernel_key in k for k in d.get("kernel", [])):
+            files.append((f, d))
     if not files:
         return None, None
-    d = json.load(open(files[-1]))
-    return d["hbm_bytes_per_problem"] * problems_per_launch, os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+    f, d = files[-1]
+    return d["hbm_bytes_per_problem"] * problems_per_launch, os.path.relpath(f, root)
+
+
+def band_problem_flops(n, p, fwd):
+    """2·64³ block-product flops of one problem's fused sweep (gpx_api.hip band_fused_flops)."""
+    U = 2.0 * 64 ** 3
+    nb = (n + 63) // 64
+    f = 0.0
+    for k in range(nb):
+        q = min(p, nb - 1 - k)
+        f += (2.0 / 3.0 + q + q * (q + 1) / 2.0) * U if fwd else (1.0 + q + q * q + q) * U
+    return f
 
 
 def contract_traffic(n, flops_per_launch):
@@ -172,10 +188,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 256)),
                     help="independent series fitted per GPU per step")
-    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 512)),
+    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 576)),
                     help="resident device slots (continuous-batching width)")
-    ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 2)),
-                    help="alternating device batches (host/device overlap)")
+    ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 3)),
+                    help="device batches kept in flight by the one host thread (host/device overlap)")
     ap.add_argument("--points", "--n", dest="n", type=int, default=N_POINTS,
                     help="points per series (use --points under torch.distributed.run, whose parser takes --n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -325,11 +341,11 @@ def main():
     # fused K⁻¹ + gradient contraction
     band_kernels = {
         "band_fwd1_kernel (p<=1 class: banded Cholesky + z solve, one workgroup per problem)":
-            (tm.band_fwd_ms_total, tm.band_fwd_flops),
+            (tm.band_fwd_ms_total, tm.band_fwd_flops, "band_fwd1_kernel", True),
         "band_bwd1_kernel<1> (p<=1 class: selected inversion + alpha solve + gradient contraction)":
-            (tm.band_bwd_ms_total, tm.band_bwd_flops),
+            (tm.band_bwd_ms_total, tm.band_bwd_flops, "band_bwd1_kernel", False),
     }
-    kname, (kms, kflops) = max(band_kernels.items(), key=lambda kv: kv[1][0])
+    kname, (kms, kflops, kkey, kfwd) = max(band_kernels.items(), key=lambda kv: kv[1][0])
     if kms > tm.contract_ms_total:
         launches = tm.band_fused_launches
         b_ms = kms / max(launches, 1.0)
@@ -337,7 +353,8 @@ def main():
         b_ach = b_flops / (b_ms * 1e-3) / 1e12 if b_ms > 0 else 0.0
         # problems per timed launch: its flops / one p-weighted problem's (mean p of the class)
         from_p = tm.band_p_sum / max(tm.band_evals, 1.0)
-        b_traffic, b_src = band_traffic(tm.band_evals / max(tm.band_calls, 1.0))
+        # problems per timed launch (the p <= 1 class): its flops / one p = 1 problem's
+        b_traffic, b_src = band_traffic(kkey, b_flops / band_problem_flops(n, 1, kfwd))
         roofline = {
             "kernel": kname, "bound": "mfma", "achieved": b_ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": b_ach / FP64_PEAK_TFLOPS, "traffic": b_traffic, "traffic_source": b_src,
@@ -347,7 +364,7 @@ def main():
                      "workgroup (one CU) per problem; achieved = the 64^3 block products issued "
                      "(2*64^3 flops each, leaf 2/3 of one) / launch duration. The chain of "
                      "dependent block steps, not MFMA or HBM throughput, sets the duration "
-                     "(DESIGN.md §3c); traffic: profiles/<round>_band_traffic.json"),
+                     "(DESIGN.md §3c); traffic: the kernel's profiles/<round>_band*_traffic.json"),
             "dense_contraction_isolated": iso, "dense_contraction_frac_isolated": iso / FP64_PEAK_TFLOPS if iso else None,
         }
     else:

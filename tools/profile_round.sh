@@ -23,9 +23,10 @@ timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/writ
 timeout -s KILL 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE \
   --output-format csv -d "$OUT/mfma" -o run -- python3 "$ROOT/bench.py" $SHORT > "$OUT/mfma.log" 2>&1
 cd "$ROOT"
-python3 tools/pmc_summary.py "$OUT/fetch" "$OUT/write" 4096 "$OUT/band_traffic.json" band_bwd1_kernel > /dev/null
+python3 tools/pmc_summary.py "$OUT/fetch" "$OUT/write" 4096 "$OUT/band_bwd1_traffic.json" band_bwd1_kernel > /dev/null
 python3 tools/pmc_summary.py "$OUT/fetch" "$OUT/write" 4096 "$OUT/band_fwd1_traffic.json" band_fwd1_kernel > /dev/null
 python3 tools/mfma_summary.py "$OUT/mfma" "$OUT/mfma_summary.csv" > "$OUT/mfma_summary.txt"
 python3 tools/trace_check.py "$OUT/trace/run_kernel_trace.csv" "$OUT/trace.log" "$OUT/trace_check.json" > /dev/null
+python3 tools/trace_util.py "$OUT/trace/run_kernel_trace.csv" 0.2 > "$OUT/trace_util.txt"
 tail -1 "$OUT/bench.log"
 find "$OUT" -name "*.csv" -size +1M -exec gzip -f {} \;
