@@ -626,7 +626,7 @@ __global__ __launch_bounds__(256, 1) void band_fwd_kernel(BandFusedArgs a) {
     if (tid < 64) sv[0][tid] = yk + sv[1][tid];
     __syncthreads();
     PH(0);
-    leaf64_lds(sA, sW, ldiag + k64, &sfail);
+    leaf64_lds<false>(sA, sW, ldiag + k64, &sfail);
     PH(1);
     if (tid == 0 && sfail >= 0) {
       if (gfail == 0) gfail = k64 + sfail + 1;
@@ -723,6 +723,10 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
   const int n = a.nvalid[b], D = a.D;
   const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
   if (tid < 64) { sal[1][tid] = 0.0; sal[2][tid] = 0.0; sres[0][tid] = sres[1][tid] = sres[2][tid] = 0.0; }
+  {  // the forward sweep left L_ii in ldiag: log det's terms (read by the reduce kernel)
+    double* ldg = a.ldiag + (long long)b * a.sVec;
+    for (int e = tid; e < Np; e += 256) ldg[e] = log(ldg[e]);
+  }
   if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
   __syncthreads();
   const DevSpec spec = a.specs[b];
@@ -952,7 +956,7 @@ namespace gpx {
 
 // The trailing-updated diagonal block A_{k+1,k+1} stays in the SYRK's fragment and is the next
 // leaf's input (no global round trip); the original blocks A_{k+1,k} and A_{k+1,k+1} are
-// fetched as soon as the leaf is done (the leaf needs every register it can get).
+// fetched during the leaf's inverse phase (its diagonal chain needs every register it can get).
 __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
   __shared__ __attribute__((aligned(16))) double sA[64 * BS];   // A_kk -> (leaf) -> A_{k+1,k} -> P
   __shared__ __attribute__((aligned(16))) double sW[64 * BS];   // W_kk
@@ -989,18 +993,23 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
     if (tid < 64) sv[0][tid] = yk + sv[1][tid];
     __syncthreads();
     PH(0);
-    leaf64_lds(sA, sW, ldiag + k64, &sfail);
+    // this step's panel block and the next diagonal block, in flight during the leaf's inverse
+    leaf64_lds<false>(sA, sW, ldiag + k64, &sfail, [&]() {
+      if (q >= 1) block_fetch(pa, K + (long long)(k64 + 64) * ld + k64, ld);
+      if (k + 1 < nb) frag_load_global(nxt, K + (long long)(k64 + 64) * ld + k64 + 64, ld);
+    });
     PH(1);
-    if (q >= 1) block_fetch(pa, K + (long long)(k64 + 64) * ld + k64, ld);
-    if (k + 1 < nb) frag_load_global(nxt, K + (long long)(k64 + 64) * ld + k64 + 64, ld);
     if (tid == 0 && sfail >= 0) {
       if (gfail == 0) gfail = k64 + sfail + 1;
       sfail = -1;
     }
     // W_kk -> global (the backward sweep reads it); z_k partials; the panel block -> sA
     {
-      double* Wk = W + (long long)k64 * ld + k64;
-      for (int e = tid; e < 4096; e += 256) Wk[(e >> 6) * Np + (e & 63)] = sW[(e >> 6) * BS + (e & 63)];
+      const int t = tid_fresh();
+      double* Wk = W + (long long)k64 * ld + k64 + (t >> 6) * Np + (t & 63);
+      const double* sWt = sW + (t >> 6) * BS + (t & 63);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) Wk[4 * u * Np] = sWt[4 * u * BS];
     }
     {
       double s = 0.0;
@@ -1071,6 +1080,10 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
   const int n = a.nvalid[b], D = a.D, nx = 64 * D;
   const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
   if (tid < 64) { sal[0][tid] = sal[1][tid] = 0.0; sres[0][tid] = sres[1][tid] = 0.0; }
+  {  // the forward sweep left L_ii in ldiag: log det's terms (read by the reduce kernel)
+    double* ldg = a.ldiag + (long long)b * a.sVec;
+    for (int e = tid; e < Np; e += 256) ldg[e] = log(ldg[e]);
+  }
   if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
   // the first step's inputs (k = nb − 1 has no panel)
   double pw[16], pp[16];

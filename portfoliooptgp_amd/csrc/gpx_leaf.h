@@ -44,13 +44,14 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // trip as readlane_d needs). k must fold to a constant (unrolled loops); rows of 16 lanes that
 // hold the same 16 values (lane & 15) all see lane k's.
 __device__ __forceinline__ double bc16(double v, int k) {
+// mov_dpp (no "old" operand: every lane is written, so no zeroing move per broadcast)
 #define GPX_BC16(K) \
   case K:           \
-    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + K, 0xf, 0xf, false);
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + K, 0xf, 0xf, true);
   switch (k) {
     GPX_BC16(0) GPX_BC16(1) GPX_BC16(2) GPX_BC16(3) GPX_BC16(4) GPX_BC16(5) GPX_BC16(6) GPX_BC16(7)
     GPX_BC16(8) GPX_BC16(9) GPX_BC16(10) GPX_BC16(11) GPX_BC16(12) GPX_BC16(13) GPX_BC16(14)
-    default: return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + 15, 0xf, 0xf, false);
+    default: return __builtin_amdgcn_mov_dpp(v, 0x150 + 15, 0xf, 0xf, true);
   }
 #undef GPX_BC16
 }
@@ -70,11 +71,24 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // destroyed. Writes log L_ii to ldiag[0..63]; *sfail (LDS, -1 on entry) gets the first
 // failing local pivot. 256 threads; ends with a barrier.
 constexpr int kLeafS = 66;  // row stride (doubles): 16 rows x 1 col fragment reads are conflict-free
+// pre_inverse() is called by every thread between the factorisation and the W = L⁻¹ block
+// rows: a caller issues its next global loads there, when the diagonal factor's registers
+// are free again.
+struct LeafNoHook {
+  __device__ void operator()() const {}
+};
+// kLog = false: ldiag gets L_ii itself (the banded sweeps take the logs once per problem, in
+// their backward kernels, instead of on every step's critical path)
+template <bool kLog = true, class PreInverse = LeafNoHook>
 __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __restrict__ sW,
-                                           double* __restrict__ ldiag, int* sfail) {
+                                           double* __restrict__ ldiag, int* sfail,
+                                           PreInverse pre_inverse = PreInverse()) {
   constexpr int S = kLeafS;
   typedef double d4 __attribute__((ext_vector_type(4)));
-  const int tid = threadIdx.x;
+  // threadIdx.x through an empty asm: the leaf's LDS addresses are formed per call instead of
+  // being hoisted out of a caller's block-step loop (where they would pin registers and spill)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, l4 = lane >> 4;
   LEAF_PH_BEGIN
@@ -114,7 +128,10 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
       if (lane < 16) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sW[(c0 + i) * S + c0 + lane] = w[i];
-        sA[(c0 + lane) * S + c0 + lane] = r[lane & 15];   // L_ii, for log det at the end
+        if (kLog)
+          sA[(c0 + lane) * S + c0 + lane] = r[lane & 15];   // L_ii, for log det at the end
+        else
+          ldiag[c0 + lane] = r[lane & 15];
       }
       if (lane == 0 && fail >= 0 && *sfail < 0) *sfail = c0 + fail;
     }
@@ -158,10 +175,11 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
     __syncthreads();
     LEAF_PH(2);
   }
+  pre_inverse();
   // W = L⁻¹: block rows 1..3, blocks j < i in parallel (wave j); the idle wave 3 takes the
   // logs of L's diagonal (left on sA's diagonal by the diagonal steps)
   for (int i = 1; i < 4; ++i) {
-    if (i == 3 && wave == 3) ldiag[lane] = log(sA[lane * S + lane]);
+    if (kLog && i == 3 && wave == 3) ldiag[lane] = log(sA[lane * S + lane]);
     if (wave < i) {
       const int j = wave;
       d4 t = {0.0, 0.0, 0.0, 0.0};
