@@ -162,6 +162,16 @@ int gpx_batch_lml_grad(gpx_batch* batch, int n_active, const int32_t* active, co
 int gpx_batch_lml_grad_submit(gpx_batch* batch, int n_active, const int32_t* active, const double* theta,
                               void* stream);
 int gpx_batch_lml_grad_complete(gpx_batch* batch, double* lml, double* grad, int32_t* info);
+/* 1 when the submitted evaluation (if any) has finished on the device (complete will not
+ * wait), 0 while it runs; < 0 on error. */
+int gpx_batch_lml_grad_query(gpx_batch* batch);
+/*
+ * Host-side routing query: for rows[i] at theta (the gpx_batch_lml_grad layout), the band
+ * width in 64-blocks the evaluation would take (>= 0: the block-banded path), -1 for the
+ * dense path, -2 when the row's band tables are not known yet (a device rebind still waiting
+ * for the next call's gather). No device work.
+ */
+int gpx_batch_band_width(gpx_batch* batch, int n_rows, const int32_t* rows, const double* theta, int32_t* p_out);
 
 /*
  * Posterior marginals at Xnew for the active problems: GPflow GPR.predict_f(full_cov=False)

@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "gpx_version", "gpx_create", "gpx_destroy", "gpx_last_error", "gpx_batch_create", "gpx_batch_rebind_host",
     "gpx_batch_rebind_device",
     "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_lml_grad_submit", "gpx_batch_lml_grad_complete",
+    "gpx_batch_lml_grad_query", "gpx_batch_band_width",
     "gpx_batch_predict", "gpx_batch_predict_full_cov", "gpx_batch_predict_train",
     "gpx_batch_last_timing",
     "gpx_set_profiling", "gpx_batch_reset_timing", "gpx_batch_rebind",
@@ -124,6 +125,10 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_lml_grad_submit.argtypes = [c_void_p, c_int, c_int_p, c_double_p, c_void_p]
         lib.gpx_batch_lml_grad_complete.restype = c_int
         lib.gpx_batch_lml_grad_complete.argtypes = [c_void_p, c_double_p, c_double_p, c_int_p]
+        lib.gpx_batch_lml_grad_query.restype = c_int
+        lib.gpx_batch_lml_grad_query.argtypes = [c_void_p]
+        lib.gpx_batch_band_width.restype = c_int
+        lib.gpx_batch_band_width.argtypes = [c_void_p, c_int, c_int_p, c_double_p, c_int_p]
         lib.gpx_batch_predict.restype = c_int
         lib.gpx_batch_predict.argtypes = [c_void_p, c_int, c_int_p, c_double_p, c_void_p, c_int,
                                           c_int, c_void_p, c_void_p, c_int_p, c_void_p]

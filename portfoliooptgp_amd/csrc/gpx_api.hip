@@ -1126,6 +1126,34 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
 }
 
 
+int gpx_batch_lml_grad_query(gpx_batch* bt) {
+  if (!bt) return GPX_BAD_ARG;
+  if (!bt->pending_eval) return 1;
+  const hipError_t e = hipStreamQuery(bt->pending_eval->s);
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  return fail(bt->ctx, GPX_HIP_ERROR, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+}
+
+int gpx_batch_band_width(gpx_batch* bt, int n_rows, const int32_t* rows, const double* theta, int32_t* p_out) {
+  if (!bt) return GPX_BAD_ARG;
+  if (n_rows < 0 || (n_rows > 0 && (!rows || !theta || !p_out))) return fail(bt->ctx, GPX_BAD_ARG, "bad band-width query");
+  const int plim = band_limit(bt);
+  for (int i = 0; i < n_rows; ++i) {
+    const int b = rows[i];
+    if (b < 0 || b >= bt->B) return fail(bt->ctx, GPX_BAD_ARG, "row out of range");
+    bool pending = false;
+    for (const auto& e : bt->pend) pending = pending || e.b == b;
+    if (pending) {  // its band tables arrive with the next call's gather
+      p_out[i] = -2;
+      continue;
+    }
+    const int p = plim >= 0 ? band_width(bt, b, theta + (size_t)b * GPX_THETA_STRIDE) : -1;
+    p_out[i] = (p >= 0 && p <= plim) ? p : -1;
+  }
+  return GPX_OK;
+}
+
 int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                        double* lml, double* grad, int32_t* info, void* stream) {
   if (!bt) return GPX_BAD_ARG;

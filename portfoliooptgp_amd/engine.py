@@ -174,6 +174,27 @@ class Engine:
             self._submitted = None
             raise N.GPXError(f"gpx_batch_lml_grad_submit failed ({rc}): {self.ctx.last_error()}")
 
+    def lml_grad_ready(self) -> bool:
+        """True when the submitted evaluation has finished on the device."""
+        rc = self.lib.gpx_batch_lml_grad_query(self.handle)
+        if rc < 0:
+            raise N.GPXError(f"gpx_batch_lml_grad_query failed ({rc}): {self.ctx.last_error()}")
+        return rc == 1
+
+    def band_width(self, rows, theta: np.ndarray) -> np.ndarray:
+        """Per row, the band width (64-blocks) its evaluation at theta would take; -1 dense,
+        -2 not known yet (host-side, no device work)."""
+        rows = self._active(rows)
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        out = np.zeros(len(rows), dtype=np.int32)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        rc = self.lib.gpx_batch_band_width(self.handle, len(rows), rows.ctypes.data_as(ip),
+                                           theta.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                           out.ctypes.data_as(ip))
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_batch_band_width failed ({rc}): {self.ctx.last_error()}")
+        return out
+
     def lml_grad_complete(self):
         act, lml, grad, info = self._submitted
         self._submitted = None

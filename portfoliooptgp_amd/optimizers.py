@@ -199,7 +199,7 @@ class Scipy:
                         device: Optional[int] = None, predict_train: bool = False,
                         engine=None, groups: int = 1,
                         predict_inputs: Optional[Sequence] = None, on_not_pd: str = "raise",
-                        **scipy_kwargs):
+                        wide_group: bool = False, **scipy_kwargs):
         """Continuous batching: fit many models through ``width`` resident device slots.
 
         Every model still runs its own unmodified scipy L-BFGS-B; at most ``width`` are
@@ -213,7 +213,11 @@ class Scipy:
         the groups' evaluations run concurrently on the GPU (one group's latency-bound
         phases overlap another's large GEMMs) and one group's host work overlaps the others'
         device work. ``engine`` may be one Engine (groups then alternate on it) or a list of
-        ``groups`` Engines. Returns (results, predictions|None); models are detached afterwards.
+        ``groups`` Engines. ``wide_group``: the last engine only evaluates points whose
+        kernel band is wider than one 64-block (or dense) and the others only narrow ones; a
+        fit moves between them (its series rebound, its L-BFGS-B state kept) when its next
+        point changes class, so the narrow batches' calls never wait for the slower wide
+        sweeps. Returns (results, predictions|None); models are detached afterwards.
         """
         as_inf = _not_pd_policy(on_not_pd)
         models = list(models)
@@ -241,7 +245,7 @@ class Scipy:
         if lbfgsb.supports(method, scipy_kwargs) and not _THREADED:
             drv = _SteppedDriver(models, engines, groups, scipy_kwargs.get("options") or {}, as_inf, D,
                                  predict_train=predict_train or predict_inputs is not None,
-                                 predict_inputs=predict_inputs, width=width)
+                                 predict_inputs=predict_inputs, width=width, wide_group=wide_group)
             drv.run()
             self.last_trace = drv.trace
             self.last_stats = drv.stats
@@ -567,7 +571,7 @@ class _SteppedDriver:
 
     def __init__(self, models, engines, groups: int, options: dict, as_inf: bool, D: int,
                  predict_train: bool = False, predict_inputs=None, width: Optional[int] = None,
-                 fixed: bool = False):
+                 fixed: bool = False, wide_group: bool = False):
         self.models, self.options, self.as_inf, self.D = models, options, as_inf, D
         self.predict_train, self.predict_inputs, self.fixed = predict_train, predict_inputs, fixed
         G = max(1, groups)
@@ -602,6 +606,13 @@ class _SteppedDriver:
         # GPX_DRIVER_STATS=1: wall time per phase (bind, theta, device call, steps, finish) summed
         # over the groups' threads, in Scipy().last_stats
         self.stats = {} if os.environ.get("GPX_DRIVER_STATS") else None
+        # wide_group: the last device batch takes the evaluations whose band is wider than one
+        # 64-block (or dense): a fit is moved between batches (rebind of its series, stepper
+        # state kept) when its next point changes class and the other side has a free slot, so
+        # the narrow batches' calls are not held up by the slower wide sweeps
+        self.wide = (wide_group and not fixed and len(self.groups) > 1
+                     and all(hasattr(e, "band_width") for e, _, _, _ in self.groups))
+        self.moves = 0
 
     def _next(self) -> Optional[int]:
         with self.qlock:
@@ -621,6 +632,7 @@ class _SteppedDriver:
             finally:
                 self.first_call.set()
             return
+        self.wide = False  # class routing needs the one-thread pipeline
         self._run_groups(G, errs)
         if errs:
             raise errs[0]
@@ -692,6 +704,7 @@ class _SteppedDriver:
                         except BaseException as e:
                             drv.errors[r] = e
             self.theta = drv._theta_of(eng)
+            self.wide = drv.wide and g == len(drv.groups) - 1
             self.n_calls = 0
             self.act = self.packs = None
             self.t_call = 0.0
@@ -705,7 +718,7 @@ class _SteppedDriver:
         point. False when the group has nothing left to evaluate."""
         clk = time.perf_counter
         t0 = clk()
-        while gs.free:
+        while gs.free and not gs.wide:
             i = self._next()
             if i is None:
                 break
@@ -722,23 +735,58 @@ class _SteppedDriver:
         t0 = clk()
         lib = N.load_library()
         active = gs.active
-        gs.act = sorted(active)
         # θ rows of every requested point in one native call per variable layout (the same
         # libm softplus as Parameter.value, so the values are those of the per-model path)
-        layouts = {}
-        for r in gs.act:
-            layouts.setdefault(active[r]["key"], []).append(r)
-        gs.packs = []
-        for key, rs in layouts.items():
-            s0 = active[rs[0]]
-            P = key[0]
-            U = np.array([active[r]["st"].x for r in rs], dtype=np.float64).reshape(len(rs), P)
-            R = np.asarray(rs, dtype=np.int32)
-            lib.gpx_host_theta_rows(len(rs), P, U.ctypes.data, R.ctypes.data, s0["cols"].ctypes.data,
-                                    s0["lower"].ctypes.data, gs.theta.ctypes.data)
-            gs.packs.append((rs, P, U, R, s0["cols"]))
+        for moved in (False, True):
+            gs.act = sorted(active)
+            layouts = {}
+            for r in gs.act:
+                layouts.setdefault(active[r]["key"], []).append(r)
+            gs.packs = []
+            for key, rs in layouts.items():
+                s0 = active[rs[0]]
+                P = key[0]
+                U = np.array([active[r]["st"].x for r in rs], dtype=np.float64).reshape(len(rs), P)
+                R = np.asarray(rs, dtype=np.int32)
+                if not moved:
+                    lib.gpx_host_theta_rows(len(rs), P, U.ctypes.data, R.ctypes.data, s0["cols"].ctypes.data,
+                                            s0["lower"].ctypes.data, gs.theta.ctypes.data)
+                gs.packs.append((rs, P, U, R, s0["cols"]))
+            if moved or not self.wide or not self._migrate(gs):
+                break
         self._tick("theta", t0)
-        return True
+        return bool(gs.act)
+
+    def _migrate(self, gs) -> bool:
+        """Move the fits whose requested point belongs to the other class (band width <= 1
+        64-block: narrow; wider or dense: wide) to a free slot of a batch of that class. A fit
+        with no free slot on the other side is evaluated where it is. True if any moved."""
+        pw = gs.eng.band_width(gs.act, gs.theta)
+        moved = False
+        for r, p in zip(gs.act, pw):
+            if p == -2:
+                continue  # band tables not known yet (a rebind waiting for its gather)
+            want_wide = p > 1 or p == -1
+            if want_wide == gs.wide:
+                continue
+            if want_wide:
+                tg = self._gss[-1]
+            else:
+                tg = max((x for x in self._gss if not x.wide), key=lambda x: len(x.free))
+            if not tg.free:
+                continue
+            st = gs.active.pop(r)
+            gs.free.append(r)
+            r2 = tg.free.pop(0)
+            m = st["m"]
+            with tg.lock:
+                tg.eng.rebind(r2, m.data[0], m.data[1], compile_spec(m.kernel, self.D))
+            m._attach(tg.eng, r2)
+            tg.theta[r2] = m.theta_row()
+            tg.active[r2] = st
+            self.moves += 1
+            moved = True
+        return moved
 
     def _consume(self, gs, lml, grad, info, t_call_end):
         """Hand every fit its (loss, grad), predict + release the finished ones."""
@@ -816,7 +864,8 @@ class _SteppedDriver:
         (Engine.lml_grad_submit, on the group's stream) and completed in turn, so a group's
         host work (steps, predicts, rebinds) overlaps the other groups' device work without
         the threads' GIL hand-offs."""
-        gss = [self._Group(self, g, e, rows, lk, stm) for g, (e, rows, lk, stm) in enumerate(self.groups)]
+        gss = self._gss = [self._Group(self, g, e, rows, lk, stm)
+                           for g, (e, rows, lk, stm) in enumerate(self.groups)]
         inflight = []
 
         def submit(gs):
@@ -826,12 +875,31 @@ class _SteppedDriver:
             with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():
                 gs.eng.lml_grad_submit(gs.act, gs.theta)
             return True
+
+        def submit_idle():
+            # groups that are not in flight (e.g. the wide batch before any fit moved in)
+            for x in gss:
+                if x not in inflight and x.active and submit(x):
+                    inflight.append(x)
         for gs in gss:
             if submit(gs):
                 inflight.append(gs)
         while inflight:
-            gs = inflight.pop(0)
+            # complete whichever batch finishes first (the wide batch's calls are longer)
             t0 = time.perf_counter()
+            gs = None
+            while gs is None:
+                for x in inflight:
+                    ready = getattr(x.eng, "lml_grad_ready", None)
+                    if ready is None or ready():
+                        gs = x
+                        break
+                else:
+                    if len(inflight) == 1:
+                        gs = inflight[0]
+                    else:
+                        time.sleep(2e-5)
+            inflight.remove(gs)
             lml, grad, info = gs.eng.lml_grad_complete()
             t_end = time.perf_counter()
             self._tick("device_wait", t0)
@@ -839,6 +907,8 @@ class _SteppedDriver:
                 self._consume(gs, lml, grad, info, t_end)
                 if submit(gs):
                     inflight.append(gs)
+            if self.wide:
+                submit_idle()
 
     def _finish(self, eng, lock, active, done):
         pred_rows, xs = [], []

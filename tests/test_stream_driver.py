@@ -251,3 +251,31 @@ def test_pipelined_groups_equal_solo(width, engines):
         np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
         assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
     assert sum(sum(e.calls) for e in eng) == sum(r.nfev for r in res)
+
+
+class BandFakeEngine(AsyncFakeEngine):
+    """AsyncFakeEngine that also answers the band-width routing query: 'wide' (p = 2) when
+    the requested lengthscale exceeds 1.5, so fits cross between the narrow and wide batches."""
+
+    def band_width(self, rows, theta):
+        return np.array([2 if theta[r, 0] > 1.5 else 1 for r in rows], dtype=np.int32)
+
+    def lml_grad(self, rows, theta):
+        self.classes = getattr(self, "classes", []) + [self.band_width(rows, theta)]
+        return super().lml_grad(rows, theta)
+
+
+def test_wide_group_routing_keeps_trajectories():
+    ms = _models(17)
+    ref = [_solo(m) for m in _models(17)]
+    eng = [BandFakeEngine(4), BandFakeEngine(4), BandFakeEngine(3)]
+    opt = gpx.optimizers.Scipy()
+    res, preds = opt.minimize_stream(ms, width=11, engine=eng, groups=3, predict_train=True, wide_group=True)
+    for r, r0, m, p in zip(res, ref, ms, preds):
+        assert r.nfev == r0.nfev
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+        assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
+    # fits did move into the wide batch, which evaluated mostly wide points (a fit with no
+    # free narrow slot to go back to is evaluated where it is)
+    wide_pts = np.concatenate(getattr(eng[2], "classes", [np.zeros(0, np.int32)]))
+    assert len(wide_pts) > 0 and (wide_pts == 2).mean() > 0.5
