@@ -184,8 +184,10 @@ def contract_traffic(n, flops_per_launch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    # 10 timed steps of 256 fits: enough fits to keep the 576 slots streaming (with 2 steps the
+    # timed region is one wave of fits and its slowest fits' tail)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 256)),
                     help="independent series fitted per GPU per step")
     ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 576)),

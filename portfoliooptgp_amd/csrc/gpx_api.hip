@@ -390,13 +390,13 @@ void band_fused_eval(const Run& r, int n1, int max_terms, hipEvent_t* ev) {
   gpx_batch* bt = r.bt;
   const int Np = bt->Np;
   const long long st = mat_stride(bt);
-  const int p = n1 < r.na ? 2 : 1;
+  // K's band is built per class on that class's stream (2 block diagonals for p <= 1, 3 for
+  // p = 2), so the p <= 1 build does not pay for the wider class and the two overlap
   BuildArgs ba{};
   ba.active = r.d_act; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
   ba.X = bt->X; ba.sX = (long long)bt->Nmax * bt->D; ba.X2 = bt->X; ba.sX2 = ba.sX; ba.D = bt->D;
   ba.m2 = 0; ba.out = bt->K; ba.sOut = st; ba.ldo = Np; ba.rows = ba.cols = Np;
-  ba.symmetric = 1; ba.band1 = p + 1;
-  launch_build(ba, r.na, r.s);
+  ba.symmetric = 1;
   BandFusedArgs fa{};
   fa.active = r.d_act; fa.bandp = bt->d_bandp; fa.K = bt->K; fa.L = bt->L; fa.W = bt->W; fa.sMat = st;
   fa.Y = bt->Y; fa.sY = bt->Nmax; fa.nvalid = bt->d_n; fa.z = bt->z; fa.alpha = bt->alpha;
@@ -406,15 +406,24 @@ void band_fused_eval(const Run& r, int n1, int max_terms, hipEvent_t* ev) {
   hipStream_t sa = bt->aux[0];
   const bool fork = n1 > 0 && n1 < r.na;
   if (fork) {
-    (void)hipEventRecord(bt->ev[kEvents - 2], r.s);   // K's band is built
+    (void)hipEventRecord(bt->ev[kEvents - 2], r.s);   // the call's uploads are in
     (void)hipStreamWaitEvent(sa, bt->ev[kEvents - 2], 0);
   }
   if (n1 < r.na) {
+    hipStream_t s2 = fork ? sa : r.s;
+    BuildArgs b2 = ba;
+    b2.active = r.d_act + n1;
+    b2.band1 = 3;
+    launch_build(b2, r.na - n1, s2);
     BandFusedArgs f2 = fa;
     f2.active = r.d_act + n1;
-    launch_band_fused(f2, max_terms, r.na - n1, fork ? sa : r.s, n1 == 0 ? ev : nullptr);
+    launch_band_fused(f2, max_terms, r.na - n1, s2, n1 == 0 ? ev : nullptr);
   }
-  if (n1 > 0) launch_band_fused1(fa, max_terms, n1, r.s, ev);
+  if (n1 > 0) {
+    ba.band1 = 2;
+    launch_build(ba, n1, r.s);
+    launch_band_fused1(fa, max_terms, n1, r.s, ev);
+  }
   if (fork) {
     (void)hipEventRecord(bt->ev[kEvents - 1], sa);
     (void)hipStreamWaitEvent(r.s, bt->ev[kEvents - 1], 0);
