@@ -334,14 +334,14 @@ __device__ __forceinline__ int tid_fresh() {
 }
 
 // f += ±opA·opB over 64 k; A and B 64x64 in LDS. TA: opA(i,k) = A[k][i]; TB: opB(k,j) = B[j][k].
-template <bool TA, bool TB>
+template <bool TA, bool TB, int U = 4>
 __device__ __forceinline__ void frag_mma(Frag& f, const double* __restrict__ sA, const double* __restrict__ sB,
                                          bool neg) {
   const int t = tid_fresh();
   const int lane = t & 63, wave = t >> 6;
   const int wr = wave >> 1, wc = wave & 1, l15 = lane & 15, l4 = lane >> 4;
   const double sg = neg ? -1.0 : 1.0;
-#pragma unroll 4
+#pragma unroll U
   for (int kk = 0; kk < 16; ++kk) {
     const int k = kk * 4 + l4;
     double av[2], bv[2];
@@ -651,8 +651,8 @@ __global__ __launch_bounds__(256, 1) void band_fwd_kernel(BandFusedArgs a) {
     PH(2);
     // panels P_i = A_{k+i,k} W_kkᵀ -> L (global) and sX / sY
     Frag f1, f2;
-    if (q >= 1) { frag_zero(f1); frag_mma<false, true>(f1, sX, sW, false); }
-    if (q >= 2) { frag_zero(f2); frag_mma<false, true>(f2, sY, sW, false); }
+    if (q >= 1) { frag_zero(f1); frag_mma<false, true, 16>(f1, sX, sW, false); }
+    if (q >= 2) { frag_zero(f2); frag_mma<false, true, 16>(f2, sY, sW, false); }
     __syncthreads();
     if (q >= 1) {
       frag_store_lds(f1, sX);
@@ -675,10 +675,10 @@ __global__ __launch_bounds__(256, 1) void band_fwd_kernel(BandFusedArgs a) {
       spart[1][part][lane] = s2;
     }
     // window update in registers: D2 −= P1 P1ᵀ, A_{k+2,k+1} −= P2 P1ᵀ, A_{k+2,k+2} −= P2 P2ᵀ
-    if (q >= 1) frag_mma<false, true>(d2, sX, sX, true);
+    if (q >= 1) frag_mma<false, true, 16>(d2, sX, sX, true);
     if (q >= 2) {
-      frag_mma<false, true>(f21, sY, sX, true);
-      frag_mma<false, true>(f22, sY, sY, true);
+      frag_mma<false, true, 16>(f21, sY, sX, true);
+      frag_mma<false, true, 16>(f22, sY, sY, true);
     }
     __syncthreads();
     if (tid < 64) {
@@ -797,9 +797,9 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
     // Z_kk = W_kkᵀ W_kk − Σ_i G_iᵀ Z_{k+i,k}
     Frag g1, g2, z1, z2, zk;
     frag_zero(zk);
-    frag_mma<true, false>(zk, sW, sW, false);
-    if (q >= 1) { frag_zero(g1); frag_mma<false, false>(g1, sX, sW, false); }
-    if (q >= 2) { frag_zero(g2); frag_mma<false, false>(g2, sY, sW, false); }
+    frag_mma<true, false, 16>(zk, sW, sW, false);
+    if (q >= 1) { frag_zero(g1); frag_mma<false, false, 16>(g1, sX, sW, false); }
+    if (q >= 2) { frag_zero(g2); frag_mma<false, false, 16>(g2, sY, sW, false); }
     __syncthreads();
     PH(1);
     frag_zero(z1);
@@ -813,20 +813,20 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
       }
       __syncthreads();
       if (q >= 2) {
-        frag_mma<true, false>(z1, sA, sY, true);
-        frag_mma<false, false>(z2, sA, sX, true);
-        frag_mma<false, false>(z2, sW, sY, true);
+        frag_mma<true, false, 16>(z1, sA, sY, true);
+        frag_mma<false, false, 16>(z2, sA, sX, true);
+        frag_mma<false, false, 16>(z2, sW, sY, true);
         __syncthreads();
       }
       frag_store_lds(zA, sA);
       __syncthreads();
-      frag_mma<false, false>(z1, sA, sX, true);
+      frag_mma<false, false, 16>(z1, sA, sX, true);
       __syncthreads();
       frag_store_lds(z1, sA);
       if (q >= 2) frag_store_lds(z2, sW);
       __syncthreads();
-      frag_mma<true, false>(zk, sX, sA, true);
-      if (q >= 2) frag_mma<true, false>(zk, sY, sW, true);
+      frag_mma<true, false, 16>(zk, sX, sA, true);
+      if (q >= 2) frag_mma<true, false, 16>(zk, sY, sW, true);
       __syncthreads();                   // every wave is done reading G_1 (sX)
       frag_store_lds(zk, sX);            // contraction: Z_kk in sX, Z_{k+1,k} in sA, Z_{k+2,k} in sW
     } else {
@@ -997,7 +997,7 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
     leaf64_lds<false>(sA, sW, ldiag + k64, &sfail, [&]() {
       if (q >= 1) block_fetch(pa, K + (long long)(k64 + 64) * ld + k64, ld);
       if (k + 1 < nb) frag_load_global(nxt, K + (long long)(k64 + 64) * ld + k64 + 64, ld);
-    });
+    }, (int)(blockIdx.x & 3));
     PH(1);
     if (tid == 0 && sfail >= 0) {
       if (gfail == 0) gfail = k64 + sfail + 1;
@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
     if (q >= 1) {
       Frag f;
       frag_zero(f);
-      frag_mma<false, true>(f, sA, sW, false);      // P = A_{k+1,k} W_kkᵀ
+      frag_mma<false, true, 16>(f, sA, sW, false);      // P = A_{k+1,k} W_kkᵀ
       __syncthreads();
       PH(3);
       frag_store_lds(f, sA);
@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
         for (int c = part; c < 64; c += 4) s1 = fma(sA[lane * BS + c], sv[0][c], s1);
         spart[part][lane] = s1;
       }
-      frag_mma<false, true>(nxt, sA, sA, true);     // A_{k+1,k+1} −= P Pᵀ (the next leaf's input)
+      frag_mma<false, true, 16>(nxt, sA, sA, true);     // A_{k+1,k+1} −= P Pᵀ (the next leaf's input)
       __syncthreads();
       if (tid < 64) sv[1][tid] = -((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]));
       PH(5);
@@ -1144,21 +1144,21 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
     // Z_kk = W_kkᵀW_kk − Gᵀ Z_{k+1,k}, Z_{k+1,k} = −Z_{k+1,k+1} G, G = P W_kk
     Frag zk, g, z1;
     frag_zero(zk);
-    frag_mma<true, false>(zk, sW, sW, false);
+    frag_mma<true, false, 16>(zk, sW, sW, false);
     if (q >= 1) {
       frag_zero(g);
-      frag_mma<false, false>(g, sA, sW, false);
+      frag_mma<false, false, 16>(g, sA, sW, false);
       __syncthreads();
       frag_store_lds(g, sA);
       frag_store_lds(zprev, sW);
       __syncthreads();
       PH(1);
       frag_zero(z1);
-      frag_mma<false, false>(z1, sW, sA, true);
+      frag_mma<false, false, 16>(z1, sW, sA, true);
       __syncthreads();
       frag_store_lds(z1, sW);
       __syncthreads();
-      frag_mma<true, false>(zk, sA, sW, true);
+      frag_mma<true, false, 16>(zk, sA, sW, true);
     }
     __syncthreads();                     // every wave is done reading G (sA)
     PH(2);

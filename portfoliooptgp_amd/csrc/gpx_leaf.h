@@ -79,17 +79,20 @@ struct LeafNoHook {
 };
 // kLog = false: ldiag gets L_ii itself (the banded sweeps take the logs once per problem, in
 // their backward kernels, instead of on every step's critical path)
+// rot: the hardware wave that plays wave 0 (the serial diagonal chain) is (rot & 3); callers
+// with several workgroups per CU pass a per-workgroup rotation so co-resident workgroups'
+// diagonal chains tend to sit on different SIMDs
 template <bool kLog = true, class PreInverse = LeafNoHook>
 __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __restrict__ sW,
                                            double* __restrict__ ldiag, int* sfail,
-                                           PreInverse pre_inverse = PreInverse()) {
+                                           PreInverse pre_inverse = PreInverse(), int rot = 0) {
   constexpr int S = kLeafS;
   typedef double d4 __attribute__((ext_vector_type(4)));
   // threadIdx.x through an empty asm: the leaf's LDS addresses are formed per call instead of
   // being hoisted out of a caller's block-step loop (where they would pin registers and spill)
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = ((tid >> 6) - rot) & 3;
   const int l15 = lane & 15, l4 = lane >> 4;
   LEAF_PH_BEGIN
   for (int jb = 0; jb < 4; ++jb) {
