@@ -874,6 +874,7 @@ class _SteppedDriver:
             gs.t_call = time.perf_counter()
             with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():
                 gs.eng.lml_grad_submit(gs.act, gs.theta)
+            self._tick("submit", gs.t_call)
             return True
 
         def submit_idle():
@@ -900,9 +901,11 @@ class _SteppedDriver:
                     else:
                         time.sleep(2e-5)
             inflight.remove(gs)
+            self._tick("device_wait", t0)
+            t1 = time.perf_counter()
             lml, grad, info = gs.eng.lml_grad_complete()
             t_end = time.perf_counter()
-            self._tick("device_wait", t0)
+            self._tick("complete", t1)
             with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():
                 self._consume(gs, lml, grad, info, t_end)
                 if submit(gs):
