@@ -109,12 +109,35 @@ def _single_thread_blas():
     thread pool, which costs ≈10× the call itself (423 → 41 µs per step measured)."""
     global _TPC
     try:
-        if _TPC is None:
+        if _TPC is None:  # the BLAS libraries' thread controls, found once
             from threadpoolctl import ThreadpoolController
-            _TPC = ThreadpoolController()
-        return _TPC.limit(limits=1, user_api="blas")
+            _TPC = ThreadpoolController().select(user_api="blas").lib_controllers
+        return _BlasThreads(_TPC)
     except Exception:  # pragma: no cover - threadpoolctl missing
         return contextlib.nullcontext()
+
+
+class _BlasThreads:
+    """set_num_threads(1) on each BLAS library for the duration (direct calls, not a fresh
+    threadpool_limits scan: this wraps every single-model minimize)."""
+
+    def __init__(self, libs):
+        self.libs = libs
+
+    def __enter__(self):
+        self.prev = []
+        for lib in self.libs:
+            n = lib.get_num_threads()
+            self.prev.append(n)
+            if n != 1:
+                lib.set_num_threads(1)
+        return self
+
+    def __exit__(self, *exc):
+        for lib, n in zip(self.libs, self.prev):
+            if n != 1:
+                lib.set_num_threads(n)
+        return False
 
 
 class Scipy:
