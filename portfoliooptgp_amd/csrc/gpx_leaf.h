@@ -95,52 +95,73 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
   const int lane = tid & 63, wave = ((tid >> 6) - rot) & 3;
   const int l15 = lane & 15, l4 = lane >> 4;
   LEAF_PH_BEGIN
+  // wave 0's 16x16 diagonal step on block jb: L_jj, D_j = L_jj⁻¹ (-> sW), L_ii (-> ldiag / sA)
+  auto diag = [&](int jb) {
+    const int c0 = jb * 16;
+    double r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = sA[(c0 + l15) * S + c0 + k];
+    int fail = -1;
+    double invd[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const double piv = bc16(r[j], j);
+      if (!(piv > 0.0) && fail < 0) fail = j;
+      const double inv = rsqrt_nr(piv);
+      const double ljj = piv * inv;
+      invd[j] = inv;
+      r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
+#pragma unroll
+      for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], bc16(r[j], k), r[k]);
+    }
+    // lane l15 holds row l15 of L_jj (r[0..l15]); column l15 of D = L_jj⁻¹ by substitution,
+    // right-looking so the 16 steps' FMAs are independent across i
+    double w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = (i == l15) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      w[k] *= invd[k];
+      // column k's broadcasts wait for w_k (else all 120 are hoisted: ~240 registers)
+      double rk = r[k];
+      asm volatile("" : "+v"(rk) : "v"(w[k]));
+#pragma unroll
+      for (int i = k + 1; i < 16; ++i) w[i] = fma(-bc16(rk, i), w[k], w[i]);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sW[(c0 + i) * S + c0 + lane] = w[i];
+      if (kLog)
+        sA[(c0 + lane) * S + c0 + lane] = r[lane & 15];   // L_ii, for log det at the end
+      else
+        ldiag[c0 + lane] = r[lane & 15];
+    }
+    if (lane == 0 && fail >= 0 && *sfail < 0) *sfail = c0 + fail;
+  };
+  // A_ik −= L_ij L_kjᵀ on one 16x16 tile (rows ri, columns rk; column block c0 of L)
+  auto tile_update = [&](int ri, int rk, int c0) {
+    d4 acc;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = sA[(ri + l4 + 4 * u) * S + rk + l15];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const double av = sA[(ri + l15) * S + c0 + 4 * kk + l4];
+      const double bv = sA[(rk + l15) * S + c0 + 4 * kk + l4];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sA[(ri + l4 + 4 * u) * S + rk + l15] = acc[u];
+  };
+  // Right-looking over the 4 column blocks with look-ahead: wave 0 computes the next diagonal
+  // tile's update itself (from the panel tile it just produced) and factors it while waves
+  // 1-3 apply the rest of the trailing update, so that update is off the diagonal chain.
+  if (wave == 0) diag(0);
   for (int jb = 0; jb < 4; ++jb) {
     const int c0 = jb * 16;
-    if (wave == 0) {
-      double r[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) r[k] = sA[(c0 + l15) * S + c0 + k];
-      int fail = -1;
-      double invd[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const double piv = bc16(r[j], j);
-        if (!(piv > 0.0) && fail < 0) fail = j;
-        const double inv = rsqrt_nr(piv);
-        const double ljj = piv * inv;
-        invd[j] = inv;
-        r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
-#pragma unroll
-        for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], bc16(r[j], k), r[k]);
-      }
-      // lane l15 holds row l15 of L_jj (r[0..l15]); column l15 of D = L_jj⁻¹ by substitution,
-      // right-looking so the 16 steps' FMAs are independent across i
-      double w[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) w[i] = (i == l15) ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        w[k] *= invd[k];
-        // column k's broadcasts wait for w_k (else all 120 are hoisted: ~240 registers)
-        double rk = r[k];
-        asm volatile("" : "+v"(rk) : "v"(w[k]));
-#pragma unroll
-        for (int i = k + 1; i < 16; ++i) w[i] = fma(-bc16(rk, i), w[k], w[i]);
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sW[(c0 + i) * S + c0 + lane] = w[i];
-        if (kLog)
-          sA[(c0 + lane) * S + c0 + lane] = r[lane & 15];   // L_ii, for log det at the end
-        else
-          ldiag[c0 + lane] = r[lane & 15];
-      }
-      if (lane == 0 && fail >= 0 && *sfail < 0) *sfail = c0 + fail;
-    }
     __syncthreads();
     LEAF_PH(0);
-    // panel: L_(ib,jb) = A_(ib,jb) · Dᵀ for ib = jb+1 .. 3, one wave per block
+    // panel: L_(ib,jb) = A_(ib,jb) · Dᵀ for ib = jb+1 .. 3, one wave per block (wave 0 takes
+    // ib = jb + 1, the tile its look-ahead needs)
     const int nblk = 3 - jb;
     if (wave < nblk) {
       const int r0 = (jb + 1 + wave) * 16;
@@ -156,28 +177,25 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
     }
     __syncthreads();
     LEAF_PH(1);
-    // trailing update of the lower blocks (ib, kb), jb < kb <= ib
+    // trailing update of the lower blocks (ib, kb), jb < kb <= ib: tile 0 = (jb+1, jb+1) by
+    // wave 0 with the next diagonal step, the others over waves 1..3
     const int ntr = nblk * (nblk + 1) / 2;
-    for (int t = wave; t < ntr; t += 4) {
-      int p = 0;
-      while ((p + 1) * (p + 2) / 2 <= t) ++p;
-      const int q = t - p * (p + 1) / 2;
-      const int ri = (jb + 1 + p) * 16, rk = (jb + 1 + q) * 16;
-      d4 acc;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = sA[(ri + l4 + 4 * u) * S + rk + l15];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const double av = sA[(ri + l15) * S + c0 + 4 * kk + l4];
-        const double bv = sA[(rk + l15) * S + c0 + 4 * kk + l4];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc, 0, 0, 0);
+    if (wave == 0) {
+      if (jb < 3) {
+        tile_update((jb + 1) * 16, (jb + 1) * 16, c0);
+        diag(jb + 1);
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) sA[(ri + l4 + 4 * u) * S + rk + l15] = acc[u];
+    } else {
+      for (int t = wave; t < ntr; t += 3) {
+        int p = 0;
+        while ((p + 1) * (p + 2) / 2 <= t) ++p;
+        const int q = t - p * (p + 1) / 2;
+        tile_update((jb + 1 + p) * 16, (jb + 1 + q) * 16, c0);
+      }
     }
-    __syncthreads();
     LEAF_PH(2);
   }
+  __syncthreads();
   pre_inverse();
   // W = L⁻¹: block rows 1..3, blocks j < i in parallel (wave j); the idle wave 3 takes the
   // logs of L's diagonal (left on sA's diagonal by the diagonal steps)
