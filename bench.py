@@ -277,13 +277,14 @@ def main():
             traces.append(opt.last_trace)
         if getattr(opt, "last_stats", None):
             stats.append(dict(opt.last_stats))
-        summary = torch.stack([
-            torch.stack([
-                torch.tensor(m.kernel.lengthscales.value, device=dev, dtype=torch.float64),
-                torch.tensor(m.kernel.variance.value, device=dev, dtype=torch.float64),
-                torch.tensor(r.fun, device=dev, dtype=torch.float64),
-                torch.tensor(float(r.nfev), device=dev, dtype=torch.float64),
-                p[0][-1, 0], p[1][-1, 0]]) for m, r, p in zip(models, res, preds)])
+        # per fit [ℓ*, σ²*, loss*, nfev, mean and var of its last training-point prediction]:
+        # the host columns as one table, the device ones as two gathers (one tensor per fit
+        # and column cost ~0.3 s at 5120 fits)
+        host = torch.tensor([[m.kernel.lengthscales.value, m.kernel.variance.value, float(r.fun), float(r.nfev)]
+                             for m, r in zip(models, res)], dtype=torch.float64).to(dev)
+        mu = torch.cat([p[0][-1:, 0] for p in preds])
+        var = torch.cat([p[1][-1:, 0] for p in preds])
+        summary = torch.cat([host, mu[:, None], var[:, None]], dim=1)
         if world > 1:
             summary = summary.to(cdev)
             gathered = [torch.empty_like(summary) for _ in range(world)]

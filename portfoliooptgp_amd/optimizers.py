@@ -19,6 +19,7 @@ each fit's ``scipy.optimize.minimize`` in its own host thread around a barrier
 from __future__ import annotations
 
 import contextlib
+import gc
 import os
 import sys
 import queue
@@ -663,8 +664,18 @@ class _SteppedDriver:
         # scipy's L-BFGS-B calls BLAS/LAPACK on n-vectors and m×m matrices; a multi-threaded
         # OpenBLAS hands each of those tiny calls to its thread pool (≈10× the cost of the call
         # itself on this host), so the fits' host steps run with single-threaded BLAS
-        with _single_thread_blas():
-            self._run_all()
+        # the cyclic garbage collector's full passes over a heap of thousands of live models
+        # stall the single host thread for milliseconds at a time; the driver's own garbage is
+        # acyclic (refcounting frees it), so the collector is paused for the run
+        gc_on = gc.isenabled() and os.environ.get("GPX_DRIVER_GC", "0") != "1"
+        if gc_on:
+            gc.disable()
+        try:
+            with _single_thread_blas():
+                self._run_all()
+        finally:
+            if gc_on:
+                gc.enable()
 
     def _run_all(self):
         G = len(self.groups)
