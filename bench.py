@@ -204,6 +204,9 @@ def main():
     ap.add_argument("--wide-slots", type=int, default=int(os.environ.get("GPX_BENCH_WIDE", 0)),
                     help="slots of an extra device batch that takes the evaluations whose band is wider "
                          "than one 64-block (0: none)")
+    ap.add_argument("--storage", choices=("band", "dense"), default=os.environ.get("GPX_BENCH_STORAGE", "band"),
+                    help="slot workspace: band storage (gpx_batch_create_banded, 25 MiB per slot) or the "
+                         "dense N x N layout (384 MiB per slot)")
     ap.add_argument("--points", "--n", dest="n", type=int, default=N_POINTS,
                     help="points per series (use --points under torch.distributed.run, whose parser takes --n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -239,14 +242,15 @@ def main():
     data = [synthetic_series(n, s) for s in seeds]
     Xd = [torch.as_tensor(x, device=dev) for x, _ in data]  # resident in HBM before timing
     Yd = [torch.as_tensor(y, device=dev) for _, y in data]
-    def make_models():
+    def make_model(f):
         # GPflow defaults (σ²=1, ℓ=1), σn² = 1e-5 frozen — GPR/model_trainer.py:15-17
-        ms = [gpx.models.GPR(data=(Xd[f], Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=gpu)
-              for f in range(F)]
-        for m in ms:
-            m.likelihood.variance.assign(NOISE)
-            gpx.set_trainable(m.likelihood.variance, False)
-        return ms
+        m = gpx.models.GPR(data=(Xd[f], Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=gpu)
+        m.likelihood.variance.assign(NOISE)
+        gpx.set_trainable(m.likelihood.variance, False)
+        return m
+
+    def make_models():
+        return [make_model(f) for f in range(F)]
 
     # W resident device slots (continuous batching), sized for N-point problems, split into
     # `groups` independent device batches evaluated concurrently on their own streams
@@ -257,7 +261,8 @@ def main():
     proto = make_models()
     # slot shapes only: every slot is rebound to its fit's series when the fit starts
     engines = [Engine([Xd[(g * per + i) % F] for i in range(sz)], [Yd[(g * per + i) % F] for i in range(sz)],
-                      [compile_spec(proto[(g * per + i) % F].kernel, 1) for i in range(sz)], device=gpu)
+                      [compile_spec(proto[(g * per + i) % F].kernel, 1) for i in range(sz)], device=gpu,
+                      band_storage=args.storage == "band" and not (WS > 0 and g == G))
                for g, sz in enumerate(sizes)]
     NG = len(engines)
     engines[0].ctx.set_profiling(True)
@@ -270,7 +275,10 @@ def main():
         """k steps (k × F fits, each from GPflow defaults) streamed back to back through the
         slots — the next step's fits fill slots as the previous step's finish, no drain in
         between — then every fit's summary row, all_gathered across ranks."""
-        models = [m for _ in range(k) for m in make_models()]
+        # every fit's model is built inside the timed region, on demand (as the reference's loop
+        # builds each GPR right before fitting it), while the host thread waits for the device
+        models = gpx.optimizers.ModelStream(k * F, lambda i: make_model(i % F), input_dim=1, max_points=n,
+                                            device=gpu)
         res, preds = opt.minimize_stream(models, width=W, engine=engines, predict_train=True, groups=NG,
                                          options=dict(maxiter=MAXITER), wide_group=WS > 0)
         if getattr(opt, "last_trace", None):
@@ -422,7 +430,7 @@ def main():
         "data": "synthetic (C2 generator, seeded per rank/series)",
         "config": {"workload": "C2: exact GPR fit, synthetic 1-D series, N=4096, SquaredExponential, "
                                "fp64, sigma_n^2=1e-5 fixed, L-BFGS-B maxiter=100 + predict_f(X_train)",
-                   "N": n, "fits_per_gpu_per_step": F, "device_slots": W, "device_batches": NG,
+                   "N": n, "fits_per_gpu_per_step": F, "device_slots": W, "device_batches": NG, "slot_storage": args.storage,
                    "wide_batch_slots": WS,
                    "kernel": "SquaredExponential",
                    "parallelism": f"independent fits, {world} process(es) x 1 GPU, RCCL all_gather of results"},

@@ -115,6 +115,19 @@ const char* gpx_last_error(const gpx_ctx* ctx);
  */
 int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, const double* Y,
                      const int32_t* n, const gpx_kernel_spec* specs, gpx_batch** out);
+/*
+ * gpx_batch_create with BAND STORAGE, for many resident slots of banded problems (the
+ * continuous-batching fits of configuration C2: SE / Matern / Exponential kernels on sorted
+ * day offsets, GPR/data_handler.py:42-44 + GPR/model_trainer.py:15, whose K is exactly zero in
+ * fp64 beyond one or two 64-blocks off the diagonal). The workspace keeps only the band of two
+ * 64-blocks: 3 * Np * 257 * 8 bytes per slot (25 MiB at N = 4096 instead of 384 MiB), so ~10x
+ * more slots fit in HBM. Same calls and results as a gpx_batch_create batch; evaluations the
+ * fused banded sweeps cannot take (a wider band, another kernel family, a failed band check)
+ * and predictions that need a fresh factor run densely on 4 internal fallback slots in the
+ * same call. 449 <= N_max <= 8192.
+ */
+int gpx_batch_create_banded(gpx_ctx* ctx, int B, int N_max, int D, const double* X, const double* Y,
+                            const int32_t* n, const gpx_kernel_spec* specs, gpx_batch** out);
 int gpx_batch_destroy(gpx_batch* batch);
 
 /*

@@ -25,7 +25,8 @@ LIB_PATH = os.environ.get("GPX_LIB") or os.path.join(os.path.dirname(os.path.abs
 
 # every symbol include/gpx.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
-    "gpx_version", "gpx_create", "gpx_destroy", "gpx_last_error", "gpx_batch_create", "gpx_batch_rebind_host",
+    "gpx_version", "gpx_create", "gpx_destroy", "gpx_last_error", "gpx_batch_create", "gpx_batch_create_banded",
+    "gpx_batch_rebind_host",
     "gpx_batch_rebind_device",
     "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_lml_grad_submit", "gpx_batch_lml_grad_complete",
     "gpx_batch_lml_grad_query", "gpx_batch_band_width",
@@ -116,6 +117,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_create.restype = c_int
         lib.gpx_batch_create.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int_p,
                                          ctypes.POINTER(GpxKernelSpec), ctypes.POINTER(c_void_p)]
+        lib.gpx_batch_create_banded.restype = c_int
+        lib.gpx_batch_create_banded.argtypes = lib.gpx_batch_create.argtypes
         lib.gpx_batch_destroy.restype = c_int
         lib.gpx_batch_destroy.argtypes = [c_void_p]
         lib.gpx_batch_lml_grad.restype = c_int

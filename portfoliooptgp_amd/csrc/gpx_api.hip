@@ -395,14 +395,14 @@ void band_fused_eval(const Run& r, int n1, int max_terms, hipEvent_t* ev) {
   BuildArgs ba{};
   ba.active = r.d_act; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
   ba.X = bt->X; ba.sX = (long long)bt->Nmax * bt->D; ba.X2 = bt->X; ba.sX2 = ba.sX; ba.D = bt->D;
-  ba.m2 = 0; ba.out = bt->K; ba.sOut = st; ba.ldo = Np; ba.rows = ba.cols = Np;
+  ba.m2 = 0; ba.out = bt->K; ba.sOut = st; ba.ldo = mat_ld(bt); ba.rows = ba.cols = Np;
   ba.symmetric = 1;
   BandFusedArgs fa{};
   fa.active = r.d_act; fa.bandp = bt->d_bandp; fa.K = bt->K; fa.L = bt->L; fa.W = bt->W; fa.sMat = st;
   fa.Y = bt->Y; fa.sY = bt->Nmax; fa.nvalid = bt->d_n; fa.z = bt->z; fa.alpha = bt->alpha;
   fa.ldiag = bt->ldiag; fa.sVec = Np; fa.X = bt->X; fa.sX = (long long)bt->Nmax * bt->D; fa.D = bt->D;
   fa.specs = bt->d_specs; fa.theta = bt->d_theta; fa.partial = bt->partial; fa.sPartial = bt->partial_stride;
-  fa.info = bt->d_info; fa.results = bt->results; fa.Np = Np;
+  fa.info = bt->d_info; fa.results = bt->results; fa.Np = Np; fa.ld = mat_ld(bt);
   hipStream_t sa = bt->aux[0];
   const bool fork = n1 > 0 && n1 < r.na;
   if (fork) {
@@ -596,8 +596,8 @@ int gpx_set_profiling(gpx_ctx* ctx, int enabled) {
   return GPX_OK;
 }
 
-int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, const double* Y,
-                     const int32_t* n, const gpx_kernel_spec* specs, gpx_batch** out) {
+static int batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, const double* Y,
+                        const int32_t* n, const gpx_kernel_spec* specs, bool compact, gpx_batch** out) {
   if (!ctx || !out) return GPX_BAD_ARG;
   *out = nullptr;
   if (B <= 0 || N_max <= 0 || D <= 0 || D > GPX_MAX_DIM || !X || !Y || !n || !specs)
@@ -618,6 +618,8 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
   }
   if (((long long)N_max + kLeaf - 1) / kLeaf * kLeaf > kGemmMaxLd)
     return fail(ctx, GPX_BAD_ARG, "N_max exceeds the GEMM buffer-load window (kGemmMaxLd)");
+  if (compact && (N_max < 8 * kLeaf - (kLeaf - 1) || N_max > 8192))
+    return fail(ctx, GPX_BAD_ARG, "band storage needs 449 <= N_max <= 8192 (8 to 128 64-blocks)");
   HIPX(ctx, hipSetDevice(ctx->device));
   gpx_batch* bt = new gpx_batch();
   bt->ctx = ctx; bt->B = B; bt->Nmax = N_max; bt->D = D;
@@ -625,10 +627,20 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
   bt->X = X; bt->Y = Y;
   bt->n.assign(n, n + B);
   bt->specs.assign(specs, specs + B);
-  const size_t mat = (size_t)B * bt->Np * bt->Np * sizeof(double);
+  // band storage: rows of ldm + 1 doubles holding columns i − 64·(kBandStoreP+1) .. i + 63
+  // (band_c0 = the column offset of the diagonal in a row), plus a 64-double guard
+  const long long band_c0 = 64LL * kBandStoreP + 64;
+  if (compact) {
+    bt->compact = 1;
+    bt->ldm = 64 * (kBandStoreP + 2);
+    bt->smat = (long long)bt->Np * (bt->ldm + 1);
+  }
+  const size_t mat = ((size_t)B * mat_stride(bt) + (compact ? 64 : 0)) * sizeof(double);
   const size_t vec = (size_t)B * bt->Np * sizeof(double);
   const int t64 = bt->Np / 64;
-  bt->partial_stride = (long long)t64 * (t64 + 1) / 2 * GPX_THETA_STRIDE;
+  // the dense contraction writes one row of partials per lower 64-tile; the fused band
+  // sweeps (band storage's only path) one row per problem
+  bt->partial_stride = compact ? GPX_THETA_STRIDE : (long long)t64 * (t64 + 1) / 2 * GPX_THETA_STRIDE;
   auto cleanup = [&](const std::string& m) {
     gpx_batch_destroy(bt);
     return fail(ctx, GPX_HIP_ERROR, m);
@@ -666,6 +678,10 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
   if (hipMemset(bt->W, 0, mat) != hipSuccess || hipMemset(bt->L, 0, mat) != hipSuccess ||
       hipMemset(bt->K, 0, mat) != hipSuccess)
     return cleanup("memset failed");
+  if (compact) {
+    bt->Kraw = bt->K; bt->Lraw = bt->L; bt->Wraw = bt->W;
+    bt->K += band_c0; bt->L += band_c0; bt->W += band_c0;
+  }
   for (int g = 0; g < kAux; ++g)
     if (hipStreamCreateWithFlags(&bt->aux[g], hipStreamNonBlocking) != hipSuccess)
       return cleanup("stream creation failed");
@@ -688,8 +704,37 @@ int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, con
       return cleanup("upload failed");
     for (int b = 0; b < B; ++b) band_tables(bt, b, hx.data() + (size_t)b * N_max * D);
   }
+  if (compact) {
+    // the dense fallback: kShadowSlots ordinary slots with their own X / Y rows
+    const size_t nx = (size_t)kShadowSlots * N_max * D, ny = (size_t)kShadowSlots * N_max;
+    if (hipMalloc(&bt->shX, nx * sizeof(double)) != hipSuccess ||
+        hipMalloc(&bt->shY, ny * sizeof(double)) != hipSuccess ||
+        hipMemset(bt->shX, 0, nx * sizeof(double)) != hipSuccess ||
+        hipMemset(bt->shY, 0, ny * sizeof(double)) != hipSuccess)
+      return cleanup("out of device memory for the dense fallback slots");
+    std::vector<int32_t> n1(kShadowSlots, 1);
+    std::vector<gpx_kernel_spec> sp1(kShadowSlots, specs[0]);
+    const int rc = batch_create(ctx, kShadowSlots, N_max, D, bt->shX, bt->shY, n1.data(), sp1.data(), false,
+                                &bt->shadow);
+    if (rc != GPX_OK) {
+      const std::string m = last_error_slot();
+      gpx_batch_destroy(bt);
+      return fail(ctx, rc, "dense fallback slots: " + m);
+    }
+    bt->shadow->force_dense = 1;
+  }
   *out = bt;
   return GPX_OK;
+}
+
+int gpx_batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, const double* Y,
+                     const int32_t* n, const gpx_kernel_spec* specs, gpx_batch** out) {
+  return batch_create(ctx, B, N_max, D, X, Y, n, specs, false, out);
+}
+
+int gpx_batch_create_banded(gpx_ctx* ctx, int B, int N_max, int D, const double* X, const double* Y,
+                            const int32_t* n, const gpx_kernel_spec* specs, gpx_batch** out) {
+  return batch_create(ctx, B, N_max, D, X, Y, n, specs, true, out);
 }
 
 int gpx_batch_destroy(gpx_batch* bt) {
@@ -699,6 +744,12 @@ int gpx_batch_destroy(gpx_batch* bt) {
     (void)hipStreamSynchronize(bt->pending_eval->s);
     bt->pending_eval.reset();
   }
+  if (bt->shadow) gpx_batch_destroy(bt->shadow);
+  if (bt->compact && bt->Kraw) {  // K/L/W point into the raw allocations (band storage's row offset)
+    bt->K = bt->Kraw; bt->L = bt->Lraw; bt->W = bt->Wraw;
+  }
+  for (void* p : {(void*)bt->shX, (void*)bt->shY})
+    if (p) (void)hipFree(p);
   for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
                   (void*)bt->ldiag, (void*)bt->partial, (void*)bt->d_io, (void*)bt->d_n,
                   (void*)bt->d_specs, (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw,
@@ -851,6 +902,45 @@ int gpx_batch_rebind_host(gpx_batch* bt, int b, int n, const double* X, const do
   return GPX_OK;
 }
 
+// Band storage's dense fallback: problem b of bt is rebound to a slot of bt->shadow (its X / Y
+// rows gathered device to device by the shadow's next call) and evaluated there, in chunks of
+// kShadowSlots; outputs land at row b as gpx_batch_lml_grad writes them.
+static int shadow_lml_grad(gpx_batch* bt, const std::vector<int32_t>& ids, const double* theta,
+                           double* lml, double* grad, int32_t* info, hipStream_t s) {
+  gpx_batch* sh = bt->shadow;
+  const size_t nx = (size_t)bt->Nmax * bt->D;
+  std::vector<double> th((size_t)kShadowSlots * GPX_THETA_STRIDE, 1.0), l(kShadowSlots);
+  std::vector<double> g((size_t)kShadowSlots * GPX_THETA_STRIDE);
+  std::vector<int32_t> inf(kShadowSlots), act(kShadowSlots);
+  int status = GPX_OK;
+  for (size_t c = 0; c < ids.size(); c += kShadowSlots) {
+    const int cnt = (int)std::min<size_t>(kShadowSlots, ids.size() - c);
+    for (int k = 0; k < cnt; ++k) {
+      const int b = ids[c + k];
+      const int rc = gpx_batch_rebind_device(sh, k, bt->n[b], bt->X + b * nx, bt->Y + (size_t)b * bt->Nmax,
+                                             &bt->specs[b], s);
+      if (rc != GPX_OK) return rc;
+      std::memcpy(&th[(size_t)k * GPX_THETA_STRIDE], theta + (size_t)b * GPX_THETA_STRIDE,
+                  sizeof(double) * GPX_THETA_STRIDE);
+      act[k] = k;
+    }
+    const int rc = gpx_batch_lml_grad(sh, cnt, act.data(), th.data(), l.data(), g.data(), inf.data(), s);
+    if (rc != GPX_OK && rc != GPX_NOT_PD) return rc;
+    for (int k = 0; k < cnt; ++k) {
+      const int b = ids[c + k];
+      info[b] = inf[k];
+      if (inf[k] != 0) status = GPX_NOT_PD;
+      lml[b] = l[k];
+      for (int p = 0; p <= bt->specs[b].n_params; ++p)
+        grad[(size_t)b * GPX_THETA_STRIDE + p] = g[(size_t)k * GPX_THETA_STRIDE + p];
+      bt->fac_valid[b] = 0;  // no factor of b is kept in bt
+      bt->fac_band[b] = 0;
+    }
+  }
+  if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
+  return status;
+}
+
 int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                               void* stream) {
   if (!bt) return GPX_BAD_ARG;
@@ -867,9 +957,10 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   // The device active list is [dense problems | banded problems].
   std::vector<int32_t> order;
   order.reserve(n_active);
-  std::vector<int32_t> band_ids, fused_ids;
+  std::vector<int32_t> band_ids, fused_ids, shadow_ids;
   int pband = 0, pfused = 0;
-  const int plim = band_limit(bt);
+  int plim = band_limit(bt);
+  if (bt->compact) plim = std::min(plim, kBandStoreP);
   const char* ef = getenv("GPX_BAND_FUSED");  // 0: p <= 2 problems take the per-block launches too
   const bool fused_on = !(ef && atoi(ef) == 0);
   for (int i = 0; i < n_active; ++i) {
@@ -881,15 +972,34 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
       if (fused_on && (p <= 1 || (p == 2 && bt->D <= 12))) {
         fused_ids.push_back(b);
         pfused = std::max(pfused, p);
+      } else if (bt->compact) {
+        shadow_ids.push_back(b);  // band storage runs the fused sweeps only
       } else {
         band_ids.push_back(b);
         pband = std::max(pband, p);
       }
+    } else if (bt->compact) {
+      shadow_ids.push_back(b);    // dense on the fallback slots, at _complete
     } else {
       order.push_back(b);
     }
   }
   const int n_dense = (int)order.size(), n_band = (int)band_ids.size(), n_fused = (int)fused_ids.size();
+  // the problems launched by this call (band storage: without the shadowed ones)
+  n_active = n_dense + n_band + n_fused;
+  if (n_active == 0) {  // everything on the dense fallback: just land the pending rebinds
+    const int rc0 = flush_rebinds(bt, s);
+    if (rc0 != GPX_OK) return rc0;
+    std::unique_ptr<gpx_batch::PendingEval> pe0(new gpx_batch::PendingEval());
+    pe0->s = s;
+    pe0->theta.assign(theta, theta + (size_t)bt->B * GPX_THETA_STRIDE);
+    pe0->total.reset(new PhaseTimer(false, s));
+    pe0->ct.reset(new PhaseTimer(false, s));
+    pe0->bp.reset(new PhaseTimer(false, s));
+    pe0->shadow_ids = std::move(shadow_ids);
+    bt->pending_eval = std::move(pe0);
+    return GPX_OK;
+  }
   order.insert(order.end(), band_ids.begin(), band_ids.end());
   // fused problems: the p <= 1 class first (its own two-blocks-per-CU kernels), then p = 2
   int n_fused1 = 0;
@@ -1028,6 +1138,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   pe->n_band = n_band;
   pe->n_fused = n_fused;
   pe->n_fused1 = n_fused1;
+  pe->shadow_ids = std::move(shadow_ids);
   bt->pending_eval = std::move(pe);
   return GPX_OK;
 }
@@ -1123,6 +1234,19 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
     bt->fac_band[b] = i >= n_dense;
   }
   if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
+  if (bt->compact) {
+    // band storage: the problems routed dense and those whose band check failed run on the
+    // dense fallback slots
+    if (total.on) bt->timing.band_fallbacks += (double)redo.size();
+    std::vector<int32_t> ids = pe->shadow_ids;
+    ids.insert(ids.end(), redo.begin(), redo.end());
+    if (!ids.empty()) {
+      const int rc2 = shadow_lml_grad(bt, ids, theta, lml, grad, info, s);
+      if (rc2 != GPX_OK && rc2 != GPX_NOT_PD) return rc2;
+      if (rc2 == GPX_NOT_PD) status = GPX_NOT_PD;
+    }
+    return status;
+  }
   if (!redo.empty()) {
     if (total.on) bt->timing.band_fallbacks += (double)redo.size();
     bt->force_dense = 1;
@@ -1185,6 +1309,49 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
     return fail(ctx, GPX_BAD_ARG, "too many prediction points for one call (kGemmMaxLd): split Xnew");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  // band storage: only predict at the training inputs from a cached banded factor at exactly
+  // this θ stays here; every other problem is predicted on the dense fallback slots, one by one
+  std::vector<int32_t> keep;
+  int shadow_status = GPX_OK;
+  if (bt->compact) {
+    if (n_active <= 0 || n_active > bt->B || !active || !theta)
+      return fail(ctx, GPX_BAD_ARG, "bad active set / theta");
+    gpx_batch* sh = bt->shadow;
+    const size_t nx = (size_t)bt->Nmax * bt->D;
+    std::vector<double> th((size_t)kShadowSlots * GPX_THETA_STRIDE, 1.0);
+    std::vector<int32_t> inf(kShadowSlots, 0);
+    const int32_t act0 = 0;
+    for (int i = 0; i < n_active; ++i) {
+      const int b = active[i];
+      if (b < 0 || b >= bt->B) return fail(ctx, GPX_BAD_ARG, "active index out of range");
+      const bool cached = train && bt->fac_valid[b] && bt->fac_band[b] &&
+                          std::memcmp(&bt->fac_theta[(size_t)b * GPX_THETA_STRIDE],
+                                      theta + (size_t)b * GPX_THETA_STRIDE,
+                                      sizeof(double) * GPX_THETA_STRIDE) == 0;
+      if (cached) {
+        keep.push_back(b);
+        continue;
+      }
+      int rc = gpx_batch_rebind_device(sh, 0, bt->n[b], bt->X + b * nx, bt->Y + (size_t)b * bt->Nmax,
+                                       &bt->specs[b], s);
+      if (rc != GPX_OK) return rc;
+      std::memcpy(th.data(), theta + (size_t)b * GPX_THETA_STRIDE, sizeof(double) * GPX_THETA_STRIDE);
+      inf[0] = 0;
+      if (train)
+        rc = predict_impl(sh, 1, &act0, th.data(), nullptr, 0, add_noise, mean + (size_t)b * bt->Nmax,
+                          var + (size_t)b * bt->Nmax, nullptr, inf.data(), s, true);
+      else
+        rc = predict_impl(sh, 1, &act0, th.data(), Xnew + (size_t)b * M * bt->D, M, add_noise,
+                          mean + (size_t)b * M, var ? var + (size_t)b * M : nullptr,
+                          cov ? cov + (size_t)b * M * M : nullptr, inf.data(), s);
+      if (rc != GPX_OK && rc != GPX_NOT_PD) return rc;
+      info[b] = inf[0];
+      if (rc == GPX_NOT_PD) shadow_status = GPX_NOT_PD;
+    }
+    if (keep.empty()) return shadow_status;
+    active = keep.data();
+    n_active = (int)keep.size();
+  }
   int rc = upload_common(bt, n_active, active, theta, s);
   if (rc != GPX_OK) return rc;
   PhaseTimer pt(ctx->profiling != 0, s);
@@ -1232,7 +1399,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
     if (n_dense < n_active) {
       // banded: diag(K⁻¹) from the selected inverse in K's diagonal blocks
       TrainPredArgs tb = ta;
-      tb.active = bt->d_active + n_dense; tb.W = bt->K;
+      tb.active = bt->d_active + n_dense; tb.W = bt->K; tb.ld = mat_ld(bt);
       launch_band_train_pred(tb, n_active - n_dense, Np, s);
     }
   } else {
@@ -1341,6 +1508,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
       bt->fac_band[b] = 0;
     }
   }
+  if (shadow_status == GPX_NOT_PD) status = GPX_NOT_PD;
   if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
   return status;
 }

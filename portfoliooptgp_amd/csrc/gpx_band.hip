@@ -587,7 +587,7 @@ __global__ __launch_bounds__(256, 1) void band_fwd_kernel(BandFusedArgs a) {
   __shared__ int sfail;
   const int b = a.active[blockIdx.x];
   const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
-  const long long ld = Np;
+  const long long ld = a.ld;
   const double* K = a.K + (long long)b * a.sMat;
   double* L = a.L + (long long)b * a.sMat;
   double* W = a.W + (long long)b * a.sMat;
@@ -634,7 +634,7 @@ __global__ __launch_bounds__(256, 1) void band_fwd_kernel(BandFusedArgs a) {
     }
     {
       double* Wk = W + (long long)k64 * ld + k64;
-      for (int e = tid; e < 4096; e += 256) Wk[(e >> 6) * Np + (e & 63)] = sW[(e >> 6) * BS + (e & 63)];
+      for (int e = tid; e < 4096; e += 256) Wk[(e >> 6) * ld + (e & 63)] = sW[(e >> 6) * BS + (e & 63)];
     }
     {  // z_k = W_kk (y_k + u_k)
       double s = 0.0;
@@ -713,7 +713,7 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
   extern __shared__ double sxr[];     // [3][64·D] X rows, block k in slot k % 3
   const int b = a.active[blockIdx.x];
   const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
-  const long long ld = Np;
+  const long long ld = a.ld;
   double* K = a.K + (long long)b * a.sMat;
   const double* L = a.L + (long long)b * a.sMat;
   const double* W = a.W + (long long)b * a.sMat;
@@ -784,13 +784,7 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
         const int r = part + 4 * u;
         s = (r >= lane) ? fma(pw[u], st[r], s) : s;
       }
-      spart[1][part][lane] = s;
-    }
-    __syncthreads();
-    if (tid < 64) {
-      const double ak = (spart[1][0][tid] + spart[1][1][tid]) + (spart[1][2][tid] + spart[1][3][tid]);
-      sal[0][tid] = ak;
-      alpha[k64 + tid] = ak;
+      spart[1][part][lane] = s;  // summed after the MFMAs' barrier below (no barrier of its own)
     }
     PH(0);
     // G_i = P_i W_kk;  Z_{k+i,k} = −Σ_j Z_{k+i,k+j} G_j  (Z_{k+1,k+2} = Z_{k+2,k+1}ᵀ);
@@ -801,6 +795,11 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
     if (q >= 1) { frag_zero(g1); frag_mma<false, false, 16>(g1, sX, sW, false); }
     if (q >= 2) { frag_zero(g2); frag_mma<false, false, 16>(g2, sY, sW, false); }
     __syncthreads();
+    if (tid < 64) {
+      const double ak = (spart[1][0][tid] + spart[1][1][tid]) + (spart[1][2][tid] + spart[1][3][tid]);
+      sal[0][tid] = ak;
+      alpha[k64 + tid] = ak;
+    }
     PH(1);
     frag_zero(z1);
     frag_zero(z2);
@@ -965,7 +964,7 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
   __shared__ int sfail;
   const int b = a.active[blockIdx.x];
   const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
-  const long long ld = Np;
+  const long long ld = a.ld;
   const double* K = a.K + (long long)b * a.sMat;
   double* L = a.L + (long long)b * a.sMat;
   double* W = a.W + (long long)b * a.sMat;
@@ -1006,10 +1005,10 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
     // W_kk -> global (the backward sweep reads it); z_k partials; the panel block -> sA
     {
       const int t = tid_fresh();
-      double* Wk = W + (long long)k64 * ld + k64 + (t >> 6) * Np + (t & 63);
+      double* Wk = W + (long long)k64 * ld + k64 + (t >> 6) * ld + (t & 63);
       const double* sWt = sW + (t >> 6) * BS + (t & 63);
 #pragma unroll
-      for (int u = 0; u < 16; ++u) Wk[4 * u * Np] = sWt[4 * u * BS];
+      for (int u = 0; u < 16; ++u) Wk[4 * u * ld] = sWt[4 * u * BS];
     }
     {
       double s = 0.0;
@@ -1070,7 +1069,7 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
   __shared__ double sres[2][64];      // Σ_i K_ji Z_ij ring: the columns of block k in slot k & 1
   const int b = a.active[blockIdx.x];
   const int p = a.bandp[b], Np = a.Np, nb = Np / 64;
-  const long long ld = Np;
+  const long long ld = a.ld;
   double* K = a.K + (long long)b * a.sMat;
   const double* L = a.L + (long long)b * a.sMat;
   const double* W = a.W + (long long)b * a.sMat;
@@ -1125,7 +1124,8 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
     __syncthreads();
     if (tid < 64) st[tid] = zpre - ((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]));
     __syncthreads();
-    {
+    {  // W_kkᵀ st partials; their sum (α_k) is taken after the next barrier, so the MFMAs
+       // below issue without a barrier of their own for it
       double s = 0.0;
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
@@ -1134,12 +1134,13 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
       }
       spart[part][lane] = s;
     }
-    __syncthreads();
-    if (tid < 64) {
-      const double ak = (spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]);
-      sal[cs][tid] = ak;
-      alpha[k64 + tid] = ak;
-    }
+    auto alpha_out = [&]() {  // after a barrier that follows the partials' stores
+      if (tid < 64) {
+        const double ak = (spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]);
+        sal[cs][tid] = ak;
+        alpha[k64 + tid] = ak;
+      }
+    };
     PH(0);
     // Z_kk = W_kkᵀW_kk − Gᵀ Z_{k+1,k}, Z_{k+1,k} = −Z_{k+1,k+1} G, G = P W_kk
     Frag zk, g, z1;
@@ -1149,6 +1150,7 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
       frag_zero(g);
       frag_mma<false, false, 16>(g, sA, sW, false);
       __syncthreads();
+      alpha_out();
       frag_store_lds(g, sA);
       frag_store_lds(zprev, sW);
       __syncthreads();
@@ -1161,6 +1163,7 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
       frag_mma<true, false, 16>(zk, sA, sW, true);
     }
     __syncthreads();                     // every wave is done reading G (sA)
+    if (q == 0) alpha_out();
     PH(2);
     frag_store_lds(zk, sA);
     frag_store_diag(zk, K + (long long)k64 * ld + k64, ld);

@@ -34,7 +34,18 @@ struct gpx_batch {
   double* d_theta = nullptr;
   int* d_active = nullptr;
   int* d_info = nullptr;
-  double *K = nullptr, *L = nullptr, *W = nullptr;     // [B][Np][Np]
+  double *K = nullptr, *L = nullptr, *W = nullptr;     // [B][Np][Np] (band storage: see below)
+  // band storage (gpx_batch_create_banded): K, L, W keep only the 64-block band of width
+  // kBandStoreP; element (i, j) of problem b lives at X_b + i·ldm + j with ldm = 64·(kBandStoreP+2)
+  // and X_b = raw + b·smat + band_c0, i.e. row i occupies [i·(ldm+1), (i+1)·(ldm+1)) of the slot
+  // for j − i in [−64·(kBandStoreP+1), 63]: 257 doubles per row instead of Np. Problems that
+  // need the dense path run on `shadow`, a small dense batch inside this one.
+  int compact = 0;
+  int ldm = 0;                     // leading dimension of K/L/W (0: Np)
+  long long smat = 0;              // per-problem stride of K/L/W in doubles (0: Np²)
+  double *Kraw = nullptr, *Lraw = nullptr, *Wraw = nullptr;
+  gpx_batch* shadow = nullptr;     // dense fallback slots (band storage only)
+  double *shX = nullptr, *shY = nullptr;
   double *z = nullptr, *alpha = nullptr, *ldiag = nullptr;  // [B][Np]
   double* partial = nullptr;       // [B][ntiles64][16]
   long long partial_stride = 0;
@@ -120,7 +131,10 @@ inline int fail(gpx_ctx* ctx, int code, const std::string& msg) {
       return fail(ctx, GPX_HIP_ERROR, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
-inline long long mat_stride(const gpx_batch* bt) { return (long long)bt->Np * bt->Np; }
+inline long long mat_stride(const gpx_batch* bt) { return bt->smat ? bt->smat : (long long)bt->Np * bt->Np; }
+inline int mat_ld(const gpx_batch* bt) { return bt->ldm ? bt->ldm : bt->Np; }
+constexpr int kBandStoreP = 2;     // band width (64-blocks) held by band storage
+constexpr int kShadowSlots = 4;    // dense fallback slots of a band-storage batch
 
 // One pipeline instance: a contiguous range of the device active list on one stream.
 struct Run {
@@ -194,6 +208,7 @@ struct gpx_batch::PendingEval {
   hipStream_t s = nullptr;
   int n_active = 0, n_dense = 0, n_band = 0, n_fused = 0, n_fused1 = 0, ng = 0;
   std::vector<int32_t> order;
+  std::vector<int32_t> shadow_ids;  // band storage: problems evaluated on the dense shadow at _complete
   std::vector<double> theta;
   std::unique_ptr<gpx::PhaseTimer> total, ct, bp;
   std::vector<gpx::PhaseTimer> pts;

@@ -159,6 +159,7 @@ struct BandFusedArgs {
   int* info;
   double* results;                               // [B][kResStride]: writes [kResBandCheck]
   int Np;
+  int ld;                                        // leading dimension of K/L/W (Np, or band storage's)
 };
 void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s,
                        hipEvent_t* ev = nullptr);  // ev[4]: fwd start/stop, bwd start/stop

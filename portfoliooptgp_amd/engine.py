@@ -72,7 +72,11 @@ def screen_theta(act: np.ndarray, theta: np.ndarray, n_params: np.ndarray, info:
 
 class Engine:
     def __init__(self, Xs: Sequence, Ys: Sequence, specs: Sequence[N.GpxKernelSpec],
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, band_storage: bool = False):
+        """B problem slots (gpx_batch). ``band_storage``: the workspace keeps only the 64-block
+        band of width 2 (gpx_batch_create_banded: 25 MiB per slot at N = 4096 instead of
+        384 MiB), for many resident slots of banded fits; anything else runs on the batch's
+        dense fallback slots. Same results either way."""
         self.device = require_gpu(device)
         self.ctx = N.Context.get(self.device)
         self.lib = self.ctx.lib
@@ -101,7 +105,9 @@ class Engine:
         self.specs = (N.GpxKernelSpec * B)(*specs)
         torch.cuda.synchronize(self.device)
         h = ctypes.c_void_p()
-        rc = self.lib.gpx_batch_create(
+        create = self.lib.gpx_batch_create_banded if band_storage else self.lib.gpx_batch_create
+        self.band_storage = bool(band_storage)
+        rc = create(
             self.ctx.handle, B, self.Nmax, D, ctypes.c_void_p(self.X.data_ptr()),
             ctypes.c_void_p(self.Y.data_ptr()),
             self.n.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), self.specs, ctypes.byref(h))

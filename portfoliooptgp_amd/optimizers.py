@@ -42,6 +42,49 @@ from .kernels import compile_spec
 _THREADED = os.environ.get("GPX_THREADED_DRIVER", "0") not in ("", "0")
 
 
+class ModelStream(Sequence):
+    """``n`` models built on demand by ``factory(i)``, for ``minimize_stream``.
+
+    The reference builds each GPR right before fitting it, inside its per-ticker loop
+    (GPR/model_trainer.py:14-15). A list of thousands of models built up front keeps the device
+    idle for the whole construction (≈35 µs per GPR). Given a ModelStream, ``minimize_stream``
+    builds model i when a slot takes it, or earlier while its host thread waits for the device,
+    so construction overlaps device work. ``input_dim`` and ``max_points`` size the device slots
+    without building every model first; a model that does not fit them fails alone (its
+    rebind raises)."""
+
+    def __init__(self, n: int, factory: Callable[[int], object], input_dim: int, max_points: int,
+                 device: Optional[int] = None):
+        self._n, self._factory = int(n), factory
+        self.input_dim, self.max_points, self.device = int(input_dim), int(max_points), device
+        self._built: List[object] = [None] * self._n
+        self.next_unbuilt = 0  # every model below this index is built
+
+    def __len__(self) -> int:
+        return self._n
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(self._n))]
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError(i)
+        m = self._built[i]
+        if m is None:
+            m = self._built[i] = self._factory(i)
+        return m
+
+    def build_ahead(self) -> bool:
+        """Build the lowest-indexed model not built yet; False when all are built."""
+        while self.next_unbuilt < self._n and self._built[self.next_unbuilt] is not None:
+            self.next_unbuilt += 1
+        if self.next_unbuilt >= self._n:
+            return False
+        self[self.next_unbuilt]
+        return True
+
+
 def _new_stream(device):
     """A HIP stream from torch's pool (None without a device: the CPU test doubles)."""
     return torch.cuda.Stream(device=device) if torch.cuda.is_available() else None
@@ -262,16 +305,24 @@ class Scipy:
         sweeps. Returns (results, predictions|None); models are detached afterwards.
         """
         as_inf = _not_pd_policy(on_not_pd)
-        models = list(models)
-        if not models:
+        lazy = isinstance(models, ModelStream)
+        if not lazy:
+            models = list(models)
+        if len(models) == 0:
             return [], ([] if predict_train else None)
         width = max(1, min(int(width), len(models)))
         groups = max(1, min(int(groups), width))
-        D = models[0].data[0].shape[1]
-        if any(m.data[0].shape[1] != D for m in models):
-            raise ValueError("all models must have the same input dimension")
-        nmax = max(m.data[0].shape[0] for m in models)
-        dev = device if device is not None else models[0].device
+        if lazy:  # slot shapes from the stream's declaration, not from building every model
+            D, nmax = models.input_dim, models.max_points
+        else:
+            D = models[0].data[0].shape[1]
+            if any(m.data[0].shape[1] != D for m in models):
+                raise ValueError("all models must have the same input dimension")
+            nmax = max(m.data[0].shape[0] for m in models)
+        if device is not None:
+            dev = device
+        else:
+            dev = models.device if lazy and models.device is not None else models[0].device
         if engine is None:
             # slot shapes sized for the largest problem; one engine per group
             per = -(-width // groups)
@@ -941,6 +992,8 @@ class _SteppedDriver:
             for x in gss:
                 if x not in inflight and x.active and submit(x):
                     inflight.append(x)
+        # a ModelStream's models are built while this thread waits for the device
+        build_ahead = getattr(self.models, "build_ahead", None)
         for gs in gss:
             if submit(gs):
                 inflight.append(gs)
@@ -955,6 +1008,9 @@ class _SteppedDriver:
                         gs = x
                         break
                 else:
+                    if build_ahead is not None and build_ahead():
+                        continue
+                    build_ahead = None
                     if len(inflight) == 1:
                         gs = inflight[0]
                     else:

@@ -1,0 +1,170 @@
+"""GPU parity of band storage (gpx_batch_create_banded, ``Engine(..., band_storage=True)``):
+the same problems evaluated in a band-storage batch and in an ordinary (dense-layout) batch.
+
+Band storage keeps only the 64-block band of width 2 of K, L and W (257 doubles per row), so
+the fused banded sweeps run with a different leading dimension but the same arithmetic, and
+everything else (wider bands, Periodic, failed band checks, predictions that need a fresh
+factor) runs on the batch's dense fallback slots through the ordinary dense path. Both are
+therefore expected to agree with the dense-layout batch to rounding (asserted at 1e-12
+relative; observed bit-identical). The dense-layout batch itself is pinned against the oracle by
+test_band_gpu.py / test_gpu_parity.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import portfoliooptgp_amd as gpx  # noqa: E402
+from portfoliooptgp_amd import _native as N  # noqa: E402
+from portfoliooptgp_amd.engine import Engine  # noqa: E402
+from portfoliooptgp_amd.kernels import compile_spec  # noqa: E402
+from oracle import gp_oracle as O  # noqa: E402
+from tests.test_band_gpu import _Env  # noqa: E402
+
+K = gpx.kernels
+
+
+def _pair(xs, ys, kerns):
+    specs = [compile_spec(k, xs[0].shape[1]) for k in kerns]
+    band = Engine(xs, ys, specs, band_storage=True)
+    dense = Engine(xs, ys, specs)
+    band.ctx.set_profiling(True)
+    return band, dense
+
+
+def _theta(B, rows):
+    th = np.ones((B, N.GPX_THETA_STRIDE))
+    for b, r in enumerate(rows):
+        th[b, :len(r)] = r
+    return th
+
+
+def _close(a, b, rel=1e-12):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    assert a.shape == b.shape
+    assert np.all(np.abs(a - b) <= rel * np.maximum(1.0, np.abs(b))), (a, b)
+
+
+def _c2_batch():
+    n = 4096
+    data = [O.synthetic_series(n, seed=s) for s in range(6)]
+    xs = [d[0] for d in data]
+    ys = [d[1] for d in data]
+    xs[3], ys[3] = xs[3][:3001], ys[3][:3001]          # ragged member
+    kerns = [K.SquaredExponential()] * 5 + [K.Periodic(K.SquaredExponential())]
+    # p = 1, p = 2, p = 3 (fallback), p = 1 ragged, p = 16 (fallback), Periodic (fallback)
+    rows = [(1.0, 1.0, 1e-5), (1.7146, 0.8649, 1e-5), (3.5, 0.6, 1e-5), (1.1795, 0.5632, 1e-5),
+            (26.0, 1.1, 1e-5), (1.0, 1.0, 3.0, 1e-2)]
+    return xs, ys, kerns, rows
+
+
+def test_band_storage_equals_dense_layout():
+    """lml/grad of one call mixing fused-band problems (p <= 2) with ones the band storage
+    sends to its fallback slots; predict at the training inputs from the cached band factor
+    and through the fallback; predict at new inputs (fallback)."""
+    xs, ys, kerns, rows = _c2_batch()
+    band, dense = _pair(xs, ys, kerns)
+    th = _theta(band.B, rows)
+    act = list(range(6))
+    band.reset_timing()
+    lb, gb, ib = band.lml_grad(act, th)
+    t = band.last_timing()
+    assert t.band_evals == 3     # problems 0, 1, 3 in the fused sweeps; 2, 4, 5 on the fallback
+    # the dense-layout batch capped at the same band width (GPX_BAND_PMAX), so problem 2
+    # (p = 3) takes the dense path there too and every problem runs the same arithmetic
+    with _Env("GPX_BAND_PMAX", "2"):
+        ld, gd, idn = dense.lml_grad(act, th)
+    assert not ib.any() and not idn.any()
+    for b in act:
+        _close(lb[b], ld[b])
+        _close(gb[b, :4], gd[b, :4])
+    # predict_f at the training inputs: 0, 1, 3 from the cached banded factor, the rest refactor
+    mb, vb, _ = band._predict_train(np.asarray(act, dtype=np.int32), th, False)
+    md, vd, _ = dense._predict_train(np.asarray(act, dtype=np.int32), th, False)
+    for b in act:
+        _close(mb[b].cpu().numpy(), md[b].cpu().numpy(), 1e-10)
+        _close(vb[b].cpu().numpy(), vd[b].cpu().numpy(), 1e-10)
+    # at another θ nothing is cached: every problem through the fallback (predict_y)
+    th2 = th.copy()
+    th2[:5, 0] *= 1.01
+    mb, vb, _ = band._predict_train(np.asarray(act, dtype=np.int32), th2, True)
+    md, vd, _ = dense._predict_train(np.asarray(act, dtype=np.int32), th2, True)
+    for b in act:
+        _close(mb[b].cpu().numpy(), md[b].cpu().numpy(), 1e-10)
+        _close(vb[b].cpu().numpy(), vd[b].cpu().numpy(), 1e-10)
+    # new inputs: 30 points past the end of each series
+    xn = [np.arange(4096, 4126, dtype=np.float64)[:, None] for _ in act]
+    mb, vb, _ = band.predict(act, th, xn, False)
+    md, vd, _ = dense.predict(act, th, xn, False)
+    for b in act:
+        _close(mb[b].cpu().numpy(), md[b].cpu().numpy(), 1e-10)
+        _close(vb[b].cpu().numpy(), vd[b].cpu().numpy(), 1e-10)
+
+
+def test_band_storage_failed_check_uses_fallback():
+    """A band check that fails (forced with GPX_BAND_TOL < 0) sends the problem to the
+    fallback slots inside the same call: the dense path's values."""
+    xs, ys, kerns, rows = _c2_batch()
+    band, dense = _pair(xs[:2], ys[:2], kerns[:2])
+    th = _theta(2, rows[:2])
+    with _Env("GPX_BAND_TOL", "-1"):
+        band.reset_timing()
+        lb, gb, _ = band.lml_grad([0, 1], th)
+        assert band.last_timing().band_fallbacks == 2
+    with _Env("GPX_BAND", "0"):
+        ld, gd, _ = dense.lml_grad([0, 1], th)
+    for b in range(2):
+        _close(lb[b], ld[b])
+        _close(gb[b, :3], gd[b, :3])
+
+
+def test_band_storage_not_positive_definite():
+    """NOT_PD from the fused sweeps (pivot 701) and from a fallback problem."""
+    n = 1024
+    x = np.arange(n, dtype=np.float64)[:, None]
+    xb = x.copy()
+    xb[700] = np.nan
+    y = np.random.default_rng(2).standard_normal((n, 1))
+    band, _ = _pair([xb, xb], [y, y], [K.SquaredExponential()] * 2)
+    th = _theta(2, [(1.0, 1.0, 1e-5), (30.0, 1.0, 1e-5)])   # banded / fallback
+    lml, grad, info = band.lml_grad([0, 1], th)
+    assert info[0] == 701 and np.isnan(lml[0])
+    assert info[1] > 0 and np.isnan(lml[1])
+
+
+def test_band_storage_stream_matches_dense_layout():
+    """Streamed fits (C2 protocol, N=2048) through band-storage engines reach exactly the
+    dense-layout engines' trajectories and predictions."""
+    data = [O.synthetic_series(2048, seed=s) for s in range(5)]
+
+    def make():
+        out = []
+        for x, y in data:
+            m = gpx.models.GPR((x, y), kernel=K.SquaredExponential())
+            m.likelihood.variance.assign(1e-5)
+            gpx.set_trainable(m.likelihood.variance, False)
+            out.append(m)
+        return out
+
+    def engines(band):
+        ms = make()
+        return [Engine([ms[g].data[0]] * 2, [ms[g].data[1]] * 2, [compile_spec(ms[g].kernel, 1)] * 2,
+                       band_storage=band) for g in range(2)]
+    opt = gpx.optimizers.Scipy()
+    res_b, pred_b = opt.minimize_stream(make(), width=4, engine=engines(True), groups=2, predict_train=True,
+                                        options=dict(maxiter=100))
+    with _Env("GPX_BAND_PMAX", "2"):
+        res_d, pred_d = opt.minimize_stream(make(), width=4, engine=engines(False), groups=2, predict_train=True,
+                                            options=dict(maxiter=100))
+    for rb, rd, (mb, vb), (md, vd) in zip(res_b, res_d, pred_b, pred_d):
+        assert rb.nfev == rd.nfev
+        np.testing.assert_allclose(rb.x, rd.x, rtol=1e-12, atol=0)
+        _close(mb.cpu().numpy(), md.cpu().numpy(), 1e-10)
+        _close(vb.cpu().numpy(), vd.cpu().numpy(), 1e-10)
+
+
+def test_band_storage_shape_limits():
+    x = np.arange(256, dtype=np.float64)[:, None]
+    with pytest.raises(N.GPXError):
+        Engine([x], [x[:, 0]], [compile_spec(K.SquaredExponential(), 1)], band_storage=True)

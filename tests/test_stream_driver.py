@@ -279,3 +279,28 @@ def test_wide_group_routing_keeps_trajectories():
     # free narrow slot to go back to is evaluated where it is)
     wide_pts = np.concatenate(getattr(eng[2], "classes", [np.zeros(0, np.int32)]))
     assert len(wide_pts) > 0 and (wide_pts == 2).mean() > 0.5
+
+
+@pytest.mark.parametrize("engines", [1, 3])
+def test_model_stream_builds_on_demand_and_keeps_trajectories(engines):
+    # a ModelStream (models built when a slot takes them, or while the host waits for the
+    # device) gives the same fits as the list of the same models, each model built once
+    src = _models(13)
+    ref = [_solo(m) for m in _models(13)]
+    calls = []
+
+    def factory(i):
+        calls.append(i)
+        return src[i]
+    ms = gpx.optimizers.ModelStream(13, factory, input_dim=1, max_points=10)
+    assert len(ms) == 13 and calls == []
+    eng = [AsyncFakeEngine(2) for _ in range(engines)] if engines > 1 else FakeEngine(4)
+    res, preds = gpx.optimizers.Scipy().minimize_stream(ms, width=4 if engines == 1 else 6, engine=eng,
+                                                        groups=engines, predict_train=True)
+    assert sorted(calls) == list(range(13))
+    for r, r0, m, p in zip(res, ref, ms, preds):
+        assert r.nfev == r0.nfev
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+        assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
+    with pytest.raises(IndexError):
+        ms[13]

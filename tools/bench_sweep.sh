@@ -18,5 +18,5 @@ run() {  # name, then bench args
 }
 run g3w576
 run g4w640 --groups 4 --width 640
-run g2w576 --groups 2 --width 576
+run g3w640wide64 --groups 3 --width 640 --wide-slots 64
 GPX_HW_QUEUES=12 run g4w640q12 --groups 4 --width 640
