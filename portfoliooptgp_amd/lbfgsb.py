@@ -131,7 +131,9 @@ class LbfgsbStepper:
                     sf_key = key
                     fx, gx = yield sf_x
                     self.nfev += 1
-                    sf_f, sf_g = self._scalar(fx), np.atleast_1d(gx)
+                    # np.atleast_1d(gx), without its dispatch for the usual 1-D float64 row
+                    sf_f = self._scalar(fx)
+                    sf_g = gx if type(gx) is np.ndarray and gx.ndim == 1 else np.atleast_1d(gx)
                 f, g = sf_f, sf_g.copy()  # setulb gets its own g, as scipy's per-pass astype copy
             elif t0 == 1:  # new iteration
                 n_iterations += 1

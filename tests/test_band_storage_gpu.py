@@ -78,7 +78,7 @@ def test_band_storage_equals_dense_layout():
     assert not ib.any() and not idn.any()
     for b in act:
         _close(lb[b], ld[b])
-        _close(gb[b, :4], gd[b, :4])
+        _close(gb[b, :len(rows[b])], gd[b, :len(rows[b])])
     # predict_f at the training inputs: 0, 1, 3 from the cached banded factor, the rest refactor
     mb, vb, _ = band._predict_train(np.asarray(act, dtype=np.int32), th, False)
     md, vd, _ = dense._predict_train(np.asarray(act, dtype=np.int32), th, False)
