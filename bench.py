@@ -197,9 +197,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 256)),
                     help="independent series fitted per GPU per step")
-    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 576)),
+    # band storage (25 MiB per slot) lets 1536 slots stay resident: every device call then
+    # carries ~320 problems, so the chip's 512 two-per-CU places stay full while a batch is on
+    # the host (dense layout, 384 MiB per slot: 576 slots, 3833–3955 fits/s; band storage
+    # 3 x 1536: 4205, 4 x 1536: 4263–4415, 6 x 1536 on 16 queues: 4446 — tools/bench_sweep3.sh)
+    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 1536)),
                     help="resident device slots (continuous-batching width)")
-    ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 3)),
+    ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 4)),
                     help="device batches kept in flight by the one host thread (host/device overlap)")
     ap.add_argument("--wide-slots", type=int, default=int(os.environ.get("GPX_BENCH_WIDE", 0)),
                     help="slots of an extra device batch that takes the evaluations whose band is wider "
