@@ -39,7 +39,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # HIP hardware queues for this process, set before the runtime starts (torch is imported
-# inside main): the 3 device batches each evaluate on their own stream (+ one forked stream
+# inside main): the 4 device batches each evaluate on their own stream (+ one forked stream
 # for the p = 2 class), and with the runtime's default 4 queues some of those streams share a
 # queue and serialise (3 batches: 2460–2630 fits/s at 4 queues, 2800 at 8)
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPX_HW_QUEUES", "8")
@@ -328,7 +328,8 @@ def main():
         pass
     tm = _Tm()
     for f in ("contract_ms_total", "contract_launches", "contract_alg_flops", "eval_ms_total", "evals",
-              "band_ms_total", "band_calls", "band_evals", "band_p_sum"):
+              "band_ms_total", "band_calls", "band_evals", "band_p_sum", "band_fallbacks", "shadow_evals",
+              "shadow_predicts"):
         setattr(tm, f, sum(getattr(t, f) for t in tms))
     # the roofline's fused-sweep launches: the narrow batches' (p <= 1 class), not the wide
     # batch's p = 2 sweeps
@@ -386,11 +387,19 @@ def main():
         from_p = tm.band_p_sum / max(tm.band_evals, 1.0)
         # problems per timed launch (the p <= 1 class): its flops / one p = 1 problem's
         b_traffic, b_src = band_traffic(kkey, b_flops / band_problem_flops(n, 1, kfwd))
+        f2 = min(max(from_p - 1.0, 0.0), 1.0)
+        per_eval = ((1.0 - f2) * (band_problem_flops(n, 1, True) + band_problem_flops(n, 1, False))
+                    + f2 * (band_problem_flops(n, 2, True) + band_problem_flops(n, 2, False)))
+        chip_ach = tm.band_evals * per_eval / elapsed / 1e12
         roofline = {
             "kernel": kname, "bound": "mfma", "achieved": b_ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": b_ach / FP64_PEAK_TFLOPS, "traffic": b_traffic, "traffic_source": b_src,
             "traffic_unit": "bytes/launch", "mean_p_blocks": from_p,
             "avg_launch_ms": b_ms, "launches": launches, "alg_flops_per_launch": b_flops,
+            # the whole chip over the timed region: every banded evaluation's block products
+            # (both sweeps; p = 1 and p = 2 classes mixed by the mean band width) / wall time.
+            # Several device batches' launches overlap, so this is the MFMA rate the chip sustains
+            "chip_achieved": chip_ach, "chip_frac": chip_ach / FP64_PEAK_TFLOPS,
             "note": ("banded path: each launch walks its problems' 64 block steps in sequence, one "
                      "workgroup (one CU) per problem; achieved = the 64^3 block products issued "
                      "(2*64^3 flops each, leaf 2/3 of one) / launch duration. The chain of "
@@ -441,6 +450,8 @@ def main():
         "nfev_mean": nfev_mean,
         "band_path": {"evals": tm.band_evals, "dense_evals": tm.evals - tm.band_evals,
                       "mean_p_blocks": tm.band_p_sum / max(tm.band_evals, 1.0),
+                      "check_fallbacks": tm.band_fallbacks, "fallback_slot_evals": tm.shadow_evals,
+                      "fallback_slot_predicts": tm.shadow_predicts,
                       "ms_per_call": tm.band_ms_total / max(tm.band_calls, 1.0),
                       "problems_per_call": tm.band_evals / max(tm.band_calls, 1.0)},
         "evals_per_s": evals_all / elapsed,

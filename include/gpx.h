@@ -249,6 +249,8 @@ typedef struct {
   double band_fwd_flops;
   double band_bwd_flops;
   double band_fallbacks;      /* banded evaluations whose check failed, redone densely */
+  double shadow_evals;        /* band storage: evaluations run on the dense fallback slots */
+  double shadow_predicts;     /* band storage: predictions run on the dense fallback slots */
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);

@@ -61,7 +61,8 @@ class GpxTiming(ctypes.Structure):
                 ("band_p_sum", ctypes.c_double), ("band_fwd_ms_total", ctypes.c_double),
                 ("band_bwd_ms_total", ctypes.c_double), ("band_fused_launches", ctypes.c_double),
                 ("band_fwd_flops", ctypes.c_double), ("band_bwd_flops", ctypes.c_double),
-                ("band_fallbacks", ctypes.c_double)]
+                ("band_fallbacks", ctypes.c_double), ("shadow_evals", ctypes.c_double),
+                ("shadow_predicts", ctypes.c_double)]
 
 
 class GPXError(RuntimeError):

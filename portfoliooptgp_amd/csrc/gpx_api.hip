@@ -926,6 +926,7 @@ static int shadow_lml_grad(gpx_batch* bt, const std::vector<int32_t>& ids, const
     }
     const int rc = gpx_batch_lml_grad(sh, cnt, act.data(), th.data(), l.data(), g.data(), inf.data(), s);
     if (rc != GPX_OK && rc != GPX_NOT_PD) return rc;
+    bt->timing.shadow_evals += cnt;
     for (int k = 0; k < cnt; ++k) {
       const int b = ids[c + k];
       info[b] = inf[k];
@@ -952,6 +953,11 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (active[i] < 0 || active[i] >= bt->B) return fail(ctx, GPX_BAD_ARG, "active index out of range");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  {  // slots rebound since the last call land first: their band tables (from the gather's
+     // X boxes) decide the routing below
+    const int rc0 = flush_rebinds(bt, s);
+    if (rc0 != GPX_OK) return rc0;
+  }
   // Route each problem: the block-banded path when K and every ∂K/∂θ vanish exactly beyond a
   // band of p <= band_limit 64-blocks at this θ (gpx_band.hip), the dense recursion otherwise.
   // The device active list is [dense problems | banded problems].
@@ -1345,6 +1351,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
                           mean + (size_t)b * M, var ? var + (size_t)b * M : nullptr,
                           cov ? cov + (size_t)b * M * M : nullptr, inf.data(), s);
       if (rc != GPX_OK && rc != GPX_NOT_PD) return rc;
+      bt->timing.shadow_predicts += 1;
       info[b] = inf[0];
       if (rc == GPX_NOT_PD) shadow_status = GPX_NOT_PD;
     }

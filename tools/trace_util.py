@@ -10,11 +10,11 @@ import pandas as pd
 def main():
     d = pd.read_csv(sys.argv[1]).sort_values("Start_Timestamp")
     skip = float(sys.argv[2]) if len(sys.argv) > 2 else 0.3   # skip warmup / setup
-    t0, t1 = d.Start_Timestamp.min(), d.End_Timestamp.max()
-    d = d[d.Start_Timestamp >= t0 + skip * (t1 - t0)]
-    # the fit stream only: from the first to the last banded-sweep kernel
+    # the fit stream only: from the first to the last banded-sweep kernel (engine setup's
+    # copies and fills before and after it are not part of it), minus its first `skip` share
     bk = d[d.Kernel_Name.str.contains("band_")]
-    d = d[(d.Start_Timestamp >= bk.Start_Timestamp.min()) & (d.End_Timestamp <= bk.End_Timestamp.max())]
+    t0, t1 = bk.Start_Timestamp.min(), bk.End_Timestamp.max()
+    d = d[(d.Start_Timestamp >= t0 + skip * (t1 - t0)) & (d.End_Timestamp <= t1)]
     s, e = d.Start_Timestamp.to_numpy(), d.End_Timestamp.to_numpy()
     span = e.max() - s.min()
     # union of [s, e)
