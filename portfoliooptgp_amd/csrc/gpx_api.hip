@@ -744,7 +744,9 @@ int gpx_batch_destroy(gpx_batch* bt) {
     (void)hipStreamSynchronize(bt->pending_eval->s);
     bt->pending_eval.reset();
   }
-  if (bt->shadow) gpx_batch_destroy(bt->shadow);
+  if (bt->shadow) gpx_batch_destroy(bt->shadow);  // waits for its own submitted evaluation
+  if (bt->shadow_s) (void)hipStreamDestroy(bt->shadow_s);
+  if (bt->shadow_ev) (void)hipEventDestroy(bt->shadow_ev);
   if (bt->compact && bt->Kraw) {  // K/L/W point into the raw allocations (band storage's row offset)
     bt->K = bt->Kraw; bt->L = bt->Lraw; bt->W = bt->Wraw;
   }
@@ -942,6 +944,54 @@ static int shadow_lml_grad(gpx_batch* bt, const std::vector<int32_t>& ids, const
   return status;
 }
 
+// Band storage: up to kShadowSlots fallback problems are submitted on the batch's fallback
+// stream at _submit (after the call's rebind gather on s, which their inputs come from), so the
+// dense evaluation runs beside the band sweeps; _complete collects it.
+static int shadow_submit(gpx_batch* bt, const std::vector<int32_t>& ids, const double* theta, hipStream_t s) {
+  gpx_ctx* ctx = bt->ctx;
+  gpx_batch* sh = bt->shadow;
+  if (!bt->shadow_s) {
+    HIPX(ctx, hipStreamCreateWithFlags(&bt->shadow_s, hipStreamNonBlocking));
+    HIPX(ctx, hipEventCreateWithFlags(&bt->shadow_ev, hipEventDisableTiming));
+  }
+  HIPX(ctx, hipEventRecord(bt->shadow_ev, s));
+  HIPX(ctx, hipStreamWaitEvent(bt->shadow_s, bt->shadow_ev, 0));
+  const size_t nx = (size_t)bt->Nmax * bt->D;
+  std::vector<double> th((size_t)kShadowSlots * GPX_THETA_STRIDE, 1.0);
+  std::vector<int32_t> act(ids.size());
+  for (size_t k = 0; k < ids.size(); ++k) {
+    const int b = ids[k];
+    const int rc = gpx_batch_rebind_device(sh, (int)k, bt->n[b], bt->X + b * nx, bt->Y + (size_t)b * bt->Nmax,
+                                           &bt->specs[b], bt->shadow_s);
+    if (rc != GPX_OK) return rc;
+    std::memcpy(&th[k * GPX_THETA_STRIDE], theta + (size_t)b * GPX_THETA_STRIDE, sizeof(double) * GPX_THETA_STRIDE);
+    act[k] = (int32_t)k;
+  }
+  return gpx_batch_lml_grad_submit(sh, (int)ids.size(), act.data(), th.data(), bt->shadow_s);
+}
+
+static int shadow_collect(gpx_batch* bt, const std::vector<int32_t>& ids, double* lml, double* grad,
+                          int32_t* info) {
+  gpx_batch* sh = bt->shadow;
+  std::vector<double> l(kShadowSlots), g((size_t)kShadowSlots * GPX_THETA_STRIDE);
+  std::vector<int32_t> inf(kShadowSlots);
+  const int rc = gpx_batch_lml_grad_complete(sh, l.data(), g.data(), inf.data());
+  if (rc != GPX_OK && rc != GPX_NOT_PD) return rc;
+  bt->timing.shadow_evals += (double)ids.size();
+  int status = GPX_OK;
+  for (size_t k = 0; k < ids.size(); ++k) {
+    const int b = ids[k];
+    info[b] = inf[k];
+    if (inf[k] != 0) status = GPX_NOT_PD;
+    lml[b] = l[k];
+    for (int p = 0; p <= bt->specs[b].n_params; ++p)
+      grad[(size_t)b * GPX_THETA_STRIDE + p] = g[k * GPX_THETA_STRIDE + p];
+    bt->fac_valid[b] = 0;
+    bt->fac_band[b] = 0;
+  }
+  return status;
+}
+
 int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                               void* stream) {
   if (!bt) return GPX_BAD_ARG;
@@ -993,9 +1043,14 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   const int n_dense = (int)order.size(), n_band = (int)band_ids.size(), n_fused = (int)fused_ids.size();
   // the problems launched by this call (band storage: without the shadowed ones)
   n_active = n_dense + n_band + n_fused;
-  if (n_active == 0) {  // everything on the dense fallback: just land the pending rebinds
-    const int rc0 = flush_rebinds(bt, s);
-    if (rc0 != GPX_OK) return rc0;
+  // band storage: a few fallback problems go out at once on the fallback stream (more than the
+  // fallback slots hold run in chunks at _complete)
+  const bool shadow_async = !shadow_ids.empty() && (int)shadow_ids.size() <= kShadowSlots;
+  if (shadow_async) {
+    const int rcs = shadow_submit(bt, shadow_ids, theta, s);
+    if (rcs != GPX_OK) return rcs;
+  }
+  if (n_active == 0) {  // everything on the dense fallback (the rebinds landed above)
     std::unique_ptr<gpx_batch::PendingEval> pe0(new gpx_batch::PendingEval());
     pe0->s = s;
     pe0->theta.assign(theta, theta + (size_t)bt->B * GPX_THETA_STRIDE);
@@ -1003,6 +1058,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     pe0->ct.reset(new PhaseTimer(false, s));
     pe0->bp.reset(new PhaseTimer(false, s));
     pe0->shadow_ids = std::move(shadow_ids);
+    pe0->shadow_async = shadow_async;
     bt->pending_eval = std::move(pe0);
     return GPX_OK;
   }
@@ -1145,6 +1201,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   pe->n_fused = n_fused;
   pe->n_fused1 = n_fused1;
   pe->shadow_ids = std::move(shadow_ids);
+  pe->shadow_async = shadow_async;
   bt->pending_eval = std::move(pe);
   return GPX_OK;
 }
@@ -1244,7 +1301,14 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
     // band storage: the problems routed dense and those whose band check failed run on the
     // dense fallback slots
     if (total.on) bt->timing.band_fallbacks += (double)redo.size();
-    std::vector<int32_t> ids = pe->shadow_ids;
+    std::vector<int32_t> ids;
+    if (pe->shadow_async) {
+      const int rc1 = shadow_collect(bt, pe->shadow_ids, lml, grad, info);
+      if (rc1 != GPX_OK && rc1 != GPX_NOT_PD) return rc1;
+      if (rc1 == GPX_NOT_PD) status = GPX_NOT_PD;
+    } else {
+      ids = pe->shadow_ids;
+    }
     ids.insert(ids.end(), redo.begin(), redo.end());
     if (!ids.empty()) {
       const int rc2 = shadow_lml_grad(bt, ids, theta, lml, grad, info, s);
@@ -1268,7 +1332,8 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
 int gpx_batch_lml_grad_query(gpx_batch* bt) {
   if (!bt) return GPX_BAD_ARG;
   if (!bt->pending_eval) return 1;
-  const hipError_t e = hipStreamQuery(bt->pending_eval->s);
+  hipError_t e = hipStreamQuery(bt->pending_eval->s);
+  if (e == hipSuccess && bt->pending_eval->shadow_async) e = hipStreamQuery(bt->shadow_s);
   if (e == hipSuccess) return 1;
   if (e == hipErrorNotReady) return 0;
   return fail(bt->ctx, GPX_HIP_ERROR, std::string("hipStreamQuery: ") + hipGetErrorString(e));

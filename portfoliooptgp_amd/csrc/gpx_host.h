@@ -46,6 +46,8 @@ struct gpx_batch {
   double *Kraw = nullptr, *Lraw = nullptr, *Wraw = nullptr;
   gpx_batch* shadow = nullptr;     // dense fallback slots (band storage only)
   double *shX = nullptr, *shY = nullptr;
+  hipStream_t shadow_s = nullptr;  // the fallback evaluation runs here, beside the band sweeps
+  hipEvent_t shadow_ev = nullptr;
   double *z = nullptr, *alpha = nullptr, *ldiag = nullptr;  // [B][Np]
   double* partial = nullptr;       // [B][ntiles64][16]
   long long partial_stride = 0;
@@ -208,7 +210,8 @@ struct gpx_batch::PendingEval {
   hipStream_t s = nullptr;
   int n_active = 0, n_dense = 0, n_band = 0, n_fused = 0, n_fused1 = 0, ng = 0;
   std::vector<int32_t> order;
-  std::vector<int32_t> shadow_ids;  // band storage: problems evaluated on the dense shadow at _complete
+  std::vector<int32_t> shadow_ids;  // band storage: problems evaluated on the dense shadow
+  bool shadow_async = false;         // shadow_ids were submitted on bt->shadow_s by _submit
   std::vector<double> theta;
   std::unique_ptr<gpx::PhaseTimer> total, ct, bp;
   std::vector<gpx::PhaseTimer> pts;
