@@ -356,6 +356,9 @@ def main():
     iso = None
     if G > 1:
         e0 = engines[0]
+        if e0.band_storage:  # the dense path's own rate needs dense-layout slots (128 of them)
+            e0 = Engine([Xd[i % F] for i in range(128)], [Yd[i % F] for i in range(128)],
+                        [compile_spec(proto[0].kernel, 1)] * 128, device=gpu)
         th = np.ones((e0.B, 16))
         th[:, :3] = [40.0, 1.0, NOISE]
         e0.lml_grad(list(range(e0.B)), th)  # warm
