@@ -270,9 +270,10 @@ class Engine:
             outs_v = [var[b, : x.shape[0]] for b, x in zip(act, xs)]
         return outs_m, outs_v, info
 
-    def _predict_train(self, act: np.ndarray, theta: np.ndarray, add_noise: bool):
+    def _predict_train(self, act: np.ndarray, theta: np.ndarray, add_noise: bool, column: bool = False):
         """predict at each problem's own training inputs: O(N²) from the cached factor
-        (gpx_batch_predict_train)."""
+        (gpx_batch_predict_train). ``column``: each output as an [n, 1] view (GPflow's
+        predict_f shape) made by one indexing op per problem."""
         dev = f"cuda:{self.device}"
         mean = torch.empty(self.B, self.Nmax, dtype=torch.float64, device=dev)
         var = torch.empty(self.B, self.Nmax, dtype=torch.float64, device=dev)
@@ -290,6 +291,8 @@ class Engine:
                 "positive definite", info)
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_predict_train failed ({rc}): {self.ctx.last_error()}")
+        if column:
+            mean, var = mean.unsqueeze(-1), var.unsqueeze(-1)
         return ([mean[b, : self.n[b]] for b in act], [var[b, : self.n[b]] for b in act], info)
 
     def rebind(self, b: int, X, Y, spec: N.GpxKernelSpec) -> None:

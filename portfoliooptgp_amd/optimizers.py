@@ -1050,11 +1050,14 @@ class _SteppedDriver:
                     if self.predict_inputs is None and hasattr(eng, "_predict_train"):
                         # predict_f at each fit's own training inputs (GPR/model_trainer.py:20):
                         # known here, so the engine's input comparison is skipped
-                        mu, var, _ = eng._predict_train(np.asarray(pred_rows, dtype=np.int32), theta, False)
+                        mu, var, _ = eng._predict_train(np.asarray(pred_rows, dtype=np.int32), theta, False,
+                                                        column=True)
                     else:
                         mu, var, _ = eng.predict(pred_rows, theta, xs, False)
+                        mu = [t.reshape(-1, 1) for t in mu]
+                        var = [t.reshape(-1, 1) for t in var]
                 for k, r in enumerate(pred_rows):
-                    self.preds[active[r]["i"]] = (mu[k].reshape(-1, 1), var[k].reshape(-1, 1))
+                    self.preds[active[r]["i"]] = (mu[k], var[k])
             except BaseException as e:
                 for r in pred_rows:
                     self.errors[active[r]["i"]] = e
