@@ -46,6 +46,36 @@ def supports(method: str, scipy_kwargs: dict) -> bool:
     return not (set(opts) - set(_DEFAULTS) - _INERT)
 
 
+class _Result(OptimizeResult):
+    """scipy's OptimizeResult whose ``hess_inv`` (an LbfgsInvHessProduct: ≈9 µs to construct,
+    most of a finished fit's host cost, rarely read) is built on first access. Every dict view
+    (keys, items, iteration, repr, ``in``) builds it first, so the result reads as scipy's."""
+
+    def _hess(self):
+        if not dict.__contains__(self, "hess_inv"):
+            s, y = dict.pop(self, "_sy")
+            dict.__setitem__(self, "hess_inv", LbfgsInvHessProduct(s, y))
+
+    def __missing__(self, key):
+        if key == "hess_inv" and dict.__contains__(self, "_sy"):
+            self._hess()
+            return dict.__getitem__(self, "hess_inv")
+        raise KeyError(key)
+
+    def _views(name):  # noqa: N805 - method factory
+        def f(self, *a, **k):
+            if dict.__contains__(self, "_sy"):
+                self._hess()
+            return getattr(OptimizeResult, name)(self, *a, **k)
+        f.__name__ = name
+        return f
+
+    for _n in ("keys", "items", "values", "__iter__", "__len__", "__repr__", "__contains__", "get",
+               "copy", "__eq__", "__reduce__", "__dir__", "pop", "__str__"):
+        locals()[_n] = _views(_n)
+    del _n, _views
+
+
 class LbfgsbStepper:
     """One L-BFGS-B minimisation. ``x`` is the point whose (f, g) is wanted next (None once
     finished); ``tell(f, g)`` supplies it; ``result()`` is scipy's OptimizeResult."""
@@ -153,6 +183,6 @@ class LbfgsbStepper:
         y = wa[m * n: 2 * m * n].reshape(m, n)
         n_corrs = min(isave[30], m)
         msg = status_messages[task[0]] + ": " + task_messages[task[1]]
-        self._res = OptimizeResult(fun=f, jac=g, nfev=self.nfev, njev=self.nfev, nit=n_iterations,
-                                   status=warnflag, message=msg, x=x, success=(warnflag == 0),
-                                   hess_inv=LbfgsInvHessProduct(s[:n_corrs], y[:n_corrs]))
+        self._res = _Result(fun=f, jac=g, nfev=self.nfev, njev=self.nfev, nit=n_iterations,
+                            status=warnflag, message=msg, x=x, success=(warnflag == 0),
+                            _sy=(s[:n_corrs], y[:n_corrs]))

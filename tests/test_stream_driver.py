@@ -304,3 +304,21 @@ def test_model_stream_builds_on_demand_and_keeps_trajectories(engines):
         assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
     with pytest.raises(IndexError):
         ms[13]
+
+
+def test_stepper_result_reads_as_scipys():
+    # the stepper's result builds hess_inv lazily; keys, `in`, attribute and item access and
+    # the operator itself are scipy's
+    from portfoliooptgp_amd import lbfgsb
+
+    def f(x):
+        return float(((x - np.arange(3)) ** 2).sum() + np.sin(x).sum()), 2 * (x - np.arange(3)) + np.cos(x)
+    st = lbfgsb.LbfgsbStepper(np.zeros(3))
+    while not st.done:
+        st.tell(*f(st.x))
+    r = st.result()
+    r0 = scipy.optimize.minimize(f, np.zeros(3), jac=True, method="L-BFGS-B")
+    assert "hess_inv" in r and sorted(r.keys()) == sorted(r0.keys())
+    np.testing.assert_array_equal(r.hess_inv.todense(), r0.hess_inv.todense())
+    assert r["hess_inv"] is r.hess_inv
+    np.testing.assert_array_equal(r.x, r0.x)
