@@ -14,8 +14,9 @@ mkdir -p "$OUT"
 timeout -k 10 600 python3 "$ROOT/bench.py" --steps 20 --warmup 5 > "$OUT/bench.log" 2>&1
 cd /tmp && export TMPDIR=/tmp
 SHORT="--no-cpu-baseline --steps 3 --warmup 1"
+# the kernel trace over 8 steps: with 1536 slots a 3-step stream is mostly fill and drain
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/bench.py" $SHORT > "$OUT/trace.log" 2>&1
+  python3 "$ROOT/bench.py" --no-cpu-baseline --steps 8 --warmup 1 > "$OUT/trace.log" 2>&1
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
   python3 "$ROOT/bench.py" $SHORT > "$OUT/fetch.log" 2>&1
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
