@@ -80,7 +80,7 @@ def c1():
             "gpu_msg": str(getattr(res[i], "message", ""))[:60]}
            for i in range(len(res)) if not rel[i] <= 1e-5]
     rounds = _last_rounds
-    return {"rounds": len(rounds), "round_ms_mean": float(np.mean(np.diff([t for t, _ in rounds])) * 1e3)
+    return {"rounds": len(rounds), "round_ms_mean": float(np.mean(np.diff([r[1] for r in rounds])) * 1e3)
             if len(rounds) > 1 else None, "nfev_max": int(max(r.nfev for r in res)), "mismatches": off,
             "config": "C1", "workload": f"8-kernel sweep x {len(series)} daily ticker series (N=68), "
             "noise 1e-5 fixed, maxiter 100, predict_f(X_train)", "fits": len(res),
