@@ -38,12 +38,6 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# HIP hardware queues for this process, set before the runtime starts (torch is imported
-# inside main): the 4 device batches each evaluate on their own stream (+ one forked stream
-# for the p = 2 class), and with the runtime's default 4 queues some of those streams share a
-# queue and serialise (3 batches: 2460–2630 fits/s at 4 queues, 2800 at 8)
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPX_HW_QUEUES", "8")
-
 N_POINTS = 4096
 NOISE = 1e-5
 MAXITER = 100
@@ -188,6 +182,11 @@ def contract_traffic(n, flops_per_launch):
 
 
 def main():
+    # HIP hardware queues for this process, set before the runtime starts (torch is imported
+    # below): the 4 device batches each evaluate on their own stream (+ one forked stream for
+    # the p = 2 class), and with the runtime's default 4 queues some of those streams share a
+    # queue and serialise (3 batches: 2460–2630 fits/s at 4 queues, 2800 at 8)
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPX_HW_QUEUES", "8")
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # 20 timed steps of 256 fits: enough fits to keep the 576 slots streaming (with 2 steps the

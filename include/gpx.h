@@ -150,8 +150,9 @@ int gpx_batch_rebind_host(gpx_batch* batch, int b, int n, const double* X, const
 /* The same with the inputs in DEVICE memory (X [n, D], Y [n], e.g. a model's resident tensors):
  * only recorded; the next device call on the batch gathers every pending slot in one kernel on
  * its stream (which also returns the per-64-block boxes of X for the band tables), so X and Y
- * must stay valid and unchanged until that call has been issued and completed. No HIP call is
- * made here. `stream` is unused (kept for the ABI). */
+ * must stay valid and unchanged until that call has been issued and completed. `stream` (may be
+ * NULL) is the stream in whose order X and Y are ready (their producer's): an event recorded on
+ * it here is waited on by the gather when that runs on another stream. */
 int gpx_batch_rebind_device(gpx_batch* batch, int b, int n, const double* X, const double* Y,
                             const gpx_kernel_spec* spec, void* stream);
 

@@ -112,9 +112,45 @@ class OKernel:
         raise NotImplementedError
 
 
+# How the scaled squared distance r² is formed. "gpflow" (the default) is GPflow 2.9.1's
+# ``Stationary.scale`` (X / ℓ) followed by ``gpflow.utilities.ops.square_distance``:
+#     a = x/ℓ, b = x'/ℓ;   r² = (−2·(a·b)) + (‖a‖² + ‖b‖²)
+# each operation rounded on its own (TF evaluates op by op, no FMA contraction). For D = 1 that
+# order is fully determined; for D > 1 the dot product and the norms are summed over d in
+# order (TF's matmul/reduce_sum order for a 2–7 wide inner dimension is not specified; any
+# order differs by an ulp). The expansion loses ~eps·max‖a‖² absolutely to cancellation, which
+# at C2 size (x up to 4095, ℓ ≈ 1) moves logML by ~3e-7 and the gradient by ~5e-6 relative
+# against the direct form — so the GPU path computes r² the same way (gpx_kfun.h sqdist).
+# "direct" = Σ_d ((x_d − x'_d)/ℓ)² as squared differences, kept as a documented alternate
+# (more accurate in exact-arithmetic terms, not what GPflow computes).
+R2_FORM = "gpflow"
+
+
+def scaled_sqdist(A: np.ndarray, B: np.ndarray, ell: float, form: Optional[str] = None) -> np.ndarray:
+    """r²(a_i, b_j) for rows of A [n1, D] and B [n2, D] (already sliced to active dims)."""
+    form = R2_FORM if form is None else form
+    A = np.asarray(A, np.float64)
+    B = np.asarray(B, np.float64)
+    if form == "direct":
+        diff = A[:, None, :] - B[None, :, :]
+        return np.sum(diff * diff, axis=-1) / (ell * ell)
+    a = A / ell
+    b = B / ell
+    D = a.shape[1]
+    sa = a[:, 0] * a[:, 0]
+    sb = b[:, 0] * b[:, 0]
+    dot = a[:, 0:1] * b[None, :, 0]
+    for d in range(1, D):
+        sa = sa + a[:, d] * a[:, d]
+        sb = sb + b[:, d] * b[:, d]
+        dot = dot + a[:, d:d + 1] * b[None, :, d]
+    return -2.0 * dot + (sa[:, None] + sb[None, :])
+
+
 class OStationary(OKernel):
-    """IsotropicStationary: r² = Σ_d ((x_d - x'_d)/ℓ)² over active dims (GPflow
-    ``scaled_squared_euclid_dist``), r = sqrt(max(r², 1e-36)) for the K_r kernels."""
+    """IsotropicStationary: r² = Σ_d ((x_d - x'_d)/ℓ)² over active dims, formed as GPflow's
+    ``scaled_squared_euclid_dist`` forms it (``scaled_sqdist``), r = sqrt(max(r², 1e-36)) for
+    the K_r kernels."""
 
     kind = "stationary"
 
@@ -126,11 +162,10 @@ class OStationary(OKernel):
     def params(self):
         return [self.lengthscales, self.variance]          # sorted attribute names
 
-    def _d2(self, X, X2):
+    def _r2(self, X, X2):
         A = _slice_dims(np.asarray(X, np.float64), self.active_dims)
         B = A if X2 is None else _slice_dims(np.asarray(X2, np.float64), self.active_dims)
-        diff = A[:, None, :] - B[None, :, :]
-        return np.sum(diff * diff, axis=-1)                 # unscaled squared distance
+        return scaled_sqdist(A, B, self.lengthscales.value)
 
     # shape functions of the scaled r² (unit variance)
     def _g(self, r2):
@@ -140,16 +175,14 @@ class OStationary(OKernel):
         raise NotImplementedError
 
     def K(self, X, X2=None):
-        ell = self.lengthscales.value
-        return self.variance.value * self._g(self._d2(X, X2) / (ell * ell))
+        return self.variance.value * self._g(self._r2(X, X2))
 
     def K_diag(self, X):
         return np.full(np.asarray(X).shape[0], self.variance.value)
 
     def dK(self, X):
         ell, var = self.lengthscales.value, self.variance.value
-        d2 = self._d2(X, None)
-        r2 = d2 / (ell * ell)
+        r2 = self._r2(X, None)
         g = self._g(r2)
         dl = var * self._dg_dr2(r2) * (-2.0 * r2 / ell)     # d r²/dℓ = -2 r²/ℓ
         return [dl, g]
@@ -158,7 +191,7 @@ class OStationary(OKernel):
         X = np.asarray(X, np.float64)
         X2 = np.asarray(X2, np.float64)
         ell, var = self.lengthscales.value, self.variance.value
-        r2 = self._d2(X, X2) / (ell * ell)
+        r2 = self._r2(X, X2)
         f = var * self._dg_dr2(r2) * 2.0 / (ell * ell)        # ∂k/∂x_d = f · (x_d − x'_d)
         out = np.zeros(X.shape[:1] + X2.shape[:1] + X.shape[1:])
         cols = np.arange(X.shape[1])
@@ -254,8 +287,7 @@ class ORationalQuadratic(OStationary):
     def dK(self, X):
         dl, dv = super().dK(X)
         a, var = self.alpha.value, self.variance.value
-        ell = self.lengthscales.value
-        r2 = self._d2(X, None) / (ell * ell)
+        r2 = self._r2(X, None)
         b = 1.0 + 0.5 * r2 / a
         # d/dα b^(-α) = b^(-α) (-log b + r²/(2α b))
         da = var * b ** (-a) * (-np.log(b) + 0.5 * r2 / (a * b))
@@ -293,7 +325,7 @@ class OPeriodic(OKernel):
         diff, arg = self._parts(X, None)
         ell, var, p = self.base.lengthscales.value, self.base.variance.value, self.period.value
         sn = np.sin(arg)
-        s2 = np.sum(sn * sn, axis=-1) / (ell * ell)
+        s2 = np.sum((sn / ell) ** 2, axis=-1)               # as K: Σ (sin/ℓ)²
         g = np.exp(-0.5 * s2)
         dl = var * g * s2 / ell
         # d s2/dp = Σ 2 sin cos (-π diff / p²) / ℓ²
@@ -325,17 +357,27 @@ class OLinear(OKernel):
     def params(self):
         return [self.variance]
 
-    def _xx(self, X, X2):
-        A = _slice_dims(np.asarray(X, np.float64), self.active_dims)
-        B = A if X2 is None else _slice_dims(np.asarray(X2, np.float64), self.active_dims)
-        return A @ B.T
+    def _xx(self, X, X2, scale=1.0):
+        """Σ_d (x_d·scale)·x'_d, summed over d in order (gpflow.kernels.Linear.K:
+        ``tf.linalg.matmul(X * variance, X2, transpose_b=True)``)."""
+        A = _slice_dims(np.asarray(X, np.float64), self.active_dims) * scale
+        B = _slice_dims(np.asarray(X if X2 is None else X2, np.float64), self.active_dims)
+        out = A[:, 0:1] * B[None, :, 0]
+        for d in range(1, A.shape[1]):
+            out = out + A[:, d:d + 1] * B[None, :, d]
+        return out
 
     def K(self, X, X2=None):
-        return self.variance.value * self._xx(X, X2)
+        return self._xx(X, X2, self.variance.value)
 
     def K_diag(self, X):
+        # Linear.K_diag: reduce_sum(square(X) * variance, -1)
         A = _slice_dims(np.asarray(X, np.float64), self.active_dims)
-        return self.variance.value * np.sum(A * A, axis=-1)
+        sq = (A * A) * self.variance.value
+        out = sq[:, 0]
+        for d in range(1, sq.shape[1]):
+            out = out + sq[:, d]
+        return out
 
     def dK(self, X):
         return [self._xx(X, None)]
@@ -476,6 +518,41 @@ class OGPR:
         if self.noise.trainable:
             grads.append(0.5 * float(np.trace(Wm)) * self.noise.dtheta_du())
         return -lml, -np.array(grads, dtype=np.float64)
+
+    def loss_and_grad_u_extended(self):
+        """loss_and_grad_u with the linear algebra in x87 extended precision (np.longdouble, a
+        64-bit significand: ~2000x fp64's precision) on the SAME fp64 K and ∂K/∂θ. The fp64
+        gradient ½Σ(ααᵀ − K⁻¹)∘∂K is a cancellation whose error grows with cond(K); this is the
+        near-exact value of the fp64 problem, used to tell where the fp64 oracle itself is off
+        (tests/golden/make_golden.py stores it per fixture). O(N³) numpy vector ops: N ≲ 512."""
+        ld = np.longdouble
+        Ky = self._Ky().astype(ld)
+        n = Ky.shape[0]
+        L = np.zeros((n, n), dtype=ld)
+        for j in range(n):
+            s = Ky[j:, j] - L[j:, :j] @ L[j, :j]
+            if s[0] <= 0:
+                raise np.linalg.LinAlgError("not positive definite (extended precision)")
+            L[j, j] = np.sqrt(s[0])
+            L[j + 1:, j] = s[1:] / L[j, j]
+        W = np.zeros((n, n), dtype=ld)          # W = L⁻¹ by forward substitution, column by column
+        for i in range(n):
+            W[i, :] = -(L[i, :i] @ W[:i, :])
+            W[i, i] += 1
+            W[i, :] /= L[i, i]
+        y = self.Y[:, 0].astype(ld)
+        z = W @ y
+        alpha = W.T @ z
+        Kinv = W.T @ W
+        lml = -0.5 * (z @ z) - np.sum(np.log(np.diag(L))) - ld(0.5) * n * ld(LOG2PI)
+        Wm = np.outer(alpha, alpha) - Kinv
+        grads = []
+        for p, dk in zip(self.kernel.params(), self.kernel.dK(self.X)):
+            if p.trainable:
+                grads.append(float(ld(0.5) * np.sum(Wm * dk.astype(ld))) * p.dtheta_du())
+        if self.noise.trainable:
+            grads.append(float(ld(0.5) * np.trace(Wm)) * self.noise.dtheta_du())
+        return -float(lml), -np.array(grads, dtype=np.float64)
 
     def predict_f(self, Xnew, full_cov=False):
         """GPflow base_conditional(kmn, kmm+σ²I, knn, err, white=False)."""

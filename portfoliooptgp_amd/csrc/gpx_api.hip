@@ -11,6 +11,7 @@
 //   5. logML = −½‖z‖² − Σ log L_ii − (n/2) log 2π;  ∂logML/∂θ = ½ Σ (ααᵀ − K⁻¹)∘∂K/∂θ
 // Algorithmic flops per problem: N³/3 (potrf) + N³/3 (trtri) + N³/3 (WᵀW) ≈ N³.
 #include <hip/hip_runtime.h>
+#include <cfloat>
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -193,7 +194,11 @@ void reduce(const Run& r) {
 // 745.13) and so is the whole entry (0 times a finite polynomial). band_rmin bounds r from
 // below for every pair of points in blocks (k, k − d) (bounding boxes of the blocks' valid
 // rows, per term's active dims); the margin 746 − 745.13 covers the rounding of r²/ℓ² on the
-// device many times over. A sum vanishes when all its terms do, a product when any does.
+// device many times over. The device forms r² as GPflow does, (−2a·b) + (‖a‖² + ‖b‖²) with
+// a = x/ℓ, which can fall short of the true (Δx/ℓ)² by cancellation, by at most a few
+// eps·(‖a‖² + ‖b‖² + ‖a−b‖·max‖a‖): band_width shaves 64 eps·(M² + sM + 1) off s² (M = the
+// largest ‖x/ℓ‖ of the problem's valid rows, kept in slot 0 of each term's table).
+// A sum vanishes when all its terms do, a product when any does.
 namespace {
 bool band_kind(int kind) { return kind >= GPX_SE && kind <= GPX_EXPONENTIAL; }
 
@@ -218,6 +223,16 @@ static void band_tables_lohi(gpx_batch* bt, int b, const std::vector<double>& lo
   for (int t = 0; t < sp.n_terms; ++t) {
     const int d0 = sp.terms[t].dim_start, dn = sp.terms[t].dim_count;
     double* rt = out + (size_t)t * nb;
+    double m2 = 0.0;  // max ‖x‖² over the valid rows (active dims), bounded by the boxes
+    for (int k = 0; k < nvb; ++k) {
+      double s2 = 0.0;
+      for (int d = d0; d < d0 + dn; ++d) {
+        const double mx = std::max(std::fabs(lo[(size_t)k * D + d]), std::fabs(hi[(size_t)k * D + d]));
+        s2 += mx * mx;
+      }
+      m2 = std::max(m2, s2);
+    }
+    rt[0] = std::sqrt(m2) * (1.0 + 1e-12);
     for (int dd = 1; dd < nvb; ++dd) {
       double m = INFINITY;
       for (int k = dd; k < nvb; ++k) {
@@ -275,7 +290,12 @@ int band_width(const gpx_batch* bt, int b, const double* th) {
     for (int t = 0; t < sp.n_terms; ++t) {
       const double ell = th[sp.terms[t].param_offset];
       const double r = tab[(size_t)t * nb + d];
-      const bool term_nz = !(r == INFINITY || band_arg(sp.terms[t].kind, r / ell) >= 746.0);
+      bool term_nz = false;
+      if (r != INFINITY) {
+        const double sv = r / ell, M = tab[(size_t)t * nb] / ell;
+        const double s2 = sv * sv - 64.0 * DBL_EPSILON * (M * M + sv * M + 1.0);
+        term_nz = !(band_arg(sp.terms[t].kind, s2 > 0.0 ? std::sqrt(s2) : 0.0) >= 746.0);
+      }
       nz = prod ? (nz && term_nz) : (nz || term_nz);
     }
     if (nz) return d;
@@ -501,6 +521,11 @@ int flush_rebinds(gpx_batch* bt, hipStream_t s) {
   for (const auto& e : bt->pend)
     bt->h_rdesc[m++] = RebindDesc{e.x, e.y, const_cast<double*>(bt->X) + (size_t)e.b * nx,
                                   const_cast<double*>(bt->Y) + (size_t)e.b * ny, e.n, tables ? nbox++ : -1};
+  for (auto& w : bt->rebind_waits)  // the device sources' producers (gpx_batch_rebind_device)
+    if (w.armed) {
+      if (w.s != s) HIPX(ctx, hipStreamWaitEvent(s, w.ev, 0));
+      w.armed = false;
+    }
   if (m > 0) {
     launch_rebind_gather(bt->h_rdesc, m, bt->Nmax, bt->D, bt->d_box, s);
     HIPX(ctx, hipGetLastError());
@@ -522,8 +547,8 @@ int flush_rebinds(gpx_batch* bt, hipStream_t s) {
   return GPX_OK;
 }
 
-int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
-                  hipStream_t s) {
+// the active set and every active row's θ (kernel parameters + σn²: finite and > 0)
+int check_active_theta(gpx_batch* bt, int n_active, const int32_t* active, const double* theta) {
   gpx_ctx* ctx = bt->ctx;
   if (n_active <= 0 || n_active > bt->B || !active || !theta)
     return fail(ctx, GPX_BAD_ARG, "bad active set / theta");
@@ -537,6 +562,16 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
       if (!(v > 0.0) || !std::isfinite(v))
         return fail(ctx, GPX_BAD_ARG, "theta must be finite and > 0 (constrained space)");
     }
+  }
+  return GPX_OK;
+}
+
+int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                  hipStream_t s) {
+  gpx_ctx* ctx = bt->ctx;
+  {
+    const int e = check_active_theta(bt, n_active, active, theta);
+    if (e != GPX_OK) return e;
   }
   {
     const int e = flush_rebinds(bt, s);
@@ -747,6 +782,7 @@ int gpx_batch_destroy(gpx_batch* bt) {
   if (bt->shadow) gpx_batch_destroy(bt->shadow);  // waits for its own submitted evaluation
   if (bt->shadow_s) (void)hipStreamDestroy(bt->shadow_s);
   if (bt->shadow_ev) (void)hipEventDestroy(bt->shadow_ev);
+  for (auto& w : bt->rebind_waits) (void)hipEventDestroy(w.ev);
   if (bt->compact && bt->Kraw) {  // K/L/W point into the raw allocations (band storage's row offset)
     bt->K = bt->Kraw; bt->L = bt->Lraw; bt->W = bt->Wraw;
   }
@@ -848,9 +884,25 @@ int gpx_batch_rebind_device(gpx_batch* bt, int b, int n, const double* X, const 
   if (!X || !Y) return fail(ctx, GPX_BAD_ARG, "null device inputs");
   int rc = check_rebind(bt, b, n, spec);
   if (rc != GPX_OK) return rc;
-  (void)stream;
   // recorded only: the next device call's flush_rebinds gathers every pending slot in one
-  // kernel on that call's stream (X and Y must stay valid until then)
+  // kernel on that call's stream (X and Y must stay valid until then). X and Y are ready in
+  // the order of `stream` (the caller's current stream, where their producers ran): an event
+  // recorded on it now orders the gather after them, whichever stream the gather runs on
+  if (stream) {
+    HIPX(ctx, hipSetDevice(ctx->device));
+    const hipStream_t s = (hipStream_t)stream;
+    gpx_batch::RebindWait* w = nullptr;
+    for (auto& x : bt->rebind_waits)
+      if (x.s == s) w = &x;
+    if (!w) {
+      hipEvent_t ev;
+      HIPX(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      bt->rebind_waits.push_back(gpx_batch::RebindWait{s, ev, false});
+      w = &bt->rebind_waits.back();
+    }
+    HIPX(ctx, hipEventRecord(w->ev, s));
+    w->armed = true;
+  }
   bt->n[b] = n;
   bt->specs[b] = *spec;
   bt->fac_valid[b] = 0;
@@ -997,10 +1049,10 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   if (!bt) return GPX_BAD_ARG;
   gpx_ctx* ctx = bt->ctx;
   if (bt->pending_eval) return fail(ctx, GPX_BAD_ARG, "an evaluation is already submitted on this batch");
-  if (n_active <= 0 || n_active > bt->B || !active || !theta)
-    return fail(ctx, GPX_BAD_ARG, "bad active set / theta");
-  for (int i = 0; i < n_active; ++i)
-    if (active[i] < 0 || active[i] >= bt->B) return fail(ctx, GPX_BAD_ARG, "active index out of range");
+  {  // every argument check before anything is routed or submitted (the fallback slots included)
+    const int e = check_active_theta(bt, n_active, active, theta);
+    if (e != GPX_OK) return e;
+  }
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   {  // slots rebound since the last call land first: their band tables (from the gather's
@@ -1046,9 +1098,18 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   // band storage: a few fallback problems go out at once on the fallback stream (more than the
   // fallback slots hold run in chunks at _complete)
   const bool shadow_async = !shadow_ids.empty() && (int)shadow_ids.size() <= kShadowSlots;
+  // a failure after the fallback evaluation went out leaves nothing pending on the fallback
+  // slots: drain its stream and drop its state, so later calls are not refused
+  auto drop_shadow = [&](int rc) {
+    if (shadow_async && bt->shadow && bt->shadow->pending_eval) {
+      (void)hipStreamSynchronize(bt->shadow->pending_eval->s);
+      bt->shadow->pending_eval.reset();
+    }
+    return rc;
+  };
   if (shadow_async) {
     const int rcs = shadow_submit(bt, shadow_ids, theta, s);
-    if (rcs != GPX_OK) return rcs;
+    if (rcs != GPX_OK) return drop_shadow(rcs);
   }
   if (n_active == 0) {  // everything on the dense fallback (the rebinds landed above)
     std::unique_ptr<gpx_batch::PendingEval> pe0(new gpx_batch::PendingEval());
@@ -1071,12 +1132,12 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (bt->h_bandp[b] > 1) order.push_back(b);
   if (n_band > 0) {
     const int e = ensure(ctx, bt->bres, bt->bres_cap, (size_t)bt->B * bt->Np);
-    if (e != GPX_OK) return e;
+    if (e != GPX_OK) return drop_shadow(e);
   }
   int rc = upload_common(bt, n_active, order.data(), theta, s);
-  if (rc != GPX_OK) return rc;
+  if (rc != GPX_OK) return drop_shadow(rc);
   rc = match_aux_priority(bt, s);
-  if (rc != GPX_OK) return rc;
+  if (rc != GPX_OK) return drop_shadow(rc);
   bt->flops_acc = 0.0;
   std::unique_ptr<gpx_batch::PendingEval> pe(new gpx_batch::PendingEval());
   pe->s = s;

@@ -162,21 +162,25 @@ __global__ __launch_bounds__(256) void band_contract_kernel(BandContractArgs a) 
   const int n = a.nvalid[b];
   const double* X = a.X + (long long)b * a.sX;
   const double* al = a.alpha + (long long)b * a.sVec;
+  const DevSpec spec = a.specs[b];
+  const int fkind = spec.terms[0].kind;
+  const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
+  const int fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
+  const double fell = a.theta[b * GPX_THETA_STRIDE + spec.terms[0].param_offset];
+  const double fvar = a.theta[b * GPX_THETA_STRIDE + spec.terms[0].param_offset + 1];
+  const double finv_ell = 1.0 / fell;
+  // one stationary term: inputs staged pre-scaled by 1/ℓ (GPflow's Stationary.scale)
   for (int e = tid; e < 64 * D; e += 256) {
     const int r = e / D, dd = e - (e / D) * D;
-    sxi[e] = (i0 + r < n) ? X[(long long)(i0 + r) * D + dd] : 0.0;
-    sxj[e] = (j0 + r < n) ? X[(long long)(j0 + r) * D + dd] : 0.0;
+    const double xi = (i0 + r < n) ? X[(long long)(i0 + r) * D + dd] : 0.0;
+    const double xj = (j0 + r < n) ? X[(long long)(j0 + r) * D + dd] : 0.0;
+    sxi[e] = fast ? xi / fell : xi;
+    sxj[e] = fast ? xj / fell : xj;
   }
   if (tid < 64) { sai[tid] = al[i0 + tid]; saj[tid] = al[j0 + tid]; }
   if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
   __syncthreads();
-  const DevSpec spec = a.specs[b];
   const double* Z = a.Z + (long long)b * a.sMat;
-  const int fkind = spec.terms[0].kind;
-  const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
-  const int fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
-  const double fell = sth[spec.terms[0].param_offset], fvar = sth[spec.terms[0].param_offset + 1];
-  const double finv_ell = 1.0 / fell, finv_l2 = finv_ell * finv_ell;
   double sums[NT][3];
 #pragma unroll
   for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
@@ -194,12 +198,7 @@ __global__ __launch_bounds__(256) void band_contract_kernel(BandContractArgs a) 
       double dk[NT][3];
       double kij;
       if (fast) {
-        double d2 = 0.0;
-        for (int q = 0; q < fdn; ++q) {
-          const double diff = sxi[il * D + fd0 + q] - sxj[jl * D + fd0 + q];
-          d2 = fma(diff, diff, d2);
-        }
-        stationary_grad(fkind, d2 * finv_l2, fvar, finv_ell, dk[0]);
+        stationary_grad(fkind, sqdist_scaled(sxi + il * D + fd0, sxj + jl * D + fd0, fdn), fvar, finv_ell, dk[0]);
         kij = fvar * dk[0][1];
       } else {
         kij = eval_k_grad<NT>(spec, sth, sxi + il * D, sxj + jl * D, dk);
@@ -447,11 +446,12 @@ __device__ __forceinline__ double xrows_fetch(const double* __restrict__ X, int 
   const double v = X[idx];
   return (e < 64 * D && r0 + e / D < n) ? v : 0.0;
 }
+// (scaled by 1/ell, a division as GPflow's Stationary.scale; ell = 1 stores them as they are)
 __device__ __forceinline__ void xrows_store(double xr, double* __restrict__ s, const double* __restrict__ X,
-                                            int r0, int n, int D) {
+                                            int r0, int n, int D, double ell) {
   const int nx = 64 * D, tid = threadIdx.x;
-  if (tid < nx) s[tid] = xr;
-  for (int e = tid + 256; e < nx; e += 256) s[e] = (r0 + e / D < n) ? X[r0 * D + e] : 0.0;
+  if (tid < nx) s[tid] = xr / ell;
+  for (int e = tid + 256; e < nx; e += 256) s[e] = (r0 + e / D < n) ? X[r0 * D + e] / ell : 0.0;
 }
 
 // Kernel-function context of one problem's gradient contraction
@@ -461,7 +461,8 @@ struct ContractCtx {
   const double* sth;
   int D, n, fkind, fd0, fdn;
   bool fast;  // one stationary term (SE / Matern / Exponential): closed form below
-  double fvar, finv_ell, finv_l2, noise;
+  double fvar, finv_ell, noise;
+  double xscale;  // the X rows in LDS are divided by this: ℓ when fast, else 1
   double sums[NT][3];
   double snoise;
 };
@@ -471,10 +472,11 @@ struct ContractCtx {
 // products K_ij Z_ij into colacc (this thread's column). A diagonal block is taken whole (both
 // triangles, w = 1: Z_kk and K_kk are symmetric); an off-diagonal block stands for itself and
 // its mirror (w = 2), and its K_ij Z_ij overwrite Z in place for the row sums (block_rowsum).
-// Inputs come from LDS: Z, the α slices and the X rows of both blocks (sxi, sxj).
+// Inputs come from LDS: Z, the α slices and the X rows of both blocks (sxi, sxj; pre-scaled by
+// 1/ℓ when cx.fast).
 // The same for the reference's kernel (one SquaredExponential term on one input column), as
-// straight-line code: g = exp(−r²/2), ∂K/∂ℓ = σ² g r²/ℓ, ∂K/∂σ² = g (stationary_grad's SE case,
-// operation for operation)
+// straight-line code: r² = sqdist1(a_i, a_j) (GPflow's square_distance), g = exp(−r²/2),
+// ∂K/∂ℓ = σ² g r²/ℓ, ∂K/∂σ² = g (stationary_grad's SE case, operation for operation)
 template <int NT>
 __device__ __forceinline__ void contract_block_se1(ContractCtx<NT>& cx, double* __restrict__ sZ,
                                                    const double* __restrict__ sxi, const double* __restrict__ sxj,
@@ -483,15 +485,14 @@ __device__ __forceinline__ void contract_block_se1(ContractCtx<NT>& cx, double* 
   const int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int jl = lane, j = j0 + jl, D = cx.D, d0 = cx.fd0;
   const double ajl = aj[jl], w = diag ? 1.0 : 2.0, xj = sxj[jl * D + d0];
-  const double var = cx.fvar, inv_ell = cx.finv_ell, inv_l2 = cx.finv_l2;
+  const double var = cx.fvar, inv_ell = cx.finv_ell;
   const bool jok = j < cx.n;
   double s0 = 0.0, s1 = 0.0, sn = 0.0, ca = 0.0;
 #pragma unroll 4
   for (int t = 0; t < 16; ++t) {
     const int il = part * 16 + t, i = i0 + il;
     const double zij = sZ[il * BS + jl];
-    const double diff = sxi[il * D + d0] - xj;
-    const double r2 = fma(diff, diff, 0.0) * inv_l2;
+    const double r2 = sqdist1(sxi[il * D + d0], xj);
     const double g = exp(-0.5 * r2);
     const double v = w * fma(ai[il], ajl, -zij);
     const bool ok = jok && i < cx.n;
@@ -534,12 +535,7 @@ __device__ __forceinline__ void contract_block(ContractCtx<NT>& cx, double* __re
       double dk[NT][3];
       double kij;
       if (cx.fast) {
-        double d2 = 0.0;
-        for (int q = 0; q < cx.fdn; ++q) {
-          const double diff = xi[cx.fd0 + q] - xj[cx.fd0 + q];
-          d2 = fma(diff, diff, d2);
-        }
-        stationary_grad(cx.fkind, d2 * cx.finv_l2, cx.fvar, cx.finv_ell, dk[0]);
+        stationary_grad(cx.fkind, sqdist_scaled(xi + cx.fd0, xj + cx.fd0, cx.fdn), cx.fvar, cx.finv_ell, dk[0]);
         kij = cx.fvar * dk[0][1];  // ∂K/∂σ² = K/σ² for a single stationary term
       } else {
         kij = eval_k_grad<NT>(*cx.spec, cx.sth, xi, xj, dk);
@@ -738,7 +734,8 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
   cx.fast = (NT == 1) && spec.n_terms == 1 && cx.fkind >= GPX_SE && cx.fkind <= GPX_EXPONENTIAL;
   cx.fd0 = spec.terms[0].dim_start; cx.fdn = spec.terms[0].dim_count;
   cx.fvar = sth[spec.terms[0].param_offset + 1];
-  cx.finv_ell = 1.0 / sth[spec.terms[0].param_offset]; cx.finv_l2 = cx.finv_ell * cx.finv_ell;
+  cx.finv_ell = 1.0 / sth[spec.terms[0].param_offset];
+  cx.xscale = cx.fast ? sth[spec.terms[0].param_offset] : 1.0;
   cx.noise = sth[spec.n_params];
 #pragma unroll
   for (int t = 0; t < NT; ++t) cx.sums[t][0] = cx.sums[t][1] = cx.sums[t][2] = 0.0;
@@ -773,7 +770,7 @@ __global__ __launch_bounds__(256, 1) void band_bwd_kernel(BandFusedArgs a) {
     block_store_lds(pw, sW);
     if (q >= 1) block_store_lds(p1, sX);
     if (q >= 2) block_store_lds(p2, sY);
-    xrows_store(xr, sxr + s0 * nx, X, k64, n, D);
+    xrows_store(xr, sxr + s0 * nx, X, k64, n, D, cx.xscale);
     __syncthreads();
     if (tid < 64) st[tid] = zpre - ((spart[0][0][tid] + spart[0][1][tid]) + (spart[0][2][tid] + spart[0][3][tid]));
     __syncthreads();
@@ -1097,7 +1094,8 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
   cx.fast = (NT == 1) && spec.n_terms == 1 && cx.fkind >= GPX_SE && cx.fkind <= GPX_EXPONENTIAL;
   cx.fd0 = spec.terms[0].dim_start; cx.fdn = spec.terms[0].dim_count;
   cx.fvar = sth[spec.terms[0].param_offset + 1];
-  cx.finv_ell = 1.0 / sth[spec.terms[0].param_offset]; cx.finv_l2 = cx.finv_ell * cx.finv_ell;
+  cx.finv_ell = 1.0 / sth[spec.terms[0].param_offset];
+  cx.xscale = cx.fast ? sth[spec.terms[0].param_offset] : 1.0;
   cx.noise = sth[spec.n_params];
 #pragma unroll
   for (int t = 0; t < NT; ++t) cx.sums[t][0] = cx.sums[t][1] = cx.sums[t][2] = 0.0;
@@ -1120,7 +1118,7 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
     }
     block_store_lds(pw, sW);
     if (q >= 1) block_store_lds(pp, sA);
-    xrows_store(xr, sxr + cs * nx, X, k64, n, D);
+    xrows_store(xr, sxr + cs * nx, X, k64, n, D, cx.xscale);
     __syncthreads();
     if (tid < 64) st[tid] = zpre - ((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]));
     __syncthreads();

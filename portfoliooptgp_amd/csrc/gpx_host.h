@@ -86,6 +86,10 @@ struct gpx_batch {
   struct PendingEval;
   std::unique_ptr<PendingEval> pending_eval;
   std::vector<PendingRebind> pend;
+  // the streams the pending device sources were rebound on (their producers' order): an event
+  // recorded there at the rebind, waited on by flush_rebinds' gather stream
+  struct RebindWait { hipStream_t s; hipEvent_t ev; bool armed; };
+  std::vector<RebindWait> rebind_waits;
   gpx::RebindDesc* h_rdesc = nullptr;   // pinned (coherent), one per slot
   double* d_box = nullptr;               // [B][nb][D][2] per-block lo/hi of X
   double* h_box = nullptr;               // pinned mirror of the rows of one flush

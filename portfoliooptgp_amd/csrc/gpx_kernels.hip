@@ -71,10 +71,10 @@ __device__ __forceinline__ void build_stationary(const BuildArgs& a, const DevSp
                                                  const double* sth, const double* sxi,
                                                  const double* sxj, double noise, int n, int ncol,
                                                  int ti, int tj, double* out) {
+  // sxi / sxj hold the inputs already scaled by 1/ℓ (staged that way by build_kernel)
   const gpx_term& t = spec.terms[0];
   const double* th = sth + t.param_offset;
-  const double ell = th[0], var = th[1];
-  const double inv_l2 = 1.0 / (ell * ell);
+  const double var = th[1];
   const int D = a.D, d0 = t.dim_start, dn = t.dim_count;
   const int c = threadIdx.x & 63;
   const int gj = tj * 64 + c;
@@ -84,12 +84,9 @@ __device__ __forceinline__ void build_stationary(const BuildArgs& a, const DevSp
     double v;
     const bool valid = a.symmetric ? (gi < n && gj < n) : (gi < n && gj < ncol);
     if (valid) {
-      double d2 = 0.0;
-      for (int d = 0; d < dn; ++d) {
-        const double diff = sxi[r * D + d0 + d] - sxj[c * D + d0 + d];
-        d2 = fma(diff, diff, d2);
-      }
-      v = stationary_value<KIND>(d2 * inv_l2, var);
+      const double r2 = dn == 1 ? sqdist1(sxi[r * D + d0], sxj[c * D + d0])
+                                : sqdist_scaled(sxi + r * D + d0, sxj + c * D + d0, dn);
+      v = stationary_value<KIND>(r2, var);
       if (a.symmetric && gi == gj) v += noise;
     } else {
       v = (a.symmetric && gi == gj) ? 1.0 : 0.0;
@@ -122,24 +119,30 @@ __global__ __launch_bounds__(256) void build_kernel(BuildArgs a) {
   const int ncol = a.symmetric ? n : a.m2;
   const double* X = a.X + (long long)b * a.sX;
   const double* X2 = a.symmetric ? X : a.X2 + (long long)b * a.sX2;
+  const DevSpec spec = a.specs[b];
+  // single-term isotropic stationary kernels (the reference's SE / Matern / Exponential sweeps)
+  // take a compact loop on inputs staged pre-scaled by 1/ℓ (GPflow's Stationary.scale, one
+  // division per staged value instead of two per element): the generic term interpreter below
+  // unrolls into tens of KiB of code per kernel, which thrashed the instruction cache of this
+  // HBM-write kernel
+  const int k0 = spec.terms[0].kind;
+  const bool fast = spec.n_terms == 1 && k0 >= GPX_SE && k0 <= GPX_EXPONENTIAL;
+  const double fell = fast ? a.theta[b * GPX_THETA_STRIDE + spec.terms[0].param_offset] : 1.0;
   for (int e = tid; e < 64 * D; e += 256) {
     const int r = e / D, d = e - (e / D) * D;
     const int gi = ti * 64 + r, gj = tj * 64 + r;
-    sxi[e] = gi < n ? X[(long long)gi * D + d] : 0.0;
-    sxj[e] = gj < ncol ? X2[(long long)gj * D + d] : 0.0;
+    const double xi = gi < n ? X[(long long)gi * D + d] : 0.0;
+    const double xj = gj < ncol ? X2[(long long)gj * D + d] : 0.0;
+    sxi[e] = fast ? xi / fell : xi;
+    sxj[e] = fast ? xj / fell : xj;
   }
   if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
   __syncthreads();
-  const DevSpec spec = a.specs[b];
   const double noise = sth[spec.n_params];
   double* out = a.out + (long long)b * a.sOut;
   const int c = tid & 63;
   const int gj = tj * 64 + c;
-  // single-term isotropic stationary kernels (the reference's SE / Matern / Exponential sweeps)
-  // take a compact loop with 1/ℓ² hoisted: the generic term interpreter below unrolls into tens
-  // of KiB of code per kernel, which thrashed the instruction cache of this HBM-write kernel
-  const int k0 = spec.terms[0].kind;
-  if (spec.n_terms == 1 && k0 >= GPX_SE && k0 <= GPX_EXPONENTIAL) {
+  if (fast) {
     switch (k0) {
       case GPX_SE:          build_stationary<GPX_SE>(a, spec, sth, sxi, sxj, noise, n, ncol, ti, tj, out); return;
       case GPX_MATERN12:    build_stationary<GPX_MATERN12>(a, spec, sth, sxi, sxj, noise, n, ncol, ti, tj, out); return;
@@ -628,14 +631,25 @@ void gemm_kernel(GemmArgs a) {
     const int n = a.nvalid[b];
     const double* X = a.X + (long long)b * a.sX;
     const double* al = a.vec + (long long)b * a.sVec;
+    const DevSpec spec = a.specs[b];
+    // single-term isotropic stationary specs (the SE / Matern / Exponential fits): the inputs
+    // are staged pre-scaled by 1/ℓ and ℓ-dependent factors hoisted out of the per-element
+    // derivative (no division per element)
+    const int fkind = spec.terms[0].kind;
+    const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
+    const int fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
+    const double fell = a.theta[b * GPX_THETA_STRIDE + spec.terms[0].param_offset];
+    const double fvar = a.theta[b * GPX_THETA_STRIDE + spec.terms[0].param_offset + 1];
+    const double finv_ell = 1.0 / fell;
     for (int e = tid; e < BM * D; e += 256) {
       const int r = e / D, d = e - (e / D) * D;
-      sxi[e] = (i0 + r < n) ? X[(long long)(i0 + r) * D + d] : 0.0;
-      sxj[e] = (j0 + r < n) ? X[(long long)(j0 + r) * D + d] : 0.0;
+      const double xi = (i0 + r < n) ? X[(long long)(i0 + r) * D + d] : 0.0;
+      const double xj = (j0 + r < n) ? X[(long long)(j0 + r) * D + d] : 0.0;
+      sxi[e] = fast ? xi / fell : xi;
+      sxj[e] = fast ? xj / fell : xj;
     }
     if (tid < BM) { sai[tid] = al[i0 + tid]; saj[tid] = al[j0 + tid]; }
     if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
-    const DevSpec spec = a.specs[b];
     double sums[NT][3];
 #pragma unroll
     for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
@@ -647,14 +661,6 @@ void gemm_kernel(GemmArgs a) {
     const int cl = lane % WT, rg = lane / WT;
     const int jl = wc * WT + cl;            // this lane's column within the tile
     const int j = j0 + jl;
-    // single-term isotropic stationary specs (the SE / Matern / Exponential fits): ℓ-dependent
-    // factors hoisted out of the per-element derivative (no division per element)
-    const int fkind = spec.terms[0].kind;
-    const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
-    const int fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
-    const double fell = a.theta[b * GPX_THETA_STRIDE + spec.terms[0].param_offset];
-    const double fvar = a.theta[b * GPX_THETA_STRIDE + spec.terms[0].param_offset + 1];
-    const double finv_ell = 1.0 / fell, finv_l2 = finv_ell * finv_ell;
 #pragma unroll
     for (int h = 0; h < MT; ++h) {
 #pragma unroll
@@ -674,12 +680,8 @@ void gemm_kernel(GemmArgs a) {
             const double v = w * fma(sai[il], aj, -wacc[rr * WT + cl]);
             double dk[NT][3];
             if (fast) {
-              double d2 = 0.0;
-              for (int d = 0; d < fdn; ++d) {
-                const double diff = sxi[il * D + fd0 + d] - sxj[jl * D + fd0 + d];
-                d2 = fma(diff, diff, d2);
-              }
-              stationary_grad(fkind, d2 * finv_l2, fvar, finv_ell, dk[0]);
+              stationary_grad(fkind, sqdist_scaled(sxi + il * D + fd0, sxj + jl * D + fd0, fdn), fvar,
+                              finv_ell, dk[0]);
             } else {
               eval_k_grad<NT>(spec, sth, sxi + il * D, sxj + jl * D, dk);
             }

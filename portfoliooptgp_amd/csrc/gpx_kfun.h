@@ -1,10 +1,12 @@
 // gpx_kfun.h — device-side covariance functions and their θ-derivatives.
 //
 // Restates the GPflow 2.9.1 kernels the reference builds at GPR/main.py:105-114 and
-// Multi-Input_GPR/main.py:118-135 (formulas: SURVEY.md §8 a3). Distances are taken as direct
-// differences Σ_d (x_d - x'_d)² (GPflow expands ‖x‖²+‖x'‖²-2x·x'; the two agree to rounding),
-// and the K_r kernels use r = sqrt(max(r², 1e-36)) with zero r-gradient where clamped, as
-// GPflow's IsotropicStationary.K_r2 does.
+// Multi-Input_GPR/main.py:118-135 (formulas: SURVEY.md §8 a3). Squared distances are formed the
+// way GPflow forms them (Stationary.scale divides by ℓ, then utilities.ops.square_distance
+// expands): a = x/ℓ, b = x'/ℓ, r² = (−2·(a·b)) + (‖a‖² + ‖b‖²), each operation rounded on its own
+// (no FMA contraction), sums over d in order — the same arithmetic as oracle/gp_oracle.py
+// scaled_sqdist. The K_r kernels use r = sqrt(max(r², 1e-36)) with zero r-gradient where
+// clamped, as GPflow's IsotropicStationary.K_r2 does.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "../../include/gpx.h"
@@ -26,6 +28,40 @@ __device__ __forceinline__ int term_nparams(int kind) {
   }
 }
 
+// GPflow's square_distance of two points already scaled by 1/ℓ (a, b: dn values each):
+// (−2·Σ a_d b_d) + (Σ a_d² + Σ b_d²), every product and sum rounded separately.
+__device__ __forceinline__ double sqdist_scaled(const double* __restrict__ a, const double* __restrict__ b,
+                                                int dn) {
+#pragma clang fp contract(off)
+  double dot = a[0] * b[0], sa = a[0] * a[0], sb = b[0] * b[0];
+  for (int d = 1; d < dn; ++d) {
+    dot = dot + a[d] * b[d];
+    sa = sa + a[d] * a[d];
+    sb = sb + b[d] * b[d];
+  }
+  return -2.0 * dot + (sa + sb);
+}
+// the same for one active dimension: a = x/ℓ, b = x'/ℓ given
+__device__ __forceinline__ double sqdist1(double a, double b) {
+#pragma clang fp contract(off)
+  return -2.0 * (a * b) + (a * a + b * b);
+}
+// raw inputs: scale by 1/ℓ (a division, as Stationary.scale) on the fly
+__device__ __forceinline__ double sqdist_gpflow(const double* __restrict__ xi, const double* __restrict__ xj,
+                                                int dn, double ell) {
+#pragma clang fp contract(off)
+  double a = xi[0] / ell, b = xj[0] / ell;
+  double dot = a * b, sa = a * a, sb = b * b;
+  for (int d = 1; d < dn; ++d) {
+    a = xi[d] / ell;
+    b = xj[d] / ell;
+    dot = dot + a * b;
+    sa = sa + a * a;
+    sb = sb + b * b;
+  }
+  return -2.0 * dot + (sa + sb);
+}
+
 // Value and derivatives (w.r.t. the term's own params, GPflow order) of one term.
 template <bool GRAD>
 __device__ __forceinline__ double eval_term(const gpx_term& t, const double* __restrict__ th,
@@ -34,12 +70,18 @@ __device__ __forceinline__ double eval_term(const gpx_term& t, const double* __r
   const int d0 = t.dim_start, dn = t.dim_count;
   switch (t.kind) {
     case GPX_LINEAR: {
-      double s = 0.0;
-      for (int d = 0; d < dn; ++d) s = fma(xi[d0 + d], xj[d0 + d], s);
-      if (GRAD) dk[0] = s;
-      return th[0] * s;
+      // gpflow.kernels.Linear.K: matmul(X * variance, X2ᵀ) -> Σ_d (x_d σ²)·x'_d; ∂/∂σ² = Σ x_d x'_d
+#pragma clang fp contract(off)
+      double s = (xi[d0] * th[0]) * xj[d0], sd = xi[d0] * xj[d0];
+      for (int d = 1; d < dn; ++d) {
+        s = s + (xi[d0 + d] * th[0]) * xj[d0 + d];
+        sd = sd + xi[d0 + d] * xj[d0 + d];
+      }
+      if (GRAD) dk[0] = sd;
+      return s;
     }
     case GPX_PERIODIC_SE: {
+      // Periodic.K: r = π(x − x')/p, s² = Σ (sin r / ℓ)², K = σ² exp(−s²/2)
       const double ell = th[0], var = th[1], p = th[2];
       const double inv_l2 = 1.0 / (ell * ell);
       double s2 = 0.0, sc = 0.0;
@@ -47,10 +89,10 @@ __device__ __forceinline__ double eval_term(const gpx_term& t, const double* __r
         const double diff = xi[d0 + d] - xj[d0 + d];
         double sn, cs;
         sincos(M_PI * diff / p, &sn, &cs);
-        s2 = fma(sn, sn, s2);
+        const double q = sn / ell;
+        s2 = s2 + q * q;
         if (GRAD) sc = fma(sn * cs, diff, sc);
       }
-      s2 *= inv_l2;
       const double g = exp(-0.5 * s2);
       if (GRAD) {
         dk[0] = var * g * s2 / ell;
@@ -65,12 +107,7 @@ __device__ __forceinline__ double eval_term(const gpx_term& t, const double* __r
   const bool rq = (t.kind == GPX_RQ);
   const double ell = rq ? th[1] : th[0];
   const double var = rq ? th[2] : th[1];
-  double d2 = 0.0;
-  for (int d = 0; d < dn; ++d) {
-    const double diff = xi[d0 + d] - xj[d0 + d];
-    d2 = fma(diff, diff, d2);
-  }
-  const double r2 = d2 / (ell * ell);
+  const double r2 = sqdist_gpflow(xi + d0, xj + d0, dn, ell);
   switch (t.kind) {
     case GPX_SE: {
       const double g = exp(-0.5 * r2);
@@ -221,10 +258,10 @@ __device__ __forceinline__ double eval_term_dx1(const gpx_term& t, const double*
       const double inv_l2 = 1.0 / (ell * ell);
       double s2 = 0.0;
       for (int d = 0; d < dn; ++d) {
-        const double sn = sin(M_PI * (xi[d0 + d] - xj[d0 + d]) / p);
-        s2 = fma(sn, sn, s2);
+        const double q = sin(M_PI * (xi[d0 + d] - xj[d0 + d]) / p) / ell;
+        s2 = s2 + q * q;
       }
-      const double k = var * exp(-0.5 * s2 * inv_l2);
+      const double k = var * exp(-0.5 * s2);
 #pragma unroll
       for (int d = 0; d < DM; ++d)
         if (d >= d0 && d < d0 + dn) {
@@ -239,13 +276,8 @@ __device__ __forceinline__ double eval_term_dx1(const gpx_term& t, const double*
   const bool rq = (t.kind == GPX_RQ);
   const double ell = rq ? th[1] : th[0];
   const double var = rq ? th[2] : th[1];
-  double d2 = 0.0;
-  for (int d = 0; d < dn; ++d) {
-    const double diff = xi[d0 + d] - xj[d0 + d];
-    d2 = fma(diff, diff, d2);
-  }
   const double inv_l2 = 1.0 / (ell * ell);
-  const double r2 = d2 * inv_l2;
+  const double r2 = sqdist_gpflow(xi + d0, xj + d0, dn, ell);
   double k, dgdr2;  // K = var·g(r²), dgdr2 = var·g'(r²)
   switch (t.kind) {
     case GPX_SE: { k = var * exp(-0.5 * r2); dgdr2 = -0.5 * k; break; }
@@ -312,10 +344,29 @@ __device__ __forceinline__ double eval_k_dx1(const DevSpec& s, const double* __r
   return P;
 }
 
-// K_diag(x): σ² for stationary terms, σ² Σ x² for Linear.
+// K_diag(x) as GPflow's K_diag methods: σ² for the stationary terms (Stationary.K_diag fills the
+// variance; Periodic takes its base kernel's), Σ_d (x_d²)·σ² for Linear (reduce_sum(square(X) *
+// variance)); sums / products of the terms'.
 __device__ __forceinline__ double eval_kdiag(const DevSpec& s, const double* __restrict__ th,
                                              const double* __restrict__ x) {
-  return eval_k(s, th, x, x);
+  const bool prod = (s.combine == GPX_PRODUCT && s.n_terms > 1);
+  double acc = prod ? 1.0 : 0.0;
+#pragma unroll
+  for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+    if (t >= s.n_terms) break;
+    const gpx_term& tm = s.terms[t];
+    const double* tth = th + tm.param_offset;
+    double v;
+    if (tm.kind == GPX_LINEAR) {
+#pragma clang fp contract(off)
+      v = (x[tm.dim_start] * x[tm.dim_start]) * tth[0];
+      for (int d = 1; d < tm.dim_count; ++d) v = v + (x[tm.dim_start + d] * x[tm.dim_start + d]) * tth[0];
+    } else {
+      v = tm.kind == GPX_RQ ? tth[2] : tth[1];
+    }
+    if (prod) acc *= v; else acc += v;
+  }
+  return acc;
 }
 
 }  // namespace gpx

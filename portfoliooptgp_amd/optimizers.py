@@ -735,7 +735,10 @@ class _SteppedDriver:
         # wait out another group's whole 5 ms switch interval before stepping its fits
         # several device batches: one host thread submits and completes their evaluations in
         # turn (GPX_PIPELINE=0: one thread per batch instead)
+        # (only when every group has an engine of its own: the groups of ONE engine split
+        # row-wise would each submit on the same batch, which holds one pending evaluation)
         if (G > 1 and os.environ.get("GPX_PIPELINE", "1") != "0"
+                and len({id(e) for e, _, _, _ in self.groups}) == G
                 and all(hasattr(e, "lml_grad_submit") for e, _, _, _ in self.groups)):
             try:
                 self._pipeline()

@@ -83,8 +83,10 @@ def kernel_cases():
                 m = O.OGPR(x, y, k, noise_variance=noise)
                 try:
                     loss, g = m.loss_and_grad_u()
+                    _, g_hp = m.loss_and_grad_u_extended()
                     m.noise.trainable = False
                     loss_nt, g_nt = m.loss_and_grad_u()
+                    _, g_nt_hp = m.loss_and_grad_u_extended()
                     cond = float(np.linalg.cond(m._Ky()))
                     m.noise.trainable = True
                     mu, var = m.predict_f(xf)
@@ -97,6 +99,10 @@ def kernel_cases():
                 arrays[key + "|loss"] = np.array([loss])
                 arrays[key + "|grad_u"] = g              # noise trainable (last entry = noise)
                 arrays[key + "|grad_u_fixed_noise"] = g_nt
+                # the same gradients with extended-precision linear algebra on the same fp64
+                # K and ∂K (oracle loss_and_grad_u_extended): where the fp64 oracle is off
+                arrays[key + "|grad_u_hp"] = g_hp
+                arrays[key + "|grad_u_fixed_noise_hp"] = g_nt_hp
                 arrays[key + "|cond"] = np.array([cond])
                 arrays[key + "|xnew"] = xf
                 arrays[key + "|fmean"] = mu[:, 0]
@@ -147,7 +153,8 @@ def reference_sweep():
 def multi_input_case():
     """C4 shape: D=5 (4 z-scored features + z-scored time), Exponential(dims 0..3) *
     Exponential(dim 4) as Multi-Input_GPR/main.py:118-135, and Matern52 over all dims, N=67,
-    noise 1e-3 fixed (main.py:422), plus the train_likelihood variant with trainable noise."""
+    noise 1e-3 fixed (main.py:422), plus the train_likelihood variant with trainable noise
+    (keys tl|*)."""
     rng = np.random.default_rng(100)
     n = 67
     feats = np.cumsum(rng.standard_normal((n, 4)) * 0.01, axis=0)
@@ -175,6 +182,59 @@ def multi_input_case():
         mu, var = m.predict_f(X)
         arrays[f"{name}|fmean"] = mu[:, 0]
         arrays[f"{name}|fvar"] = var[:, 0]
+    # Multi-Input_GPR/models/model_trainer.py:26-54 train_likelihood on the reference's composite
+    # kernel: for each starting noise variance a fresh GPR((X, Y), deepcopy(kernel),
+    # noise_variance=v) with the likelihood trainable, Scipy().minimize at scipy's default
+    # maxiter; the lowest opt_logs.fun wins (strict <, first wins)
+    starts = [1e-5, 1e-3, 1e-1, 1.0]
+    arrays["tl|starts"] = np.array(starts)
+    best, best_loss = -1, np.inf
+    for r_i, v in enumerate(starts):
+        k = O.OProduct([O.OExponential(), O.OExponential()])
+        k.kernels[0].active_dims = slice(0, 4)
+        k.kernels[1].active_dims = slice(4, 5)
+        m = O.OGPR(X, Y, k, noise_variance=v)
+        m.noise.trainable = True
+        r = O.scipy_minimize(m, None)
+        arrays[f"tl|{r_i}|loss_fit"] = np.array([r.fun])
+        arrays[f"tl|{r_i}|theta_fit"] = np.array([p.value for p in k.params()])
+        arrays[f"tl|{r_i}|noise_fit"] = np.array([m.noise.value])
+        arrays[f"tl|{r_i}|nfev"] = np.array([r.nfev])
+        if r.fun < best_loss:
+            best, best_loss = r_i, r.fun
+    arrays["tl|best"] = np.array([best])
+    arrays["tl|best_loss"] = np.array([best_loss])
+    return arrays
+
+
+def meta_sweep():
+    """C1 real-data N≈252 variant: test_data/Stocks/META_EOD/meta_us_eod.csv (251
+    rows, 2023-05-30..2024-05-28) through the restated GPR/data_handler.py:26-65 with
+    train_start = the first date, and the 8-kernel sweep of GPR/model_trainer.py:14-25 with
+    fresh GPflow defaults per kernel (noise 1e-5 fixed, maxiter 100, predict_f at X, MSE)."""
+    x, y, mean, std = O.prepare_series(f"{REF}/test_data/Stocks/META_EOD/meta_us_eod.csv",
+                                       train_start_date="2023-05-30")
+    arrays = {"x": x, "y": y, "mean": np.array([mean]), "std": np.array([std])}
+    best = (np.inf, -1)
+    for i, k in enumerate(O.reference_kernel_list()):
+        m = O.OGPR(x, y, k, noise_variance=1.0)
+        m.noise.value = 1e-5
+        m.noise.trainable = False
+        loss0, g0 = m.loss_and_grad_u()
+        arrays[f"{i}|loss0"] = np.array([loss0])
+        arrays[f"{i}|grad0"] = g0
+        r = O.scipy_minimize(m, 100)
+        mu, var = m.predict_f(x)
+        mse = float(np.mean((y - mu) ** 2))
+        arrays[f"{i}|theta_fit"] = np.array([p.value for p in k.params()])
+        arrays[f"{i}|loss_fit"] = np.array([r.fun])
+        arrays[f"{i}|nfev"] = np.array([r.nfev])
+        arrays[f"{i}|mse"] = np.array([mse])
+        arrays[f"{i}|fmean"] = mu[:, 0]
+        arrays[f"{i}|fvar"] = var[:, 0]
+        if mse < best[0]:
+            best = (mse, i)
+    arrays["best_index"] = np.array([best[1]])
     return arrays
 
 
@@ -200,6 +260,7 @@ def main():
         json.dump(reference_sweep(), f, indent=1)
     np.savez_compressed(os.path.join(HERE, "multi_input.npz"), **multi_input_case())
     np.savez_compressed(os.path.join(HERE, "tickers.npz"), **tickers())
+    np.savez_compressed(os.path.join(HERE, "meta_sweep.npz"), **meta_sweep())
     ds = datasets()
     x, y, meta = ds["aapl_d"]
     pin = O.OGPR(x, y, O.OSquaredExponential(), noise_variance=1e-5)

@@ -6,7 +6,7 @@ The banded path is taken when K and every ∂K/∂θ are exactly zero in fp64 be
 against the spacing of sorted inputs — the C2 bench regime (X = day offsets 0..N-1, GPflow's
 default ℓ = 1; every evaluation of a C2 fit stays at ℓ ∈ [1, 1.72]) and the reference's own
 (GPR/data_handler.py:42-44 leaves day offsets unnormalised). Tolerances as test_gpu_parity.py
-(κ-scaled logML / gradient bars); the dense path of the same build is a second
+(κ-scaled logML bar, 1e-6 relative gradient bar); the dense path of the same build is a second
 reference at full size (N=4096), where the oracle is too slow to call per case.
 """
 import os
@@ -96,7 +96,7 @@ def test_band_against_oracle_n1024(fam, ell):
     lo, go = om.loss_and_grad_u()
     cond = _cond(x, ko, 1e-5)
     check_loss(loss, lo, cond)
-    check_grad(g, go, cond)
+    check_grad(g, go)
     # predict at the training inputs from the banded factor (diag of K⁻¹ from the selected
     # inverse) and at new inputs (re-factorised densely)
     mu, var = m.predict_f(x)
@@ -195,7 +195,7 @@ def test_band_two_dimensional_inputs():
     lo, go = om.loss_and_grad_u()
     cond = _cond(x, O.OMatern32(lengthscales=0.05, variance=1.1), 1e-4)
     check_loss(loss, lo, cond)
-    check_grad(g, go, cond)
+    check_grad(g, go)
 
 
 def test_band_not_positive_definite_reports_pivot():

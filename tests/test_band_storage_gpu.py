@@ -168,3 +168,50 @@ def test_band_storage_shape_limits():
     x = np.arange(256, dtype=np.float64)[:, None]
     with pytest.raises(N.GPXError):
         Engine([x], [x[:, 0]], [compile_spec(K.SquaredExponential(), 1)], band_storage=True)
+
+
+def test_bad_theta_with_fallback_problems_leaves_batch_usable():
+    """a submit whose θ is invalid for one row, on a band-storage batch whose call
+    also routes problems to the fallback slots, is refused BEFORE anything is submitted (so the
+    fallback batch is not left with a pending evaluation) and the next valid call works."""
+    xs, ys, kerns, rows = _c2_batch()
+    band, dense = _pair(xs, ys, kerns)
+    th = _theta(band.B, rows)
+    bad = th.copy()
+    bad[0, 0] = -1.0                                   # invalid ℓ for a banded problem
+    import ctypes
+    act = np.arange(band.B, dtype=np.int32)
+    ip, dp = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)
+    rc = band.lib.gpx_batch_lml_grad_submit(band.handle, band.B, act.ctypes.data_as(ip), bad.ctypes.data_as(dp),
+                                            band._stream())
+    assert rc == N.GPX_BAD_ARG
+    lb, gb, ib = band.lml_grad(list(range(band.B)), th)   # fallback problems 2, 4, 5 included
+    ld, gd, idn = dense.lml_grad(list(range(band.B)), th)
+    assert not ib.any() and not idn.any()
+    _close(lb, ld)
+    _close(gb[:, :4], gd[:, :4])
+
+
+def test_device_rebind_waits_for_the_producer_stream():
+    """X / Y produced by kernels on a side stream right before a device rebind (the
+    rebind made with that stream current) are gathered only after they are written, though the
+    evaluation runs on another stream."""
+    n = 2048
+    x, y = O.synthetic_series(n, seed=31)
+    spec = compile_spec(K.SquaredExponential(), 1)
+    eng = Engine([np.zeros((n, 1))], [np.zeros((n, 1))], [spec], band_storage=True)
+    ref = Engine([x], [y], [spec], band_storage=True)
+    th = _theta(1, [(1.2, 0.9, 1e-5)])
+    l0, g0, _ = ref.lml_grad([0], th)
+    side = torch.cuda.Stream()
+    xd = torch.zeros(n, 1, dtype=torch.float64, device="cuda:0")
+    yd = torch.zeros(n, dtype=torch.float64, device="cuda:0")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(20_000_000)                  # ~10 ms of spinning before the writes
+        xd.copy_(torch.as_tensor(x, device="cuda:0"))
+        yd.copy_(torch.as_tensor(y[:, 0], device="cuda:0"))
+        eng.rebind(0, xd, yd, spec)
+    l1, g1, info = eng.lml_grad([0], th)              # evaluated on the default stream
+    assert not info.any()
+    assert l1[0] == l0[0] and np.array_equal(g1[0, :3], g0[0, :3])

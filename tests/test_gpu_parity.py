@@ -3,11 +3,16 @@
 Tolerances (fp64, SURVEY.md §8c and BASELINE.json north_star "within 1e-5 relative on
 posterior mean/variance and log-ML"):
   logML         |Δ| <= (1e-9 + 1e-14 · κ) · max(1, |ref|)   (north-star bar: 1e-5 rel)
-  ∂loss/∂u      |Δ| <= (1e-7 + 3e-11 · κ) · (1 + max|g_ref|),  κ = cond(K + σn²I)
-                (SURVEY: rel 1e-6). The gradient ½Σ(ααᵀ − K⁻¹)∘∂K is a cancellation whose
-                fp64 error grows with κ in ANY algorithm: on the worst fixture (κ ≈ 9e6) the
-                oracle itself is 7.4e-5 from the 40-digit exact value and the GPU 2.4e-4
-                (test_gradient_accuracy_vs_exact).
+  ∂loss/∂u      max|Δ| <= 1e-6 · max|g_ref|   (rel 1e-6 vs the oracle)
+                — except where the fp64 oracle is itself off: each fixture also stores the
+                gradient with extended-precision linear algebra on the same K (grad_u*_hp,
+                oracle.loss_and_grad_u_extended). The gradient ½Σ(ααᵀ − K⁻¹)∘∂K is a
+                cancellation whose fp64 error grows with κ = cond(K + σn²I) in ANY algorithm;
+                on the 12 of 336 fixture gradients (κ >= 2.5e5: Periodic / Linear on day
+                offsets) where the oracle is more than 1e-7 from that value, the GPU must be
+                within max(1e-6 · max|g|, 10 × the oracle's own error) of it (the 40-digit
+                mpmath check of the worst one, test_gradient_accuracy_vs_exact: oracle 7.4e-5
+                from exact, GPU 2.4e-4).
   mean          |Δ| <= 1e-6 · max|ref| + 1e-14 · κ · max(1, max|y|)   (bar: 1e-5 rel)
   variance      |Δ| <= 1e-5 · |ref| + 1e-10 · σ²_max    (SURVEY: cancellation-aware)
   fitted loss   |Δ| <= 1e-5 · |ref|
@@ -60,10 +65,19 @@ def check_loss(got, ref, cond=1.0):
     assert abs(got - ref) <= (1e-9 + 1e-14 * float(cond)) * max(1.0, abs(ref)), (got, ref, cond)
 
 
-def check_grad(got, ref, cond=1.0):
-    got, ref = np.asarray(got), np.asarray(ref)
-    tol = (1e-7 + 3e-11 * float(cond)) * (1.0 + np.abs(ref).max())
-    assert np.all(np.abs(got - ref) <= tol), (got, ref, cond)
+def check_grad(got, ref, hp=None):
+    """SURVEY's 1e-6 relative gradient bar against the oracle; where the fp64 oracle is more
+    than 1e-7 from the extended-precision value hp, against hp within 10x the oracle's error."""
+    got, ref = np.asarray(got, dtype=np.float64), np.asarray(ref, dtype=np.float64)
+    scale = max(float(np.abs(ref).max()), 1e-300)
+    if hp is not None:
+        hp = np.asarray(hp, dtype=np.float64)
+        err_oracle = float(np.abs(ref - hp).max())
+        if err_oracle > 1e-7 * float(np.abs(hp).max()):
+            tol = max(1e-6 * float(np.abs(hp).max()), 10.0 * err_oracle)
+            assert float(np.abs(got - hp).max()) <= tol, (got, ref, hp)
+            return
+    assert float(np.abs(got - ref).max()) <= 1e-6 * scale, (got, ref, np.abs(got - ref).max() / scale)
 
 
 def check_mean(got, ref, cond=1.0, yscale=1.0):
@@ -98,10 +112,10 @@ def test_golden_single_models(golden):
         cond = d[key + "|cond"][0]
         loss, g = m.loss_and_grad_unconstrained()
         check_loss(loss, float(d[key + "|loss"][0]), cond)
-        check_grad(g, d[key + "|grad_u"], cond)
+        check_grad(g, d[key + "|grad_u"], d[key + "|grad_u_hp"])
         gpx.set_trainable(m.likelihood.variance, False)
         _, g2 = m.loss_and_grad_unconstrained()
-        check_grad(g2, d[key + "|grad_u_fixed_noise"], d[key + "|cond"][0])
+        check_grad(g2, d[key + "|grad_u_fixed_noise"], d[key + "|grad_u_fixed_noise_hp"])
         xnew = d[key + "|xnew"]
         mu, var = m.predict_f(xnew)
         _, vy = m.predict_y(xnew)
@@ -123,7 +137,7 @@ def test_golden_ragged_batch(golden):
     for b, (m, key) in enumerate(zip(models, idx)):
         loss, g = m.loss_and_grad_unconstrained(lml=lml[b], grad_theta=grad[b])
         check_loss(loss, float(d[key + "|loss"][0]), d[key + "|cond"][0])
-        check_grad(g, d[key + "|grad_u"], d[key + "|cond"][0])
+        check_grad(g, d[key + "|grad_u"], d[key + "|grad_u_hp"])
     for b, m in enumerate(models):
         m._attach(eng, b)
     outs = predict_f_batch(models, [d[k + "|xnew"] for k in idx])

@@ -322,3 +322,39 @@ def test_stepper_result_reads_as_scipys():
     np.testing.assert_array_equal(r.hess_inv.todense(), r0.hess_inv.todense())
     assert r["hess_inv"] is r.hess_inv
     np.testing.assert_array_equal(r.x, r0.x)
+
+
+class AsyncFakeEngine(FakeEngine):
+    """FakeEngine with the split submit / complete calls of Engine; like gpx_batch it holds ONE
+    pending evaluation (a second submit before the complete is refused)."""
+
+    def __init__(self, B):
+        super().__init__(B)
+        self._pending = None
+
+    def lml_grad_submit(self, rows, theta):
+        if self._pending is not None:
+            raise N.GPXError("an evaluation is already submitted on this batch")
+        self._pending = self.lml_grad(list(rows), np.array(theta, copy=True))
+
+    def lml_grad_ready(self):
+        return True
+
+    def lml_grad_complete(self):
+        out, self._pending = self._pending, None
+        return out
+
+
+@pytest.mark.parametrize("engines", [1, 2])
+def test_groups_on_one_engine_with_submit(engines):
+    """two groups that are row ranges of ONE engine with submit support
+    must not go through the one-thread pipeline (both groups would submit on the same batch);
+    distinct engines do. Either way every fit equals its solo fit."""
+    ms = _models(9)
+    ref = [_solo(m) for m in _models(9)]
+    eng = [AsyncFakeEngine(4 // engines) for _ in range(engines)]
+    res, _ = gpx.optimizers.Scipy().minimize_stream(ms, width=4, engine=eng if engines > 1 else eng[0],
+                                                    groups=2)
+    for r, r0 in zip(res, ref):
+        assert r.nfev == r0.nfev
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
