@@ -12,14 +12,28 @@ unconstrained variables to termination, then predict_f at the N training points.
 One *step* = fitting `--fits` independent series per GPU (each driven by its own unmodified
 scipy L-BFGS-B, from a fresh GPR model at GPflow defaults) through `--width` resident device
 slots with continuous batching: the evaluations of all resident fits run as batched device
-passes (`--groups` concurrent device batches), and a slot is refilled as soon as its fit
-converges and has run its predict_f. The K timed steps are streamed back to back through the
-slots (the next step's fits take slots as the previous step's finish; no drain between steps),
-bracketed by one barrier + synchronize on each side. For N > 1 GPUs the step ends with an
-RCCL all_gather of every fit's (θ*, loss*, nfev, last predicted mean/var) — the per-asset
-hand-off to the portfolio step.
-Inputs are resident in HBM before the timed region. Each rank fits its own series
-(seed = rank * fits + f): weak scaling.
+passes (`--groups` concurrent device batches per host process), and a slot is refilled as soon
+as its fit converges and has run its predict_f. The K timed steps are streamed back to back
+through the slots (no drain between steps), bracketed by one barrier + synchronize on each
+side. For N > 1 GPUs the timed region ends with an RCCL all_gather of every fit's (θ*, loss*,
+nfev, last predicted mean/var) — the per-asset hand-off to the portfolio step.
+
+Host processes per GPU (``--procs``, default 2): scipy's L-BFGS-B steps hold the GIL, so one
+host thread stepping ~1500 fits becomes the limit before the GPU does. The rank process starts
+``procs - 1`` helper processes (multiprocessing "spawn", BEFORE any GPU call in the rank) that
+share the GPU; each fits its own slice of the step's series through its own slots and device
+batches. All of them finish their warmup and report ready; the rank starts its clock, signals
+the helpers and fits its own slice; each helper synchronises its device work and then hands back
+its per-fit summary rows and timing through a queue; the rank stops the clock when it has all of
+them (and, for N > 1, after the all_gather and a barrier across ranks).
+
+Inputs are resident in HBM before the timed region. Each rank fits its own series (seed =
+rank * fits + f): weak scaling.
+
+After the timed region (rank 0, one GPU only; never part of `value`): the CPU baseline, and two
+secondary lines the driver times with the rest of the run — config C4 on the dense path
+(Matern52, D = 5, N = 4096: fits/s and the fused K⁻¹ + gradient contraction's roofline) and
+config C5 (SVGP, N = 65536, M = 1024: ms per ELBO + gradient evaluation).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N>1 the driver uses
 python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -181,56 +195,293 @@ def contract_traffic(n, flops_per_launch):
     return d["hbm_bytes_per_problem"] * problems, os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
 
 
-def main():
-    # HIP hardware queues for this process, set before the runtime starts (torch is imported
-    # below): the 4 device batches each evaluate on their own stream (+ one forked stream for
-    # the p = 2 class), and with the runtime's default 4 queues some of those streams share a
-    # queue and serialise (3 batches: 2460–2630 fits/s at 4 queues, 2800 at 8)
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPX_HW_QUEUES", "8")
+
+
+# GpxTiming fields summed over a worker's device batches (all groups), and those summed over the
+# narrow groups only (the roofline's fused p <= 1 sweeps)
+SUM_FIELDS = ("contract_ms_total", "contract_launches", "contract_alg_flops", "eval_ms_total", "evals",
+              "band_ms_total", "band_calls", "band_evals", "band_p_sum", "band_fallbacks", "shadow_evals",
+              "shadow_predicts")
+NARROW_FIELDS = ("band_fwd_ms_total", "band_bwd_ms_total", "band_fused_launches", "band_fwd_flops", "band_bwd_flops")
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 20 timed steps of 256 fits: enough fits to keep the 576 slots streaming (with 2 steps the
-    # timed region is one wave of fits and its slowest fits' tail) and to average over the
-    # batches' phase alignment (10-step runs spread by about ±8 %)
-    ap.add_argument("--steps", type=int, default=20)
+    # 200 timed steps of 256 fits: a timed region of ~10 s (a 1 s region was too short for the
+    # driver's GPU-busy sampler and for a stable figure: runs spread ±8 % at 10 steps)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 256)),
                     help="independent series fitted per GPU per step")
     # band storage (25 MiB per slot) lets 1536 slots stay resident: every device call then
     # carries ~320 problems, so the chip's 512 two-per-CU places stay full while a batch is on
-    # the host (dense layout, 384 MiB per slot: 576 slots, 3833–3955 fits/s; band storage
-    # 3 x 1536: 4205, 4 x 1536: 4263–4415, 6 x 1536 on 16 queues: 4446 — tools/bench_sweep3.sh)
+    # the host (dense layout, 384 MiB per slot: 576 slots, 3833–3955 fits/s)
     ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 1536)),
-                    help="resident device slots (continuous-batching width)")
+                    help="resident device slots per GPU (continuous-batching width), split over --procs")
     ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 4)),
-                    help="device batches kept in flight by the one host thread (host/device overlap)")
-    ap.add_argument("--wide-slots", type=int, default=int(os.environ.get("GPX_BENCH_WIDE", 0)),
-                    help="slots of an extra device batch that takes the evaluations whose band is wider "
-                         "than one 64-block (0: none)")
+                    help="device batches kept in flight by each host process")
+    ap.add_argument("--procs", type=int, default=int(os.environ.get("GPX_BENCH_PROCS", 2)),
+                    help="host processes per GPU (the rank + procs-1 spawned helpers)")
     ap.add_argument("--storage", choices=("band", "dense"), default=os.environ.get("GPX_BENCH_STORAGE", "band"),
                     help="slot workspace: band storage (gpx_batch_create_banded, 25 MiB per slot) or the "
                          "dense N x N layout (384 MiB per slot)")
     ap.add_argument("--points", "--n", dest="n", type=int, default=N_POINTS,
                     help="points per series (use --points under torch.distributed.run, whose parser takes --n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C4 / C5 secondary lines")
+    return ap.parse_args(argv)
 
+
+def share(total, parts, i):
+    """Item count of part i when `total` items are split as evenly as possible."""
+    return total // parts + (1 if i < total % parts else 0)
+
+
+class FitWorker:
+    """One host process's part of a step on one GPU: its slice of the step's series (fits
+    f0 .. f0 + F_w − 1 of the rank's F), its slots (width / procs) in `groups` device batches,
+    fitted by one host thread through minimize_stream."""
+
+    def __init__(self, args, w, P, rank, gpu):
+        import torch
+        import portfoliooptgp_amd as gpx
+        from portfoliooptgp_amd.engine import Engine
+        from portfoliooptgp_amd.kernels import compile_spec
+        self.torch, self.gpx = torch, gpx
+        self.args, self.w, self.gpu = args, w, gpu
+        F = args.fits
+        self.F = share(F, P, w)
+        f0 = sum(share(F, P, i) for i in range(w))
+        n = self.n = args.n
+        dev = torch.device(f"cuda:{gpu}")
+        data = [synthetic_series(n, rank * F + f0 + f) for f in range(self.F)]
+        self.Xd = [torch.as_tensor(x, device=dev) for x, _ in data]  # resident in HBM before timing
+        self.Yd = [torch.as_tensor(y, device=dev) for _, y in data]
+        W = share(args.width, P, w)
+        G = max(1, min(args.groups, W))
+        sizes = [share(W, G, g) for g in range(G)]
+        spec = compile_spec(gpx.kernels.SquaredExponential(), 1)
+        # slot shapes only: every slot is rebound to its fit's series when the fit starts
+        self.engines = [Engine([self.Xd[i % self.F] for i in range(sz)], [self.Yd[i % self.F] for i in range(sz)],
+                               [spec] * sz, device=gpu, band_storage=args.storage == "band")
+                        for sz in sizes]
+        self.engines[0].ctx.set_profiling(True)
+        self.opt = gpx.optimizers.Scipy()
+        self.width, self.groups = W, G
+        self.traces, self.driver_stats = [], []
+
+    def make_model(self, f):
+        # GPflow defaults (σ²=1, ℓ=1), σn² = 1e-5 frozen — GPR/model_trainer.py:15-17
+        gpx = self.gpx
+        m = gpx.models.GPR(data=(self.Xd[f], self.Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=self.gpu)
+        m.likelihood.variance.assign(NOISE)
+        gpx.set_trainable(m.likelihood.variance, False)
+        return m
+
+    def run_steps(self, k):
+        """k steps (k × F_w fits, each from GPflow defaults) streamed back to back through the
+        slots; returns (nfev list, summary rows [k·F_w, 6] on the host: ℓ*, σ²*, loss*, nfev,
+        mean and var of the last training-point prediction)."""
+        torch, F = self.torch, self.F
+        # every fit's model is built inside the timed region, on demand (as the reference's loop
+        # builds each GPR right before fitting it), while the host thread waits for the device
+        models = self.gpx.optimizers.ModelStream(k * F, lambda i: self.make_model(i % F), input_dim=1,
+                                                 max_points=self.n, device=self.gpu)
+        res, preds = self.opt.minimize_stream(models, width=self.width, engine=self.engines, predict_train=True,
+                                              groups=len(self.engines), options=dict(maxiter=MAXITER))
+        if getattr(self.opt, "last_trace", None):
+            self.traces.append(self.opt.last_trace)
+        if getattr(self.opt, "last_stats", None):
+            self.driver_stats.append(dict(self.opt.last_stats))
+        host = np.array([[m.kernel.lengthscales.value, m.kernel.variance.value, float(r.fun), float(r.nfev)]
+                         for m, r in zip(models, res)], dtype=np.float64)
+        mu = torch.cat([p[0][-1:, 0] for p in preds]).cpu().numpy()
+        var = torch.cat([p[1][-1:, 0] for p in preds]).cpu().numpy()
+        return [r.nfev for r in res], np.concatenate([host, mu[:, None], var[:, None]], axis=1)
+
+    def reset_timing(self):
+        for e in self.engines:
+            e.reset_timing()
+        self.driver_stats = []
+
+    def timing(self):
+        tms = [e.last_timing() for e in self.engines]
+        out = {f: float(sum(getattr(t, f) for t in tms)) for f in SUM_FIELDS}
+        out.update({f: float(sum(getattr(t, f) for t in tms)) for f in NARROW_FIELDS})
+        return out
+
+
+def helper_main(w, P, argv, rank, gpu, start, q):
+    """A helper host process (spawned before the rank touched the GPU): warm up, report ready,
+    wait for the rank's start signal, fit its slice of the K steps, synchronise, hand back its
+    results (the message means its device work is done)."""
+    os.environ["GPX_DEVICE"] = str(gpu)
+    args = parse_args(argv)
+    import torch
+    torch.cuda.set_device(gpu)
+    wk = FitWorker(args, w, P, rank, gpu)
+    if args.warmup > 0:
+        wk.run_steps(args.warmup)
+    wk.reset_timing()
+    torch.cuda.synchronize()
+    q.put(("ready", w))
+    start.wait()
+    t0 = time.perf_counter()
+    nfev, summary = wk.run_steps(args.steps)
+    torch.cuda.synchronize()
+    busy = time.perf_counter() - t0
+    q.put(("done", (w, nfev, summary, wk.timing(), wk.driver_stats[-1] if wk.driver_stats else None, busy)))
+
+
+def collect(q, helpers, kind, timeout):
+    """The helpers' `kind` messages; raises if a helper dies or the wait exceeds `timeout`."""
+    import queue as _q
+    got, t_end = [], time.monotonic() + timeout
+    while len(got) < len(helpers):
+        try:
+            k, v = q.get(timeout=1.0)
+        except _q.Empty:
+            # a helper that exits cleanly has flushed its message into the queue first
+            failed = [h for h in helpers if not h.is_alive() and h.exitcode != 0]
+            if failed:
+                raise RuntimeError(f"bench helper process failed (exit code {failed[0].exitcode}) before '{kind}'")
+            if time.monotonic() > t_end:
+                raise TimeoutError(f"bench helpers: no '{kind}' after {timeout} s")
+            continue
+        assert k == kind, (k, kind)
+        got.append(v)
+    return got
+
+
+def secondary_c4(gpu, fits=32):
+    """Config C4 (BASELINE.json configs[3]) on the dense path: D = 5 (4 z-scored random-walk
+    features + z-scored time), Matern52, N = 4096, fp64 (the reference's precision), σn² = 1e-3
+    fixed, scipy defaults + maxiter 100, predict_f at the training inputs; `fits` series in two
+    device batches. Also the fused K⁻¹ + gradient contraction's rate over those launches."""
+    import torch
+    import portfoliooptgp_amd as gpx
+    n = 4096
+    data = []
+    for s in range(fits):
+        rng = np.random.default_rng(100 + s)
+        X = np.hstack([np.cumsum(rng.standard_normal((n, 4)), axis=0), np.linspace(0.0, 1.0, n)[:, None]])
+        X = (X - X.mean(0)) / X.std(0, ddof=1)
+        data.append((torch.as_tensor(X, device=f"cuda:{gpu}"),
+                     torch.as_tensor(synthetic_series(n, s)[1], device=f"cuda:{gpu}")))
+
+    def models(k):
+        out = []
+        for x, y in data[:k]:
+            m = gpx.models.GPR((x, y), kernel=gpx.kernels.Matern52(), device=gpu)
+            m.likelihood.variance.assign(1e-3)
+            gpx.set_trainable(m.likelihood.variance, False)
+            out.append(m)
+        return out
+    from portfoliooptgp_amd.engine import Engine
+    from portfoliooptgp_amd.kernels import compile_spec
+    spec = compile_spec(gpx.kernels.Matern52(), 5)
+    engines = [Engine([d[0] for d in data[g::2]], [d[1] for d in data[g::2]], [spec] * len(data[g::2]), device=gpu)
+               for g in range(2)]
+    engines[0].ctx.set_profiling(True)
+    opt = gpx.optimizers.Scipy()
+    opt.minimize_stream(models(2), width=2, engine=engines, groups=2, predict_train=True,
+                        options=dict(maxiter=MAXITER))  # warm-up
+    for e in engines:
+        e.reset_timing()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res, _ = opt.minimize_stream(models(fits), width=fits, engine=engines, groups=2, predict_train=True,
+                                 options=dict(maxiter=MAXITER))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tms = [e.last_timing() for e in engines]
+    c_ms = sum(t.contract_ms_total for t in tms)
+    c_l = sum(t.contract_launches for t in tms)
+    c_f = sum(t.contract_alg_flops for t in tms)
+    evals = sum(t.evals for t in tms)
+    ach = c_f / (c_ms * 1e-3) / 1e12 if c_ms > 0 else 0.0
+    P = 2
+    return {"config": "C4", "workload": f"Multi-Input shape: D=5, Matern52, N=4096, fp64, sigma_n^2=1e-3 fixed, "
+            f"{fits} fits, L-BFGS-B maxiter=100 + predict_f(X_train), dense path, 2 device batches",
+            "fits_per_s": fits / dt, "fits": fits, "seconds": dt, "nfev_mean": float(np.mean([r.nfev for r in res])),
+            "evals_per_s": evals / dt, "dense_evals": evals - sum(t.band_evals for t in tms),
+            "eval_alg_tflops": evals * (n ** 3 + 2 * (P + 1) * n ** 2) / dt / 1e12,
+            "contraction_roofline": {
+                "kernel": "gemm_kernel<128,T,N,EPI_CONTRACT1> (K^-1 = W^T W fused with the gradient contraction)",
+                "bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / FP64_PEAK_TFLOPS, "avg_launch_ms": c_ms / max(c_l, 1.0), "launches": c_l,
+                "alg_flops_per_launch": c_f / max(c_l, 1.0)}}
+
+
+def secondary_c5(gpu, reps=20):
+    """Config C5 (BASELINE.json configs[4]): SVGP ELBO + gradients at N = 65536, M = 1024, D = 1,
+    SE, whitened full q_sqrt, fp64; ms per evaluation (one GPU)."""
+    import torch
+    import portfoliooptgp_amd as gpx
+    from portfoliooptgp_amd.engine import SVGPEngine
+    from portfoliooptgp_amd.kernels import compile_spec
+    n, M = 65536, 1024
+    rng = np.random.default_rng(0)
+    X = np.sort(rng.uniform(0, 360, (n, 1)), axis=0)
+    Y = np.sin(X / 20.0) + 0.1 * rng.standard_normal((n, 1))
+    Z = np.linspace(0, 360, M)[:, None]
+    eng = SVGPEngine(X, Y, compile_spec(gpx.kernels.SquaredExponential(), 1), M, num_data=n, device=gpu)
+    theta = np.ones(16)
+    theta[:3] = [2.0, 1.0, 1e-4]
+    q = rng.standard_normal(M) * 0.3
+    R = np.tril(rng.standard_normal((M, M)) * 1e-3)
+    R[np.diag_indices(M)] = rng.uniform(0.05, 0.2, M)
+    eng.elbo_grad(theta, Z, q, R)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eng.elbo_grad(theta, Z, q, R)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    Mp = (M + 63) // 64 * 64
+    flops = 3.0 * Mp * Mp * n + 14.0 * Mp ** 3   # SYRK G (M²N) + Y = 2c·P·Kmn (2M²N) + the O(M³) tail
+    return {"config": "C5", "workload": f"SVGP N={n}, M={M}, SE, whitened full q_sqrt, fp64: one ELBO+gradient "
+            f"evaluation (mean of {reps})", "ms_per_eval": dt * 1e3, "alg_tflops": flops / dt / 1e12,
+            "frac_fp64_peak": flops / dt / 1e12 / FP64_PEAK_TFLOPS}
+
+
+def main():
+    # HIP hardware queues for this process (and the helpers, which inherit the environment), set
+    # before the runtime starts: each process's 4 device batches evaluate on their own streams
+    # (+ one forked stream for the p = 2 class); with the runtime's default 4 queues some of
+    # them share a queue and serialise (3 batches: 2460–2630 fits/s at 4 queues, 2800 at 8)
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPX_HW_QUEUES", "8")
+    # driver phase times (host share of the timed region), cheap perf_counter reads
+    os.environ.setdefault("GPX_DRIVER_STATS", "1")
+    argv = sys.argv[1:]
+    args = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("GPX_DEVICE", str(local_rank))
+    gpu = int(os.environ["GPX_DEVICE"])
+    P = max(1, args.procs)
+
+    # helper processes first, before anything here touches the GPU (a process that has
+    # initialised HIP must not fork/exec)
+    helpers, start, q = [], None, None
+    if P > 1:
+        import multiprocessing as mp
+        ctx = mp.get_context("spawn")
+        start = ctx.Event()
+        q = ctx.Queue()
+        helpers = [ctx.Process(target=helper_main, args=(w, P, argv, rank, gpu, start, q), daemon=True)
+                   for w in range(1, P)]
+        for h in helpers:
+            h.start()
 
     import torch
     import torch.distributed as dist
-    import portfoliooptgp_amd as gpx
-    from portfoliooptgp_amd.engine import Engine
-    from portfoliooptgp_amd.kernels import compile_spec
-    from portfoliooptgp_amd.models import predict_f_batch
 
     # GPX_BENCH_BACKEND=gloo + GPX_DEVICE=0: rehearsal of the multi-rank path with every rank
     # on one GPU (collectives on host tensors); the real run is RCCL, one GPU per rank
     backend = os.environ.get("GPX_BENCH_BACKEND", "nccl")
-    gpu = int(os.environ["GPX_DEVICE"])
     torch.cuda.set_device(gpu)
     dev = torch.device(f"cuda:{gpu}")
     cdev = dev if backend == "nccl" else torch.device("cpu")
@@ -240,196 +491,117 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    F, W, n = args.fits, args.width, args.n
-    seeds = [rank * F + f for f in range(F)]
-    data = [synthetic_series(n, s) for s in seeds]
-    Xd = [torch.as_tensor(x, device=dev) for x, _ in data]  # resident in HBM before timing
-    Yd = [torch.as_tensor(y, device=dev) for _, y in data]
-    def make_model(f):
-        # GPflow defaults (σ²=1, ℓ=1), σn² = 1e-5 frozen — GPR/model_trainer.py:15-17
-        m = gpx.models.GPR(data=(Xd[f], Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=gpu)
-        m.likelihood.variance.assign(NOISE)
-        gpx.set_trainable(m.likelihood.variance, False)
-        return m
-
-    def make_models():
-        return [make_model(f) for f in range(F)]
-
-    # W resident device slots (continuous batching), sized for N-point problems, split into
-    # `groups` independent device batches evaluated concurrently on their own streams
-    G = max(1, args.groups)
-    WS = max(0, min(args.wide_slots, W // 4)) if G > 1 else 0
-    per = (W - WS) // G
-    sizes = [per] * G + ([WS] if WS > 0 else [])
-    proto = make_models()
-    # slot shapes only: every slot is rebound to its fit's series when the fit starts
-    engines = [Engine([Xd[(g * per + i) % F] for i in range(sz)], [Yd[(g * per + i) % F] for i in range(sz)],
-                      [compile_spec(proto[(g * per + i) % F].kernel, 1) for i in range(sz)], device=gpu,
-                      band_storage=args.storage == "band" and not (WS > 0 and g == G))
-               for g, sz in enumerate(sizes)]
-    NG = len(engines)
-    engines[0].ctx.set_profiling(True)
-    opt = gpx.optimizers.Scipy()
-
-    traces = []
-    stats = []
-
-    def run_steps(k):
-        """k steps (k × F fits, each from GPflow defaults) streamed back to back through the
-        slots — the next step's fits fill slots as the previous step's finish, no drain in
-        between — then every fit's summary row, all_gathered across ranks."""
-        # every fit's model is built inside the timed region, on demand (as the reference's loop
-        # builds each GPR right before fitting it), while the host thread waits for the device
-        models = gpx.optimizers.ModelStream(k * F, lambda i: make_model(i % F), input_dim=1, max_points=n,
-                                            device=gpu)
-        res, preds = opt.minimize_stream(models, width=W, engine=engines, predict_train=True, groups=NG,
-                                         options=dict(maxiter=MAXITER), wide_group=WS > 0)
-        if getattr(opt, "last_trace", None):
-            traces.append(opt.last_trace)
-        if getattr(opt, "last_stats", None):
-            stats.append(dict(opt.last_stats))
-        # per fit [ℓ*, σ²*, loss*, nfev, mean and var of its last training-point prediction]:
-        # the host columns as one table, the device ones as two gathers (one tensor per fit
-        # and column cost ~0.3 s at 5120 fits)
-        host = torch.tensor([[m.kernel.lengthscales.value, m.kernel.variance.value, float(r.fun), float(r.nfev)]
-                             for m, r in zip(models, res)], dtype=torch.float64).to(dev)
-        mu = torch.cat([p[0][-1:, 0] for p in preds])
-        var = torch.cat([p[1][-1:, 0] for p in preds])
-        summary = torch.cat([host, mu[:, None], var[:, None]], dim=1)
-        if world > 1:
-            summary = summary.to(cdev)
-            gathered = [torch.empty_like(summary) for _ in range(world)]
-            dist.all_gather(gathered, summary)
-            summary = torch.cat(gathered)
-        return res, summary
-
+    wk = FitWorker(args, 0, P, rank, gpu)
     if args.warmup > 0:
-        run_steps(args.warmup)
-    for e in engines:
-        e.reset_timing()
+        wk.run_steps(args.warmup)
+    wk.reset_timing()
+    torch.cuda.synchronize()
+    collect(q, helpers, "ready", 1800)  # every host process of this GPU has warmed up
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     # trace markers (a ~1 us spin kernel) delimit the timed region in a rocprofv3 kernel trace,
-    # so tools/trace_check.py can average the same contraction launches the bench timed
+    # so tools/trace_check.py can average the same launches the bench timed
     torch.cuda._sleep(1000)
-    res, summary = run_steps(args.steps)
-    nfev = [r.nfev for r in res]
+    if start is not None:
+        start.set()                     # the helpers start their steps
+    nfev, summary = wk.run_steps(args.steps)
     torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
+    busy0 = time.perf_counter() - t0
+    parts = [(0, nfev, summary, wk.timing(), wk.driver_stats[-1] if wk.driver_stats else None, busy0)]
+    parts += collect(q, helpers, "done", 1800)  # each sent after synchronising its device work
+    parts.sort(key=lambda p: p[0])
+    table = np.concatenate([p[2] for p in parts])
+    if world > 1:  # the per-asset hand-off: one all_gather of every fit's summary row
+        t = torch.as_tensor(table, device=cdev)
+        gathered = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(gathered, t)
+        table = torch.cat(gathered).cpu().numpy()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    tms = [e.last_timing() for e in engines]
+    for h in helpers:
+        h.join(timeout=120)
 
-    class _Tm:  # timing summed over the device batches
-        pass
-    tm = _Tm()
-    for f in ("contract_ms_total", "contract_launches", "contract_alg_flops", "eval_ms_total", "evals",
-              "band_ms_total", "band_calls", "band_evals", "band_p_sum", "band_fallbacks", "shadow_evals",
-              "shadow_predicts"):
-        setattr(tm, f, sum(getattr(t, f) for t in tms))
-    # the roofline's fused-sweep launches: the narrow batches' (p <= 1 class), not the wide
-    # batch's p = 2 sweeps
-    for f in ("band_fwd_ms_total", "band_bwd_ms_total", "band_fused_launches", "band_fwd_flops", "band_bwd_flops"):
-        setattr(tm, f, sum(getattr(t, f) for t in tms[:G]))
+    tm = {f: sum(p[3][f] for p in parts) for f in SUM_FIELDS + NARROW_FIELDS}
+    nfev_all = [n for p in parts for n in p[1]]
     if world > 1:
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        nf = torch.tensor([float(sum(nfev)), float(len(nfev)), float(tm.evals)], device=cdev,
+        nf = torch.tensor([float(sum(nfev_all)), float(len(nfev_all)), tm["evals"]], device=cdev,
                           dtype=torch.float64)
         dist.all_reduce(nf)
         nfev_mean = float(nf[0] / nf[1])
         evals_all = float(nf[2])  # device evaluations over all ranks
     else:
-        nfev_mean = float(np.mean(nfev))
-        evals_all = float(tm.evals)
-
-    total_fits = F * args.steps * world
+        nfev_mean = float(np.mean(nfev_all))
+        evals_all = tm["evals"]
+    total_fits = args.fits * args.steps * world
+    assert table.shape[0] == total_fits, (table.shape, total_fits)
     value = total_fits / elapsed
-    # isolated calibration (after the timed region, not part of `value`): one evaluation of a
-    # full device batch with nothing else on the GPU, to separate the contraction kernel's own
-    # rate from the sharing with the concurrent batch during the timed steps
-    iso = None
-    if G > 1:
-        e0 = engines[0]
-        if e0.band_storage:  # the dense path's own rate needs dense-layout slots (128 of them)
-            e0 = Engine([Xd[i % F] for i in range(128)], [Yd[i % F] for i in range(128)],
-                        [compile_spec(proto[0].kernel, 1)] * 128, device=gpu)
-        th = np.ones((e0.B, 16))
-        th[:, :3] = [40.0, 1.0, NOISE]
-        e0.lml_grad(list(range(e0.B)), th)  # warm
-        e0.reset_timing()
-        e0.lml_grad(list(range(e0.B)), th)
-        ti = e0.last_timing()
-        iso = ti.contract_alg_flops / (ti.contract_ms_total * 1e-3) / 1e12 if ti.contract_ms_total else None
-    contract_ms = tm.contract_ms_total / max(tm.contract_launches, 1.0)
-    contract_flops = tm.contract_alg_flops / max(tm.contract_launches, 1.0)
-    achieved = contract_flops / (contract_ms * 1e-3) / 1e12 if contract_ms > 0 else 0.0
-    traffic, traffic_src = contract_traffic(n, contract_flops)
-    eval_alg = (n ** 3 + 2 * 3 * n ** 2) * evals_all  # SURVEY §8d F_eval(N), P=2, all ranks (dense count)
-    # the kernel with the most device time in the timed region: the fused banded sweep kernels
-    # when the fits' evaluations take the banded path (C2: every evaluation), else the dense
-    # fused K⁻¹ + gradient contraction
-    band_kernels = {
-        "band_fwd1_kernel (p<=1 class: banded Cholesky + z solve, one workgroup per problem)":
-            (tm.band_fwd_ms_total, tm.band_fwd_flops, "band_fwd1_kernel", True),
-        "band_bwd1_kernel<1> (p<=1 class: selected inversion + alpha solve + gradient contraction)":
-            (tm.band_bwd_ms_total, tm.band_bwd_flops, "band_bwd1_kernel", False),
-    }
-    kname, (kms, kflops, kkey, kfwd) = max(band_kernels.items(), key=lambda kv: kv[1][0])
-    if kms > tm.contract_ms_total:
-        launches = tm.band_fused_launches
-        b_ms = kms / max(launches, 1.0)
-        b_flops = kflops / max(launches, 1.0)
-        b_ach = b_flops / (b_ms * 1e-3) / 1e12 if b_ms > 0 else 0.0
-        # problems per timed launch: its flops / one p-weighted problem's (mean p of the class)
-        from_p = tm.band_p_sum / max(tm.band_evals, 1.0)
-        # problems per timed launch (the p <= 1 class): its flops / one p = 1 problem's
-        b_traffic, b_src = band_traffic(kkey, b_flops / band_problem_flops(n, 1, kfwd))
-        f2 = min(max(from_p - 1.0, 0.0), 1.0)
-        per_eval = ((1.0 - f2) * (band_problem_flops(n, 1, True) + band_problem_flops(n, 1, False))
-                    + f2 * (band_problem_flops(n, 2, True) + band_problem_flops(n, 2, False)))
-        chip_ach = tm.band_evals * per_eval / elapsed / 1e12
+    n = args.n
+
+    # roofline: the fused sweep kernel with the most device time (both reported), when the fits'
+    # evaluations take the banded path (C2: every evaluation); the dense contraction otherwise
+    sweeps = {}
+    for key, ms, fl, fwd in (("band_fwd1_kernel", tm["band_fwd_ms_total"], tm["band_fwd_flops"], True),
+                             ("band_bwd1_kernel<1>", tm["band_bwd_ms_total"], tm["band_bwd_flops"], False)):
+        launches = tm["band_fused_launches"]
+        b_ms = ms / max(launches, 1.0)
+        b_fl = fl / max(launches, 1.0)
+        ach = b_fl / (b_ms * 1e-3) / 1e12 if b_ms > 0 else 0.0
+        traffic, src = band_traffic(key.split("<")[0], b_fl / band_problem_flops(n, 1, fwd)) if b_fl > 0 else (None, None)
+        sweeps[key] = {"achieved": ach, "frac": ach / FP64_PEAK_TFLOPS, "avg_launch_ms": b_ms, "launches": launches,
+                       "alg_flops_per_launch": b_fl, "traffic": traffic, "traffic_source": src, "ms_total": ms}
+    from_p = tm["band_p_sum"] / max(tm["band_evals"], 1.0)
+    f2 = min(max(from_p - 1.0, 0.0), 1.0)
+    per_eval = ((1.0 - f2) * (band_problem_flops(n, 1, True) + band_problem_flops(n, 1, False))
+                + f2 * (band_problem_flops(n, 2, True) + band_problem_flops(n, 2, False)))
+    chip_ach = tm["band_evals"] * per_eval / elapsed / 1e12
+    kname = max(sweeps, key=lambda k: sweeps[k]["ms_total"])
+    if sweeps[kname]["ms_total"] > tm["contract_ms_total"]:
+        k = sweeps[kname]
         roofline = {
-            "kernel": kname, "bound": "mfma", "achieved": b_ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": b_ach / FP64_PEAK_TFLOPS, "traffic": b_traffic, "traffic_source": b_src,
-            "traffic_unit": "bytes/launch", "mean_p_blocks": from_p,
-            "avg_launch_ms": b_ms, "launches": launches, "alg_flops_per_launch": b_flops,
+            "kernel": f"{kname} (p<=1 class: one workgroup walks a problem's 64 block steps)",
+            "bound": "mfma", "achieved": k["achieved"], "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": k["frac"], "traffic": k["traffic"], "traffic_source": k["traffic_source"],
+            "traffic_unit": "bytes/launch", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
+            "alg_flops_per_launch": k["alg_flops_per_launch"], "mean_p_blocks": from_p,
+            # both fused sweeps of the p <= 1 class, each timed at its launches' actual start/end
+            "fwd1_frac": sweeps["band_fwd1_kernel"]["frac"], "bwd1_frac": sweeps["band_bwd1_kernel<1>"]["frac"],
+            "fwd1_avg_launch_ms": sweeps["band_fwd1_kernel"]["avg_launch_ms"],
+            "bwd1_avg_launch_ms": sweeps["band_bwd1_kernel<1>"]["avg_launch_ms"],
             # the whole chip over the timed region: every banded evaluation's block products
-            # (both sweeps; p = 1 and p = 2 classes mixed by the mean band width) / wall time.
-            # Several device batches' launches overlap, so this is the MFMA rate the chip sustains
+            # (both sweeps; p = 1 and p = 2 classes mixed by the mean band width) / wall time
             "chip_achieved": chip_ach, "chip_frac": chip_ach / FP64_PEAK_TFLOPS,
-            "note": ("banded path: each launch walks its problems' 64 block steps in sequence, one "
-                     "workgroup (one CU) per problem; achieved = the 64^3 block products issued "
-                     "(2*64^3 flops each, leaf 2/3 of one) / launch duration. The chain of "
-                     "dependent block steps, not MFMA or HBM throughput, sets the duration "
-                     "(DESIGN.md §3c); traffic: the kernel's profiles/<round>_band*_traffic.json"),
-            "dense_contraction_isolated": iso, "dense_contraction_frac_isolated": iso / FP64_PEAK_TFLOPS if iso else None,
+            "note": ("banded path (DESIGN.md §3c): achieved = the 64^3 block products a launch's problems issue "
+                     "(2*64^3 flops each, leaf 2/3 of one) / the launch's HIP-event duration; launches of "
+                     "several device batches and host processes overlap on the GPU; traffic: the kernel's "
+                     "profiles/<round>_band*_traffic.json x problems per launch"),
         }
     else:
-        roofline = {
-            "kernel": "gemm_kernel<128,T,N,EPI_CONTRACT1> (K^-1 = W^T W fused with the gradient contraction)",
-            "bound": "mfma",
-            "achieved": achieved,
-            "peak": FP64_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved / FP64_PEAK_TFLOPS,
-            "traffic": traffic,
-            "traffic_unit": "bytes/launch",
-            "traffic_source": traffic_src,
-            "avg_launch_ms": contract_ms,
-            "launches": tm.contract_launches,
-            "alg_flops_per_launch": contract_flops,
-            "note": (f"timed region runs {G} device batches concurrently on separate streams, so the "
-                     "kernel's launches share the GPU with the other batch's kernels; "
-                     "achieved_isolated = the same kernel alone (one full batch, after the timed region)"
-                     if G > 1 else "one device batch"),
-            "achieved_isolated": iso,
-            "frac_isolated": iso / FP64_PEAK_TFLOPS if iso else None,
-        }
+        c_ms = tm["contract_ms_total"] / max(tm["contract_launches"], 1.0)
+        c_fl = tm["contract_alg_flops"] / max(tm["contract_launches"], 1.0)
+        ach = c_fl / (c_ms * 1e-3) / 1e12 if c_ms > 0 else 0.0
+        traffic, src = contract_traffic(n, c_fl)
+        roofline = {"kernel": "gemm_kernel<128,T,N,EPI_CONTRACT1> (K^-1 = W^T W fused with the gradient contraction)",
+                    "bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": ach / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                    "traffic_source": src, "avg_launch_ms": c_ms, "launches": tm["contract_launches"],
+                    "alg_flops_per_launch": c_fl}
+    # host side: per process, the share of the timed region its one host thread was not waiting
+    # for the device (driver stats), and its busy span
+    host = []
+    for p in parts:
+        st = p[4] or {}
+        wait = st.get("device_wait", 0.0)
+        host.append({"proc": p[0], "fits": int(len(p[1])), "busy_s": p[5],
+                     "host_share": (p[5] - wait) / p[5] if p[5] > 0 else None,
+                     "rounds": st.get("rounds"), "fit_evals": st.get("fit_evals")})
     out = {
         "metric": "GP fits/sec (N=4096, 1-D RBF)",
         "value": value,
@@ -445,31 +617,34 @@ def main():
         "data": "synthetic (C2 generator, seeded per rank/series)",
         "config": {"workload": "C2: exact GPR fit, synthetic 1-D series, N=4096, SquaredExponential, "
                                "fp64, sigma_n^2=1e-5 fixed, L-BFGS-B maxiter=100 + predict_f(X_train)",
-                   "N": n, "fits_per_gpu_per_step": F, "device_slots": W, "device_batches": NG, "slot_storage": args.storage,
-                   "wide_batch_slots": WS,
-                   "kernel": "SquaredExponential",
-                   "parallelism": f"independent fits, {world} process(es) x 1 GPU, RCCL all_gather of results"},
+                   "N": n, "fits_per_gpu_per_step": args.fits, "device_slots_per_gpu": args.width,
+                   "host_processes_per_gpu": P, "device_batches_per_process": args.groups,
+                   "slot_storage": args.storage, "kernel": "SquaredExponential",
+                   "parallelism": f"independent fits, {world} rank(s) x 1 GPU x {P} host processes, "
+                                  "RCCL all_gather of the per-fit results"},
         "nfev_mean": nfev_mean,
-        "band_path": {"evals": tm.band_evals, "dense_evals": tm.evals - tm.band_evals,
-                      "mean_p_blocks": tm.band_p_sum / max(tm.band_evals, 1.0),
-                      "check_fallbacks": tm.band_fallbacks, "fallback_slot_evals": tm.shadow_evals,
-                      "fallback_slot_predicts": tm.shadow_predicts,
-                      "ms_per_call": tm.band_ms_total / max(tm.band_calls, 1.0),
-                      "problems_per_call": tm.band_evals / max(tm.band_calls, 1.0)},
         "evals_per_s": evals_all / elapsed,
-        # the dense algorithm's count F_eval(N) x evaluations / wall time: what the same job
-        # would have to sustain on the dense path (the banded path does far fewer flops)
-        "eval_dense_equiv_tflops": eval_alg / elapsed / 1e12,
+        "band_path": {"evals": tm["band_evals"], "dense_evals": tm["evals"] - tm["band_evals"],
+                      "mean_p_blocks": from_p, "check_fallbacks": tm["band_fallbacks"],
+                      "fallback_slot_evals": tm["shadow_evals"], "fallback_slot_predicts": tm["shadow_predicts"],
+                      "ms_per_call": tm["band_ms_total"] / max(tm["band_calls"], 1.0),
+                      "problems_per_call": tm["band_evals"] / max(tm["band_calls"], 1.0)},
+        "host": host,
         "roofline": roofline,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, nfev_mean)
-        out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
-    if stats and rank == 0:
-        out["driver_stats_last_call"] = stats[-1]
-    if traces and rank == 0:
+    if rank == 0 and world == 1 and not args.no_secondary:
+        for name, fn in (("secondary_c4_dense", lambda: secondary_c4(gpu)), ("secondary_c5_svgp", lambda: secondary_c5(gpu))):
+            try:
+                out[name] = fn()
+            except Exception as e:  # reported, never fatal to the headline line
+                out[name] = {"error": f"{type(e).__name__}: {e}"}
+    if rank == 0 and wk.driver_stats:
+        out["driver_stats_last_call"] = wk.driver_stats[-1]
+    if wk.traces and rank == 0:
         with open(os.environ.get("GPX_TRACE_OUT", "rounds_trace.json"), "w") as f:
-            json.dump([[list(e) for e in tr] for tr in traces], f)
+            json.dump([[list(e) for e in tr] for tr in wk.traces], f)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -155,6 +155,17 @@ int gpx_batch_rebind_host(gpx_batch* batch, int b, int n, const double* X, const
  * it here is waited on by the gather when that runs on another stream. */
 int gpx_batch_rebind_device(gpx_batch* batch, int b, int n, const double* X, const double* Y,
                             const gpx_kernel_spec* spec, void* stream);
+/* gpx_batch_rebind_device with the per-64-row-block bounding boxes of X supplied by the caller
+ * (host array, for each of the ceil(n/64) blocks and each of the D columns the pair (min, max)
+ * of that column over the block's rows: [ceil(n/64)][D][2]), as gpx_batch_slot_boxes returned
+ * them for the same X earlier: the band tables are computed here and the next call's gather
+ * needs no box download (and no stream synchronise) for this slot. */
+int gpx_batch_rebind_device_boxed(gpx_batch* batch, int b, int n, const double* X, const double* Y,
+                                  const gpx_kernel_spec* spec, const double* boxes, void* stream);
+/* The boxes of slot b's X (layout as above) as computed when its inputs were last gathered;
+ * GPX_BAD_ARG if unknown (not gathered yet, host-staged, or no band tables for this batch's
+ * shape). For a caller that caches them per series. */
+int gpx_batch_slot_boxes(const gpx_batch* batch, int b, double* boxes);
 
 /*
  * logML and ∂logML/∂θ at theta for the n_active problems listed in active (host int32).

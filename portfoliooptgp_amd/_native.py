@@ -27,7 +27,7 @@ LIB_PATH = os.environ.get("GPX_LIB") or os.path.join(os.path.dirname(os.path.abs
 EXPORTED_SYMBOLS = (
     "gpx_version", "gpx_create", "gpx_destroy", "gpx_last_error", "gpx_batch_create", "gpx_batch_create_banded",
     "gpx_batch_rebind_host",
-    "gpx_batch_rebind_device",
+    "gpx_batch_rebind_device", "gpx_batch_rebind_device_boxed", "gpx_batch_slot_boxes",
     "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_lml_grad_submit", "gpx_batch_lml_grad_complete",
     "gpx_batch_lml_grad_query", "gpx_batch_band_width",
     "gpx_batch_predict", "gpx_batch_predict_full_cov", "gpx_batch_predict_train",
@@ -152,6 +152,11 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_rebind_device.restype = c_int
         lib.gpx_batch_rebind_device.argtypes = [c_void_p, c_int, c_int, c_void_p, c_void_p,
                                                 ctypes.POINTER(GpxKernelSpec), c_void_p]
+        lib.gpx_batch_rebind_device_boxed.restype = c_int
+        lib.gpx_batch_rebind_device_boxed.argtypes = [c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                                      ctypes.POINTER(GpxKernelSpec), c_void_p, c_void_p]
+        lib.gpx_batch_slot_boxes.restype = c_int
+        lib.gpx_batch_slot_boxes.argtypes = [c_void_p, c_int, c_void_p]
         lib.gpx_batch_reset_timing.restype = c_int
         lib.gpx_batch_reset_timing.argtypes = [c_void_p]
         spec_p = ctypes.POINTER(GpxKernelSpec)

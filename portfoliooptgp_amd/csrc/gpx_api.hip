@@ -486,9 +486,35 @@ int ensure_rebind_meta(gpx_batch* bt) {
   return GPX_OK;
 }
 
+// remember slot b's per-block X boxes (rows of its valid blocks; the rest of the slot's row
+// is left as it was)
+void keep_slot_box(gpx_batch* bt, int b, const double* box) {
+  const int nbx = (bt->Nmax + kLeaf - 1) / kLeaf;
+  const size_t row = (size_t)nbx * bt->D * 2;
+  if (bt->slot_box.empty()) {
+    bt->slot_box.assign(row * bt->B, 0.0);
+    bt->slot_box_ok.assign(bt->B, 0);
+  }
+  const int nvb = (bt->n[b] + kLeaf - 1) / kLeaf;
+  std::memcpy(bt->slot_box.data() + row * b, box, sizeof(double) * (size_t)nvb * bt->D * 2);
+  bt->slot_box_ok[b] = 1;
+}
+
+int wait_io(gpx_batch* bt) {
+  if (!bt->io_pending) return GPX_OK;
+  gpx_ctx* ctx = bt->ctx;
+  HIPX(ctx, hipEventSynchronize(bt->io_ev));
+  bt->io_pending = false;
+  return GPX_OK;
+}
+
 int flush_rebinds(gpx_batch* bt, hipStream_t s) {
   if (bt->n_dirty == 0 && bt->pend.empty()) return GPX_OK;
   gpx_ctx* ctx = bt->ctx;
+  {
+    const int e = wait_io(bt);
+    if (e != GPX_OK) return e;
+  }
   {
     const int rc = ensure_rebind_meta(bt);
     if (rc != GPX_OK) return rc;
@@ -520,7 +546,8 @@ int flush_rebinds(gpx_batch* bt, hipStream_t s) {
   int nbox = 0;
   for (const auto& e : bt->pend)
     bt->h_rdesc[m++] = RebindDesc{e.x, e.y, const_cast<double*>(bt->X) + (size_t)e.b * nx,
-                                  const_cast<double*>(bt->Y) + (size_t)e.b * ny, e.n, tables ? nbox++ : -1};
+                                  const_cast<double*>(bt->Y) + (size_t)e.b * ny, e.n,
+                                  tables && !e.boxed ? nbox++ : -1};
   for (auto& w : bt->rebind_waits)  // the device sources' producers (gpx_batch_rebind_device)
     if (w.armed) {
       if (w.s != s) HIPX(ctx, hipStreamWaitEvent(s, w.ev, 0));
@@ -535,7 +562,12 @@ int flush_rebinds(gpx_batch* bt, hipStream_t s) {
     HIPX(ctx, hipMemcpyAsync(bt->h_box, bt->d_box, sizeof(double) * row * nbox, hipMemcpyDeviceToHost, s));
     HIPX(ctx, hipStreamSynchronize(s));
     int i = 0;
-    for (const auto& e : bt->pend) band_tables_boxes(bt, e.b, bt->h_box + row * i++);
+    for (const auto& e : bt->pend) {
+      if (e.boxed) continue;
+      const double* box = bt->h_box + row * i++;
+      band_tables_boxes(bt, e.b, box);
+      keep_slot_box(bt, e.b, box);
+    }
   }
   bt->pend.clear();
   for (int b = 0; b < bt->B; ++b) {
@@ -575,6 +607,10 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
   }
   {
     const int e = flush_rebinds(bt, s);
+    if (e != GPX_OK) return e;
+  }
+  {
+    const int e = wait_io(bt);
     if (e != GPX_OK) return e;
   }
   // one DMA from the pinned block (allocated non-coherent: the host reads and writes it as
@@ -783,6 +819,10 @@ int gpx_batch_destroy(gpx_batch* bt) {
   if (bt->shadow_s) (void)hipStreamDestroy(bt->shadow_s);
   if (bt->shadow_ev) (void)hipEventDestroy(bt->shadow_ev);
   for (auto& w : bt->rebind_waits) (void)hipEventDestroy(w.ev);
+  if (bt->io_ev) {
+    (void)hipEventSynchronize(bt->io_ev);
+    (void)hipEventDestroy(bt->io_ev);
+  }
   if (bt->compact && bt->Kraw) {  // K/L/W point into the raw allocations (band storage's row offset)
     bt->K = bt->Kraw; bt->L = bt->Lraw; bt->W = bt->Wraw;
   }
@@ -911,12 +951,38 @@ int gpx_batch_rebind_device(gpx_batch* bt, int b, int n, const double* X, const 
     bt->dirty[b] = 0;
     --bt->n_dirty;
   }
+  if (!bt->slot_box_ok.empty()) bt->slot_box_ok[b] = 0;
   for (auto& e : bt->pend)
     if (e.b == b) {
-      e = gpx_batch::PendingRebind{b, n, X, Y};
+      e = gpx_batch::PendingRebind{b, n, X, Y, false};
       return GPX_OK;
     }
-  bt->pend.push_back(gpx_batch::PendingRebind{b, n, X, Y});
+  bt->pend.push_back(gpx_batch::PendingRebind{b, n, X, Y, false});
+  return GPX_OK;
+}
+
+int gpx_batch_rebind_device_boxed(gpx_batch* bt, int b, int n, const double* X, const double* Y,
+                                  const gpx_kernel_spec* spec, const double* box, void* stream) {
+  if (!bt) return GPX_BAD_ARG;
+  if (!box) return fail(bt->ctx, GPX_BAD_ARG, "null boxes");
+  const int rc = gpx_batch_rebind_device(bt, b, n, X, Y, spec, stream);
+  if (rc != GPX_OK) return rc;
+  for (auto& e : bt->pend)
+    if (e.b == b) e.boxed = true;
+  if (band_shape(bt)) {  // the band tables now, from the caller's boxes: no download at the gather
+    band_tables_boxes(bt, b, box);
+    keep_slot_box(bt, b, box);
+  }
+  return GPX_OK;
+}
+
+int gpx_batch_slot_boxes(const gpx_batch* bt, int b, double* out) {
+  if (!bt || !out || b < 0 || b >= bt->B) return GPX_BAD_ARG;
+  if (bt->slot_box_ok.empty() || !bt->slot_box_ok[b] || !bt->pend.empty()) return GPX_BAD_ARG;
+  const int nbx = (bt->Nmax + kLeaf - 1) / kLeaf;
+  const size_t row = (size_t)nbx * bt->D * 2;
+  const int nvb = (bt->n[b] + kLeaf - 1) / kLeaf;
+  std::memcpy(out, bt->slot_box.data() + row * b, sizeof(double) * (size_t)nvb * bt->D * 2);
   return GPX_OK;
 }
 
@@ -952,6 +1018,7 @@ int gpx_batch_rebind_host(gpx_batch* bt, int b, int n, const double* X, const do
     ++bt->n_dirty;
   }
   (void)s;
+  if (!bt->slot_box_ok.empty()) bt->slot_box_ok[b] = 0;
   if (band_shape(bt)) band_tables(bt, b, hx);
   return GPX_OK;
 }
@@ -1054,6 +1121,10 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (e != GPX_OK) return e;
   }
   HIPX(ctx, hipSetDevice(ctx->device));
+  {  // routing writes h_bandp inside h_io
+    const int e = wait_io(bt);
+    if (e != GPX_OK) return e;
+  }
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   {  // slots rebound since the last call land first: their band tables (from the gather's
      // X boxes) decide the routing below
@@ -1487,9 +1558,6 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   }
   int rc = upload_common(bt, n_active, active, theta, s);
   if (rc != GPX_OK) return rc;
-  PhaseTimer pt(ctx->profiling != 0, s);
-  bt->flops_acc = 0.0;
-  pt.mark();
   // re-factorise the problems whose cached factor is not at exactly this theta. A cached
   // block-banded factorisation (gpx_band.hip) serves predict at the training inputs (it holds
   // α and the diagonal of K⁻¹); any other predict re-factorises densely.
@@ -1503,6 +1571,12 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
     if (!same || (bt->fac_band[b] && !train)) refac.push_back(b);
     else if (bt->fac_band[b]) band_cached.push_back(b);
   }
+  // the asynchronous case (see below) records no phase events: destroying an event the device
+  // has not reached yet would wait for it
+  const bool async = train && refac.empty() && stream;
+  PhaseTimer pt(ctx->profiling != 0 && !async, s);
+  bt->flops_acc = 0.0;
+  pt.mark();
   // device active list: [dense-factored problems | band-cached problems]
   std::vector<int32_t> order;
   order.reserve(n_active);
@@ -1615,6 +1689,19 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   }
   pt.mark();
   HIPX(ctx, hipGetLastError());
+  if (async) {
+    // every problem predicted from its cached factor at exactly this θ (the fit's last
+    // evaluation): nothing can fail, so the call returns without waiting for the device — the
+    // outputs are ready in the order of the CALLER's stream (not with stream == NULL: the
+    // library's own non-blocking stream is not ordered with the caller's default stream);
+    // the upload out of h_io is fenced by io_ev
+    if (!bt->io_ev) HIPX(ctx, hipEventCreateWithFlags(&bt->io_ev, hipEventDisableTiming));
+    HIPX(ctx, hipEventRecord(bt->io_ev, s));
+    bt->io_pending = true;
+    for (int i = 0; i < n_active; ++i) info[active[i]] = 0;
+    if (shadow_status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
+    return shadow_status;
+  }
   HIPX(ctx, hipMemcpyAsync(bt->h_info, bt->d_info, sizeof(int) * bt->B, hipMemcpyDeviceToHost, s));
   HIPX(ctx, hipStreamSynchronize(s));
   if (pt.on) {

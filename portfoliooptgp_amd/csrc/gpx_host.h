@@ -81,7 +81,12 @@ struct gpx_batch {
   // gpx_batch_rebind_device only records the source pointers; flush_rebinds copies every
   // pending slot (device sources and host-staged ones) with ONE gather kernel that also takes
   // the per-64-block bounding boxes of X for the band tables (one small download per call)
-  struct PendingRebind { int b, n; const double* x; const double* y; };
+  struct PendingRebind { int b, n; const double* x; const double* y; bool boxed; };
+  // the per-64-block boxes of each slot's X as last bound ([B][nbx][D][2], valid where
+  // slot_box_ok): a caller that rebinds the same series again hands them back
+  // (gpx_batch_rebind_device_boxed) and the gather needs no box download + synchronise
+  std::vector<double> slot_box;
+  std::vector<char> slot_box_ok;
   // the evaluation submitted by gpx_batch_lml_grad_submit, completed by _complete (gpx_api.hip)
   struct PendingEval;
   std::unique_ptr<PendingEval> pending_eval;
@@ -89,6 +94,11 @@ struct gpx_batch {
   // the streams the pending device sources were rebound on (their producers' order): an event
   // recorded there at the rebind, waited on by flush_rebinds' gather stream
   struct RebindWait { hipStream_t s; hipEvent_t ev; bool armed; };
+  // a call that returns without synchronising its stream (predict at the training inputs from
+  // cached factors) leaves its upload DMA out of h_io in flight: the next writer of the pinned
+  // blocks waits on this event first (wait_io)
+  hipEvent_t io_ev = nullptr;
+  bool io_pending = false;
   std::vector<RebindWait> rebind_waits;
   gpx::RebindDesc* h_rdesc = nullptr;   // pinned (coherent), one per slot
   double* d_box = nullptr;               // [B][nb][D][2] per-block lo/hi of X
@@ -204,6 +214,7 @@ void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                   hipStream_t s);
 int flush_rebinds(gpx_batch* bt, hipStream_t s);  // pending rebinds -> device (one gather on s)
+int wait_io(gpx_batch* bt);                        // the last asynchronous call's uploads have left h_io
 int ensure_rebind_meta(gpx_batch* bt);             // pinned n/spec mirrors + dirty flags
 
 }  // namespace gpx

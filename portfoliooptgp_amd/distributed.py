@@ -7,8 +7,8 @@ predicted_variances), Multi-Input_GPR/Portfolio/portfolio.py:92-165). Here:
 
 * one process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on MI355X,
   "gloo" for CPU tests);
-* fits are assigned to ranks longest-processing-time first on cost N³ (no communication
-  while fitting);
+* fits are assigned to ranks longest-processing-time first on their cost (N³ dense, N·w² on
+  the block-banded path; no communication while fitting);
 * every rank fits its shard through the continuous-batching driver and predicts its
   horizon;
 * ONE all_gather of a packed fp64 tensor (θ*, loss*, nfev, mean[H], var[H] per asset) is the
@@ -40,9 +40,47 @@ def shard_lpt(costs: Sequence[float], world: int) -> List[List[int]]:
     return out
 
 
-def fit_cost(n: int) -> float:
-    """Relative cost of one exact-GP fit (evaluations are O(N³))."""
-    return float(n) ** 3
+def band_blocks_estimate(x, lengthscale: float = 1.0, cutoff: float = 38.63) -> Optional[int]:
+    """Band width, in 64-row blocks, that a fit on inputs x starts on: the smallest p such that
+    every pair of points more than p blocks apart is at least ``cutoff`` lengthscales apart
+    (SquaredExponential: exp(−r²/2) underflows to exactly 0 in fp64 beyond r = 38.6; the device
+    bounds it the same way from per-block boxes, gpx_api.hip band_width). At GPflow's default
+    ℓ = 1 on the reference's unnormalised day offsets (GPR/data_handler.py:42-44) that is one
+    block. None when the band does not apply (fewer than 8 blocks, as the device requires, or no
+    block offset vanishes): the fit runs dense."""
+    x = np.asarray(x, dtype=np.float64)
+    x = x.reshape(len(x), -1)
+    n = len(x)
+    nb = (n + 63) // 64
+    if nb < 8:
+        return None
+    lo = np.array([x[k * 64:(k + 1) * 64].min(0) for k in range(nb)])
+    hi = np.array([x[k * 64:(k + 1) * 64].max(0) for k in range(nb)])
+    for p in range(0, nb - 1):
+        d = p + 1   # every offset >= d must vanish; the box gap only grows with d for sorted inputs
+        ok = True
+        for dd in range(d, nb):
+            gap = np.maximum(0.0, np.maximum(lo[dd:] - hi[:nb - dd], lo[:nb - dd] - hi[dd:]))
+            if np.sqrt((gap * gap).sum(1)).min() / lengthscale < cutoff:
+                ok = False
+                break
+        if ok:
+            return p
+    return None
+
+
+def fit_cost(n: int, band_blocks: Optional[int] = None) -> float:
+    """Relative cost of one exact-GP fit: O(N³) per evaluation on the dense path, O(N·w²) with
+    w = 64·(p + 1) rows on the block-banded path (band of p blocks)."""
+    if band_blocks is None:
+        return float(n) ** 3
+    w = 64.0 * (band_blocks + 1)
+    return float(n) * w * w
+
+
+def series_cost(x) -> float:
+    """fit_cost of a series for the default fitter (SE at GPflow's default ℓ = 1)."""
+    return fit_cost(len(x), band_blocks_estimate(x))
 
 
 def pack_results(indices: Sequence[int], results: Sequence[dict], horizon: int, n_theta: int) -> torch.Tensor:
@@ -97,6 +135,31 @@ def portfolio_inputs(gathered: Dict[int, dict], order: Sequence[int]) -> Tuple[l
     return means, varis
 
 
+def portfolio_day_moments(returns, variances, day: int, log_return: bool = True):
+    """What the portfolio step computes from the gathered lists on ``day``: the indexing of
+    Portfolio.evaluate_portfolio (Multi-Input_GPR/Portfolio/portfolio.py:111-124: returns[i][0][0]
+    on day 0, returns[i][:(day+1)] afterwards, sqrt(variances[i][day][0]) for the std devs)
+    followed by the reference Optimizer's set_predictions (day 0), set_cml_log_return
+    (log returns) or set_predictions_cml (Multi-Input_GPR/optimization/optimizer.py:20-56).
+    Returns (mu [A], Sigma [A, A] diagonal, std_devs [A]). Host code, the same numpy calls as
+    the reference (pinned against its own outputs by tests/golden/portfolio.npz)."""
+    A = len(returns)
+    if day == 0:
+        mu = np.array([returns[i][0][0] for i in range(A)])
+        sigma = np.diag(np.array([variances[i][0][0] for i in range(A)]))
+        std = [np.sqrt(variances[i][0][0]) for i in range(A)]
+    else:
+        rets = [returns[i][:(day + 1)] for i in range(A)]
+        vols = [variances[i][:(day + 1)] for i in range(A)]
+        std = [np.sqrt(variances[i][day][0]) for i in range(A)]
+        if log_return:
+            mu = np.array([np.sum(r) for r in rets])
+        else:
+            mu = np.array([np.prod([1 + r for r in rl]) - 1 for rl in rets])
+        sigma = np.diag(np.array([np.sum(v) for v in vols]))
+    return mu, sigma, np.asarray(std, dtype=np.float64)
+
+
 def asset_fingerprint(x, y, horizon) -> str:
     """Content hash of one asset's fit inputs (training series and prediction inputs)."""
     h = hashlib.sha1()
@@ -107,19 +170,43 @@ def asset_fingerprint(x, y, horizon) -> str:
     return h.hexdigest()
 
 
+def _canonical(obj) -> str:
+    """A run-independent text form of a fit configuration value: containers element by
+    element, numpy arrays and ctypes structures (a compiled gpx_kernel_spec) by their bytes,
+    scalars and strings by repr. A value whose repr carries a memory address (' at 0x', the
+    default object repr) has no stable form — hashing it would change the fingerprint on every
+    run and silently discard every checkpoint — so it is refused."""
+    import ctypes
+    if isinstance(obj, dict):
+        return "{" + ",".join(f"{_canonical(k)}:{_canonical(v)}" for k, v in
+                              sorted(obj.items(), key=lambda kv: repr(kv[0]))) + "}"
+    if isinstance(obj, (list, tuple)):
+        return ("[" if isinstance(obj, list) else "(") + ",".join(_canonical(v) for v in obj) + ")"
+    if isinstance(obj, np.ndarray):
+        return f"ndarray{obj.dtype.str}{obj.shape}:{np.ascontiguousarray(obj).tobytes().hex()}"
+    if isinstance(obj, (ctypes.Structure, ctypes.Array)):
+        return f"{type(obj).__name__}:{bytes(obj).hex()}"
+    r = repr(obj)
+    if " at 0x" in r:
+        raise ValueError(f"fit configuration value {r} has no stable representation (its repr holds a "
+                         "memory address); pass plain values, arrays or a compiled kernel spec")
+    return r
+
+
 def config_fingerprint(fit_fn: Callable, fit_config=None) -> str:
     """Hash of what produced a checkpoint's results: the fit function's qualified name (with a
     functools.partial's bound arguments) and the caller's ``fit_config`` (kernel spec, maxiter,
-    noise, ... — anything whose repr changes when the fit would). A rerun whose configuration
-    differs refits everything instead of reusing results of another fit protocol."""
+    noise, ...), in the canonical form of ``_canonical`` (so the same configuration hashes the
+    same in every process). A rerun whose configuration differs refits everything instead of
+    reusing results of another fit protocol."""
     import functools
     parts = []
     f = fit_fn
     while isinstance(f, functools.partial):
-        parts.append(repr((f.args, sorted(f.keywords.items()))))
+        parts.append(_canonical((tuple(f.args), sorted(f.keywords.items()))))
         f = f.func
     parts.append(f"{getattr(f, '__module__', '?')}.{getattr(f, '__qualname__', repr(f))}")
-    parts.append(repr(fit_config))
+    parts.append(_canonical(fit_config))
     return hashlib.sha1("\x1f".join(parts).encode()).hexdigest()
 
 
@@ -152,7 +239,8 @@ def _save_checkpoint(path: str, table: torch.Tensor, fingerprints: Sequence[str]
 
 def fit_assets(series: Sequence[Tuple[np.ndarray, np.ndarray]], horizons: Sequence[np.ndarray],
                fit_fn: Optional[Callable] = None, n_theta: int = 2, group=None,
-               checkpoint: Optional[str] = None, fit_config=None) -> Dict[int, dict]:
+               checkpoint: Optional[str] = None, fit_config=None,
+               cost_fn: Optional[Callable] = None) -> Dict[int, dict]:
     """Shard the assets over the ranks of `group`, fit the local shard with `fit_fn`
     (default: GPU exact GPR with a SquaredExponential kernel and σn² = 1e-5 fixed, the
     GPR/model_trainer.py:15-19 protocol, continuous-batched), predict each asset at its
@@ -165,10 +253,14 @@ def fit_assets(series: Sequence[Tuple[np.ndarray, np.ndarray]], horizons: Sequen
     granularity; changed inputs are refitted. The file also records a fingerprint of the fit
     configuration (``fit_fn``'s qualified name and bound arguments plus ``fit_config``, e.g. the
     kernel spec / maxiter / noise of a custom fitter); a file written under another
-    configuration is discarded. The reference has no checkpointing."""
+    configuration is discarded. The reference has no checkpointing.
+
+    ``cost_fn(x)``: relative cost of fitting a series for the LPT shard (default ``series_cost``:
+    O(N·w²) for the banded fits of the default SE fitter on day offsets, O(N³) for dense ones)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    shards = shard_lpt([fit_cost(len(x)) for x, _ in series], world)
+    cost_fn = cost_fn or series_cost
+    shards = shard_lpt([cost_fn(x) for x, _ in series], world)
     mine = shards[rank]
     fit_fn = fit_fn or gpu_fit_shard
     H = max(len(h) for h in horizons)

@@ -70,6 +70,19 @@ def screen_theta(act: np.ndarray, theta: np.ndarray, n_params: np.ndarray, info:
     return np.ascontiguousarray(act[ok])
 
 
+# Per-64-row-block bounding boxes of device-resident series (the band tables' input), kept
+# per series so that rebinding the same series into a slot again (continuous batching refits the
+# same assets step after step) skips the gather's box download and stream synchronise. Keyed by
+# the tensor's identity and its version counter (an in-place write bumps it), holding a
+# reference so the storage cannot be reused under the key.
+_BOX_CACHE: "OrderedDict" = None
+_BOX_CACHE_MAX = 16384
+
+
+def _box_key(x: torch.Tensor, n: int, D: int):
+    return (x.device.index, x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), n, D)
+
+
 class Engine:
     def __init__(self, Xs: Sequence, Ys: Sequence, specs: Sequence[N.GpxKernelSpec],
                  device: Optional[int] = None, band_storage: bool = False):
@@ -117,6 +130,7 @@ class Engine:
         self.n_params = np.asarray([s.n_params for s in specs], dtype=np.int64)
         self.eval_count = 0
         self._rebound = {}  # slot -> device tensors of its last rebind (kept alive for the gather)
+        self._box_want = {}  # slot -> (box key, X) of a device rebind whose boxes are not cached yet
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -133,6 +147,24 @@ class Engine:
     @staticmethod
     def _active(active) -> np.ndarray:
         return np.ascontiguousarray(np.asarray(active, dtype=np.int32))
+
+    def _harvest_boxes(self) -> None:
+        """After a device call gathered the pending rebinds: cache the boxes of the series that
+        were not cached yet (gpx_batch_slot_boxes)."""
+        global _BOX_CACHE
+        if not self._box_want:
+            return
+        from collections import OrderedDict
+        if _BOX_CACHE is None:
+            _BOX_CACHE = OrderedDict()
+        for b, (key, x) in self._box_want.items():
+            buf = np.empty(((int(self.n[b]) + 63) // 64) * self.D * 2, dtype=np.float64)
+            if self.lib.gpx_batch_slot_boxes(self.handle, int(b), buf.ctypes.data) == N.GPX_OK:
+                _BOX_CACHE[key] = (x, buf)
+                _BOX_CACHE.move_to_end(key)
+                while len(_BOX_CACHE) > _BOX_CACHE_MAX:
+                    _BOX_CACHE.popitem(last=False)
+        self._box_want.clear()
 
     def lml_grad(self, active: Sequence[int], theta: np.ndarray):
         """logML [B], ∂logML/∂θ [B, 16], info [B] for the active rows (others untouched).
@@ -153,6 +185,7 @@ class Engine:
                                          theta.ctypes.data_as(dp), lml.ctypes.data_as(dp),
                                          grad.ctypes.data_as(dp), info.ctypes.data_as(ip),
                                          self._stream())
+        self._harvest_boxes()
         if rc not in (N.GPX_OK, N.GPX_NOT_PD):
             raise N.GPXError(f"gpx_batch_lml_grad failed ({rc}): {self.ctx.last_error()}")
         self.eval_count += len(act)
@@ -176,6 +209,7 @@ class Engine:
         rc = self.lib.gpx_batch_lml_grad_submit(self.handle, len(act), act.ctypes.data_as(ip),
                                                 theta.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                                 self._stream())
+        self._harvest_boxes()
         if rc != N.GPX_OK:
             self._submitted = None
             raise N.GPXError(f"gpx_batch_lml_grad_submit failed ({rc}): {self.ctx.last_error()}")
@@ -256,6 +290,7 @@ class Engine:
                                             ctypes.c_void_p(mean.data_ptr()),
                                             ctypes.c_void_p(var.data_ptr()),
                                             info.ctypes.data_as(ip), self._stream())
+        self._harvest_boxes()
         if rc == N.GPX_NOT_PD:
             bad = [int(b) for b in act if info[b] != 0]
             raise N.NotPositiveDefiniteError(
@@ -284,6 +319,7 @@ class Engine:
                                               theta.ctypes.data_as(dp), 1 if add_noise else 0,
                                               ctypes.c_void_p(mean.data_ptr()), ctypes.c_void_p(var.data_ptr()),
                                               info.ctypes.data_as(ip), self._stream())
+        self._harvest_boxes()
         if rc == N.GPX_NOT_PD:
             bad = [int(b) for b in act if info[b] != 0]
             raise N.NotPositiveDefiniteError(
@@ -304,12 +340,17 @@ class Engine:
         ok_dev = (isinstance(X, torch.Tensor) and isinstance(Y, torch.Tensor) and X.is_cuda and Y.is_cuda
                   and X.device.index == self.device and Y.device.index == self.device
                   and X.dtype == torch.float64 and Y.dtype == torch.float64)
+        box = None
         if ok_dev:
             x = X.detach().contiguous()
             y = Y.detach().contiguous()
             x2 = x.reshape(x.shape[0], -1)
             n, D, ny = x2.shape[0], x2.shape[1], y.numel()
             fn = self.lib.gpx_batch_rebind_device
+            key = _box_key(x, n, D) if X.is_contiguous() else None
+            hit = _BOX_CACHE.get(key) if (key is not None and _BOX_CACHE is not None) else None
+            if hit is not None:
+                box = hit[1]
         else:
             x = np.ascontiguousarray(_host_f64(X))
             y = np.ascontiguousarray(_host_f64(Y)).reshape(-1)
@@ -321,12 +362,20 @@ class Engine:
         self.specs[b] = spec
         self.n_params[b] = spec.n_params
         self.n[b] = n
-        rc = fn(self.handle, int(b), int(n), ctypes.c_void_p(x.data_ptr() if ok_dev else x.ctypes.data),
-                ctypes.c_void_p(y.data_ptr() if ok_dev else y.ctypes.data), ctypes.byref(spec), self._stream())
+        if box is not None:
+            rc = self.lib.gpx_batch_rebind_device_boxed(
+                self.handle, int(b), int(n), ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+                ctypes.byref(spec), box.ctypes.data, self._stream())
+        else:
+            rc = fn(self.handle, int(b), int(n), ctypes.c_void_p(x.data_ptr() if ok_dev else x.ctypes.data),
+                    ctypes.c_void_p(y.data_ptr() if ok_dev else y.ctypes.data), ctypes.byref(spec), self._stream())
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_rebind failed ({rc}): {self.ctx.last_error()}")
+        self._box_want.pop(b, None)
         if ok_dev:
             self._rebound[b] = (x, y)  # read by the deferred gather
+            if box is None and key is not None:
+                self._box_want[b] = (key, X)
         else:
             self._rebound.pop(b, None)
 

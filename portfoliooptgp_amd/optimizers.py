@@ -724,6 +724,10 @@ class _SteppedDriver:
         try:
             with _single_thread_blas():
                 self._run_all()
+            # predictions from cached factors return without waiting for the device (in their
+            # group stream's order); the caller reads them on its own stream
+            if self.predict_train and torch.cuda.is_available():
+                torch.cuda.synchronize(self.groups[0][0].device)
         finally:
             if gc_on:
                 gc.enable()
@@ -859,7 +863,9 @@ class _SteppedDriver:
             for key, rs in layouts.items():
                 s0 = active[rs[0]]
                 P = key[0]
-                U = np.array([active[r]["st"].x for r in rs], dtype=np.float64).reshape(len(rs), P)
+                # a finished fit held for one more evaluation at its result's x (see _finish)
+                U = np.array([active[r]["st"].x if active[r].get("reeval") is None else active[r]["reeval"]
+                              for r in rs], dtype=np.float64).reshape(len(rs), P)
                 R = np.asarray(rs, dtype=np.int32)
                 if not moved:
                     lib.gpx_host_theta_rows(len(rs), P, U.ctypes.data, R.ctypes.data, s0["cols"].ctypes.data,
@@ -916,6 +922,11 @@ class _SteppedDriver:
                                      lml.ctypes.data, grad.ctypes.data, loss.ctypes.data, gu.ctypes.data)
             for k, r in enumerate(rs):
                 s = active[r]
+                if s.get("reeval") is not None:
+                    # the extra evaluation at the result's x (its factor serves the predict)
+                    done.append((r, info[r] == 0))
+                    continue
+                s["last_u"] = U[k]
                 try:
                     if info[r] != 0:
                         if info[r] == N.INFO_BAD_THETA:
@@ -938,7 +949,7 @@ class _SteppedDriver:
                     done.append((r, True))
         self._tick("steps", t0)
         t_steps = clk()
-        self._finish(eng, gs.lock, active, done)
+        held = self._finish(eng, gs.lock, active, done)
         self._tick("finish", t_steps)
         if self.trace is not None:  # GPX_TRACE_ROUNDS: (group, call start, call end, steps end, finish end, n)
             self.trace.append((gs.g, gs.t_call, t_call_end, t_steps, clk(), len(gs.act)))
@@ -946,6 +957,8 @@ class _SteppedDriver:
             self.stats["rounds"] = self.stats.get("rounds", 0) + 1
             self.stats["fit_evals"] = self.stats.get("fit_evals", 0) + len(gs.act)
         for r, _ in done:
+            if r in held:
+                continue
             del active[r]
             if not self.fixed:
                 gs.free.append(r)
@@ -1032,16 +1045,35 @@ class _SteppedDriver:
                 submit_idle()
 
     def _finish(self, eng, lock, active, done):
-        pred_rows, xs = [], []
+        """Results of the finished fits and their predictions. Returns the rows held back for
+        one more evaluation: predict at the training inputs reuses the factor of the fit's last
+        evaluated point, which is the result's x unless L-BFGS-B returned an earlier point (its
+        line search backed off); such a fit is evaluated once more at its result's x in the
+        next batched round (banded and asynchronous, like any other evaluation) instead of being
+        re-factorised alone by the predict call."""
+        pred_rows, xs, held = [], [], set()
         for r, ok in done:
             s = active[r]
             if ok:
-                res = s["st"].result()
+                res = s.get("res") or s["st"].result()
+                if (self.predict_train and self.predict_inputs is None and s.get("reeval") is None
+                        and s.get("last_u") is not None and not np.array_equal(res.x, s["last_u"])):
+                    s["res"] = res
+                    s["reeval"] = np.array(res.x, dtype=np.float64)
+                    held.add(r)
+                    continue
                 _unpack(s["v"], res.x)
                 self.results[s["i"]] = res
                 if self.predict_train:
                     pred_rows.append(r)
                     xs.append(s["m"].data[0] if self.predict_inputs is None else self.predict_inputs[s["i"]])
+            elif s.get("reeval") is not None:
+                # the extra evaluation failed: the result stands, the predict re-factorises
+                res = s["res"]
+                _unpack(s["v"], res.x)
+                self.results[s["i"]] = res
+                pred_rows.append(r)
+                xs.append(s["m"].data[0])
             elif not self.fixed:
                 s["m"]._engine = None
         if pred_rows:
@@ -1066,5 +1098,6 @@ class _SteppedDriver:
                     self.errors[active[r]["i"]] = e
         if not self.fixed:
             for r, ok in done:
-                if ok:
+                if r not in held and (ok or active[r].get("reeval") is not None):
                     active[r]["m"]._engine = None
+        return held

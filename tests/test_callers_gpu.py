@@ -1,0 +1,250 @@
+"""The reference's callers of the hot path, on device fits, against the oracle and the golden
+vectors:
+
+* Predictor.predict_single (GPR/predictor.py:5-8) and predict_combined / upsample_predictions
+  (:10-51) on device models, and BlendOptimizer against the α/β the reference's own
+  GPR/optimizer.py gave (tests/golden/blend.npz);
+* MultiInputTrainer.train_likelihood (Multi-Input_GPR/models/model_trainer.py:26-54: four
+  trainable-noise restarts, lowest opt_logs.fun wins) against the oracle's four restarts;
+* ModelTrainer.train_model's 8-kernel sweep (GPR/model_trainer.py:14-25) on the C1 real-data
+  N = 251 series (test_data/Stocks/META_EOD) and on the 18 daily ticker series of
+  config C1 (N = 68), with the Periodic fits whose L-BFGS-B paths are chaotic pinned at
+  evaluation level (the oracle's loss and gradient at the GPU's own θ*);
+* distributed.fit_assets → portfolio_inputs → portfolio_day_moments on device fits (f3).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import portfoliooptgp_amd as gpx  # noqa: E402
+from oracle import gp_oracle as O  # noqa: E402
+from tests.test_gpu_parity import check_grad, check_loss, check_mean, check_var  # noqa: E402
+
+K = gpx.kernels
+
+
+def ref_kernels():
+    """GPR/main.py:105-114, in order (gpx classes)."""
+    return [K.SquaredExponential(), K.Matern12(), K.RationalQuadratic(), K.Exponential(),
+            K.SquaredExponential() + K.Matern12(),
+            K.Exponential() + K.Periodic(K.SquaredExponential()) + K.Linear(),
+            K.Exponential() + K.Periodic(K.SquaredExponential()),
+            K.SquaredExponential() * K.Matern12()]
+
+
+PERIODIC = (5, 6)
+
+
+@pytest.fixture(scope="module")
+def blend(golden_dir):
+    return np.load(os.path.join(golden_dir, "blend.npz"))
+
+
+def _cond(okernel, x, noise):
+    return float(np.linalg.cond(okernel.K(x) + noise * np.eye(len(x))))
+
+
+def _device_model(index, theta, x, y, noise=1e-5):
+    k = ref_kernels()[index]
+    for p, v in zip(k.parameters, theta):
+        p.assign(float(v))
+    m = gpx.models.GPR(data=(x, y), kernel=k)
+    m.likelihood.variance.assign(noise)
+    gpx.set_trainable(m.likelihood.variance, False)
+    return m
+
+
+def _oracle_model(index, theta, x, y, noise=1e-5):
+    k = O.reference_kernel_list()[index]
+    for p, v in zip(k.params(), theta):
+        p.value = float(v)
+    m = O.OGPR(x, y, k, noise_variance=noise)
+    m.noise.trainable = False
+    return m
+
+
+def test_predict_single_and_predict_combined(blend):
+    """a10 + f1 on the AAPL d/w/m best models (θ from the oracle's shared-kernel sweep, the
+    GPR/main.py flow): predict_single on the device = the oracle's predict_f / predict_y;
+    upsampling + BlendOptimizer reproduce the reference Optimizer's α/β; predict_combined at
+    the extended inputs = the golden blend."""
+    from portfoliooptgp_amd.trainer import BlendOptimizer, Predictor
+    pr = Predictor()
+    models, f_means = {}, {}
+    for t in "dwm":
+        x, y = blend[f"aapl|{t}|x"], blend[f"aapl|{t}|y"]
+        idx, th = int(blend[f"aapl|{t}|kernel_index"][0]), blend[f"aapl|{t}|theta"]
+        m = _device_model(idx, th, x, y)
+        models[t] = m
+        cond = _cond(_oracle_model(idx, th, x, y).kernel, x, 1e-5)
+        fm, fv, ym, yv = pr.predict_single(m, x)
+        for got in (fm, fv, ym, yv):
+            assert tuple(got.shape) == (len(x), 1) and hasattr(got, "numpy")
+        s2 = max(float(np.abs(blend[f"aapl|{t}|fv"]).max()), 1.0)
+        check_mean(fm.numpy(), blend[f"aapl|{t}|fm"], cond, float(np.abs(y).max()))
+        check_var(fv.numpy(), blend[f"aapl|{t}|fv"], s2)
+        check_mean(ym.numpy(), blend[f"aapl|{t}|ym"], cond, float(np.abs(y).max()))
+        check_var(yv.numpy(), blend[f"aapl|{t}|yv"], s2)
+        np.testing.assert_allclose(yv.numpy() - fv.numpy(), 1e-5, rtol=1e-6)
+        f_means[t] = fm
+    xd = torch.as_tensor(blend["aapl|d|x"])
+    fw_up = pr.upsample_predictions(xd, torch.as_tensor(blend["aapl|w|x"]), f_means["w"], "w")
+    fm_up = pr.upsample_predictions(xd, torch.as_tensor(blend["aapl|m|x"]), f_means["m"], "m")
+    ab = BlendOptimizer(float(blend["aapl|lambda"][0])).optimize_weights(blend["aapl|d|y"], f_means["d"], fw_up, fm_up)
+    np.testing.assert_allclose(ab, blend["aapl|alpha_beta"], rtol=0, atol=1e-6)
+    a, b = blend["aapl|combined|alpha_beta"]
+    out = pr.predict_combined(a, b, models["d"], models["w"], models["m"],
+                              *(blend[f"aapl|{t}|xc"] for t in "dwm"))
+    for got, key in zip(out, ("cm", "cv", "cym", "cyv")):
+        ref = blend["aapl|combined|" + key]
+        got = np.asarray(got)
+        ok = np.isfinite(ref)
+        assert np.array_equal(ok, np.isfinite(got))        # leading NaNs of the upsampling kept
+        scale = float(np.abs(ref[ok]).max())
+        assert np.abs(got[ok] - ref[ok]).max() <= 1e-6 * scale, (key, np.abs(got[ok] - ref[ok]).max(), scale)
+
+
+def test_train_likelihood_four_restarts(golden_dir):
+    """a11: Multi-Input_GPR/models/model_trainer.py:26-54 on the C4-shaped fixture (D = 5,
+    Exponential(dims 0-3) × Exponential(dim 4), N = 67): four restarts from σn² ∈ {1e-5, 1e-3,
+    1e-1, 1}, noise trainable, scipy defaults; the returned model is the lowest final loss.
+    Per restart (run as one batch here) the fitted loss matches the oracle's to 1e-5; the best
+    loss too."""
+    from portfoliooptgp_amd.trainer import MultiInputTrainer
+    d = np.load(os.path.join(golden_dir, "multi_input.npz"))
+    X, Y = d["X"], d["Y"]
+
+    def comp():
+        return K.Exponential(active_dims=slice(0, 4)) * K.Exponential(active_dims=slice(4, 5))
+    best = MultiInputTrainer.train_likelihood(X, Y, comp(), verbose=False)
+    assert float(best.training_loss()) == pytest.approx(float(d["tl|best_loss"][0]), rel=1e-5)
+    assert best.likelihood.variance.trainable
+    # the four restarts one by one, as the reference loops
+    ms = []
+    for v in d["tl|starts"]:
+        m = gpx.models.GPR((X, Y), kernel=comp(), noise_variance=float(v))
+        gpx.set_trainable(m.likelihood, True)
+        ms.append(m)
+    logs = gpx.optimizers.Scipy().minimize_batch(ms)
+    for i, r in enumerate(logs):
+        assert r.fun == pytest.approx(float(d[f"tl|{i}|loss_fit"][0]), rel=1e-5), i
+
+
+def _pin_at_theta(i, k, m, x, y):
+    """Evaluation-level pin of fit i at the GPU's own θ*: the oracle's loss and gradient there
+    (gradient against the extended-precision value where the fp64 oracle is itself off)."""
+    th = [p.value for p in k.parameters]
+    if not all(v > 0.0 for v in th):   # a parameter underflowed to 0 on the way: no valid θ to pin
+        return
+    om = _oracle_model(i, th, x, y)
+    cond = _cond(om.kernel, x, 1e-5)
+    lo, go = om.loss_and_grad_u()
+    loss, g = m.loss_and_grad_unconstrained()
+    check_loss(loss, lo, cond)
+    hp = om.loss_and_grad_u_extended()[1]
+    # a parameter at a degenerate extreme (ℓ ~ 1e-300 after a chaotic path) can make the
+    # oracle's ∂K/∂θ 0·inf = NaN where the device's is finite: compare the finite components
+    ok = np.isfinite(go) & np.isfinite(hp)
+    assert np.all(np.isfinite(np.asarray(g)[ok]))
+    if ok.any():
+        check_grad(np.asarray(g)[ok], go[ok], hp[ok], cond)
+
+
+def _sweep_check(x, y, golden_rows, tag, trainer_api=True):
+    """The 8-kernel sweep on (x, y) — through ModelTrainer.train_model, or (trainer_api=False)
+    as one minimize_batch with on_not_pd="inf" so that a chaotic Periodic path that wanders
+    into an invalid region (ℓ underflowing to 0: GPflow's Cholesky would raise there) does not
+    stop the sweep. Per kernel: loss* within 1e-5 of the oracle's fit, or — Periodic kernels
+    only — an evaluation-level pin at the GPU's own θ*."""
+    from portfoliooptgp_amd.trainer import ModelTrainer
+    kernels = ref_kernels()
+    best_mse = None
+    if trainer_api:
+        trainer = ModelTrainer(kernels)
+        best_kernel, best_mse, best_model = trainer.train_model(x, y)
+        assert best_model.kernel is best_kernel
+        results, models = trainer.last_results, trainer.last_models
+    else:
+        models = []
+        for k in kernels:
+            m = gpx.models.GPR(data=(x, y), kernel=k)
+            m.likelihood.variance.assign(1e-5)
+            gpx.set_trainable(m.likelihood.variance, False)
+            models.append(m)
+        results = gpx.optimizers.Scipy().minimize_batch(models, options=dict(maxiter=100), on_not_pd="inf")
+    chaotic = []
+    for i, (k, r, m) in enumerate(zip(kernels, results, models)):
+        ref_loss = golden_rows[i]
+        if abs(r.fun - ref_loss) <= 1e-5 * abs(ref_loss):
+            continue
+        assert i in PERIODIC, (tag, i, r.fun, ref_loss)
+        chaotic.append(i)
+        if np.isfinite(r.fun):
+            _pin_at_theta(i, k, m, x, y)
+    return best_mse, chaotic
+
+
+def test_meta_sweep_n251(golden_dir):
+    """C1's real-data N ≈ 252 variant: META daily, 251 rows, 8-kernel sweep."""
+    d = np.load(os.path.join(golden_dir, "meta_sweep.npz"))
+    x, y = d["x"], d["y"]
+    assert len(x) == 251
+    best_mse, chaotic = _sweep_check(x, y, [float(d[f"{i}|loss_fit"][0]) for i in range(8)], "META")
+    assert best_mse == pytest.approx(float(d[f"{int(d['best_index'][0])}|mse"][0]), rel=1e-2)
+    print("META: chaotic Periodic fits pinned at evaluation level:", chaotic)
+
+
+def test_c1_ticker_sweeps_with_periodic_evaluation_pins(golden_dir):
+    """Config C1: the reference's 8-kernel sweep on the 18 daily ticker series (N = 68). The
+    oracle fits each series here (≈ 2 s on the host); non-Periodic fits agree to 1e-5 and
+    every Periodic fit that does not (ulp-level differences in sin() move
+    their L-BFGS-B paths apart) is pinned at the GPU's own θ*."""
+    d = np.load(os.path.join(golden_dir, "tickers.npz"))
+    names = sorted({k.split("|")[0] for k in d.files})
+    total_chaotic = 0
+    for t in names:
+        x, y = d[f"{t}|x"], d[f"{t}|y"]
+        rows = []
+        for i, k in enumerate(O.reference_kernel_list()):
+            om = O.OGPR(x, y, k, noise_variance=1.0)
+            om.noise.value = 1e-5
+            om.noise.trainable = False
+            rows.append(O.scipy_minimize(om, 100).fun)
+        _, chaotic = _sweep_check(x, y, rows, t, trainer_api=False)
+        total_chaotic += len(chaotic)
+    print(f"C1 tickers: {len(names)} series x 8 kernels, {total_chaotic} Periodic fits pinned at evaluation level")
+
+
+def test_fit_assets_to_portfolio_lists_on_device(golden_dir):
+    """f3 end to end on one GPU: five day-offset series fitted by fit_assets (SE, σn² = 1e-5,
+    maxiter 100, continuous batching), predictions at a 5-day horizon gathered into the lists
+    Portfolio(...) indexes; each asset's list holds its own device predictions, and the per-day
+    μ / Σ follow the reference's formulas (portfolio_day_moments, pinned against the
+    reference Optimizer in tests/test_distributed.py)."""
+    from portfoliooptgp_amd import distributed as D
+    d = np.load(os.path.join(golden_dir, "tickers.npz"))
+    names = sorted({k.split("|")[0] for k in d.files})[:5]
+    series = [(d[f"{t}|x"], d[f"{t}|y"]) for t in names]
+    horizons = [x[-1:] + np.arange(1, 6, dtype=np.float64)[:, None] for x, _ in series]
+    res = D.fit_assets(series, horizons)
+    rets, vols = D.portfolio_inputs(res, order=list(range(5)))
+    for i, (x, y) in enumerate(series):
+        m = gpx.models.GPR((x, y), kernel=K.SquaredExponential())
+        m.likelihood.variance.assign(1e-5)
+        gpx.set_trainable(m.likelihood.variance, False)
+        gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables, options=dict(maxiter=100))
+        mu, var = m.predict_f(horizons[i])
+        assert len(rets[i]) == 5 and all(np.asarray(r).shape == (1,) for r in rets[i])
+        np.testing.assert_allclose(np.concatenate(rets[i]), mu.numpy()[:, 0], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(np.concatenate(vols[i]), var.numpy()[:, 0], rtol=1e-9, atol=1e-15)
+    for day in range(5):
+        mu, sig, sd = D.portfolio_day_moments(rets, vols, day, True)
+        np.testing.assert_allclose(mu, [sum(float(r[0]) for r in rets[i][:day + 1]) for i in range(5)], rtol=1e-12)
+        np.testing.assert_allclose(np.diag(sig), [sum(float(v[0]) for v in vols[i][:day + 1]) for i in range(5)],
+                                   rtol=1e-12)
+        np.testing.assert_allclose(sd, [np.sqrt(float(vols[i][day][0])) for i in range(5)], rtol=1e-15)

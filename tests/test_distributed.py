@@ -218,3 +218,99 @@ def test_fit_assets_checkpoint_discarded_under_another_fit_configuration(tmp_pat
                  fit_config={"maxiter": 50})
     assert calls[-1] == ("a", 3, 2.0) and len(calls) == 4    # other bound arguments: refitted
     assert D.config_fingerprint(fit_a, 1) != D.config_fingerprint(fit_b, 1)
+
+
+def test_band_aware_fit_cost_and_shard():
+    """LPT costs follow the path a fit takes: a C2-like day-offset series of N = 4096 starts on
+    the banded path (p = 1 block at GPflow's ℓ = 1: N·128² work per evaluation), the same N on
+    normalised inputs runs dense (N³)."""
+    x_days = np.arange(4096.0)
+    assert D.band_blocks_estimate(x_days) == 1
+    assert D.band_blocks_estimate(x_days / 4096.0) is None        # dense
+    assert D.band_blocks_estimate(np.arange(300.0)) is None       # < 8 blocks: dense
+    assert D.band_blocks_estimate(np.arange(4096.0), lengthscale=1.72) == 2
+    assert D.series_cost(x_days) == D.fit_cost(4096, 1) == 4096 * 128.0 ** 2
+    assert D.series_cost(x_days / 4096.0) == D.fit_cost(4096) == 4096.0 ** 3
+    # one dense N=2048 fit outweighs eight banded N=4096 ones: it goes alone
+    series = [np.arange(4096.0)] * 8 + [np.arange(2048.0) / 2048.0]
+    sh = D.shard_lpt([D.series_cost(x) for x in series], 2)
+    assert [8] in sh
+
+
+def _portfolio_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = np.load(os.path.join(os.path.dirname(__file__), "golden", "portfolio.npz"))
+        means, varis = g["means"], g["vars"]
+        A, H = means.shape
+        series = [(np.arange(10.0 + i)[:, None], np.zeros((10 + i, 1))) for i in range(A)]
+        horizons = [np.zeros((H, 1))] * A
+
+        def fit(ss, hs):   # stand-in fitter: the golden per-asset predictions as the fit results
+            out = []
+            for x, _ in ss:
+                i = len(x) - 10
+                out.append(dict(loss=0.0, nfev=1, theta=[1.0, 1.0], mean=means[i], var=varis[i]))
+            return out
+        res = D.fit_assets(series, horizons, fit_fn=fit, n_theta=2)
+        rets, vols = D.portfolio_inputs(res, order=list(range(A)))
+        out = {}
+        for tag, log_ret in (("log", True), ("cml", False)):
+            mus, sig, sd = zip(*[D.portfolio_day_moments(rets, vols, day, log_ret) for day in range(H)])
+            out[tag] = (np.stack(mus).tolist(), np.stack(sig).tolist(), np.stack(sd).tolist())
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_portfolio_format_against_reference_optimizer_golden():
+    """f3: per-asset predictions gathered over 2 gloo ranks, rebuilt into the lists
+    Portfolio(...) indexes (Multi-Input_GPR/Portfolio/portfolio.py:111-124), give per day the
+    same μ / Σ / σ the REFERENCE's Optimizer computes from those lists
+    (Multi-Input_GPR/optimization/optimizer.py:20-56; tests/golden/portfolio.npz, made by
+    tests/golden/make_ref_golden.py importing the reference module)."""
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "portfolio.npz"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_portfolio_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out in outs:
+        for tag in ("log", "cml"):
+            mu, sig, sd = (np.asarray(a) for a in out[tag])
+            np.testing.assert_array_equal(mu, g[f"{tag}|mu"])
+            np.testing.assert_array_equal(sig, g[f"{tag}|Sigma"])
+            np.testing.assert_array_equal(sd, g[f"{tag}|std"])
+
+
+def _fingerprint_worker(q):
+    import portfoliooptgp_amd as gpx
+    from portfoliooptgp_amd.kernels import compile_spec
+    spec = compile_spec(gpx.kernels.Exponential(active_dims=slice(0, 4)) * gpx.kernels.Exponential(active_dims=slice(4, 5)), 5)
+    q.put(D.config_fingerprint(_stand_in_fit, {"spec": spec, "maxiter": 100, "x": np.arange(3.0)}))
+
+
+def test_config_fingerprint_is_stable_across_processes():
+    """a compiled kernel spec (ctypes structure) in fit_config hashes by its bytes,
+    so two processes with the same configuration agree (and a checkpoint is reused); a value
+    whose repr is a memory address is refused instead of silently changing every run."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fingerprint_worker, args=(q,)) for _ in range(2)]
+    for p in procs:
+        p.start()
+    fps = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert fps[0] == fps[1]
+
+    class Opaque:
+        pass
+    with pytest.raises(ValueError, match="stable representation"):
+        D.config_fingerprint(_stand_in_fit, {"k": Opaque()})

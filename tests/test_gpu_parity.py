@@ -9,10 +9,10 @@ posterior mean/variance and log-ML"):
                 oracle.loss_and_grad_u_extended). The gradient ½Σ(ααᵀ − K⁻¹)∘∂K is a
                 cancellation whose fp64 error grows with κ = cond(K + σn²I) in ANY algorithm;
                 on the 12 of 336 fixture gradients (κ >= 2.5e5: Periodic / Linear on day
-                offsets) where the oracle is more than 1e-7 from that value, the GPU must be
-                within max(1e-6 · max|g|, 10 × the oracle's own error) of it (the 40-digit
-                mpmath check of the worst one, test_gradient_accuracy_vs_exact: oracle 7.4e-5
-                from exact, GPU 2.4e-4).
+                offsets) where the oracle is more than 1e-7 from that value, the GPU is held
+                to that value with the κ-scaled bar (1e-7 + 3e-11 κ)(1 + max|g|) (the 40-digit
+                mpmath check of the worst Periodic one, test_gradient_accuracy_vs_exact: oracle
+                7.4e-5 from exact, GPU 2.4e-4).
   mean          |Δ| <= 1e-6 · max|ref| + 1e-14 · κ · max(1, max|y|)   (bar: 1e-5 rel)
   variance      |Δ| <= 1e-5 · |ref| + 1e-10 · σ²_max    (SURVEY: cancellation-aware)
   fitted loss   |Δ| <= 1e-5 · |ref|
@@ -65,17 +65,21 @@ def check_loss(got, ref, cond=1.0):
     assert abs(got - ref) <= (1e-9 + 1e-14 * float(cond)) * max(1.0, abs(ref)), (got, ref, cond)
 
 
-def check_grad(got, ref, hp=None):
-    """SURVEY's 1e-6 relative gradient bar against the oracle; where the fp64 oracle is more
-    than 1e-7 from the extended-precision value hp, against hp within 10x the oracle's error."""
+def check_grad(got, ref, hp=None, cond=1.0):
+    """SURVEY's 1e-6 relative gradient bar against the oracle. Where the fp64 oracle is itself
+    more than 1e-7 from the extended-precision value hp (the 12 of 336 fixture gradients with
+    κ >= 2.5e5), against hp with the κ-scaled bar (1e-7 + 3e-11 κ)(1 + max|g|): there the
+    gradient's cancellation leaves κ·eps-sized errors in ANY fp64 algorithm, the oracle's
+    LAPACK included."""
     got, ref = np.asarray(got, dtype=np.float64), np.asarray(ref, dtype=np.float64)
     scale = max(float(np.abs(ref).max()), 1e-300)
     if hp is not None:
         hp = np.asarray(hp, dtype=np.float64)
         err_oracle = float(np.abs(ref - hp).max())
         if err_oracle > 1e-7 * float(np.abs(hp).max()):
-            tol = max(1e-6 * float(np.abs(hp).max()), 10.0 * err_oracle)
-            assert float(np.abs(got - hp).max()) <= tol, (got, ref, hp)
+            tol = max(1e-6 * float(np.abs(hp).max()),
+                      (1e-7 + 3e-11 * float(cond)) * (1.0 + float(np.abs(hp).max())))
+            assert float(np.abs(got - hp).max()) <= tol, (got, ref, hp, cond)
             return
     assert float(np.abs(got - ref).max()) <= 1e-6 * scale, (got, ref, np.abs(got - ref).max() / scale)
 
@@ -112,10 +116,10 @@ def test_golden_single_models(golden):
         cond = d[key + "|cond"][0]
         loss, g = m.loss_and_grad_unconstrained()
         check_loss(loss, float(d[key + "|loss"][0]), cond)
-        check_grad(g, d[key + "|grad_u"], d[key + "|grad_u_hp"])
+        check_grad(g, d[key + "|grad_u"], d[key + "|grad_u_hp"], cond)
         gpx.set_trainable(m.likelihood.variance, False)
         _, g2 = m.loss_and_grad_unconstrained()
-        check_grad(g2, d[key + "|grad_u_fixed_noise"], d[key + "|grad_u_fixed_noise_hp"])
+        check_grad(g2, d[key + "|grad_u_fixed_noise"], d[key + "|grad_u_fixed_noise_hp"], cond)
         xnew = d[key + "|xnew"]
         mu, var = m.predict_f(xnew)
         _, vy = m.predict_y(xnew)
@@ -137,7 +141,7 @@ def test_golden_ragged_batch(golden):
     for b, (m, key) in enumerate(zip(models, idx)):
         loss, g = m.loss_and_grad_unconstrained(lml=lml[b], grad_theta=grad[b])
         check_loss(loss, float(d[key + "|loss"][0]), d[key + "|cond"][0])
-        check_grad(g, d[key + "|grad_u"], d[key + "|grad_u_hp"])
+        check_grad(g, d[key + "|grad_u"], d[key + "|grad_u_hp"], d[key + "|cond"][0])
     for b, m in enumerate(models):
         m._attach(eng, b)
     outs = predict_f_batch(models, [d[k + "|xnew"] for k in idx])
@@ -353,6 +357,27 @@ def test_large_n_against_oracle():
     assert np.all(np.abs(var.numpy() - vo) <= 1e-5 * np.abs(vo) + 1e-9)
 
 
+def _check_fd(m, g, rel=1e-5):
+    """Richardson-extrapolated central differences of the model's GPU loss against g."""
+    u0 = np.array([v.numpy() for v in m.trainable_variables], dtype=float)
+
+    def loss_at(u):
+        for v, ui in zip(m.trainable_variables, u):
+            v.assign(ui)
+        return float(m.training_loss())
+
+    for i in range(len(u0)):
+        d = {}
+        for h in (2e-3, 1e-3):
+            up, dn = u0.copy(), u0.copy()
+            up[i] += h
+            dn[i] -= h
+            d[h] = (loss_at(up) - loss_at(dn)) / (2 * h)
+        fd = (4.0 * d[1e-3] - d[2e-3]) / 3.0
+        assert fd == pytest.approx(g[i], rel=rel, abs=1e-4), (i, fd, g[i], d)
+    loss_at(u0)
+
+
 def test_full_size_properties_n4096():
     """BASELINE config C2 size: size-independent properties of the GPU path alone."""
     n = 4096
@@ -368,24 +393,17 @@ def test_full_size_properties_n4096():
     mp = gpx.models.GPR((x[perm], y[perm]), kernel=K.SquaredExponential(lengthscales=theta[0], variance=theta[1]))
     mp.likelihood.variance.assign(noise)
     assert float(mp.log_marginal_likelihood()) == pytest.approx(lml, rel=1e-9)
-    # (2) gradient = central finite difference of the GPU logML itself
+    # (2) gradient = finite differences of the GPU logML itself (Richardson-extrapolated central
+    # differences at h = 2e-3 / 1e-3: GPflow's expanded r² makes the computed loss a slightly
+    # rough function of ℓ, ~1e-8 absolute here, which a step of 1e-4 would amplify to 1e-4)
     loss, g = m.loss_and_grad_unconstrained()
-    u0 = np.array([v.numpy() for v in m.trainable_variables], dtype=float)
-    h = 1e-4
-    for i in range(2):
-        for s, store in ((1, "p"), (-1, "m")):
-            u = u0.copy()
-            u[i] += s * h
-            for v, ui in zip(m.trainable_variables, u):
-                v.assign(ui)
-            if store == "p":
-                lp = float(m.training_loss())
-            else:
-                lm = float(m.training_loss())
-        fd = (lp - lm) / (2 * h)
-        assert fd == pytest.approx(g[i], rel=1e-5, abs=1e-4)
-    for v, ui in zip(m.trainable_variables, u0):
-        v.assign(ui)
+    _check_fd(m, g)
+    # (2b) and against the oracle's analytic gradient at the full size (one host evaluation)
+    om2 = O.OGPR(x, y, O.OSquaredExponential(lengthscales=theta[0], variance=theta[1]), noise_variance=noise)
+    om2.noise.trainable = False
+    lo2, go2 = om2.loss_and_grad_u()
+    check_loss(loss, lo2)
+    check_grad(g, go2)
     # (3) predict_y = predict_f + σn², and far from the data the prior is recovered
     xs = np.concatenate([x[:50], [[1e6]]])
     mu, var = m.predict_f(xs)
@@ -563,19 +581,7 @@ def test_n8192_logml_and_gradient_properties():
     loss, g = m.loss_and_grad_unconstrained()
     om = O.OGPR(x, y, O.OSquaredExponential(lengthscales=50.0, variance=1.1), noise_variance=1e-2)
     assert -loss == pytest.approx(om.log_marginal_likelihood(), rel=1e-10)
-    u0 = np.array([v.numpy() for v in m.trainable_variables], dtype=float)
-    h = 1e-4
-    for i in range(2):
-        vals = []
-        for sgn in (1, -1):
-            u = u0.copy()
-            u[i] += sgn * h
-            for v, ui in zip(m.trainable_variables, u):
-                v.assign(ui)
-            vals.append(float(m.training_loss()))
-        assert (vals[0] - vals[1]) / (2 * h) == pytest.approx(g[i], rel=1e-5, abs=1e-4)
-    for v, ui in zip(m.trainable_variables, u0):
-        v.assign(ui)
+    _check_fd(m, g)
     mu, var = m.predict_f(x)
     mg, vg = m.predict_f(np.concatenate([x, x[:1]]))
     np.testing.assert_allclose(mu.numpy(), mg.numpy()[:-1], rtol=1e-7, atol=1e-9)

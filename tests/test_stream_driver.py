@@ -358,3 +358,46 @@ def test_groups_on_one_engine_with_submit(engines):
     for r, r0 in zip(res, ref):
         assert r.nfev == r0.nfev
         np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+
+
+class CachedPredictEngine(FakeEngine):
+    """FakeEngine with a rough (noisy) objective, so that L-BFGS-B's line search sometimes backs
+    off and returns a point other than the last one evaluated, and a predict at the training
+    inputs that, like the band-storage engine's, is only served from the factor of the row's
+    LAST evaluated θ (it records any other request)."""
+
+    def __init__(self, B):
+        super().__init__(B)
+        self.last_theta = {}
+        self.uncached = 0
+
+    def lml_grad(self, rows, theta):
+        lml, grad, info = super().lml_grad(rows, theta)
+        for r in rows:
+            lml[r] += 1e-7 * np.sin(1e9 * theta[r, 0])     # rounding-level roughness
+            self.last_theta[r] = theta[r].copy()
+        return lml, grad, info
+
+    def _predict_train(self, rows, theta, add_noise, column=False):
+        for r in rows:
+            if not np.array_equal(theta[r], self.last_theta.get(r)):
+                self.uncached += 1
+        mu = [torch.full((10, 1), float(theta[r, 0]), dtype=torch.float64) for r in rows]
+        var = [torch.full((10, 1), float(theta[r, 1]), dtype=torch.float64) for r in rows]
+        return mu, var, None
+
+
+def test_predict_after_backed_off_line_search_uses_a_fresh_evaluation():
+    """A fit whose result is not its last evaluated point gets one more (batched) evaluation at
+    the result's x before its predict, so the predict at the training inputs always finds the
+    factor of its θ; the results (x, nfev) are scipy's, untouched."""
+    ms = _models(12)
+    for m in ms:
+        m.kernel.lengthscales.assign(3.0)
+    eng = CachedPredictEngine(4)
+    res, preds = gpx.optimizers.Scipy().minimize_stream(ms, width=4, engine=eng, predict_train=True)
+    assert eng.uncached == 0
+    assert sum(eng.calls) > sum(r.nfev for r in res)      # some fits were evaluated once more
+    for r, m, p in zip(res, ms, preds):
+        assert float(p[0][0, 0]) == m.kernel.lengthscales.value
+        assert m.kernel.lengthscales.unconstrained == r.x[0]
