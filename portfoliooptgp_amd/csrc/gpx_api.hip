@@ -599,7 +599,7 @@ int check_active_theta(gpx_batch* bt, int n_active, const int32_t* active, const
 }
 
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
-                  hipStream_t s) {
+                  hipStream_t s, bool predict_block) {
   gpx_ctx* ctx = bt->ctx;
   {
     const int e = check_active_theta(bt, n_active, active, theta);
@@ -609,18 +609,21 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
     const int e = flush_rebinds(bt, s);
     if (e != GPX_OK) return e;
   }
-  {
+  char* hio = bt->h_io;
+  if (predict_block) {  // (the last asynchronous predict's upload out of it has completed)
     const int e = wait_io(bt);
     if (e != GPX_OK) return e;
+    if (!bt->h_io_pred) HIPX(ctx, hipHostMalloc(&bt->h_io_pred, bt->io_bytes, hipHostMallocNonCoherent));
+    hio = bt->h_io_pred;
   }
   // one DMA from the pinned block (allocated non-coherent: the host reads and writes it as
   // ordinary cached memory, the DMAs at the call boundaries see it whole):
   // [active | info = 0 | bandp | theta] (every call ends with a stream synchronize, so the previous call's transfers out of h_io have completed; bandp is
   // written into h_bandp by gpx_batch_lml_grad before this)
-  std::memcpy(bt->h_io, active, sizeof(int) * n_active);
-  std::memset(bt->h_io + bt->io_info_off, 0, sizeof(int) * bt->B);
-  std::memcpy(bt->h_io + bt->io_theta_off, theta, sizeof(double) * GPX_THETA_STRIDE * bt->B);
-  HIPX(ctx, hipMemcpyAsync(bt->d_io, bt->h_io, bt->io_res_off, hipMemcpyHostToDevice, s));
+  std::memcpy(hio, active, sizeof(int) * n_active);
+  std::memset(hio + bt->io_info_off, 0, sizeof(int) * bt->B);
+  std::memcpy(hio + bt->io_theta_off, theta, sizeof(double) * GPX_THETA_STRIDE * bt->B);
+  HIPX(ctx, hipMemcpyAsync(bt->d_io, hio, bt->io_res_off, hipMemcpyHostToDevice, s));
   return GPX_OK;
 }
 
@@ -834,6 +837,7 @@ int gpx_batch_destroy(gpx_batch* bt) {
                   (void*)bt->bres})
     if (p) (void)hipFree(p);
   if (bt->h_io) (void)hipHostFree(bt->h_io);
+  if (bt->h_io_pred) (void)hipHostFree(bt->h_io_pred);
   if (bt->h_stage) (void)hipHostFree(bt->h_stage);
   if (bt->h_rdesc) (void)hipHostFree(bt->h_rdesc);
   if (bt->h_box) (void)hipHostFree(bt->h_box);
@@ -1121,10 +1125,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (e != GPX_OK) return e;
   }
   HIPX(ctx, hipSetDevice(ctx->device));
-  {  // routing writes h_bandp inside h_io
-    const int e = wait_io(bt);
-    if (e != GPX_OK) return e;
-  }
+
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   {  // slots rebound since the last call land first: their band tables (from the gather's
      // X boxes) decide the routing below
@@ -1556,7 +1557,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
     active = keep.data();
     n_active = (int)keep.size();
   }
-  int rc = upload_common(bt, n_active, active, theta, s);
+  int rc = upload_common(bt, n_active, active, theta, s, true);
   if (rc != GPX_OK) return rc;
   // re-factorise the problems whose cached factor is not at exactly this theta. A cached
   // block-banded factorisation (gpx_band.hip) serves predict at the training inputs (it holds

@@ -437,6 +437,146 @@ __device__ __forceinline__ void frag_store_diag(const Frag& f, double* __restric
       }
 }
 
+// ---- 16x16-tile primitives of the p <= 1 sweeps (band_fwd1_kernel / band_bwd1_kernel) ----
+// A tile's C fragment (v_mfma_f64_16x16x4_f64): lane holds rows l4 + 4r (r = 0..3), column l15.
+__device__ __forceinline__ void tile_zero(bd4& c) { c = (bd4){0.0, 0.0, 0.0, 0.0}; }
+__device__ __forceinline__ void tile_store_lds(const bd4& c, double* __restrict__ s, int i0, int j0) {
+  const int lane = tid_fresh() & 63;
+  double* p = s + (i0 + (lane >> 4)) * BS + j0 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[4 * r * BS] = c[r];
+}
+// the tile's transpose at (j0, i0)
+__device__ __forceinline__ void tile_store_lds_t(const bd4& c, double* __restrict__ s, int i0, int j0) {
+  const int lane = tid_fresh() & 63;
+  double* p = s + (j0 + (lane & 15)) * BS + i0 + (lane >> 4);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[4 * r] = c[r];
+}
+__device__ __forceinline__ void tile_load_lds(bd4& c, const double* __restrict__ s, int i0, int j0) {
+  const int lane = tid_fresh() & 63;
+  const double* p = s + (i0 + (lane >> 4)) * BS + j0 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[r] = p[4 * r * BS];
+}
+__device__ __forceinline__ void tile_load_global(bd4& c, const double* __restrict__ g, long long ld, int i0, int j0) {
+  const int lane = tid_fresh() & 63;
+  const double* p = g + (long long)(i0 + (lane >> 4)) * ld + j0 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[r] = p[4 * r * ld];
+}
+__device__ __forceinline__ void tile_store_global(const bd4& c, double* __restrict__ g, long long ld, int i0, int j0) {
+  const int lane = tid_fresh() & 63;
+  double* p = g + (long long)(i0 + (lane >> 4)) * ld + j0 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[4 * r * ld] = c[r];
+}
+
+// Tile row ib (tiles (ib, jb), jb = 0..3) of ±opA · opB over the 64 k, skipping the k-blocks a
+// triangular operand makes exactly zero: MODE 0 every k-block; MODE 1 k-blocks kb <= jb
+// (opB = Wᵀ, W lower triangular: P = A Wᵀ); MODE 2 kb >= jb (opB = W lower: G = P W). One wave;
+// the A fragment of each k-step is shared by the row's tiles. TA: opA(i,k) = A[k][i];
+// TB: opB(k,j) = B[j][k].
+template <bool TA, bool TB, int MODE>
+__device__ __forceinline__ void row_mma(bd4 (&c)[4], const double* __restrict__ sA, const double* __restrict__ sB,
+                                        int i0, bool neg) {
+  const int lane = tid_fresh() & 63, l15 = lane & 15, l4 = lane >> 4;
+  const double sg = neg ? -1.0 : 1.0;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = kb * 16 + q * 4 + l4;
+      const double av = sg * (TA ? sA[k * BS + i0 + l15] : sA[(i0 + l15) * BS + k]);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        if (MODE == 1 && kb > jb) continue;
+        if (MODE == 2 && kb < jb) continue;
+        const double bv = TB ? sB[(jb * 16 + l15) * BS + k] : sB[k * BS + jb * 16 + l15];
+        c[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c[jb], 0, 0, 0);
+      }
+    }
+}
+
+// The 10 lower 16x16 tiles of a symmetric 64x64 product over the 4 waves, up to 3 per wave
+// (slot s of wave w: (ib, jb), ib >= jb), balanced for the backward sweep's Z_kk = WᵀW − GᵀZ1
+// (WᵀW's tile (ib, jb) has 4 − ib nonzero k-blocks, W lower triangular): every wave 20 k-steps of
+// WᵀW, 32 or 48 of GᵀZ1 (a 2x2-quadrant split: 64 and 64).
+//   w0: (0,0) (3,0) | w1: (1,0) (2,0) | w2: (1,1) (3,1) (3,2) | w3: (2,1) (2,2) (3,3)
+__device__ __forceinline__ bool sym_tile(int w, int s, int& ib, int& jb) {
+  const unsigned long long T = 0x7a92e6960824180ull;  // 5 bits per (w, s): ib * 4 + jb, 16 = none
+  const int v = (int)((T >> (5 * (w * 3 + s))) & 31ull);
+  ib = v >> 2;
+  jb = v & 3;
+  return v < 16;
+}
+
+// c[s] += ±opA · opB on this wave's symmetric tiles; TRI: k-blocks from max(ib, jb) only
+// (opA = Wᵀ, opB = W with W lower triangular: WᵀW)
+template <bool TA, bool TB, bool TRI>
+__device__ __forceinline__ void sym_mma(bd4 (&c)[3], const double* __restrict__ sA, const double* __restrict__ sB,
+                                        int w, bool neg) {
+  const int lane = tid_fresh() & 63, l15 = lane & 15, l4 = lane >> 4;
+  const double sg = neg ? -1.0 : 1.0;
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    int ib, jb;
+    if (!sym_tile(w, s, ib, jb)) continue;
+    const int i0 = ib * 16, j0 = jb * 16, kb0 = TRI ? ib : 0;   // (ib >= jb: max(ib, jb) = ib)
+#pragma unroll 1
+    for (int kb = kb0; kb < 4; ++kb) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = kb * 16 + q * 4 + l4;
+        const double av = sg * (TA ? sA[k * BS + i0 + l15] : sA[(i0 + l15) * BS + k]);
+        const double bv = TB ? sB[(j0 + l15) * BS + k] : sB[k * BS + j0 + l15];
+        c[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c[s], 0, 0, 0);
+      }
+    }
+  }
+}
+__device__ __forceinline__ void sym_zero(bd4 (&c)[3]) {
+#pragma unroll
+  for (int s = 0; s < 3; ++s) tile_zero(c[s]);
+}
+__device__ __forceinline__ void sym_load_global(bd4 (&c)[3], const double* __restrict__ g, long long ld, int w) {
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    int ib, jb;
+    if (sym_tile(w, s, ib, jb)) tile_load_global(c[s], g, ld, ib * 16, jb * 16);
+  }
+}
+// lower tiles only (the leaf reads the lower triangle of its input)
+__device__ __forceinline__ void sym_store_lds(const bd4 (&c)[3], double* __restrict__ s, int w) {
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    int ib, jb;
+    if (sym_tile(w, t, ib, jb)) tile_store_lds(c[t], s, ib * 16, jb * 16);
+  }
+}
+// lower tiles and their mirror images: the full symmetric matrix
+__device__ __forceinline__ void sym_store_lds_full(const bd4 (&c)[3], double* __restrict__ s, int w) {
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    int ib, jb;
+    if (!sym_tile(w, t, ib, jb)) continue;
+    tile_store_lds(c[t], s, ib * 16, jb * 16);
+    if (ib != jb) tile_store_lds_t(c[t], s, ib * 16, jb * 16);
+  }
+}
+// the diagonal of the matrix (its diagonal tiles') -> g[i * ld + i]
+__device__ __forceinline__ void sym_store_diag(const bd4 (&c)[3], double* __restrict__ g, long long ld, int w) {
+  const int lane = tid_fresh() & 63, l15 = lane & 15, l4 = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    int ib, jb;
+    if (!sym_tile(w, t, ib, jb) || ib != jb) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (l4 + 4 * r == l15) g[(long long)(ib * 16 + l15) * ld + ib * 16 + l15] = c[t][r];
+  }
+}
+
 // X rows of one 64-row block -> LDS in two parts: xrows_fetch loads the first 256 elements
 // (all of it for D <= 4) into a register a phase ahead, from a clamped (always valid) address
 // and without a branch, so the load stays in flight; xrows_store writes it and loads any rest
@@ -950,9 +1090,13 @@ void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipS
 // =======================================================================================
 namespace gpx {
 
-// The trailing-updated diagonal block A_{k+1,k+1} stays in the SYRK's fragment and is the next
-// leaf's input (no global round trip); the original blocks A_{k+1,k} and A_{k+1,k+1} are
-// fetched during the leaf's inverse phase (its diagonal chain needs every register it can get).
+// The trailing-updated diagonal block A_{k+1,k+1} stays in registers (each wave its lower 16x16
+// tiles, sym_tile) and is the next leaf's input (no global round trip); the original blocks
+// A_{k+1,k} and A_{k+1,k+1} are fetched during the leaf's inverse phase. The products skip what
+// is exactly zero or redundant: the panel P = A_{k+1,k}W_kkᵀ only the k-blocks below W's
+// diagonal (tile row per wave, 40 of 64 k-steps), the update A_{k+1,k+1} −= PPᵀ only its 10 lower
+// tiles (at most 48 k-steps per wave). Sums are unchanged: the skipped terms are exact zeros
+// (W's upper triangle) or the upper tiles the leaf never reads.
 __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
   __shared__ __attribute__((aligned(16))) double sA[64 * BS];   // A_kk -> (leaf) -> A_{k+1,k} -> P
   __shared__ __attribute__((aligned(16))) double sW[64 * BS];   // W_kk
@@ -973,14 +1117,14 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
   if (tid < 64) sv[1][tid] = 0.0;
   if (tid == 0) sfail = -1;
   int gfail = 0;
-  Frag cur, nxt;
+  bd4 cur[3], nxt[3];
   double pa[16];
-  frag_load_global(cur, K, ld);  // A_00
+  sym_load_global(cur, K, ld, part);  // A_00 (this wave's lower tiles)
   PH_BEGIN
   for (int k = 0; k < nb; ++k) {
     const int q = min(p, nb - 1 - k), k64 = k * 64;
     const double yk = (tid < 64 && k64 + tid < n) ? y[k64 + tid] : 0.0;
-    frag_store_lds(cur, sA);
+    sym_store_lds(cur, sA, part);
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int e = tid + 256 * u;
@@ -992,7 +1136,7 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
     // this step's panel block and the next diagonal block, in flight during the leaf's inverse
     leaf64_lds<false>(sA, sW, ldiag + k64, &sfail, [&]() {
       if (q >= 1) block_fetch(pa, K + (long long)(k64 + 64) * ld + k64, ld);
-      if (k + 1 < nb) frag_load_global(nxt, K + (long long)(k64 + 64) * ld + k64 + 64, ld);
+      if (k + 1 < nb) sym_load_global(nxt, K + (long long)(k64 + 64) * ld + k64 + 64, ld, part);
     }, (int)(blockIdx.x & 3));
     PH(1);
     if (tid == 0 && sfail >= 0) {
@@ -1021,13 +1165,17 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
     }
     PH(2);
     if (q >= 1) {
-      Frag f;
-      frag_zero(f);
-      frag_mma<false, true, 16>(f, sA, sW, false);      // P = A_{k+1,k} W_kkᵀ
+      bd4 prow[4];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) tile_zero(prow[jb]);
+      row_mma<false, true, 1>(prow, sA, sW, part * 16, false);   // P = A_{k+1,k} W_kkᵀ (tile row)
       __syncthreads();
       PH(3);
-      frag_store_lds(f, sA);
-      frag_store_global(f, L + (long long)(k64 + 64) * ld + k64, ld);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        tile_store_lds(prow[jb], sA, part * 16, jb * 16);
+        tile_store_global(prow[jb], L + (long long)(k64 + 64) * ld + k64, ld, part * 16, jb * 16);
+      }
       __syncthreads();
       PH(4);
       {  // u_{k+1} = −P z_k
@@ -1035,14 +1183,15 @@ __global__ __launch_bounds__(256, 2) void band_fwd1_kernel(BandFusedArgs a) {
         for (int c = part; c < 64; c += 4) s1 = fma(sA[lane * BS + c], sv[0][c], s1);
         spart[part][lane] = s1;
       }
-      frag_mma<false, true, 16>(nxt, sA, sA, true);     // A_{k+1,k+1} −= P Pᵀ (the next leaf's input)
+      sym_mma<false, true, false>(nxt, sA, sA, part, true);    // A_{k+1,k+1} −= P Pᵀ (lower tiles)
       __syncthreads();
       if (tid < 64) sv[1][tid] = -((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid]));
       PH(5);
     } else if (tid < 64) {
       sv[1][tid] = 0.0;
     }
-    cur = nxt;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) cur[t] = nxt[t];
     __syncthreads();
     PH(6);
   }
@@ -1101,8 +1250,9 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
   for (int t = 0; t < NT; ++t) cx.sums[t][0] = cx.sums[t][1] = cx.sums[t][2] = 0.0;
   cx.snoise = 0.0;
   double resmax = 0.0;
-  Frag zprev;  // Z_{k+1,k+1}
-  frag_zero(zprev);
+  bd4 zrow[4];  // this wave's tile row of Z_{k+1,k+1}
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) tile_zero(zrow[jb]);
   PH_BEGIN
   for (int k = nb - 1; k >= 0; --k) {
     const int q = min(p, nb - 1 - k), k64 = k * 64, cs = k & 1, ns = cs ^ 1;
@@ -1140,31 +1290,41 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
       }
     };
     PH(0);
-    // Z_kk = W_kkᵀW_kk − Gᵀ Z_{k+1,k}, Z_{k+1,k} = −Z_{k+1,k+1} G, G = P W_kk
-    Frag zk, g, z1;
-    frag_zero(zk);
-    frag_mma<true, false, 16>(zk, sW, sW, false);
+    // Z_kk = W_kkᵀW_kk − Gᵀ Z_{k+1,k}, Z_{k+1,k} = −Z_{k+1,k+1} G, G = P W_kk, by 16x16 tiles:
+    // G and Z_{k+1,k} a tile row per wave (G only the k-blocks below W's diagonal), Z_kk (symmetric)
+    // only its 10 lower tiles (WᵀW only the k-blocks below W's diagonal), mirrored into LDS
+    bd4 zk[3];
+    sym_zero(zk);
+    sym_mma<true, false, true>(zk, sW, sW, part, false);         // WᵀW
     if (q >= 1) {
-      frag_zero(g);
-      frag_mma<false, false, 16>(g, sA, sW, false);
+      bd4 g[4];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) tile_zero(g[jb]);
+      row_mma<false, false, 2>(g, sA, sW, part * 16, false);     // G = P W (tile row)
       __syncthreads();
       alpha_out();
-      frag_store_lds(g, sA);
-      frag_store_lds(zprev, sW);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        tile_store_lds(g[jb], sA, part * 16, jb * 16);
+        tile_store_lds(zrow[jb], sW, part * 16, jb * 16);        // Z_{k+1,k+1}
+      }
       __syncthreads();
       PH(1);
-      frag_zero(z1);
-      frag_mma<false, false, 16>(z1, sW, sA, true);
+      bd4 z1[4];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) tile_zero(z1[jb]);
+      row_mma<false, false, 0>(z1, sW, sA, part * 16, true);     // Z_{k+1,k} = −Z_{k+1,k+1} G
       __syncthreads();
-      frag_store_lds(z1, sW);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) tile_store_lds(z1[jb], sW, part * 16, jb * 16);
       __syncthreads();
-      frag_mma<true, false, 16>(zk, sA, sW, true);
+      sym_mma<true, false, false>(zk, sA, sW, part, true);       // − Gᵀ Z_{k+1,k}
     }
     __syncthreads();                     // every wave is done reading G (sA)
     if (q == 0) alpha_out();
     PH(2);
-    frag_store_lds(zk, sA);
-    frag_store_diag(zk, K + (long long)k64 * ld + k64, ld);
+    sym_store_lds_full(zk, sA, part);
+    sym_store_diag(zk, K + (long long)k64 * ld + k64, ld, part);
     // the next step's inputs, in flight during the contraction
     if (k > 0) {
       const int k1 = k64 - 64;
@@ -1190,7 +1350,8 @@ __global__ __launch_bounds__(256, 2) void band_bwd1_kernel(BandFusedArgs a) {
       const double rs = block_rowsum(sW);
       if ((tid & 3) == 0) sres[ns][tid >> 2] += rs;
     }
-    frag_load_lds(zprev, sA);            // Z_kk, the next step's Z_{k+1,k+1} (not held through the contraction)
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) tile_load_lds(zrow[jb], sA, part * 16, jb * 16);  // the next Z_{k+1,k+1}
     __syncthreads();
     // block k + p has all its band contributions now; slot ns is block k − 1's next
     if (tid < 64) {

@@ -99,6 +99,9 @@ struct gpx_batch {
   // blocks waits on this event first (wait_io)
   hipEvent_t io_ev = nullptr;
   bool io_pending = false;
+  // predict calls upload [active | info | bandp | theta] from their own pinned block, so an
+  // asynchronous predict's upload never holds up the next evaluation's (which writes h_io)
+  char* h_io_pred = nullptr;
   std::vector<RebindWait> rebind_waits;
   gpx::RebindDesc* h_rdesc = nullptr;   // pinned (coherent), one per slot
   double* d_box = nullptr;               // [B][nb][D][2] per-block lo/hi of X
@@ -212,7 +215,7 @@ double band_fused_flops(int Np, int p, bool fwd);  // block-product flops of one
 void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W = L⁻¹)
 void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z
 int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
-                  hipStream_t s);
+                  hipStream_t s, bool predict_block = false);
 int flush_rebinds(gpx_batch* bt, hipStream_t s);  // pending rebinds -> device (one gather on s)
 int wait_io(gpx_batch* bt);                        // the last asynchronous call's uploads have left h_io
 int ensure_rebind_meta(gpx_batch* bt);             // pinned n/spec mirrors + dirty flags
