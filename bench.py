@@ -332,6 +332,8 @@ def helper_main(w, P, argv, rank, gpu, start, q):
     torch.cuda.synchronize()
     busy = time.perf_counter() - t0
     q.put(("done", (w, nfev, summary, wk.timing(), wk.driver_stats[-1] if wk.driver_stats else None, busy)))
+    if os.environ.get("GPX_SUBMIT_STATS"):
+        wk.engines.clear()  # destroyed now: the library prints the per-batch submit phases
 
 
 def collect(q, helpers, kind, timeout):
@@ -525,6 +527,8 @@ def main():
     elapsed = time.perf_counter() - t0
     for h in helpers:
         h.join(timeout=120)
+    if os.environ.get("GPX_SUBMIT_STATS"):
+        wk.engines.clear()  # destroyed now: the library prints the per-batch submit phases
 
     tm = {f: sum(p[3][f] for p in parts) for f in SUM_FIELDS + NARROW_FIELDS}
     nfev_all = [n for p in parts for n in p[1]]

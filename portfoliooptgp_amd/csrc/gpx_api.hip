@@ -18,6 +18,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <string>
+#include <chrono>
 #include <vector>
 #include "gpx_host.h"
 
@@ -500,6 +501,32 @@ void keep_slot_box(gpx_batch* bt, int b, const double* box) {
   bt->slot_box_ok[b] = 1;
 }
 
+// GPX_SUBMIT_STATS: wall-clock phase accumulators of the submit/complete calls (host profiling)
+static bool submit_stats_on() {
+  static const bool on = [] {
+    const char* e = getenv("GPX_SUBMIT_STATS");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+struct SubClock {
+  gpx_batch* bt;
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  explicit SubClock(gpx_batch* b) : bt(b), on(submit_stats_on()) {
+    if (on) t = std::chrono::steady_clock::now();
+  }
+  void skip() {
+    if (on) t = std::chrono::steady_clock::now();
+  }
+  void lap(int i) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    bt->sub_s[i] += std::chrono::duration<double>(n - t).count();
+    t = n;
+  }
+};
+
 int wait_io(gpx_batch* bt) {
   if (!bt->io_pending) return GPX_OK;
   gpx_ctx* ctx = bt->ctx;
@@ -511,10 +538,12 @@ int wait_io(gpx_batch* bt) {
 int flush_rebinds(gpx_batch* bt, hipStream_t s) {
   if (bt->n_dirty == 0 && bt->pend.empty()) return GPX_OK;
   gpx_ctx* ctx = bt->ctx;
+  SubClock fc(bt);
   {
     const int e = wait_io(bt);
     if (e != GPX_OK) return e;
   }
+  fc.lap(6);
   {
     const int rc = ensure_rebind_meta(bt);
     if (rc != GPX_OK) return rc;
@@ -560,7 +589,10 @@ int flush_rebinds(gpx_batch* bt, hipStream_t s) {
   if (nbox > 0) {
     const size_t row = (size_t)nbx * bt->D * 2;
     HIPX(ctx, hipMemcpyAsync(bt->h_box, bt->d_box, sizeof(double) * row * nbox, hipMemcpyDeviceToHost, s));
+    fc.skip();
     HIPX(ctx, hipStreamSynchronize(s));
+    fc.lap(7);
+    ++bt->box_syncs;
     int i = 0;
     for (const auto& e : bt->pend) {
       if (e.boxed) continue;
@@ -628,6 +660,7 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
 }
 
 }  // namespace gpx
+
 
 extern "C" {
 
@@ -818,6 +851,11 @@ int gpx_batch_destroy(gpx_batch* bt) {
     (void)hipStreamSynchronize(bt->pending_eval->s);
     bt->pending_eval.reset();
   }
+  if (submit_stats_on() && bt->sub_calls > 0)
+    fprintf(stderr, "[gpx submit stats] batch B=%d calls=%lld flush=%.3f route=%.3f upload=%.3f launch=%.3f "
+            "download=%.3f complete_sync=%.3f (flush: wait_io=%.3f box_sync=%.3f over %lld syncs) s\n", bt->B,
+            bt->sub_calls, bt->sub_s[0], bt->sub_s[1], bt->sub_s[2], bt->sub_s[3], bt->sub_s[4], bt->sub_s[5],
+            bt->sub_s[6], bt->sub_s[7], bt->box_syncs);
   if (bt->shadow) gpx_batch_destroy(bt->shadow);  // waits for its own submitted evaluation
   if (bt->shadow_s) (void)hipStreamDestroy(bt->shadow_s);
   if (bt->shadow_ev) (void)hipEventDestroy(bt->shadow_ev);
@@ -1125,6 +1163,8 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (e != GPX_OK) return e;
   }
   HIPX(ctx, hipSetDevice(ctx->device));
+  SubClock sc(bt);
+  ++bt->sub_calls;
 
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   {  // slots rebound since the last call land first: their band tables (from the gather's
@@ -1132,6 +1172,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     const int rc0 = flush_rebinds(bt, s);
     if (rc0 != GPX_OK) return rc0;
   }
+  sc.lap(0);
   // Route each problem: the block-banded path when K and every ∂K/∂θ vanish exactly beyond a
   // band of p <= band_limit 64-blocks at this θ (gpx_band.hip), the dense recursion otherwise.
   // The device active list is [dense problems | banded problems].
@@ -1206,8 +1247,10 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     const int e = ensure(ctx, bt->bres, bt->bres_cap, (size_t)bt->B * bt->Np);
     if (e != GPX_OK) return drop_shadow(e);
   }
+  sc.lap(1);
   int rc = upload_common(bt, n_active, order.data(), theta, s);
   if (rc != GPX_OK) return drop_shadow(rc);
+  sc.lap(2);
   rc = match_aux_priority(bt, s);
   if (rc != GPX_OK) return drop_shadow(rc);
   bt->flops_acc = 0.0;
@@ -1325,9 +1368,11 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   bp.mark();
   total.mark();
   HIPX(ctx, hipGetLastError());
+  sc.lap(3);
   // one DMA into the pinned block: [info | theta (unchanged) | results]
   HIPX(ctx, hipMemcpyAsync(bt->h_io + bt->io_info_off, bt->d_io + bt->io_info_off,
                            bt->io_bytes - bt->io_info_off, hipMemcpyDeviceToHost, s));
+  sc.lap(4);
   pe->order = std::move(order);
   pe->n_dense = n_dense;
   pe->n_band = n_band;
@@ -1347,7 +1392,9 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
   if (!lml || !grad || !info) return fail(ctx, GPX_BAD_ARG, "null output");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = pe->s;
+  SubClock sc(bt);
   HIPX(ctx, hipStreamSynchronize(s));
+  sc.lap(5);
   const int n_active = pe->n_active, n_dense = pe->n_dense, n_band = pe->n_band, n_fused = pe->n_fused;
   const int n_fused1 = pe->n_fused1, ng = pe->ng;
   const std::vector<int32_t>& order = pe->order;
@@ -1758,6 +1805,8 @@ int gpx_batch_predict_full_cov(gpx_batch* bt, int n_active, const int32_t* activ
 int gpx_batch_reset_timing(gpx_batch* bt) {
   if (!bt) return GPX_BAD_ARG;
   bt->timing = gpx_timing{};
+  for (double& v : bt->sub_s) v = 0.0;
+  bt->sub_calls = bt->box_syncs = 0;
   return GPX_OK;
 }
 

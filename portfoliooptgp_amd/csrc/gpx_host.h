@@ -129,6 +129,10 @@ struct gpx_batch {
   // GPX_GROUPS > 1: per-batch pipelines (created on first use)
   hipStream_t workers[kGroups] = {};
   hipEvent_t fork = nullptr, join[kGroups] = {};
+  // GPX_SUBMIT_STATS=1: host wall seconds of gpx_batch_lml_grad_submit's phases (rebind flush,
+  // routing, upload, launches, download enqueue) and of _complete's wait, printed at destroy
+  double sub_s[8] = {};
+  long long sub_calls = 0, box_syncs = 0;
 };
 
 namespace gpx {
