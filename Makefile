@@ -16,7 +16,7 @@ $(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx
 $(CSRC)/gpx_host_math.o: $(CSRC)/gpx_host_math.c include/gpx.h
 	gcc -O2 -fno-builtin -fno-fast-math -fPIC -std=c11 -Wall -c $< -o $@
 
-$(LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
+$(LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band.o $(CSRC)/gpx_band16.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-soname,libgpx.so $^ -o $@
 
 # plain-C consumer of the C ABI (gcc, HIP runtime API only), run by tests/test_c_abi_gpu.py
@@ -30,7 +30,9 @@ $(CSMOKE): tests/c/gpx_c_smoke.c include/gpx.h $(LIB)
 PHASES_LIB := portfoliooptgp_amd/libgpx_phases.so
 $(CSRC)/gpx_band_phases.o: $(CSRC)/gpx_band.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_leaf.h $(CSRC)/gpx_kfun.h
 	$(HIPCC) $(HIPFLAGS) -DGPX_BAND_PHASES -c $< -o $@
-$(PHASES_LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band_phases.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
+$(CSRC)/gpx_band16_phases.o: $(CSRC)/gpx_band16.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_leaf.h $(CSRC)/gpx_kfun.h
+	$(HIPCC) $(HIPFLAGS) -DGPX_BAND_PHASES -c $< -o $@
+$(PHASES_LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band_phases.o $(CSRC)/gpx_band16_phases.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-soname,libgpx_phases.so $^ -o $@
 phases: $(PHASES_LIB)
 

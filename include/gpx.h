@@ -149,15 +149,15 @@ int gpx_batch_rebind_host(gpx_batch* batch, int b, int n, const double* X, const
                           const gpx_kernel_spec* spec, void* stream);
 /* The same with the inputs in DEVICE memory (X [n, D], Y [n], e.g. a model's resident tensors):
  * only recorded; the next device call on the batch gathers every pending slot in one kernel on
- * its stream (which also returns the per-64-block boxes of X for the band tables), so X and Y
+ * its stream (which also returns the per-16-row-block boxes of X for the band tables), so X and Y
  * must stay valid and unchanged until that call has been issued and completed. `stream` (may be
  * NULL) is the stream in whose order X and Y are ready (their producer's): an event recorded on
  * it here is waited on by the gather when that runs on another stream. */
 int gpx_batch_rebind_device(gpx_batch* batch, int b, int n, const double* X, const double* Y,
                             const gpx_kernel_spec* spec, void* stream);
-/* gpx_batch_rebind_device with the per-64-row-block bounding boxes of X supplied by the caller
- * (host array, for each of the ceil(n/64) blocks and each of the D columns the pair (min, max)
- * of that column over the block's rows: [ceil(n/64)][D][2]), as gpx_batch_slot_boxes returned
+/* gpx_batch_rebind_device with the per-16-row-block bounding boxes of X supplied by the caller
+ * (host array, for each of the ceil(n/16) blocks and each of the D columns the pair (min, max)
+ * of that column over the block's rows: [ceil(n/16)][D][2]), as gpx_batch_slot_boxes returned
  * them for the same X earlier: the band tables are computed here and the next call's gather
  * needs no box download (and no stream synchronise) for this slot. */
 int gpx_batch_rebind_device_boxed(gpx_batch* batch, int b, int n, const double* X, const double* Y,
@@ -263,6 +263,16 @@ typedef struct {
   double band_fallbacks;      /* banded evaluations whose check failed, redone densely */
   double shadow_evals;        /* band storage: evaluations run on the dense fallback slots */
   double shadow_predicts;     /* band storage: predictions run on the dense fallback slots */
+  /* 16-row-block banded sweeps (one wavefront per problem, band of Q <= 4 16-blocks): summed
+   * launch durations, launch pairs, problem-evaluations, Σ Q, and the MFMA flops they issue
+   * (2·16³ per tile product) */
+  double band16_fwd_ms_total;
+  double band16_bwd_ms_total;
+  double band16_launches;
+  double band16_evals;
+  double band16_q_sum;
+  double band16_fwd_flops;
+  double band16_bwd_flops;
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);

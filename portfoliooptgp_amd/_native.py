@@ -62,7 +62,10 @@ class GpxTiming(ctypes.Structure):
                 ("band_bwd_ms_total", ctypes.c_double), ("band_fused_launches", ctypes.c_double),
                 ("band_fwd_flops", ctypes.c_double), ("band_bwd_flops", ctypes.c_double),
                 ("band_fallbacks", ctypes.c_double), ("shadow_evals", ctypes.c_double),
-                ("shadow_predicts", ctypes.c_double)]
+                ("shadow_predicts", ctypes.c_double), ("band16_fwd_ms_total", ctypes.c_double),
+                ("band16_bwd_ms_total", ctypes.c_double), ("band16_launches", ctypes.c_double),
+                ("band16_evals", ctypes.c_double), ("band16_q_sum", ctypes.c_double),
+                ("band16_fwd_flops", ctypes.c_double), ("band16_bwd_flops", ctypes.c_double)]
 
 
 class GPXError(RuntimeError):

@@ -214,13 +214,16 @@ double band_arg(int kind, double s) {
 }
 }  // namespace
 
-// band_rmin of problem b from the per-block boxes lo/hi [nvb][D] of its valid rows
-static void band_tables_lohi(gpx_batch* bt, int b, const std::vector<double>& lo, const std::vector<double>& hi) {
-  const int nb = bt->Np / kLeaf, D = bt->D, n = bt->n[b];
-  double* out = bt->band_rmin.data() + (size_t)b * GPX_MAX_TERMS * nb;
+// band_rmin of problem b at block size bs (64: band_rmin, 16: band_rmin16) from the per-block
+// boxes lo/hi [nvb][D] of its valid rows (blocks of bs rows)
+static void band_tables_lohi(gpx_batch* bt, int b, int bs, const std::vector<double>& lo,
+                             const std::vector<double>& hi) {
+  const int nb = bt->Np / bs, D = bt->D, n = bt->n[b];
+  std::vector<double>& tabv = bs == kLeaf ? bt->band_rmin : bt->band_rmin16;
+  double* out = tabv.data() + (size_t)b * GPX_MAX_TERMS * nb;
   std::fill(out, out + (size_t)GPX_MAX_TERMS * nb, INFINITY);
   const gpx_kernel_spec& sp = bt->specs[b];
-  const int nvb = (n + kLeaf - 1) / kLeaf;  // blocks holding valid rows
+  const int nvb = (n + bs - 1) / bs;  // blocks holding valid rows
   for (int t = 0; t < sp.n_terms; ++t) {
     const int d0 = sp.terms[t].dim_start, dn = sp.terms[t].dim_count;
     double* rt = out + (size_t)t * nb;
@@ -252,39 +255,52 @@ static void band_tables_lohi(gpx_batch* bt, int b, const std::vector<double>& lo
   }
 }
 
+// both tables from the 16-row boxes box[nvb16][D][2] of problem b (the 64-row boxes are their
+// unions); band_rmin16 is kept only where the 16-row path can run (Np <= kBand16MaxNp)
+void band_tables_boxes(gpx_batch* bt, int b, const double* box) {
+  const int D = bt->D, n = bt->n[b];
+  const int nv16 = (n + kBox - 1) / kBox, nv64 = (n + kLeaf - 1) / kLeaf;
+  std::vector<double> lo((size_t)nv64 * D, INFINITY), hi((size_t)nv64 * D, -INFINITY);
+  for (int k = 0; k < nv16; ++k)
+    for (int d = 0; d < D; ++d) {
+      const size_t e = (size_t)k * D + d, f = (size_t)(k / (kLeaf / kBox)) * D + d;
+      lo[f] = std::min(lo[f], box[2 * e]);
+      hi[f] = std::max(hi[f], box[2 * e + 1]);
+    }
+  band_tables_lohi(bt, b, kLeaf, lo, hi);
+  if (!bt->band_rmin16.empty()) {
+    std::vector<double> lo16((size_t)nv16 * D), hi16((size_t)nv16 * D);
+    for (size_t e = 0; e < (size_t)nv16 * D; ++e) {
+      lo16[e] = box[2 * e];
+      hi16[e] = box[2 * e + 1];
+    }
+    band_tables_lohi(bt, b, kBox, lo16, hi16);
+  }
+}
+
 void band_tables(gpx_batch* bt, int b, const double* hostX) {
   const int D = bt->D, n = bt->n[b];
-  const int nvb = (n + kLeaf - 1) / kLeaf;
-  std::vector<double> lo((size_t)nvb * D), hi((size_t)nvb * D);
+  const int nvb = (n + kBox - 1) / kBox;
+  std::vector<double> box((size_t)nvb * D * 2);
   for (int k = 0; k < nvb; ++k)
     for (int d = 0; d < D; ++d) {
       double a = INFINITY, z = -INFINITY;
-      for (int r = k * kLeaf; r < std::min(n, (k + 1) * kLeaf); ++r) {
+      for (int r = k * kBox; r < std::min(n, (k + 1) * kBox); ++r) {
         a = std::min(a, hostX[(size_t)r * D + d]);
         z = std::max(z, hostX[(size_t)r * D + d]);
       }
-      lo[(size_t)k * D + d] = a;
-      hi[(size_t)k * D + d] = z;
+      box[2 * ((size_t)k * D + d)] = a;
+      box[2 * ((size_t)k * D + d) + 1] = z;
     }
-  band_tables_lohi(bt, b, lo, hi);
+  band_tables_boxes(bt, b, box.data());
 }
 
-void band_tables_boxes(gpx_batch* bt, int b, const double* box) {
-  const int D = bt->D, nvb = (bt->n[b] + kLeaf - 1) / kLeaf;
-  std::vector<double> lo((size_t)nvb * D), hi((size_t)nvb * D);
-  for (size_t e = 0; e < (size_t)nvb * D; ++e) {
-    lo[e] = box[2 * e];
-    hi[e] = box[2 * e + 1];
-  }
-  band_tables_lohi(bt, b, lo, hi);
-}
-
-int band_width(const gpx_batch* bt, int b, const double* th) {
+static int band_width_bs(const gpx_batch* bt, int b, const double* th, int bs) {
   const gpx_kernel_spec& sp = bt->specs[b];
   for (int t = 0; t < sp.n_terms; ++t)
     if (!band_kind(sp.terms[t].kind)) return -1;
-  const int nb = bt->Np / kLeaf;
-  const double* tab = bt->band_rmin.data() + (size_t)b * GPX_MAX_TERMS * nb;
+  const int nb = bt->Np / bs;
+  const double* tab = (bs == kLeaf ? bt->band_rmin : bt->band_rmin16).data() + (size_t)b * GPX_MAX_TERMS * nb;
   const bool prod = sp.n_terms > 1 && sp.combine == GPX_PRODUCT;
   for (int d = nb - 1; d >= 1; --d) {
     bool nz = prod;
@@ -302,6 +318,23 @@ int band_width(const gpx_batch* bt, int b, const double* th) {
     if (nz) return d;
   }
   return 0;
+}
+
+int band_width(const gpx_batch* bt, int b, const double* th) { return band_width_bs(bt, b, th, kLeaf); }
+
+// the band width in 16-row blocks (band16 kernels), or -1 when the tables are not kept
+int band_width16(const gpx_batch* bt, int b, const double* th) {
+  if (bt->band_rmin16.empty()) return -1;
+  return band_width_bs(bt, b, th, kBox);
+}
+
+// the 16-row path (gpx_band16.hip) takes p64 <= 1 problems whose band is at most this many
+// 16-blocks (GPX_BAND16=0 disables it)
+int band16_limit(const gpx_batch* bt) {
+  const char* e = getenv("GPX_BAND16");
+  if (e && atoi(e) == 0) return -1;
+  if (bt->band_rmin16.empty() || bt->D > kBand16MaxD) return -1;
+  return kBand16MaxQ;
 }
 
 // shapes the banded path handles: ≥ 8 blocks (smaller problems are a few leaves densely) and
@@ -405,12 +438,28 @@ double band_fused_flops(int Np, int p, bool fwd) {
   return f;
 }
 
-void band_fused_eval(const Run& r, int n1, int max_terms, hipEvent_t* ev) {
-  // r's active range is [p <= 1 problems (n1 of them) | p = 2 problems]; the two classes run
-  // as separate launch pairs, the p = 2 one on an auxiliary stream concurrently
+// MFMA flops the band16 sweeps issue per problem (2·16³ per 16x16x16 tile product; the leaves'
+// 16x16 factorisations are VALU work and not counted)
+double band16_flops(int Np, int Q, bool fwd) {
+  const double U = 2.0 * 16 * 16 * 16;
+  const int nb = Np / 16;
+  double f = 0.0;
+  for (int k = 0; k < nb; ++k) {
+    const double q = std::min(Q, nb - 1 - k);
+    f += fwd ? (q + q * (q + 1) / 2.0) * U          // panels, window update
+             : (q + q * q + 1.0 + q) * U;           // G, Z panel, WᵀW, GᵀZ
+  }
+  return f;
+}
+
+void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, int n1,
+                     int max_terms, hipEvent_t* ev, hipEvent_t (*ev16)[4]) {
+  // r's active range is [band16 problems (n16, by width group) | p <= 1 problems (n1) | p = 2
+  // problems]; the p = 2 class runs as a separate launch pair on an auxiliary stream concurrently
   gpx_batch* bt = r.bt;
   const int Np = bt->Np;
   const long long st = mat_stride(bt);
+  const int nlo = n16 + n1;  // the classes whose K band is two 64-block diagonals
   // K's band is built per class on that class's stream (2 block diagonals for p <= 1, 3 for
   // p = 2), so the p <= 1 build does not pay for the wider class and the two overlap
   BuildArgs ba{};
@@ -425,25 +474,36 @@ void band_fused_eval(const Run& r, int n1, int max_terms, hipEvent_t* ev) {
   fa.specs = bt->d_specs; fa.theta = bt->d_theta; fa.partial = bt->partial; fa.sPartial = bt->partial_stride;
   fa.info = bt->d_info; fa.results = bt->results; fa.Np = Np; fa.ld = mat_ld(bt);
   hipStream_t sa = bt->aux[0];
-  const bool fork = n1 > 0 && n1 < r.na;
+  const bool fork = nlo > 0 && nlo < r.na;
   if (fork) {
     (void)hipEventRecord(bt->ev[kEvents - 2], r.s);   // the call's uploads are in
     (void)hipStreamWaitEvent(sa, bt->ev[kEvents - 2], 0);
   }
-  if (n1 < r.na) {
+  if (nlo < r.na) {
     hipStream_t s2 = fork ? sa : r.s;
     BuildArgs b2 = ba;
-    b2.active = r.d_act + n1;
+    b2.active = r.d_act + nlo;
     b2.band1 = 3;
-    launch_build(b2, r.na - n1, s2);
+    launch_build(b2, r.na - nlo, s2);
     BandFusedArgs f2 = fa;
-    f2.active = r.d_act + n1;
-    launch_band_fused(f2, max_terms, r.na - n1, s2, n1 == 0 ? ev : nullptr);
+    f2.active = r.d_act + nlo;
+    launch_band_fused(f2, max_terms, r.na - nlo, s2, n1 == 0 ? ev : nullptr);
   }
-  if (n1 > 0) {
+  if (nlo > 0) {
     ba.band1 = 2;
-    launch_build(ba, n1, r.s);
-    launch_band_fused1(fa, max_terms, n1, r.s, ev);
+    launch_build(ba, nlo, r.s);
+    int off = 0;
+    for (int g = 0; g < n_g16; ++g) {
+      BandFusedArgs f16 = fa;
+      f16.active = r.d_act + off;
+      launch_band16(f16, g16_q[g], max_terms, g16_n[g], r.s, ev16 ? ev16[g] : nullptr);
+      off += g16_n[g];
+    }
+    if (n1 > 0) {
+      BandFusedArgs f1 = fa;
+      f1.active = r.d_act + n16;
+      launch_band_fused1(f1, max_terms, n1, r.s, ev);
+    }
   }
   if (fork) {
     (void)hipEventRecord(bt->ev[kEvents - 1], sa);
@@ -490,13 +550,13 @@ int ensure_rebind_meta(gpx_batch* bt) {
 // remember slot b's per-block X boxes (rows of its valid blocks; the rest of the slot's row
 // is left as it was)
 void keep_slot_box(gpx_batch* bt, int b, const double* box) {
-  const int nbx = (bt->Nmax + kLeaf - 1) / kLeaf;
+  const int nbx = (bt->Nmax + kBox - 1) / kBox;
   const size_t row = (size_t)nbx * bt->D * 2;
   if (bt->slot_box.empty()) {
     bt->slot_box.assign(row * bt->B, 0.0);
     bt->slot_box_ok.assign(bt->B, 0);
   }
-  const int nvb = (bt->n[b] + kLeaf - 1) / kLeaf;
+  const int nvb = (bt->n[b] + kBox - 1) / kBox;
   std::memcpy(bt->slot_box.data() + row * b, box, sizeof(double) * (size_t)nvb * bt->D * 2);
   bt->slot_box_ok[b] = 1;
 }
@@ -549,7 +609,7 @@ int flush_rebinds(gpx_batch* bt, hipStream_t s) {
     if (rc != GPX_OK) return rc;
   }
   const size_t nx = (size_t)bt->Nmax * bt->D, ny = bt->Nmax;
-  const int nbx = (bt->Nmax + kLeaf - 1) / kLeaf;
+  const int nbx = (bt->Nmax + kBox - 1) / kBox;
   if (!bt->h_rdesc) {
     HIPX(ctx, hipHostMalloc(&bt->h_rdesc, sizeof(RebindDesc) * bt->B, hipHostMallocCoherent));
     HIPX(ctx, hipMalloc(&bt->d_box, sizeof(double) * (size_t)bt->B * nbx * bt->D * 2));
@@ -805,6 +865,7 @@ static int batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, 
   bt->fac_valid.assign(B, 0);
   bt->fac_band.assign(B, 0);
   bt->band_rmin.assign((size_t)B * GPX_MAX_TERMS * (bt->Np / kLeaf), INFINITY);
+  if (bt->Np <= kBand16MaxNp) bt->band_rmin16.assign((size_t)B * GPX_MAX_TERMS * (bt->Np / kBox), INFINITY);
   if (band_shape(bt)) {
     std::vector<double> hx((size_t)B * N_max * D);
     if (hipMemcpy(hx.data(), X, sizeof(double) * hx.size(), hipMemcpyDeviceToHost) != hipSuccess)
@@ -1021,9 +1082,9 @@ int gpx_batch_rebind_device_boxed(gpx_batch* bt, int b, int n, const double* X, 
 int gpx_batch_slot_boxes(const gpx_batch* bt, int b, double* out) {
   if (!bt || !out || b < 0 || b >= bt->B) return GPX_BAD_ARG;
   if (bt->slot_box_ok.empty() || !bt->slot_box_ok[b] || !bt->pend.empty()) return GPX_BAD_ARG;
-  const int nbx = (bt->Nmax + kLeaf - 1) / kLeaf;
+  const int nbx = (bt->Nmax + kBox - 1) / kBox;
   const size_t row = (size_t)nbx * bt->D * 2;
-  const int nvb = (bt->n[b] + kLeaf - 1) / kLeaf;
+  const int nvb = (bt->n[b] + kBox - 1) / kBox;
   std::memcpy(out, bt->slot_box.data() + row * b, sizeof(double) * (size_t)nvb * bt->D * 2);
   return GPX_OK;
 }
@@ -1184,13 +1245,22 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   if (bt->compact) plim = std::min(plim, kBandStoreP);
   const char* ef = getenv("GPX_BAND_FUSED");  // 0: p <= 2 problems take the per-block launches too
   const bool fused_on = !(ef && atoi(ef) == 0);
+  const int q16lim = fused_on ? band16_limit(bt) : -1;
+  std::vector<int32_t> b16_ids[kBand16MaxQ + 1];  // band16 class by width Q (16-blocks)
   for (int i = 0; i < n_active; ++i) {
     const int b = active[i];
-    const int p = plim >= 0 ? band_width(bt, b, theta + (size_t)b * GPX_THETA_STRIDE) : -1;
+    const double* thb = theta + (size_t)b * GPX_THETA_STRIDE;
+    const int p = plim >= 0 ? band_width(bt, b, thb) : -1;
     if (p >= 0 && p <= plim) {
       bt->h_bandp[b] = p;
+      // p <= 1 problems whose band is at most kBand16MaxQ 16-blocks: the band16 sweeps
+      const int q16 = (p <= 1 && q16lim > 0) ? band_width16(bt, b, thb) : -1;
       // the p = 2 sweep holds four 64x64 LDS blocks plus three 64·D X-row slots (<= 160 KiB)
-      if (fused_on && (p <= 1 || (p == 2 && bt->D <= 12))) {
+      if (q16 >= 0 && q16 <= q16lim) {
+        const int Q = std::max(q16, 1);
+        bt->h_bandp[b] = Q;
+        b16_ids[Q].push_back(b);
+      } else if (fused_on && (p <= 1 || (p == 2 && bt->D <= 12))) {
         fused_ids.push_back(b);
         pfused = std::max(pfused, p);
       } else if (bt->compact) {
@@ -1205,7 +1275,9 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
       order.push_back(b);
     }
   }
-  const int n_dense = (int)order.size(), n_band = (int)band_ids.size(), n_fused = (int)fused_ids.size();
+  int n16 = 0;
+  for (int q = 1; q <= kBand16MaxQ; ++q) n16 += (int)b16_ids[q].size();
+  const int n_dense = (int)order.size(), n_band = (int)band_ids.size(), n_fused = (int)fused_ids.size() + n16;
   // the problems launched by this call (band storage: without the shadowed ones)
   n_active = n_dense + n_band + n_fused;
   // band storage: a few fallback problems go out at once on the fallback stream (more than the
@@ -1237,7 +1309,15 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     return GPX_OK;
   }
   order.insert(order.end(), band_ids.begin(), band_ids.end());
-  // fused problems: the p <= 1 class first (its own two-blocks-per-CU kernels), then p = 2
+  // fused problems: the band16 class first (by width), then p <= 1 (its own two-blocks-per-CU
+  // kernels), then p = 2
+  int g16_q[kBand16MaxQ], g16_n[kBand16MaxQ], n_g16 = 0;
+  for (int q = 1; q <= kBand16MaxQ; ++q)
+    if (!b16_ids[q].empty()) {
+      order.insert(order.end(), b16_ids[q].begin(), b16_ids[q].end());
+      g16_q[n_g16] = q;
+      g16_n[n_g16++] = (int)b16_ids[q].size();
+    }
   int n_fused1 = 0;
   for (int b : fused_ids)
     if (bt->h_bandp[b] <= 1) order.push_back(b), ++n_fused1;
@@ -1360,10 +1440,19 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   if (n_fused > 0) {
     int max_terms = 1;
     for (int i = n_dense + n_band; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
-    if (ctx->profiling)
+    const bool old_fused = n_fused > n16;  // the 64-row fused kernels run too
+    if (ctx->profiling && old_fused)
       for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&fqe[e]));
-    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, n_fused1, max_terms,
-                    ctx->profiling ? fqe : nullptr);
+    pe->n_band16 = n16;
+    pe->n_g16 = n_g16;
+    for (int g = 0; g < n_g16; ++g) {
+      pe->g16_q[g] = g16_q[g];
+      pe->g16_n[g] = g16_n[g];
+      if (ctx->profiling)
+        for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&pe->fq16[g][e]));
+    }
+    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, n16, n_g16, g16_q, g16_n, n_fused1,
+                    max_terms, (ctx->profiling && old_fused) ? fqe : nullptr, ctx->profiling ? pe->fq16 : nullptr);
   }
   bp.mark();
   total.mark();
@@ -1425,9 +1514,22 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
       bt->timing.band_ms_total += bp.ms(0, 1);
       bt->timing.band_calls += 1.0;
       bt->timing.band_evals += n_band + n_fused;
-      for (int i = n_dense; i < n_active; ++i) bt->timing.band_p_sum += bt->h_bandp[order[i]];
+      for (int i = n_dense; i < n_active; ++i)
+        bt->timing.band_p_sum += (i >= n_dense + n_band && i < n_dense + n_band + pe->n_band16) ? 1 : bt->h_bandp[order[i]];
     }
-    if (n_fused > 0) {
+    for (int g = 0; g < pe->n_g16; ++g) {
+      float f0 = 0.f, f1 = 0.f;
+      (void)hipEventElapsedTime(&f0, pe->fq16[g][0], pe->fq16[g][1]);
+      (void)hipEventElapsedTime(&f1, pe->fq16[g][2], pe->fq16[g][3]);
+      bt->timing.band16_fwd_ms_total += f0;
+      bt->timing.band16_bwd_ms_total += f1;
+      bt->timing.band16_launches += 1.0;
+      bt->timing.band16_evals += pe->g16_n[g];
+      bt->timing.band16_q_sum += (double)pe->g16_q[g] * pe->g16_n[g];
+      bt->timing.band16_fwd_flops += pe->g16_n[g] * band16_flops(bt->Np, pe->g16_q[g], true);
+      bt->timing.band16_bwd_flops += pe->g16_n[g] * band16_flops(bt->Np, pe->g16_q[g], false);
+    }
+    if (n_fused > pe->n_band16) {
       float f0 = 0.f, f1 = 0.f;
       (void)hipEventElapsedTime(&f0, fqe[0], fqe[1]);
       (void)hipEventElapsedTime(&f1, fqe[2], fqe[3]);
@@ -1435,7 +1537,7 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
       bt->timing.band_bwd_ms_total += f1;
       bt->timing.band_fused_launches += 1.0;
       // the timed launch pair is the p <= 1 class's when there is one, else the p = 2 class's
-      const int t0 = n_dense + n_band, t1 = n_fused1 > 0 ? t0 + n_fused1 : n_active;
+      const int t0 = n_dense + n_band + pe->n_band16, t1 = n_fused1 > 0 ? t0 + n_fused1 : n_active;
       for (int i = t0; i < t1; ++i) {
         const int pb = bt->h_bandp[order[i]];
         bt->timing.band_fwd_flops += band_fused_flops(bt->Np, pb, true);

@@ -1427,12 +1427,12 @@ __global__ __launch_bounds__(256) void rebind_gather_kernel(const RebindDesc* de
   for (int e = tid; e < nx; e += 256) d.dx[e] = e < nv ? d.x[e] : 0.0;
   for (int e = tid; e < Nmax; e += 256) d.dy[e] = e < n ? d.y[e] : 0.0;
   if (d.box < 0) return;
-  const int nb = (Nmax + 63) / 64;
+  const int nb = (Nmax + 15) / 16;  // 16-row boxes (kBox)
   double* out = box + (size_t)d.box * nb * D * 2;
   for (int t = tid; t < nb * D; t += 256) {
     const int k = t / D, q = t - k * D;
     double lo = INFINITY, hi = -INFINITY;
-    for (int r = k * 64; r < min(n, k * 64 + 64); ++r) {
+    for (int r = k * 16; r < min(n, k * 16 + 16); ++r) {
       const double v = d.x[(size_t)r * D + q];
       lo = fmin(lo, v);
       hi = fmax(hi, v);

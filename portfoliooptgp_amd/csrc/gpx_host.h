@@ -65,6 +65,7 @@ struct gpx_batch {
   // a lower bound on the distance between any point of block k and any point of block k − d
   // over the term's active dims, [B][GPX_MAX_TERMS][Np/64]; computed when a problem is bound
   std::vector<double> band_rmin;
+  std::vector<double> band_rmin16;  // the same per 16-row block, [B][GPX_MAX_TERMS][Np/16] (band16 path)
   double* bres = nullptr; size_t bres_cap = 0;  // [B][Np] band-check column sums (per-block path)
   int force_dense = 0;         // re-evaluation of problems whose band check failed
   // pinned staging for gpx_batch_rebind_host, one region per slot ([Nmax*D] X, [Nmax] Y, n and
@@ -157,6 +158,10 @@ inline int fail(gpx_ctx* ctx, int code, const std::string& msg) {
 inline long long mat_stride(const gpx_batch* bt) { return bt->smat ? bt->smat : (long long)bt->Np * bt->Np; }
 inline int mat_ld(const gpx_batch* bt) { return bt->ldm ? bt->ldm : bt->Np; }
 constexpr int kBandStoreP = 2;     // band width (64-blocks) held by band storage
+constexpr int kBox = 16;           // rows per bounding box of the band tables (16: the band16 path's block)
+constexpr int kBand16MaxQ = 4;     // widest band (16-blocks) of the band16 kernels (gpx_band16.hip)
+constexpr int kBand16MaxD = 8;     // input columns the band16 backward sweep stages per block
+constexpr int kBand16MaxNp = 8192;
 constexpr int kShadowSlots = 4;    // dense fallback slots of a band-storage batch
 
 // One pipeline instance: a contiguous range of the device active list on one stream.
@@ -211,10 +216,14 @@ void band_tables(gpx_batch* bt, int b, const double* hostX);  // fills band_rmin
 // the same from per-64-block boxes of X ([nb][D][2]: lo, hi over the block's valid rows)
 void band_tables_boxes(gpx_batch* bt, int b, const double* box);
 int band_width(const gpx_batch* bt, int b, const double* theta_row);  // p in 64-blocks, or -1
+int band_width16(const gpx_batch* bt, int b, const double* theta_row);  // the same in 16-row blocks
+int band16_limit(const gpx_batch* bt);  // widest band16 class (16-blocks), -1: off
 bool band_shape(const gpx_batch* bt);  // the banded path handles this batch's padded size
 int band_limit(const gpx_batch* bt);  // largest p the banded path takes (-1: path disabled)
 void band_eval(const Run& r, int p, int max_terms);  // build .. reduce for a banded active set
-void band_fused_eval(const Run& r, int n1, int max_terms, hipEvent_t* ev = nullptr);  // p <= 2: [p<=1 (n1) | p=2]
+// p <= 2: [band16 groups (sizes g16_n, widths g16_q) | p<=1 (n1) | p=2]
+void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, int n1,
+                     int max_terms, hipEvent_t* ev = nullptr, hipEvent_t (*ev16)[4] = nullptr);
 double band_fused_flops(int Np, int p, bool fwd);  // block-product flops of one problem's sweep
 void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W = L⁻¹)
 void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z
@@ -239,11 +248,19 @@ struct gpx_batch::PendingEval {
   std::vector<gpx::PhaseTimer> pts;
   hipEvent_t kev[2] = {nullptr, nullptr};
   hipEvent_t fq[4] = {nullptr, nullptr, nullptr, nullptr};
+  // band16 class: problems [n_band16] at the head of the fused range, grouped by band width Q
+  // (one launch pair per group, timestamped when profiling)
+  int n_band16 = 0;
+  int g16_q[gpx::kBand16MaxQ] = {}, g16_n[gpx::kBand16MaxQ] = {}, n_g16 = 0;
+  hipEvent_t fq16[gpx::kBand16MaxQ][4] = {};
   ~PendingEval() {
     for (auto x : kev)
       if (x) (void)hipEventDestroy(x);
     for (auto x : fq)
       if (x) (void)hipEventDestroy(x);
+    for (auto& g : fq16)
+      for (auto x : g)
+        if (x) (void)hipEventDestroy(x);
   }
 };
 

@@ -166,6 +166,10 @@ void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipS
 // the same for problems with p <= 1 (two LDS blocks per workgroup: two problems per CU)
 void launch_band_fused1(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s,
                         hipEvent_t* ev = nullptr);
+// 16-row blocks, one wavefront per problem (gpx_band16.hip); bandp holds each problem's band in
+// 16-blocks, all <= Q
+void launch_band16(const BandFusedArgs& a, int Q, int max_terms, int n_active, hipStream_t s,
+                   hipEvent_t* ev = nullptr);
 void launch_band_solve(const BandSolveArgs& a, int n_active, hipStream_t s);
 void launch_band_transpose(const BandTransposeArgs& a, int q, int n_active, hipStream_t s);
 void launch_band_contract(const BandContractArgs& a, int max_terms, int n_active, hipStream_t s);

@@ -158,7 +158,7 @@ class Engine:
         if _BOX_CACHE is None:
             _BOX_CACHE = OrderedDict()
         for b, (key, x) in self._box_want.items():
-            buf = np.empty(((int(self.n[b]) + 63) // 64) * self.D * 2, dtype=np.float64)
+            buf = np.empty(((int(self.n[b]) + 15) // 16) * self.D * 2, dtype=np.float64)  # 16-row boxes
             if self.lib.gpx_batch_slot_boxes(self.handle, int(b), buf.ctypes.data) == N.GPX_OK:
                 _BOX_CACHE[key] = (x, buf)
                 _BOX_CACHE.move_to_end(key)

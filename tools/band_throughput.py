@@ -69,6 +69,14 @@ def main():
            "mean_p": fl("band_p_sum") / max(evals, 1),
            "chip_tflops": evals * per_eval / dt / 1e12}
     out["chip_frac"] = out["chip_tflops"] / FP64_PEAK_TFLOPS
+    e16 = fl("band16_evals")
+    if e16 > 0:  # the band16 sweeps: launch times and the MFMA flops they issue
+        la = max(fl("band16_launches"), 1)
+        out.update({"band16_evals": e16, "band16_mean_q": fl("band16_q_sum") / e16,
+                    "b16_fwd_avg_ms": fl("band16_fwd_ms_total") / la, "b16_bwd_avg_ms": fl("band16_bwd_ms_total") / la,
+                    "b16_fwd_tflops": fl("band16_fwd_flops") / max(fl("band16_fwd_ms_total"), 1e-9) / 1e9,
+                    "b16_bwd_tflops": fl("band16_bwd_flops") / max(fl("band16_bwd_ms_total"), 1e-9) / 1e9,
+                    "b16_chip_mfma_tflops": (fl("band16_fwd_flops") + fl("band16_bwd_flops")) / dt / 1e12})
     print(json.dumps(out), flush=True)
 
 
