@@ -452,7 +452,7 @@ double band16_flops(int Np, int Q, bool fwd) {
   return f;
 }
 
-void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, int n1,
+void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int n1,
                      int max_terms, hipEvent_t* ev, hipEvent_t (*ev16)[4]) {
   // r's active range is [band16 problems (n16, by width group) | p <= 1 problems (n1) | p = 2
   // problems]; the p = 2 class runs as a separate launch pair on an auxiliary stream concurrently
@@ -496,7 +496,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     for (int g = 0; g < n_g16; ++g) {
       BandFusedArgs f16 = fa;
       f16.active = r.d_act + off;
-      launch_band16(f16, g16_q[g], max_terms, g16_n[g], r.s, ev16 ? ev16[g] : nullptr);
+      launch_band16(f16, g16_q[g], max_terms, se1, g16_n[g], r.s, ev16 ? ev16[g] : nullptr);
       off += g16_n[g];
     }
     if (n1 > 0) {
@@ -1451,7 +1451,14 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
       if (ctx->profiling)
         for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&pe->fq16[g][e]));
     }
-    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, n16, n_g16, g16_q, g16_n, n_fused1,
+    // the reference's kernel (one SquaredExponential term on one column) everywhere in the band16
+    // class: its backward sweep's straight-line contraction
+    bool se1 = true;
+    for (int i = n_dense + n_band; i < n_dense + n_band + n16; ++i) {
+      const gpx_kernel_spec& sp = bt->specs[order[i]];
+      se1 = se1 && sp.n_terms == 1 && sp.terms[0].kind == GPX_SE && sp.terms[0].dim_count == 1;
+    }
+    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, n16, n_g16, g16_q, g16_n, se1, n_fused1,
                     max_terms, (ctx->profiling && old_fused) ? fqe : nullptr, ctx->profiling ? pe->fq16 : nullptr);
   }
   bp.mark();

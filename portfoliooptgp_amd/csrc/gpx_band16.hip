@@ -92,18 +92,39 @@ __device__ __forceinline__ void st_t(const t4& t, double* __restrict__ g, long l
   for (int r = 0; r < 4; ++r) p[4 * r] = t[r];
 }
 
-// sums over the 4 lanes l4 = 0..3 of a column (lanes l15 + 16·l4) and over the 16 lanes of a row
+// sums over the 4 lanes l4 = 0..3 of a column (lanes l15 + 16·l4: v_permlane32_swap and
+// v_permlane16_swap, no LDS round trip) and over the 16 lanes of a row (DPP row broadcasts)
+__device__ __forceinline__ double xor_lanes(double v, bool sw32) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const int lane = threadIdx.x & 63;
+  unsigned plo, phi;
+  if (sw32) {
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const bool low = lane < 32;
+    plo = low ? a[1] : a[0];
+    phi = low ? b[1] : b[0];
+  } else {
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const bool even = ((lane >> 4) & 1) == 0;
+    plo = even ? a[1] : a[0];
+    phi = even ? b[1] : b[0];
+  }
+  return __longlong_as_double(((unsigned long long)phi << 32) | plo);
+}
 __device__ __forceinline__ double sum4(double v) {
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
+  v += xor_lanes(v, true);
+  v += xor_lanes(v, false);
   return v;
 }
 __device__ __forceinline__ double sum16(double v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
-  return v;
+  double s[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    s[q] = (bc16(v, 4 * q) + bc16(v, 4 * q + 1)) + (bc16(v, 4 * q + 2) + bc16(v, 4 * q + 3));
+  return (s[0] + s[1]) + (s[2] + s[3]);
 }
 __device__ __forceinline__ double wsum64(double v) {
 #pragma unroll
@@ -116,6 +137,8 @@ __device__ __forceinline__ double wsum64(double v) {
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
 // wait for this wave's global -> LDS copies (and its other vector memory operations)
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// wait for this wave's LDS operations
+__device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // async copy of a 16x16 tile (row-major, leading dimension ld) into a 16x16 row-major LDS tile:
 // two 16-byte global_load_lds per lane (8 rows each; LDS destination = base + lane·16 B)
@@ -203,6 +226,108 @@ __device__ __forceinline__ void leaf16(const t4& A, t4& V, double& lii, int& fai
   for (int r = 0; r < 4; ++r) V[r] = sc[l15 * kSC + 4 * r + l4];  // (L⁻¹)[l15][4r+l4]
 }
 
+// 16x16 Cholesky-and-inverse on the matrix cores: four 4-column steps, each a 4x4 diagonal
+// factorisation (every lane, uniform values from LDS), the 16x4 panel by the diagonal block's
+// inverse, ONE v_mfma_f64_16x16x4_f64 for the rank-4 trailing update of the tile and one for the
+// rank-4 update of L⁻¹ (built alongside, right-looking: W := Li·W_jb on block row jb, then
+// W_below −= L_below,jb · W_jb). A (symmetric) is read through its column blocks: fragment
+// register c at lane (l15, l4) is A[l15][4c + l4]. Returns V = fragment of (L⁻¹)ᵀ (through one LDS
+// transpose), Wr = fragment of L⁻¹ (rows: register r holds rows 4r + l4), lii = L[l15][l15] and
+// fail = the first pivot that is not > 0 (or −1).
+__device__ __forceinline__ void leaf16m(t4 A, t4& V, t4& Wr, double& lii, int& fail, double* __restrict__ sc,
+                                        int l15, int l4) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) Wr[r] = (4 * r + l4 == l15) ? 1.0 : 0.0;
+  fail = -1;
+  lii = 0.0;
+  double* sm = sc;       // [16][4] column block of A
+  double* sw = sc + 64;  // [16][4] block row of W, transposed: sw[j][b] = W[4jb + b][j]
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) {
+    wsync();
+    sm[l15 * 4 + l4] = A[jb];
+    sw[l15 * 4 + l4] = Wr[jb];
+    wsync();
+    double m[4], wv[4], d[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      m[c] = sm[l15 * 4 + c];
+      wv[c] = sw[l15 * 4 + c];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c <= a; ++c) d[a][c] = sm[(4 * jb + a) * 4 + c];  // (same address on every lane)
+    // 4x4 Cholesky L_d and its inverse Li (uniform)
+    double l[4][4], iv[4], li[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int c = 0; c < a; ++c) {
+        double t = d[a][c];
+#pragma unroll
+        for (int e = 0; e < c; ++e) t = fma(-l[a][e], l[c][e], t);
+        l[a][c] = t * iv[c];
+      }
+      double pv = d[a][a];
+#pragma unroll
+      for (int e = 0; e < a; ++e) pv = fma(-l[a][e], l[a][e], pv);
+      if (!(pv > 0.0) && fail < 0) fail = 4 * jb + a;
+      iv[a] = rsqrt_nr(pv);
+      l[a][a] = pv * iv[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      li[a][a] = iv[a];
+#pragma unroll
+      for (int c = a - 1; c >= 0; --c) {  // li[a][c] = −iv[a] Σ_{e=c}^{a−1} l[a][e] li[e][c]
+        double t = 0.0;
+#pragma unroll
+        for (int e = c; e < a; ++e) t = fma(l[a][e], li[e][c], t);
+        li[a][c] = -iv[a] * t;
+      }
+    }
+    if ((l15 >> 2) == jb) {
+      const int a = l15 & 3;
+      lii = a == 0 ? l[0][0] : a == 1 ? l[1][1] : a == 2 ? l[2][2] : l[3][3];
+    }
+    // panel column block jb of L: rows below the block m·Li_dᵀ, rows of the block L_d, above 0
+    double lrow[4];  // Li[l4][c] (0 for c > l4)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double v = 0.0;
+#pragma unroll
+      for (int a = c; a < 4; ++a) v = (l4 == a) ? li[a][c] : v;
+      lrow[c] = v;
+    }
+    double xb = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) xb = fma(m[c], lrow[c], xb);
+    const int rb = l15 - 4 * jb;  // row within the block
+    double ld = 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c <= a; ++c) ld = (rb == a && l4 == c) ? l[a][c] : ld;
+    xb = rb >= 4 ? xb : 0.0;                     // rows below the block only
+    const double x = (rb >= 0 && rb < 4) ? ld : xb;
+    A = __builtin_amdgcn_mfma_f64_16x16x4f64(-x, x, A, 0, 0, 0);  // trailing update (rank 4)
+    // block row jb of L⁻¹: Li · (its current rows), then the rows below
+    double wn = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wn = fma(lrow[c], wv[c], wn);
+    Wr[jb] = wn;
+    Wr = __builtin_amdgcn_mfma_f64_16x16x4f64(-xb, wn, Wr, 0, 0, 0);
+  }
+  // V = fragment of (L⁻¹)ᵀ
+  wsync();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sc[(4 * r + l4) * kSC + l15] = Wr[r];
+  wsync();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) V[r] = sc[l15 * kSC + 4 * r + l4];
+}
+
 // frag of A_{bi,bj}ᵀ (bi >= bj, 16-blocks) from K's stored lower band; entries in 64-block
 // offset >= 2 read as 0 (exact for the class this file serves, p64 <= 1); the diagonal tile
 // from its lower triangle
@@ -233,7 +358,7 @@ constexpr __host__ __device__ int wid(int i, int j) { return i * (i + 1) / 2 + j
 // then the window moves down one block; its new row (block k+Q+1) is loaded during the step.
 // ---------------------------------------------------------------------------------------
 template <int Q>
-__global__ __launch_bounds__(64, Q <= 2 ? 2 : 1) void band16_fwd_kernel(BandFusedArgs a) {
+__global__ __launch_bounds__(64, Q <= 3 ? 2 : 1) void band16_fwd_kernel(BandFusedArgs a) {
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   __shared__ __attribute__((aligned(16))) double snew[Q + 1][256];  // the entering row, staged by glds
   __shared__ double sv[16];
@@ -265,6 +390,7 @@ __global__ __launch_bounds__(64, Q <= 2 ? 2 : 1) void band16_fwd_kernel(BandFuse
     // during the step (the previous step's reads of snew are done: program order + wsync)
     const int bn = k + Q + 1;
     wsync();
+    lds_drain();  // the previous step's reads of snew have completed
     if (bn < nb) {
 #pragma unroll
       for (int j = 0; j <= Q; ++j) tile_glds(K + (long long)(bn * 16) * ld + (k + 1 + j) * 16, ld, snew[j], lane);
@@ -280,11 +406,12 @@ __global__ __launch_bounds__(64, Q <= 2 ? 2 : 1) void band16_fwd_kernel(BandFuse
     t4 V;
     double lii;
     int fl;
-    leaf16(T[wid(0, 0)], V, lii, fl, sc, l15, l4);
+    {
+      t4 Wr;
+      leaf16m(T[wid(0, 0)], V, Wr, lii, fl, sc, l15, l4);
+    }
     QP(1);
     if (fl >= 0 && gfail == 0) gfail = k16 + fl + 1;
-    if (l4 == 0) ldiag[k16 + l15] = lii;
-    st_t(V, W + (long long)k16 * ld + k16, ld, l15, l4);  // W_kk, row-major
     // z_k = W_kk (y_k + u_k): V[r] = W_kk[l15][4r+l4]
     wsync();
     if (l4 == 0) sv[l15] = u[0];
@@ -293,7 +420,6 @@ __global__ __launch_bounds__(64, Q <= 2 ? 2 : 1) void band16_fwd_kernel(BandFuse
 #pragma unroll
     for (int r = 0; r < 4; ++r) zp = fma(V[r], yr[r] + sv[4 * r + l4], zp);
     zp = sum4(zp);
-    if (l4 == 0) z[k16 + l15] = zp;
     wsync();
     if (l4 == 0) sv[l15] = zp;
     wsync();
@@ -308,7 +434,6 @@ __global__ __launch_bounds__(64, Q <= 2 ? 2 : 1) void band16_fwd_kernel(BandFuse
         t4 c = tzero();
         mma(c, V, T[wid(i, 0)]);
         T[wid(i, 0)] = c;
-        st_t(c, L + (long long)(k16 + 16 * i) * ld + k16, ld, l15, l4);
         double s = 0.0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) s = fma(c[r], zr[r], s);
@@ -323,6 +448,19 @@ __global__ __launch_bounds__(64, Q <= 2 ? 2 : 1) void band16_fwd_kernel(BandFuse
       for (int j = 1; j <= i; ++j)
         if (i <= qk) mms(T[wid(i, j)], T[wid(j, 0)], T[wid(i, 0)]);
     QP(4);
+    // the new row has landed (this also retires the previous step's stores, long done); this
+    // step's outputs go out now, so that the next step's wait does not cover them early:
+    // W_kk (row-major), L_ii, z_k and the panels P_i = L_{k+i,k}
+    vm_drain();
+    wsync();
+    st_t(V, W + (long long)k16 * ld + k16, ld, l15, l4);
+    if (l4 == 0) {
+      ldiag[k16 + l15] = lii;
+      z[k16 + l15] = zp;
+    }
+#pragma unroll
+    for (int i = 1; i <= Q; ++i)
+      if (i <= qk) st_t(T[wid(i, 0)], L + (long long)(k16 + 16 * i) * ld + k16, ld, l15, l4);
     // move the window down one block; its new row from LDS (fragments of A_{bn, k+1+j}ᵀ, entries
     // in 64-block offset >= 2 as exact zeros, the diagonal tile mirrored from its lower triangle)
 #pragma unroll
@@ -332,8 +470,6 @@ __global__ __launch_bounds__(64, Q <= 2 ? 2 : 1) void band16_fwd_kernel(BandFuse
       u[i] = u[i + 1];
     }
     u[Q] = 0.0;
-    vm_drain();
-    wsync();
 #pragma unroll
     for (int j = 0; j <= Q; ++j) {
       t4 t = tzero();
@@ -367,15 +503,16 @@ __global__ __launch_bounds__(64, Q <= 2 ? 2 : 1) void band16_fwd_kernel(BandFuse
 // step's tiles) and its upper-band sums from the row sums of tiles (k, k−m), m = 1..Q, at the
 // following steps: complete after step k−Q (kept in LDS rings, rows/columns by 16-lane sums).
 // ---------------------------------------------------------------------------------------
-template <int Q, int NT>
-__global__ __launch_bounds__(64, Q <= 1 ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
+// SE1: every problem of the launch is the reference's kernel (one SquaredExponential term on one
+// input column): the contraction is a straight-line loop (contract_block_se1's operations).
+template <int Q, int NT, bool SE1>
+__global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
   extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1))
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   __shared__ __attribute__((aligned(16))) double sin_[Q + 1][256];  // next step's W_kk (0), P_i (i), by glds
   __shared__ __attribute__((aligned(16))) double sz[Q + 1][256];    // this step's Z_kk (0), Z_{k+i,k} (i)
   __shared__ double sal[Q + 1][16];                    // α ring
   __shared__ double scs[Q + 1][16];                    // band check: column sums ring
-  __shared__ double srs[Q + 1][16];                    // band check: row sums ring
   __shared__ double sth[GPX_THETA_STRIDE];
   __shared__ double sred[GPX_MAX_TERMS * 3 + 2];
   const int b = a.active[blockIdx.x];
@@ -387,10 +524,25 @@ __global__ __launch_bounds__(64, Q <= 1 ? 2 : 1) void band16_bwd_kernel(BandFuse
   const double* z = a.z + (long long)b * a.sVec;
   double* alpha = a.alpha + (long long)b * a.sVec;
   const double* X = a.X + (long long)b * a.sX;
-  const int n = a.nvalid[b], D = a.D;
+  const int n = a.nvalid[b], D = a.D, nx = 16 * D;
   const int lane = threadIdx.x, l15 = lane & 15, l4 = lane >> 4;
-  // the first step's inputs (k = nb − 1: W_kk only)
-  tile_glds(W + (long long)(Np - 16) * ld + (Np - 16), ld, sin_[0], lane);
+  // inputs of a step: W_kk and P_i by glds into sin_, z_k and the block's X rows into registers
+  auto fetch = [&](int kk, double (&zr)[4], double (&xr)[2]) {
+    const int q1 = min(Q, nb - 1 - kk), c16 = kk * 16;
+    tile_glds(W + (long long)c16 * ld + c16, ld, sin_[0], lane);
+#pragma unroll
+    for (int i = 1; i <= Q; ++i)
+      if (i <= q1) tile_glds(L + (long long)(c16 + 16 * i) * ld + c16, ld, sin_[i], lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) zr[r] = z[c16 + 4 * r + l4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // the first 128 values of the rows (all of them for D <= 8)
+      const int e = lane + 64 * h;
+      xr[h] = X[min((long long)c16 * D + e, (long long)n * D - 1)];  // (clamped into the slot's rows)
+    }
+  };
+  double zr[4], xr[2];
+  fetch(nb - 1, zr, xr);
   {  // the forward sweep left L_ii: log det's terms (read by the reduce kernel)
     double* ldg = a.ldiag + (long long)b * a.sVec;
     for (int e = lane; e < Np; e += 64) ldg[e] = log(ldg[e]);
@@ -398,18 +550,17 @@ __global__ __launch_bounds__(64, Q <= 1 ? 2 : 1) void band16_bwd_kernel(BandFuse
   if (lane < GPX_THETA_STRIDE) sth[lane] = a.theta[b * GPX_THETA_STRIDE + lane];
   if (lane < 16) {
 #pragma unroll
-    for (int m = 0; m <= Q; ++m) { sal[m][lane] = 0.0; scs[m][lane] = 0.0; srs[m][lane] = 0.0; }
+    for (int m = 0; m <= Q; ++m) { sal[m][lane] = 0.0; scs[m][lane] = 0.0; }
   }
+  vm_drain();
   wsync();
   const DevSpec spec = a.specs[b];
   const int fkind = spec.terms[0].kind, fd0 = spec.terms[0].dim_start, fdn = spec.terms[0].dim_count;
   const bool fast = (NT == 1) && spec.n_terms == 1 && fkind >= GPX_SE && fkind <= GPX_EXPONENTIAL;
-  const bool se1 = fast && fkind == GPX_SE && fdn == 1;
   const double fvar = sth[spec.terms[0].param_offset + 1];
   const double finv_ell = 1.0 / sth[spec.terms[0].param_offset];
   const double xscale = fast ? sth[spec.terms[0].param_offset] : 1.0;
   const double noise = sth[spec.n_params];
-  const int nx = 16 * D;
   double sums[NT][3];
 #pragma unroll
   for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
@@ -419,36 +570,32 @@ __global__ __launch_bounds__(64, Q <= 1 ? 2 : 1) void band16_bwd_kernel(BandFuse
 #pragma unroll
   for (int e = 0; e < NS; ++e) S[e] = tzero();
   double al[Q + 1];  // α_{k+i}[l15], i = 1..Q
+  t4 R[Q + 1];       // band check: row-sum partials of blocks k+i (rows 4r + l4, unreduced over l15)
 #pragma unroll
-  for (int i = 0; i <= Q; ++i) al[i] = 0.0;
+  for (int i = 0; i <= Q; ++i) {
+    al[i] = 0.0;
+    R[i] = tzero();
+  }
   Q_BEGIN
   for (int k = nb - 1; k >= 0; --k) {
     const int qk = min(Q, nb - 1 - k), k16 = k * 16, cs = k % (Q + 1);
-    double zr[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) zr[r] = z[k16 + 4 * r + l4];
-    double xr[2];  // X rows of block k (the first 128 values; D <= 8 covers all of them)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int e = lane + 64 * h;
-      xr[h] = (e < nx) ? X[(long long)k16 * D + min(e, n * D - k16 * D - 1)] : 0.0;
-    }
-    // this step's W_kk and P_iᵀ from the staging tiles
-    vm_drain();
-    wsync();
+    // this step's W_kk and P_iᵀ (landed: drained at the end of the previous step)
     const t4 Wf = lds_n(sin_[0], l15, l4);
     t4 P[Q + 1];  // P_iᵀ, then G_i
 #pragma unroll
     for (int i = 1; i <= Q; ++i) P[i] = (i <= qk) ? lds_t(sin_[i], l15, l4) : tzero();
-    wsync();
-    // the next step's (k − 1) inputs, in flight during this step
-    if (k > 0) {
-      const int k1 = k16 - 16, q1 = min(Q, nb - k);
-      tile_glds(W + (long long)k1 * ld + k1, ld, sin_[0], lane);
+    // X rows of block k -> ring slot cs (scaled by 1/ℓ as GPflow's Stationary.scale when fast)
 #pragma unroll
-      for (int i = 1; i <= Q; ++i)
-        if (i <= q1) tile_glds(L + (long long)(k1 + 16 * i) * ld + k1, ld, sin_[i], lane);
+    for (int h = 0; h < 2; ++h) {
+      const int e = lane + 64 * h;
+      if (e < nx) sx[cs * nx + e] = (k16 + e / D < n) ? xr[h] / xscale : 0.0;
     }
+    for (int e = lane + 128; e < nx; e += 64) sx[cs * nx + e] = (k16 + e / D < n) ? X[(long long)k16 * D + e] / xscale : 0.0;
+    const double zc[4] = {zr[0], zr[1], zr[2], zr[3]};
+    lds_drain();
+    wsync();
+    // the next step's inputs, in flight during this step
+    if (k > 0) fetch(k - 1, zr, xr);
     QP(0);
     // α_k = W_kkᵀ (z_k − Σ_i P_iᵀ α_{k+i})
     double t[4] = {0.0, 0.0, 0.0, 0.0};
@@ -460,20 +607,10 @@ __global__ __launch_bounds__(64, Q <= 1 ? 2 : 1) void band16_bwd_kernel(BandFuse
       }
     double ap = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ap = fma(Wf[r], zr[r] - sum16(t[r]), ap);
+    for (int r = 0; r < 4; ++r) ap = fma(Wf[r], zc[r] - sum16(t[r]), ap);
     ap = sum4(ap);
     al[0] = ap;
-    if (l4 == 0) {
-      alpha[k16 + l15] = ap;
-      sal[cs][l15] = ap;
-    }
-    // X rows of block k -> ring slot cs (scaled by 1/ℓ as GPflow's Stationary.scale when fast)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int e = lane + 64 * h;
-      if (e < nx) sx[cs * nx + e] = (k16 + e / D < n) ? xr[h] / xscale : 0.0;
-    }
-    for (int e = lane + 128; e < nx; e += 64) sx[cs * nx + e] = (k16 + e / D < n) ? X[(long long)k16 * D + e] / xscale : 0.0;
+    if (l4 == 0) sal[cs][l15] = ap;
     QP(1);
     // G_i = P_i W_kk
 #pragma unroll
@@ -510,18 +647,6 @@ __global__ __launch_bounds__(64, Q <= 1 ? 2 : 1) void band16_bwd_kernel(BandFuse
 #pragma unroll
     for (int i = 1; i <= Q; ++i)
       if (i <= qk) mms(Zk, P[i], Zn[i]);
-    // diag(Z) -> K's diagonal (band_train_pred_kernel); the step's Z tiles -> LDS for the contraction
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (4 * r + l4 == l15) Kd[(long long)(k16 + l15) * ld + k16 + l15] = Zk[r];
-      sz[0][(4 * r + l4) * 16 + l15] = Zk[r];
-    }
-#pragma unroll
-    for (int i = 1; i <= Q; ++i)
-      if (i <= qk) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sz[i][(4 * r + l4) * 16 + l15] = Zn[i][r];
-      }
     wsync();
     QP(4);
     // gradient contraction and the band check's K∘Z sums over tile i (0: Z_kk whole, weight 1;
@@ -530,77 +655,139 @@ __global__ __launch_bounds__(64, Q <= 1 ? 2 : 1) void band16_bwd_kernel(BandFuse
     const bool jok = gj < n;
     const double* xj = sx + cs * nx + l15 * D;
     double colacc = 0.0;
-    for (int i = 0; i <= qk; ++i) {
-      const int si = (k + i) % (Q + 1);
-      const double w = i == 0 ? 1.0 : 2.0;
-      double rowp[4];
+    if constexpr (SE1) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int il = 4 * r + l4, gi = (k + i) * 16 + il;
-        const double zij = sz[i][il * 16 + l15];
-        const double ai = sal[si][il];
-        const double* xi = sx + si * nx + il * D;
-        const bool ok = jok && gi < n;
-        const bool dg = gi == gj;
-        const double v = w * fma(ai, ap, -zij);
-        double kij;
-        if (se1) {
-          const double r2 = sqdist1(xi[fd0], xj[fd0]);
-          const double g = exp(-0.5 * r2);
-          kij = fvar * g;
-          sums[0][0] = ok ? fma(v, fvar * g * r2 * finv_ell, sums[0][0]) : sums[0][0];
-          sums[0][1] = ok ? fma(v, g, sums[0][1]) : sums[0][1];
-        } else if (ok) {
-          double dk[NT][3];
-          if (fast) {
-            double d1[3];
-            stationary_grad(fkind, sqdist_scaled(xi + fd0, xj + fd0, fdn), fvar, finv_ell, d1);
-            dk[0][0] = d1[0]; dk[0][1] = d1[1]; dk[0][2] = d1[2];
-            kij = fvar * d1[1];
-          } else {
-            kij = eval_k_grad<NT>(spec, sth, xi, xj, dk);
-          }
-#pragma unroll
-          for (int q = 0; q < NT; ++q) {
-            sums[q][0] = fma(v, dk[q][0], sums[q][0]);
-            sums[q][1] = fma(v, dk[q][1], sums[q][1]);
-            sums[q][2] = fma(v, dk[q][2], sums[q][2]);
-          }
-        } else {
-          kij = 0.0;
-        }
-        if (dg) kij += noise;
-        snoise = (ok && dg) ? snoise + v : snoise;
-        const double kz = ok ? kij * zij : 0.0;
-        colacc += kz;
-        rowp[r] = kz;
-      }
-      if (i > 0) {  // row sums of tile (k+i, k): the upper-band part of block k+i's columns
+      for (int i = 0; i <= Q; ++i) {
+        if (i > qk) continue;
+        const t4& Zt = (i == 0) ? Zk : Zn[i];
+        const int si = (k + i) % (Q + 1);
+        const double w = i == 0 ? 1.0 : 2.0;
+        const double xjv = xj[fd0];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const double s = sum16(rowp[r]);
-          if (l15 == 0) srs[si][4 * r + l4] += s;
+          const int il = 4 * r + l4, gi = (k + i) * 16 + il;
+          const double zij = Zt[r];
+          const double ai = sal[si][il];
+          const double r2 = sqdist1(sx[si * nx + il * D + fd0], xjv);
+          const double g = exp(-0.5 * r2);
+          const double v = w * fma(ai, ap, -zij);
+          const bool ok = jok && gi < n;
+          const bool dg = i == 0 && gi == gj;
+          const double kij = fvar * g + (dg ? noise : 0.0);
+          const double kz = ok ? kij * zij : 0.0;
+          sums[0][0] = ok ? fma(v, fvar * g * r2 * finv_ell, sums[0][0]) : sums[0][0];
+          sums[0][1] = ok ? fma(v, g, sums[0][1]) : sums[0][1];
+          snoise = (ok && dg) ? snoise + v : snoise;
+          colacc += kz;
+          if (i > 0) R[i][r] += kz;
+        }
+      }
+    } else {
+      // generic kernels: the step's tiles through LDS and a runtime loop (the term interpreter
+      // is large; unrolled per tile it would not fit the registers)
+#pragma unroll
+      for (int i = 0; i <= Q; ++i)
+        if (i <= qk) {
+          const t4& Zt = (i == 0) ? Zk : Zn[i];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sz[i][(4 * r + l4) * 16 + l15] = Zt[r];
+        }
+      wsync();
+      double rowp[Q + 1][4];
+#pragma unroll
+      for (int i = 0; i <= Q; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rowp[i][r] = 0.0;
+      for (int i = 0; i <= qk; ++i) {
+        const int si = (k + i) % (Q + 1);
+        const double w = i == 0 ? 1.0 : 2.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int il = 4 * r + l4, gi = (k + i) * 16 + il;
+          const double zij = sz[i][il * 16 + l15];
+          const double ai = sal[si][il];
+          const double* xi = sx + si * nx + il * D;
+          const bool ok = jok && gi < n;
+          const bool dg = i == 0 && gi == gj;
+          const double v = w * fma(ai, ap, -zij);
+          double kij = 0.0;
+          if (ok) {
+            double dk[NT][3];
+            if (fast) {
+              double d1[3];
+              stationary_grad(fkind, sqdist_scaled(xi + fd0, xj + fd0, fdn), fvar, finv_ell, d1);
+              dk[0][0] = d1[0]; dk[0][1] = d1[1]; dk[0][2] = d1[2];
+              kij = fvar * d1[1];
+            } else {
+              kij = eval_k_grad<NT>(spec, sth, xi, xj, dk);
+            }
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+              sums[q][0] = fma(v, dk[q][0], sums[q][0]);
+              sums[q][1] = fma(v, dk[q][1], sums[q][1]);
+              sums[q][2] = fma(v, dk[q][2], sums[q][2]);
+            }
+          }
+          if (dg) kij += noise;
+          snoise = (ok && dg) ? snoise + v : snoise;
+          const double kz = ok ? kij * zij : 0.0;
+          colacc += kz;
+          // (runtime i: the row partials go to a statically indexed slot)
+#pragma unroll
+          for (int q = 1; q <= Q; ++q) rowp[q][r] = (q == i) ? kz : rowp[q][r];
+        }
+      }
+#pragma unroll
+      for (int i = 1; i <= Q; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) R[i][r] += rowp[i][r];
+    }
+    QP(5);
+    // band check: block k's lower-band column sums; block k+Q is complete (its last upper-band
+    // tile was (k+Q, k)): its row sums (R[Q], reduced over the row's 16 lanes) + column sums
+    colacc = sum4(colacc);
+    if (l4 == 0) scs[cs][l15] = colacc;
+    auto finish = [&](int m, const t4& Rm) {
+      const int sm = m % (Q + 1);
+      wsync();
+      if (l15 == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[4 * r + l4] = Rm[r];  // (reduced below, before the store)
+      }
+      wsync();
+      if (lane < 16) {
+        const int g = m * 16 + lane;
+        const double tot = scs[sm][lane] + sc[lane];
+        if (g < n) resmax = (tot == tot) ? fmax(resmax, fabs(tot - 1.0)) : INFINITY;
+        scs[sm][lane] = 0.0;
+      }
+    };
+    {
+      t4 Rq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Rq[r] = sum16(R[Q][r]);
+      wsync();
+      if (k + Q < nb) finish(k + Q, Rq);
+    }
+    if (k == 0) {
+#pragma unroll
+      for (int m = Q - 1; m >= 0; --m) {
+        if (m < nb) {
+          t4 Rm;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Rm[r] = sum16(R[m][r]);
+          finish(m, Rm);
         }
       }
     }
-    QP(5);
-    colacc = sum4(colacc);
-    if (l4 == 0) scs[cs][l15] = colacc;
+    // this step's inputs for the next one have landed; this step's outputs go out after the
+    // wait (α_k, diag(Z_kk) on K's diagonal for band_train_pred_kernel)
+    vm_drain();
     wsync();
-    // block k + Q is complete (its last upper-band tile was (k+Q, k)); blocks Q−1 .. 0 at the end
-    if (lane < 16) {
-      auto finish = [&](int m) {
-        const int sm = m % (Q + 1), g = m * 16 + lane;
-        const double tot = scs[sm][lane] + srs[sm][lane];
-        if (g < n) resmax = (tot == tot) ? fmax(resmax, fabs(tot - 1.0)) : INFINITY;
-        scs[sm][lane] = 0.0;
-        srs[sm][lane] = 0.0;
-      };
-      if (k + Q < nb) finish(k + Q);
-      if (k == 0)
-        for (int m = min(Q, nb) - 1; m >= 0; --m) finish(m);
-    }
-    wsync();
+    if (l4 == 0) alpha[k16 + l15] = ap;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * r + l4 == l15) Kd[(long long)(k16 + l15) * ld + k16 + l15] = Zk[r];
     // move the window up one block: S'_{11} = Z_kk, S'_{i+1,1} = Z_{k+i,k}, S'_{i+1,j+1} = S_ij
 #pragma unroll
     for (int i = Q; i >= 2; --i) {
@@ -610,7 +797,11 @@ __global__ __launch_bounds__(64, Q <= 1 ? 2 : 1) void band16_bwd_kernel(BandFuse
     }
     S[wid(0, 0)] = Zk;
 #pragma unroll
-    for (int i = Q; i >= 1; --i) al[i] = al[i - 1];
+    for (int i = Q; i >= 1; --i) {
+      al[i] = al[i - 1];
+      R[i] = R[i - 1];
+    }
+    R[1] = tzero();
     QP(6);
   }
   Q_END(1);
@@ -652,9 +843,10 @@ __global__ __launch_bounds__(64, Q <= 1 ? 2 : 1) void band16_bwd_kernel(BandFuse
 }
 
 template <int Q>
-static void launch16_q(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s, hipEvent_t* ev) {
-  auto bwd = max_terms <= 1 ? band16_bwd_kernel<Q, 1> : max_terms == 2 ? band16_bwd_kernel<Q, 2>
-                                                                       : band16_bwd_kernel<Q, GPX_MAX_TERMS>;
+static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, int n_active, hipStream_t s, hipEvent_t* ev) {
+  auto bwd = se1 ? band16_bwd_kernel<Q, 1, true>
+                 : max_terms <= 1 ? band16_bwd_kernel<Q, 1, false>
+                                  : max_terms == 2 ? band16_bwd_kernel<Q, 2, false> : band16_bwd_kernel<Q, GPX_MAX_TERMS, false>;
   const size_t xs = (size_t)(Q + 1) * 16 * a.D * sizeof(double);
   if (ev) {
     hipExtLaunchKernelGGL(band16_fwd_kernel<Q>, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
@@ -665,12 +857,13 @@ static void launch16_q(const BandFusedArgs& a, int max_terms, int n_active, hipS
   hipLaunchKernelGGL(bwd, dim3(n_active), dim3(64), xs, s, a);
 }
 
-void launch_band16(const BandFusedArgs& a, int Q, int max_terms, int n_active, hipStream_t s, hipEvent_t* ev) {
+void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int n_active, hipStream_t s,
+                   hipEvent_t* ev) {
   switch (Q) {
-    case 1: launch16_q<1>(a, max_terms, n_active, s, ev); break;
-    case 2: launch16_q<2>(a, max_terms, n_active, s, ev); break;
-    case 3: launch16_q<3>(a, max_terms, n_active, s, ev); break;
-    default: launch16_q<4>(a, max_terms, n_active, s, ev); break;
+    case 1: launch16_q<1>(a, max_terms, se1, n_active, s, ev); break;
+    case 2: launch16_q<2>(a, max_terms, se1, n_active, s, ev); break;
+    case 3: launch16_q<3>(a, max_terms, se1, n_active, s, ev); break;
+    default: launch16_q<4>(a, max_terms, se1, n_active, s, ev); break;
   }
 }
 

@@ -222,7 +222,7 @@ bool band_shape(const gpx_batch* bt);  // the banded path handles this batch's p
 int band_limit(const gpx_batch* bt);  // largest p the banded path takes (-1: path disabled)
 void band_eval(const Run& r, int p, int max_terms);  // build .. reduce for a banded active set
 // p <= 2: [band16 groups (sizes g16_n, widths g16_q) | p<=1 (n1) | p=2]
-void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, int n1,
+void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int n1,
                      int max_terms, hipEvent_t* ev = nullptr, hipEvent_t (*ev16)[4] = nullptr);
 double band_fused_flops(int Np, int p, bool fwd);  // block-product flops of one problem's sweep
 void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W = L⁻¹)

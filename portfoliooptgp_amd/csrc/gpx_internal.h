@@ -167,8 +167,8 @@ void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipS
 void launch_band_fused1(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s,
                         hipEvent_t* ev = nullptr);
 // 16-row blocks, one wavefront per problem (gpx_band16.hip); bandp holds each problem's band in
-// 16-blocks, all <= Q
-void launch_band16(const BandFusedArgs& a, int Q, int max_terms, int n_active, hipStream_t s,
+// 16-blocks, all <= Q; se1: every problem is one SquaredExponential term on one input column
+void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int n_active, hipStream_t s,
                    hipEvent_t* ev = nullptr);
 void launch_band_solve(const BandSolveArgs& a, int n_active, hipStream_t s);
 void launch_band_transpose(const BandTransposeArgs& a, int q, int n_active, hipStream_t s);
