@@ -214,14 +214,16 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 256)),
                     help="independent series fitted per GPU per step")
-    # band storage (25 MiB per slot) lets 1536 slots stay resident: every device call then
-    # carries ~320 problems, so the chip's 512 two-per-CU places stay full while a batch is on
-    # the host (dense layout, 384 MiB per slot: 576 slots, 3833–3955 fits/s)
-    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 1536)),
+    # band storage (25 MiB per slot) lets 4096 slots stay resident (100 GB of the 288): the
+    # band16 sweeps run one wavefront per problem, so the chip's ~2048 wave places need ~2000
+    # problems in flight (1536 slots: 5370 fits/s, 4096: 5847 at 2 processes, round 3)
+    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 4096)),
                     help="resident device slots per GPU (continuous-batching width), split over --procs")
-    ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 4)),
+    ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 2)),
                     help="device batches kept in flight by each host process")
-    ap.add_argument("--procs", type=int, default=int(os.environ.get("GPX_BENCH_PROCS", 2)),
+    # 4 processes x 4 HIP hardware queues: the GPU's queue scheduler time-slices once the
+    # processes' queues exceed ~16 (2 x 8: 6167 fits/s; 3 x 4: 6898; 4 x 4: 7102; round 3)
+    ap.add_argument("--procs", type=int, default=int(os.environ.get("GPX_BENCH_PROCS", 4)),
                     help="host processes per GPU (the rank + procs-1 spawned helpers)")
     ap.add_argument("--storage", choices=("band", "dense"), default=os.environ.get("GPX_BENCH_STORAGE", "band"),
                     help="slot workspace: band storage (gpx_batch_create_banded, 25 MiB per slot) or the "
@@ -450,10 +452,10 @@ def secondary_c5(gpu, reps=20):
 
 def main():
     # HIP hardware queues for this process (and the helpers, which inherit the environment), set
-    # before the runtime starts: each process's 4 device batches evaluate on their own streams
-    # (+ one forked stream for the p = 2 class); with the runtime's default 4 queues some of
-    # them share a queue and serialise (3 batches: 2460–2630 fits/s at 4 queues, 2800 at 8)
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPX_HW_QUEUES", "8")
+    # before the runtime starts: each process's 2 device batches evaluate on their own streams
+    # (+ the forked p = 2 and fallback streams); over all the GPU's processes the queues stay
+    # within what the queue scheduler maps at once (4 processes x 4)
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPX_HW_QUEUES", "4")
     # driver phase times (host share of the timed region), cheap perf_counter reads
     os.environ.setdefault("GPX_DRIVER_STATS", "1")
     argv = sys.argv[1:]
