@@ -202,7 +202,9 @@ def contract_traffic(n, flops_per_launch):
 SUM_FIELDS = ("contract_ms_total", "contract_launches", "contract_alg_flops", "eval_ms_total", "evals",
               "band_ms_total", "band_calls", "band_evals", "band_p_sum", "band_fallbacks", "shadow_evals",
               "shadow_predicts")
-NARROW_FIELDS = ("band_fwd_ms_total", "band_bwd_ms_total", "band_fused_launches", "band_fwd_flops", "band_bwd_flops")
+NARROW_FIELDS = ("band_fwd_ms_total", "band_bwd_ms_total", "band_fused_launches", "band_fwd_flops", "band_bwd_flops",
+                 "band16_fwd_ms_total", "band16_bwd_ms_total", "band16_launches", "band16_evals", "band16_q_sum",
+                 "band16_fwd_flops", "band16_bwd_flops")
 
 
 def parse_args(argv=None):
@@ -551,41 +553,57 @@ def main():
     value = total_fits / elapsed
     n = args.n
 
-    # roofline: the fused sweep kernel with the most device time (both reported), when the fits'
-    # evaluations take the banded path (C2: every evaluation); the dense contraction otherwise
+    # roofline: the banded sweep kernel with the most device time, when the fits' evaluations take
+    # the banded path (C2: every evaluation); the dense contraction otherwise.
+    #   band16 (16-row blocks, one wavefront per problem; most C2 evaluations): achieved = the
+    #     MFMA flops its problems issue (2*16^3 per tile product; gpx_api.hip band16_flops) / the
+    #     launch's HIP-event duration
+    #   64-row fused sweeps (the wider bands): the 64^3 block products (leaf 2/3 of one)
     sweeps = {}
-    for key, ms, fl, fwd in (("band_fwd1_kernel", tm["band_fwd_ms_total"], tm["band_fwd_flops"], True),
-                             ("band_bwd1_kernel<1>", tm["band_bwd_ms_total"], tm["band_bwd_flops"], False)):
-        launches = tm["band_fused_launches"]
-        b_ms = ms / max(launches, 1.0)
-        b_fl = fl / max(launches, 1.0)
+    for key, ms, fl, la in (("band16_fwd_kernel", tm["band16_fwd_ms_total"], tm["band16_fwd_flops"], tm["band16_launches"]),
+                            ("band16_bwd_kernel", tm["band16_bwd_ms_total"], tm["band16_bwd_flops"], tm["band16_launches"]),
+                            ("band_fwd1_kernel", tm["band_fwd_ms_total"], tm["band_fwd_flops"], tm["band_fused_launches"]),
+                            ("band_bwd1_kernel<1>", tm["band_bwd_ms_total"], tm["band_bwd_flops"], tm["band_fused_launches"])):
+        b_ms = ms / max(la, 1.0)
+        b_fl = fl / max(la, 1.0)
         ach = b_fl / (b_ms * 1e-3) / 1e12 if b_ms > 0 else 0.0
-        traffic, src = band_traffic(key.split("<")[0], b_fl / band_problem_flops(n, 1, fwd)) if b_fl > 0 else (None, None)
-        sweeps[key] = {"achieved": ach, "frac": ach / FP64_PEAK_TFLOPS, "avg_launch_ms": b_ms, "launches": launches,
-                       "alg_flops_per_launch": b_fl, "traffic": traffic, "traffic_source": src, "ms_total": ms}
+        sweeps[key] = {"achieved": ach, "frac": ach / FP64_PEAK_TFLOPS, "avg_launch_ms": b_ms, "launches": la,
+                       "alg_flops_per_launch": b_fl, "ms_total": ms}
+    e16 = tm["band16_evals"]
+    q_mean = tm["band16_q_sum"] / max(e16, 1.0)
+    for key in ("band16_fwd_kernel", "band16_bwd_kernel"):
+        k = sweeps[key]
+        ppl = e16 / max(k["launches"], 1.0)  # problems per launch
+        k["traffic"], k["traffic_source"] = band_traffic(key, ppl) if ppl > 0 else (None, None)
+    for key, fwd in (("band_fwd1_kernel", True), ("band_bwd1_kernel<1>", False)):
+        k = sweeps[key]
+        ppl = k["alg_flops_per_launch"] / band_problem_flops(n, 1, fwd)
+        k["traffic"], k["traffic_source"] = band_traffic(key.split("<")[0], ppl) if ppl > 0 else (None, None)
     from_p = tm["band_p_sum"] / max(tm["band_evals"], 1.0)
-    f2 = min(max(from_p - 1.0, 0.0), 1.0)
-    per_eval = ((1.0 - f2) * (band_problem_flops(n, 1, True) + band_problem_flops(n, 1, False))
-                + f2 * (band_problem_flops(n, 2, True) + band_problem_flops(n, 2, False)))
-    chip_ach = tm["band_evals"] * per_eval / elapsed / 1e12
+    # the whole chip over the timed region: the MFMA flops of every banded evaluation (band16
+    # tile products + the 64-row sweeps' block products) / wall time
+    # (the 64-row sweeps' flops are those of their timed launch pairs: the p <= 1 class's when the
+    # call has one, else the p = 2 class's)
+    chip_fl = tm["band16_fwd_flops"] + tm["band16_bwd_flops"] + tm["band_fwd_flops"] + tm["band_bwd_flops"]
+    chip_ach = chip_fl / elapsed / 1e12
     kname = max(sweeps, key=lambda k: sweeps[k]["ms_total"])
     if sweeps[kname]["ms_total"] > tm["contract_ms_total"]:
         k = sweeps[kname]
+        b16 = kname.startswith("band16")
         roofline = {
-            "kernel": f"{kname} (p<=1 class: one workgroup walks a problem's 64 block steps)",
+            "kernel": (f"{kname}<Q> (16-row blocks, one wavefront walks a problem's 256 block steps; mean Q {q_mean:.2f})"
+                       if b16 else f"{kname} (p<=1 class: one workgroup walks a problem's 64 block steps)"),
             "bound": "mfma", "achieved": k["achieved"], "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": k["frac"], "traffic": k["traffic"], "traffic_source": k["traffic_source"],
             "traffic_unit": "bytes/launch", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
             "alg_flops_per_launch": k["alg_flops_per_launch"], "mean_p_blocks": from_p,
-            # both fused sweeps of the p <= 1 class, each timed at its launches' actual start/end
-            "fwd1_frac": sweeps["band_fwd1_kernel"]["frac"], "bwd1_frac": sweeps["band_bwd1_kernel<1>"]["frac"],
-            "fwd1_avg_launch_ms": sweeps["band_fwd1_kernel"]["avg_launch_ms"],
-            "bwd1_avg_launch_ms": sweeps["band_bwd1_kernel<1>"]["avg_launch_ms"],
-            # the whole chip over the timed region: every banded evaluation's block products
-            # (both sweeps; p = 1 and p = 2 classes mixed by the mean band width) / wall time
+            "band16_share_of_band_evals": e16 / max(tm["band_evals"], 1.0), "band16_mean_q": q_mean,
+            "sweeps": {kk: {f: v[f] for f in ("achieved", "frac", "avg_launch_ms", "launches", "traffic")}
+                       for kk, v in sweeps.items() if v["launches"] > 0},
             "chip_achieved": chip_ach, "chip_frac": chip_ach / FP64_PEAK_TFLOPS,
-            "note": ("banded path (DESIGN.md §3c): achieved = the 64^3 block products a launch's problems issue "
-                     "(2*64^3 flops each, leaf 2/3 of one) / the launch's HIP-event duration; launches of "
+            "note": ("banded path (DESIGN.md §3c/§3d): achieved = the MFMA flops a launch's problems issue (band16: "
+                     "2*16^3 per 16x16x16 tile product, the 16x16 leaves' VALU work not counted; 64-row sweeps: "
+                     "2*64^3 per block product, leaf 2/3 of one) / the launch's HIP-event duration; launches of "
                      "several device batches and host processes overlap on the GPU; traffic: the kernel's "
                      "profiles/<round>_band*_traffic.json x problems per launch"),
         }

@@ -510,7 +510,10 @@ __global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel
   extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1))
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   __shared__ __attribute__((aligned(16))) double sin_[Q + 1][256];  // next step's W_kk (0), P_i (i), by glds
-  __shared__ __attribute__((aligned(16))) double sz[Q + 1][256];    // this step's Z_kk (0), Z_{k+i,k} (i)
+  // SE1: the K tiles (k+i, k) as built, double-buffered by step parity (the next step's are
+  // fetched by glds while this step's are contracted); otherwise the step's Z tiles for the
+  // runtime contraction loop
+  __shared__ __attribute__((aligned(16))) double sz[SE1 ? 2 * (Q + 1) : Q + 1][256];
   __shared__ double sal[Q + 1][16];                    // α ring
   __shared__ double scs[Q + 1][16];                    // band check: column sums ring
   __shared__ double sth[GPX_THETA_STRIDE];
@@ -533,6 +536,11 @@ __global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel
 #pragma unroll
     for (int i = 1; i <= Q; ++i)
       if (i <= q1) tile_glds(L + (long long)(c16 + 16 * i) * ld + c16, ld, sin_[i], lane);
+    if constexpr (SE1) {
+#pragma unroll
+      for (int i = 0; i <= Q; ++i)
+        if (i <= q1) tile_glds(Kd + (long long)(c16 + 16 * i) * ld + c16, ld, sz[(kk & 1) * (Q + 1) + i], lane);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) zr[r] = z[c16 + 4 * r + l4];
 #pragma unroll
@@ -656,28 +664,34 @@ __global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel
     const double* xj = sx + cs * nx + l15 * D;
     double colacc = 0.0;
     if constexpr (SE1) {
+      // K_ij from the built band (the same var·exp(−r²/2) bits the exp would give; entries in
+      // 64-block offset >= 2 are the exact zeros of the p64 <= 1 class; the diagonal tile mirrored
+      // from its lower triangle): ∂K/∂ℓ = K r²/ℓ, and Σ v ∂K/∂σ² = (Σ v K)/σ² at the end
+      const double xjv = xj[fd0];
 #pragma unroll
       for (int i = 0; i <= Q; ++i) {
         if (i > qk) continue;
         const t4& Zt = (i == 0) ? Zk : Zn[i];
         const int si = (k + i) % (Q + 1);
         const double w = i == 0 ? 1.0 : 2.0;
-        const double xjv = xj[fd0];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int il = 4 * r + l4, gi = (k + i) * 16 + il;
           const double zij = Zt[r];
           const double ai = sal[si][il];
           const double r2 = sqdist1(sx[si * nx + il * D + fd0], xjv);
-          const double g = exp(-0.5 * r2);
+          const bool up = i == 0 && il < l15;
+          const double kraw = sz[(k & 1) * (Q + 1) + i][up ? l15 * 16 + il : il * 16 + l15];
+          const bool zero = (gi >> 6) - (gj >> 6) >= 2;
           const double v = w * fma(ai, ap, -zij);
           const bool ok = jok && gi < n;
-          const bool dg = i == 0 && gi == gj;
-          const double kij = fvar * g + (dg ? noise : 0.0);
-          const double kz = ok ? kij * zij : 0.0;
-          sums[0][0] = ok ? fma(v, fvar * g * r2 * finv_ell, sums[0][0]) : sums[0][0];
-          sums[0][1] = ok ? fma(v, g, sums[0][1]) : sums[0][1];
+          const bool dg = i == 0 && il == l15;
+          const double kij = (zero || !ok) ? 0.0 : kraw;
+          const double kg = ok ? (dg ? fvar : kij) : 0.0;  // σ²·g (the noise is not part of ∂K/∂θ)
+          sums[0][0] = fma(v, kg * r2 * finv_ell, sums[0][0]);
+          sums[0][1] = fma(v, kg, sums[0][1]);
           snoise = (ok && dg) ? snoise + v : snoise;
+          const double kz = kij * zij;
           colacc += kz;
           if (i > 0) R[i][r] += kz;
         }
@@ -817,6 +831,7 @@ __global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel
   for (int t = 0; t < GPX_MAX_TERMS; ++t)
 #pragma unroll
     for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wsum64(sums[t][q]) : 0.0;
+  if (SE1) vals[1] /= fvar;  // Σ v σ² g -> Σ v ∂K/∂σ²
   vals[GPX_MAX_TERMS * 3] = wsum64(snoise);
   if (lane == 0) {
 #pragma unroll

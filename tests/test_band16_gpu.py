@@ -52,6 +52,7 @@ def test_band16_equals_band64_and_dense_n4096():
     t = eng.last_timing()
     assert not i16.any()
     assert t.band16_evals == 6 and t.band_evals == 6, (t.band16_evals, t.band_evals)
+    assert t.band_fallbacks == 0, t.band_fallbacks  # every band check passed
     qs = t.band16_q_sum
     assert qs == 1 + 2 + 3 + 3 + 4 + 4, qs
     m16, v16, _ = eng._predict_train(np.arange(6, dtype=np.int32), th, False)
@@ -94,6 +95,7 @@ def test_band16_against_oracle_n1024(fam, ell):
     eng.reset_timing()
     loss, g = m.loss_and_grad_unconstrained()
     assert eng.last_timing().band16_evals == 1, "expected the band16 path"
+    assert eng.last_timing().band_fallbacks == 0
     lo, go = om.loss_and_grad_u()
     cond = _cond(x, ko, 1e-5)
     check_loss(loss, lo, cond)
@@ -157,3 +159,32 @@ def test_band16_check_forced_failure_falls_back():
     with _Dense():
         ld, gd, _ = eng.lml_grad([0], th)
     assert lb[0] == ld[0] and np.array_equal(gb[0, :3], gd[0, :3])
+
+
+def test_band16_irregular_spacing_matches_dense():
+    """Irregularly spaced inputs (trading days with gaps: every K tile differs from its
+    neighbours, so a tile staged for the wrong block step would show): band16 vs the dense path
+    at N = 4096 over the band16 widths, no band-check fallback."""
+    n = 4096
+    rng = np.random.default_rng(11)
+    xs, ys = [], []
+    for s in range(4):
+        gaps = 1.0 + rng.choice([0.0, 0.0, 0.0, 0.0, 2.0], size=n) + 0.3 * rng.random(n)
+        x = np.cumsum(gaps)[:, None] - 1.0
+        xs.append(x)
+        ys.append(O.synthetic_series(n, seed=20 + s)[1])
+    eng = _engine(xs, ys, K.SquaredExponential())
+    th = _theta(eng, [(1.0, 1.0, 1e-5), (1.4, 0.7, 1e-5), (1.6, 0.9, 1e-5), (1.2, 1.2, 1e-5)])
+    act = [0, 1, 2, 3]
+    eng.reset_timing()
+    lb, gb, ib = eng.lml_grad(act, th)
+    t = eng.last_timing()
+    assert not ib.any() and t.band16_evals == 4 and t.band_fallbacks == 0, (t.band16_evals, t.band_fallbacks)
+    mb, vb, _ = eng._predict_train(np.arange(4, dtype=np.int32), th, False)
+    with _Dense():
+        ld, gd, _ = eng.lml_grad(act, th)
+        md, vd, _ = eng._predict_train(np.arange(4, dtype=np.int32), th, False)
+    _close(lb, gb, ld, gd, 3, "band16 vs dense (irregular)")
+    for b in range(4):
+        np.testing.assert_allclose(mb[b].cpu().numpy(), md[b].cpu().numpy(), rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(vb[b].cpu().numpy(), vd[b].cpu().numpy(), rtol=1e-7, atol=1e-13)

@@ -66,7 +66,7 @@ def main():
            "ms_per_round": dt / a.reps * 1e3, "band_evals": evals,
            "fwd1_avg_ms": fl("band_fwd_ms_total") / max(fl("band_fused_launches"), 1),
            "bwd1_avg_ms": fl("band_bwd_ms_total") / max(fl("band_fused_launches"), 1),
-           "mean_p": fl("band_p_sum") / max(evals, 1),
+           "mean_p": fl("band_p_sum") / max(evals, 1), "check_fallbacks": fl("band_fallbacks"),
            "chip_tflops": evals * per_eval / dt / 1e12}
     out["chip_frac"] = out["chip_tflops"] / FP64_PEAK_TFLOPS
     e16 = fl("band16_evals")
