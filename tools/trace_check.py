@@ -2,7 +2,7 @@
 of the same command: that kernel's dispatches between the bench's two timed-region markers (the
 spin kernel of torch.cuda._sleep) are averaged and compared with the bench line's
 roofline.avg_launch_ms / launches. The kernel is the one the bench line names: the fused
-banded sweep (band_bwd1_kernel / band_fwd1_kernel) or the dense fused contraction.
+banded sweep (band16_bwd/fwd_kernel, band_bwd1/fwd1_kernel) or the dense fused contraction.
 
 usage: python tools/trace_check.py TRACE_CSV[.gz] BENCH_LOG OUT.json
 """
@@ -18,7 +18,8 @@ def is_contract(name: str) -> bool:
 
 def matcher(bench_kernel: str):
     """Trace-name predicate for the kernel a bench line's roofline names."""
-    for tag in ("band_bwd1_kernel", "band_fwd1_kernel", "band_bwd_kernel", "band_fwd_kernel"):
+    for tag in ("band16_bwd_kernel", "band16_fwd_kernel", "band_bwd1_kernel", "band_fwd1_kernel", "band_bwd_kernel",
+                "band_fwd_kernel"):
         if bench_kernel.startswith(tag):
             return lambda name, tag=tag: tag + "<" in name or tag + "(" in name
     return is_contract
