@@ -452,8 +452,8 @@ double band16_flops(int Np, int Q, bool fwd) {
   return f;
 }
 
-void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int n1,
-                     int max_terms, hipEvent_t* ev, hipEvent_t (*ev16)[4]) {
+void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int kband16,
+                     int n1, int max_terms, hipEvent_t* ev, hipEvent_t (*ev16)[4]) {
   // r's active range is [band16 problems (n16, by width group) | p <= 1 problems (n1) | p = 2
   // problems]; the p = 2 class runs as a separate launch pair on an auxiliary stream concurrently
   gpx_batch* bt = r.bt;
@@ -490,11 +490,25 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     launch_band_fused(f2, max_terms, r.na - nlo, s2, n1 == 0 ? ev : nullptr);
   }
   if (nlo > 0) {
-    ba.band1 = 2;
-    launch_build(ba, nlo, r.s);
+    // the band16 class's K band: kband16 64-block diagonals (3 when it holds p = 2 problems)
+    if (n16 > 0 && kband16 != 2) {
+      BuildArgs b16 = ba;
+      b16.band1 = kband16;
+      launch_build(b16, n16, r.s);
+      if (n1 > 0) {
+        BuildArgs b1 = ba;
+        b1.active = r.d_act + n16;
+        b1.band1 = 2;
+        launch_build(b1, n1, r.s);
+      }
+    } else {
+      ba.band1 = 2;
+      launch_build(ba, nlo, r.s);
+    }
     int off = 0;
     for (int g = 0; g < n_g16; ++g) {
       BandFusedArgs f16 = fa;
+      f16.kband = n16 > 0 ? kband16 : 2;
       f16.active = r.d_act + off;
       launch_band16(f16, g16_q[g], max_terms, se1, g16_n[g], r.s, ev16 ? ev16[g] : nullptr);
       off += g16_n[g];
@@ -1247,19 +1261,21 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   const bool fused_on = !(ef && atoi(ef) == 0);
   const int q16lim = fused_on ? band16_limit(bt) : -1;
   std::vector<int32_t> b16_ids[kBand16MaxQ + 1];  // band16 class by width Q (16-blocks)
+  bool b16_p2 = false;                             // ... holding p = 2 problems (K band of 3 diagonals)
   for (int i = 0; i < n_active; ++i) {
     const int b = active[i];
     const double* thb = theta + (size_t)b * GPX_THETA_STRIDE;
     const int p = plim >= 0 ? band_width(bt, b, thb) : -1;
     if (p >= 0 && p <= plim) {
       bt->h_bandp[b] = p;
-      // p <= 1 problems whose band is at most kBand16MaxQ 16-blocks: the band16 sweeps
-      const int q16 = (p <= 1 && q16lim > 0) ? band_width16(bt, b, thb) : -1;
+      // p <= 2 problems whose band is at most kBand16MaxQ 16-blocks: the band16 sweeps
+      const int q16 = (p <= 2 && q16lim > 0) ? band_width16(bt, b, thb) : -1;
       // the p = 2 sweep holds four 64x64 LDS blocks plus three 64·D X-row slots (<= 160 KiB)
       if (q16 >= 0 && q16 <= q16lim) {
         const int Q = std::max(q16, 1);
         bt->h_bandp[b] = Q;
         b16_ids[Q].push_back(b);
+        b16_p2 = b16_p2 || p == 2;
       } else if (fused_on && (p <= 1 || (p == 2 && bt->D <= 12))) {
         fused_ids.push_back(b);
         pfused = std::max(pfused, p);
@@ -1458,7 +1474,8 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
       const gpx_kernel_spec& sp = bt->specs[order[i]];
       se1 = se1 && sp.n_terms == 1 && sp.terms[0].kind == GPX_SE && sp.terms[0].dim_count == 1;
     }
-    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, n16, n_g16, g16_q, g16_n, se1, n_fused1,
+    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, n16, n_g16, g16_q, g16_n, se1,
+                    b16_p2 ? 3 : 2, n_fused1,
                     max_terms, (ctx->profiling && old_fused) ? fqe : nullptr, ctx->profiling ? pe->fq16 : nullptr);
   }
   bp.mark();

@@ -7,7 +7,7 @@
 // every ∂K/∂θ vanish exactly (exp underflow) outside the band. What changes is the granularity:
 //
 //   * blocks are 16 rows, one v_mfma_f64_16x16x4_f64 tile, and the band is Q 16-blocks wide
-//     (Q = 1..4: at the reference's day-offset inputs and ℓ ∈ [1, 1.68], the band of exact
+//     (Q = 1..5: at the reference's day-offset inputs and ℓ ∈ [1, 1.68], the band of exact
 //     nonzeros is 39-65 entries: Q = 3-4 instead of the 64-row kernels' 128-wide two-block band,
 //     so a step multiplies ~(56/96)² of the 64-row kernels' block entries and none of the
 //     exactly-zero triangles of the 64-row blocks);
@@ -26,8 +26,8 @@
 //     on row-layout registers.
 //
 // Inputs / outputs are those of band_fwd1_kernel / band_bwd1_kernel (the host picks this class
-// for problems with p64 <= 1 and Q <= 4): K's band as built with two 64-block diagonals
-// (entries in 64-block offset >= 2 are read as the exact zeros they are for p64 <= 1),
+// for problems with p64 <= 2 and Q <= 5): K's band as built with kband = p64max + 1 64-block
+// diagonals (entries in 64-block offset >= kband are read as the exact zeros they are),
 // L (the 16x16 panels P_i = L_{k+i,k}), W (the diagonal blocks W_kk = L_kk⁻¹), z, log L_ii,
 // α, diag(Z) on K's diagonal (band_train_pred_kernel), the per-problem [16] gradient partial
 // row, results[kResBandCheck] = max_j |Σ_i K_ji Z_ij − 1|, info (first failing pivot).
@@ -329,16 +329,17 @@ __device__ __forceinline__ void leaf16m(t4 A, t4& V, t4& Wr, double& lii, int& f
 }
 
 // frag of A_{bi,bj}ᵀ (bi >= bj, 16-blocks) from K's stored lower band; entries in 64-block
-// offset >= 2 read as 0 (exact for the class this file serves, p64 <= 1); the diagonal tile
-// from its lower triangle
-__device__ __forceinline__ t4 ktile_t(const double* __restrict__ K, long long ld, int bi, int bj, int l15, int l4) {
+// offset >= kband (beyond the built band) read as 0 (exact: the class's p64 < kband); the
+// diagonal tile from its lower triangle
+__device__ __forceinline__ t4 ktile_t(const double* __restrict__ K, long long ld, int bi, int bj, int l15, int l4,
+                                      int kband) {
   t4 t;
   const int gi = bi * 16 + l15;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int gj = bj * 16 + 4 * r + l4;
     const int i0 = max(gi, gj), j0 = min(gi, gj);
-    const bool z = (i0 >> 6) - (j0 >> 6) >= 2;
+    const bool z = (i0 >> 6) - (j0 >> 6) >= kband;
     const double v = K[(long long)i0 * ld + (z ? i0 : j0)];
     t[r] = z ? 0.0 : v;
   }
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? 2 : 1) void band16_fwd_kernel(BandFuse
   for (int i = 0; i <= Q; ++i) {
     u[i] = 0.0;
 #pragma unroll
-    for (int j = 0; j <= i; ++j) T[wid(i, j)] = (i < nb) ? ktile_t(K, ld, i, j, l15, l4) : tzero();
+    for (int j = 0; j <= i; ++j) T[wid(i, j)] = (i < nb) ? ktile_t(K, ld, i, j, l15, l4, a.kband) : tzero();
   }
   int gfail = 0;
   Q_BEGIN
@@ -478,7 +479,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? 2 : 1) void band16_fwd_kernel(BandFuse
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int cl = 4 * r + l4, gj = (k + 1 + j) * 16 + cl;
-          const bool zero = (gi >> 6) - (gj >> 6) >= 2;
+          const bool zero = (gi >> 6) - (gj >> 6) >= a.kband;
           const double v = (j == Q && cl > l15) ? snew[j][cl * 16 + l15] : snew[j][l15 * 16 + cl];
           t[r] = zero ? 0.0 : v;
         }
@@ -507,6 +508,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? 2 : 1) void band16_fwd_kernel(BandFuse
 // input column): the contraction is a straight-line loop (contract_block_se1's operations).
 template <int Q, int NT, bool SE1>
 __global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
+  static_assert(!SE1 || Q <= 4, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 4");
   extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1))
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   __shared__ __attribute__((aligned(16))) double sin_[Q + 1][256];  // next step's W_kk (0), P_i (i), by glds
@@ -665,7 +667,7 @@ __global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel
     double colacc = 0.0;
     if constexpr (SE1) {
       // K_ij from the built band (the same var·exp(−r²/2) bits the exp would give; entries in
-      // 64-block offset >= 2 are the exact zeros of the p64 <= 1 class; the diagonal tile mirrored
+      // 64-block offset >= kband are the exact zeros of the class; the diagonal tile mirrored
       // from its lower triangle): ∂K/∂ℓ = K r²/ℓ, and Σ v ∂K/∂σ² = (Σ v K)/σ² at the end
       const double xjv = xj[fd0];
 #pragma unroll
@@ -682,7 +684,7 @@ __global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel
           const double r2 = sqdist1(sx[si * nx + il * D + fd0], xjv);
           const bool up = i == 0 && il < l15;
           const double kraw = sz[(k & 1) * (Q + 1) + i][up ? l15 * 16 + il : il * 16 + l15];
-          const bool zero = (gi >> 6) - (gj >> 6) >= 2;
+          const bool zero = (gi >> 6) - (gj >> 6) >= a.kband;
           const double v = w * fma(ai, ap, -zij);
           const bool ok = jok && gi < n;
           const bool dg = i == 0 && il == l15;
@@ -859,9 +861,10 @@ __global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel
 
 template <int Q>
 static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, int n_active, hipStream_t s, hipEvent_t* ev) {
-  auto bwd = se1 ? band16_bwd_kernel<Q, 1, true>
-                 : max_terms <= 1 ? band16_bwd_kernel<Q, 1, false>
-                                  : max_terms == 2 ? band16_bwd_kernel<Q, 2, false> : band16_bwd_kernel<Q, GPX_MAX_TERMS, false>;
+  auto bwd = (se1 && Q <= 4) ? band16_bwd_kernel<Q, 1, (Q <= 4)>
+                             : max_terms <= 1 ? band16_bwd_kernel<Q, 1, false>
+                                              : max_terms == 2 ? band16_bwd_kernel<Q, 2, false>
+                                                               : band16_bwd_kernel<Q, GPX_MAX_TERMS, false>;
   const size_t xs = (size_t)(Q + 1) * 16 * a.D * sizeof(double);
   if (ev) {
     hipExtLaunchKernelGGL(band16_fwd_kernel<Q>, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
@@ -878,7 +881,8 @@ void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int n
     case 1: launch16_q<1>(a, max_terms, se1, n_active, s, ev); break;
     case 2: launch16_q<2>(a, max_terms, se1, n_active, s, ev); break;
     case 3: launch16_q<3>(a, max_terms, se1, n_active, s, ev); break;
-    default: launch16_q<4>(a, max_terms, se1, n_active, s, ev); break;
+    case 4: launch16_q<4>(a, max_terms, se1, n_active, s, ev); break;
+    default: launch16_q<5>(a, max_terms, se1, n_active, s, ev); break;
   }
 }
 

@@ -159,7 +159,7 @@ inline long long mat_stride(const gpx_batch* bt) { return bt->smat ? bt->smat : 
 inline int mat_ld(const gpx_batch* bt) { return bt->ldm ? bt->ldm : bt->Np; }
 constexpr int kBandStoreP = 2;     // band width (64-blocks) held by band storage
 constexpr int kBox = 16;           // rows per bounding box of the band tables (16: the band16 path's block)
-constexpr int kBand16MaxQ = 4;     // widest band (16-blocks) of the band16 kernels (gpx_band16.hip)
+constexpr int kBand16MaxQ = 5;     // widest band (16-blocks) of the band16 kernels (gpx_band16.hip)
 constexpr int kBand16MaxD = 8;     // input columns the band16 backward sweep stages per block
 constexpr int kBand16MaxNp = 8192;
 constexpr int kShadowSlots = 4;    // dense fallback slots of a band-storage batch
@@ -221,9 +221,10 @@ int band16_limit(const gpx_batch* bt);  // widest band16 class (16-blocks), -1: 
 bool band_shape(const gpx_batch* bt);  // the banded path handles this batch's padded size
 int band_limit(const gpx_batch* bt);  // largest p the banded path takes (-1: path disabled)
 void band_eval(const Run& r, int p, int max_terms);  // build .. reduce for a banded active set
-// p <= 2: [band16 groups (sizes g16_n, widths g16_q) | p<=1 (n1) | p=2]
-void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int n1,
-                     int max_terms, hipEvent_t* ev = nullptr, hipEvent_t (*ev16)[4] = nullptr);
+// p <= 2: [band16 groups (sizes g16_n, widths g16_q; K band of kband16 64-block diagonals) |
+// p<=1 (n1) | p=2]
+void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int kband16,
+                     int n1, int max_terms, hipEvent_t* ev = nullptr, hipEvent_t (*ev16)[4] = nullptr);
 double band_fused_flops(int Np, int p, bool fwd);  // block-product flops of one problem's sweep
 void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W = L⁻¹)
 void alpha_solve(const Run& r);  // z = W y, α = Wᵀ z

@@ -160,6 +160,8 @@ struct BandFusedArgs {
   double* results;                               // [B][kResStride]: writes [kResBandCheck]
   int Np;
   int ld;                                        // leading dimension of K/L/W (Np, or band storage's)
+  int kband;                                     // band16: K's band was built with this many 64-block
+                                                 // diagonals; entries beyond read as 0 (exact)
 };
 void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s,
                        hipEvent_t* ev = nullptr);  // ev[4]: fwd start/stop, bwd start/stop

@@ -188,3 +188,24 @@ def test_band16_irregular_spacing_matches_dense():
     for b in range(4):
         np.testing.assert_allclose(mb[b].cpu().numpy(), md[b].cpu().numpy(), rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(vb[b].cpu().numpy(), vd[b].cpu().numpy(), rtol=1e-7, atol=1e-13)
+
+
+def test_band16_wide_class_p64_2():
+    """ℓ = 1.8 and 2.0 at the C2 inputs: p64 = 2 (K built with three 64-block diagonals) and
+    Q = 5 (the generic-contraction sweep): band16 vs the 64-row p = 2 sweep and the dense path."""
+    n = 4096
+    data = [O.synthetic_series(n, seed=30 + s) for s in range(3)]
+    eng = _engine([d[0] for d in data], [d[1] for d in data], K.SquaredExponential())
+    th = _theta(eng, [(1.8, 0.9, 1e-5), (2.0, 1.1, 1e-5), (1.2, 0.8, 1e-5)])
+    act = [0, 1, 2]
+    eng.reset_timing()
+    lb, gb, ib = eng.lml_grad(act, th)
+    t = eng.last_timing()
+    assert not ib.any() and t.band16_evals == 3 and t.band_fallbacks == 0, (t.band16_evals, t.band_fallbacks)
+    assert t.band16_q_sum == 5 + 5 + 3, t.band16_q_sum
+    with _no16():
+        l64, g64, _ = eng.lml_grad(act, th)
+    _close(lb, gb, l64, g64, 3, "band16 vs band64 (p = 2)")
+    with _Dense():
+        ld, gd, _ = eng.lml_grad(act, th)
+    _close(lb, gb, ld, gd, 3, "band16 vs dense (p = 2)")
