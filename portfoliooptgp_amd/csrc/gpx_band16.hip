@@ -85,11 +85,10 @@ __device__ __forceinline__ void mms(t4& c, const t4& x, const t4& y) {
   for (int kk = 0; kk < 4; ++kk) c = __builtin_amdgcn_mfma_f64_16x16x4f64(-x[kk], y[kk], c, 0, 0, 0);
 }
 
-// store the transpose of the tile whose fragment is t at g
-__device__ __forceinline__ void st_t(const t4& t, double* __restrict__ g, long long ld, int l15, int l4) {
-  double* p = g + (long long)l15 * ld + l4;
+// store the transpose of the tile whose fragment is t at g (uniform); lane offset lo = l15·ld + l4
+__device__ __forceinline__ void st_t(const t4& t, double* __restrict__ g, int lo) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) p[4 * r] = t[r];
+  for (int r = 0; r < 4; ++r) g[lo + 4 * r] = t[r];
 }
 
 // sums over the 4 lanes l4 = 0..3 of a column (lanes l15 + 16·l4: v_permlane32_swap and
@@ -303,15 +302,10 @@ __device__ __forceinline__ void leaf16m(t4 A, t4& V, t4& Wr, double& lii, int& f
     double xb = 0.0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) xb = fma(m[c], lrow[c], xb);
-    const int rb = l15 - 4 * jb;  // row within the block
-    double ld = 0.0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int c = 0; c <= a; ++c) ld = (rb == a && l4 == c) ? l[a][c] : ld;
-    xb = rb >= 4 ? xb : 0.0;                     // rows below the block only
-    const double x = (rb >= 0 && rb < 4) ? ld : xb;
-    A = __builtin_amdgcn_mfma_f64_16x16x4f64(-x, x, A, 0, 0, 0);  // trailing update (rank 4)
+    // rows below the block only: the update of the block's own rows and columns (L_d L_dᵀ) is
+    // never read again, so the block rows of the panel are left at 0
+    xb = l15 - 4 * jb >= 4 ? xb : 0.0;
+    A = __builtin_amdgcn_mfma_f64_16x16x4f64(-xb, xb, A, 0, 0, 0);  // trailing update (rank 4)
     // block row jb of L⁻¹: Li · (its current rows), then the rows below
     double wn = 0.0;
 #pragma unroll
@@ -374,6 +368,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? 2 : 1) void band16_fwd_kernel(BandFuse
   const double* y = a.Y + (long long)b * a.sY;
   const int n = a.nvalid[b];
   const int lane = threadIdx.x, l15 = lane & 15, l4 = lane >> 4;
+  const int lane_off = l15 * (int)ld + l4;  // this lane's element of a transposed tile store
   constexpr int NW = (Q + 1) * (Q + 2) / 2;
   t4 T[NW];
   double u[Q + 1];
@@ -454,14 +449,14 @@ __global__ __launch_bounds__(64, Q <= 3 ? 2 : 1) void band16_fwd_kernel(BandFuse
     // W_kk (row-major), L_ii, z_k and the panels P_i = L_{k+i,k}
     vm_drain();
     wsync();
-    st_t(V, W + (long long)k16 * ld + k16, ld, l15, l4);
+    st_t(V, W + (long long)k16 * (ld + 1), lane_off);
     if (l4 == 0) {
       ldiag[k16 + l15] = lii;
       z[k16 + l15] = zp;
     }
 #pragma unroll
     for (int i = 1; i <= Q; ++i)
-      if (i <= qk) st_t(T[wid(i, 0)], L + (long long)(k16 + 16 * i) * ld + k16, ld, l15, l4);
+      if (i <= qk) st_t(T[wid(i, 0)], L + (long long)(k16 + 16 * i) * ld + k16, lane_off);
     // move the window down one block; its new row from LDS (fragments of A_{bn, k+1+j}ᵀ, entries
     // in 64-block offset >= 2 as exact zeros, the diagonal tile mirrored from its lower triangle)
 #pragma unroll
@@ -763,38 +758,29 @@ __global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel
     // tile was (k+Q, k)): its row sums (R[Q], reduced over the row's 16 lanes) + column sums
     colacc = sum4(colacc);
     if (l4 == 0) scs[cs][l15] = colacc;
+    // Rm: block m's upper-band row partials (unreduced over the 16 lanes of a row): through the
+    // scratch as a 16x16 tile, each of lanes 0..15 sums one row
     auto finish = [&](int m, const t4& Rm) {
       const int sm = m % (Q + 1);
       wsync();
-      if (l15 == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sc[4 * r + l4] = Rm[r];  // (reduced below, before the store)
-      }
+      for (int r = 0; r < 4; ++r) sc[(4 * r + l4) * kSC + l15] = Rm[r];
       wsync();
       if (lane < 16) {
+        double rs = 0.0;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) rs += sc[lane * kSC + c];
         const int g = m * 16 + lane;
-        const double tot = scs[sm][lane] + sc[lane];
+        const double tot = scs[sm][lane] + rs;
         if (g < n) resmax = (tot == tot) ? fmax(resmax, fabs(tot - 1.0)) : INFINITY;
         scs[sm][lane] = 0.0;
       }
     };
-    {
-      t4 Rq;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Rq[r] = sum16(R[Q][r]);
-      wsync();
-      if (k + Q < nb) finish(k + Q, Rq);
-    }
+    if (k + Q < nb) finish(k + Q, R[Q]);
     if (k == 0) {
 #pragma unroll
-      for (int m = Q - 1; m >= 0; --m) {
-        if (m < nb) {
-          t4 Rm;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Rm[r] = sum16(R[m][r]);
-          finish(m, Rm);
-        }
-      }
+      for (int m = Q - 1; m >= 0; --m)
+        if (m < nb) finish(m, R[m]);
     }
     // this step's inputs for the next one have landed; this step's outputs go out after the
     // wait (α_k, diag(Z_kk) on K's diagonal for band_train_pred_kernel)
