@@ -353,7 +353,7 @@ constexpr __host__ __device__ int wid(int i, int j) { return i * (i + 1) / 2 + j
 // then the window moves down one block; its new row (block k+Q+1) is loaded during the step.
 // ---------------------------------------------------------------------------------------
 template <int Q>
-__global__ __launch_bounds__(64, Q <= 3 ? 2 : 1) void band16_fwd_kernel(BandFusedArgs a) {
+__global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFusedArgs a) {
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   __shared__ __attribute__((aligned(16))) double snew[Q + 1][256];  // the entering row, staged by glds
   __shared__ double sv[16];
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? 2 : 1) void band16_fwd_kernel(BandFuse
 // SE1: every problem of the launch is the reference's kernel (one SquaredExponential term on one
 // input column): the contraction is a straight-line loop (contract_block_se1's operations).
 template <int Q, int NT, bool SE1>
-__global__ __launch_bounds__(64, (Q <= 1 && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
+__global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
   static_assert(!SE1 || Q <= 4, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 4");
   extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1))
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];

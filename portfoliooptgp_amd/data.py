@@ -7,17 +7,30 @@ z-scored (pandas ddof=1) ``return`` = ``close.pct_change()`` with row 0 filled b
 return (or ``intraday_return`` = (close − open)/open). The network fetch (:15-24) and the
 entropy prints (:46-53) are out of scope. ``future_inputs`` restates ``generate_future_dates``
 (:67-90). ``load_series`` reads many tickers at once into the ragged lists the batched engine
-(``Engine`` / ``Scipy().minimize_stream`` / ``distributed.fit_assets``) consumes.
+(``Engine`` / ``Scipy().minimize_stream`` / ``distributed.fit_assets``) consumes;
+``load_batch`` does the same with the files parsed on a thread pool and every series landing on
+the device through ONE pinned host block and ONE host-to-device copy.
+
+The index series (``Stocks/Index/*/<name>.csv``) come from investing.com
+(``"Date","Price","Open","High","Low","Vol.","Change %"``, newest first, ``MM/DD/YYYY``);
+``convert_investing_csv`` restates ``handle.py:38-75`` (``convert_csv`` + ``sort_csv``) that turns
+them into the ``date,open,high,low,close,change,volume`` files next to them
+(``<name>_us_d.csv``), byte for byte (tests/test_data.py against the reference's own pairs).
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+import csv
+import io
+from concurrent.futures import ThreadPoolExecutor
+from datetime import datetime
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import pandas as pd
 import torch
 
 EOD_COLUMNS = ("date", "open", "high", "low", "close", "adjusted_close", "volume")
+INVESTING_OUT_COLUMNS = ("date", "open", "high", "low", "close", "change", "volume")
 
 
 def _frame(csv_path: str, train_start_date: str) -> pd.DataFrame:
@@ -67,4 +80,67 @@ def load_series(csv_paths: Sequence[str], train_start_date: str, predict_Y: str 
         X, Y, dates, mean, std = process_csv(p, train_start_date, predict_Y)
         series.append((X, Y))
         meta.append(dict(mean=mean, std=std, dates=dates, path=p))
+    return series, meta
+
+
+def investing_rows(input_file: str) -> List[Dict[str, str]]:
+    """The rows of an investing.com export in the converted schema, oldest first
+    (``handle.py:38-59`` per row: date ``MM/DD/YYYY`` -> ``YYYY-MM-DD``, ``Price`` -> close, an
+    empty ``Vol.`` -> ``'0'``; values kept as the file's strings, e.g. ``40,792.79``; then
+    ``sort_csv``'s stable sort by date, ``handle.py:61-75``)."""
+    rows = []
+    with open(input_file, "r", newline="") as f:
+        reader = csv.reader(f)
+        next(reader)  # header (the file's BOM is part of it)
+        for row in reader:
+            date = datetime.strptime(row[0].strip('"'), "%m/%d/%Y").strftime("%Y-%m-%d")
+            rows.append({"date": date, "open": row[2].strip('"'), "high": row[3].strip('"'),
+                         "low": row[4].strip('"'), "close": row[1].strip('"'), "change": row[6].strip('"'),
+                         "volume": row[5].strip('"') if row[5].strip('"') else "0"})
+    rows.sort(key=lambda r: datetime.strptime(r["date"], "%Y-%m-%d"))
+    return rows
+
+
+def convert_investing_csv(input_file: str, output_file: Optional[str] = None) -> str:
+    """Convert an investing.com export to the ``date,open,high,low,close,change,volume`` CSV the
+    reference keeps beside it; returns the text (csv module defaults: ``\\r\\n`` line ends, fields
+    with commas quoted) and writes it to ``output_file`` when given."""
+    buf = io.StringIO(newline="")
+    w = csv.DictWriter(buf, fieldnames=list(INVESTING_OUT_COLUMNS))
+    w.writeheader()
+    w.writerows(investing_rows(input_file))
+    text = buf.getvalue()
+    if output_file is not None:
+        with open(output_file, "w", newline="") as f:
+            f.write(text)
+    return text
+
+
+def load_batch(csv_paths: Sequence[str], train_start_date: str, predict_Y: str = "return",
+               device=None, workers: int = 8):
+    """Many tickers -> device-resident series for the batched fitters.
+
+    The files are parsed concurrently (pandas' C parser releases the GIL), each series'
+    (X, Y) written into one pinned [2, Σ N_b] float64 host block, which goes to ``device`` in one
+    copy; the returned X_b / Y_b ([N_b, 1]) are views of that device block (``Engine`` and
+    ``GPR`` take them as they are). Returns ([(X_b, Y_b)], [{mean, std, dates, path, n}]) with the
+    values of ``process_csv`` bit for bit."""
+    paths = list(csv_paths)
+    with ThreadPoolExecutor(max_workers=max(1, min(workers, len(paths) or 1))) as ex:
+        parts = list(ex.map(lambda p: process_csv(p, train_start_date, predict_Y), paths))
+    sizes = [int(X.shape[0]) for X, *_ in parts]
+    total = sum(sizes)
+    pin = device is not None and torch.device(device).type == "cuda"
+    host = torch.empty((2, total), dtype=torch.float64, pin_memory=pin)
+    off = 0
+    for (X, Y, *_), nb in zip(parts, sizes):
+        host[0, off:off + nb] = X[:, 0]
+        host[1, off:off + nb] = Y[:, 0]
+        off += nb
+    dev = host.to(device, non_blocking=pin) if device is not None else host
+    series, meta, off = [], [], 0
+    for p, (_, _, dates, mean, std), nb in zip(paths, parts, sizes):
+        series.append((dev[0, off:off + nb].view(nb, 1), dev[1, off:off + nb].view(nb, 1)))
+        meta.append(dict(mean=mean, std=std, dates=dates, path=p, n=nb))
+        off += nb
     return series, meta

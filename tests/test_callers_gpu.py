@@ -248,3 +248,36 @@ def test_fit_assets_to_portfolio_lists_on_device(golden_dir):
         np.testing.assert_allclose(np.diag(sig), [sum(float(v[0]) for v in vols[i][:day + 1]) for i in range(5)],
                                    rtol=1e-12)
         np.testing.assert_allclose(sd, [np.sqrt(float(vols[i][day][0])) for i in range(5)], rtol=1e-15)
+
+
+def test_load_batch_index_series_fit_on_device(golden_dir):
+    """f4 on the reference's own index data: the investing.com exports converted as handle.py
+    does (byte-identical to the reference's converted files, tests/test_data.py), loaded by
+    data.load_batch straight into one device block, and fitted there: the fits on the device
+    views are the fits on process_csv's host tensors bit for bit, and the logML at GPflow's
+    defaults matches the oracle."""
+    from portfoliooptgp_amd import data
+    paths = [os.path.join(golden_dir, "investing", f"{n}_us_d.csv") for n in ("RUT2000", "NasDaq100")]
+    series, meta = data.load_batch(paths, "2023-01-01", device=0)
+    assert all(x.device.type == "cuda" for x, _ in series)
+    for p, (xd, yd), mt in zip(paths, series, meta):
+        xh, yh, *_ = data.process_csv(p, "2023-01-01")
+        assert mt["n"] == 411
+        np.testing.assert_array_equal(xd.cpu().numpy(), xh.numpy())
+        np.testing.assert_array_equal(yd.cpu().numpy(), yh.numpy())
+        fits = []
+        for x, y in ((xd, yd), (xh, yh)):
+            m = gpx.models.GPR((x, y), kernel=K.SquaredExponential())
+            m.likelihood.variance.assign(1e-5)
+            gpx.set_trainable(m.likelihood.variance, False)
+            fits.append((m.loss_and_grad_unconstrained(),
+                         gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables,
+                                                         options=dict(maxiter=100))))
+        (l0, g0), r0 = fits[0]
+        (l1, g1), r1 = fits[1]
+        assert l0 == l1 and np.array_equal(g0, g1) and r0.fun == r1.fun and np.array_equal(r0.x, r1.x)
+        om = O.OGPR(xh.numpy(), yh.numpy(), O.OSquaredExponential(), noise_variance=1e-5)
+        om.noise.trainable = False
+        lo, go = om.loss_and_grad_u()
+        cond = _cond(om.kernel, xh.numpy(), 1e-5)
+        check_loss(l0, lo, cond)

@@ -1,5 +1,7 @@
 """f4: EODHD CSV → GP series (GPR/data_handler.py:26-90 semantics), against the oracle's
 restatement used to build the golden fixtures."""
+import os
+
 import numpy as np
 import pandas as pd
 import pytest
@@ -43,3 +45,32 @@ def test_future_inputs_periods(tmp_path):
     assert len(data.future_inputs(p, "2024-02-01", "m", 90)) == 3
     with pytest.raises(ValueError):
         data.future_inputs(p, "2024-02-01", "q")
+
+
+INVESTING = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "investing")
+
+
+@pytest.mark.parametrize("name", ["RUT2000", "DJI", "NasDaq100"])
+def test_convert_investing_csv_reproduces_reference_files(name, tmp_path):
+    """handle.py:38-75 (convert_csv + sort_csv) on the reference's own investing.com exports
+    reproduces the converted files the reference keeps beside them, byte for byte (DJI carries
+    quoted thousands separators, RUT2000 empty volumes, NasDaq100 'M' volume suffixes)."""
+    out = tmp_path / f"{name}_us_d.csv"
+    text = data.convert_investing_csv(os.path.join(INVESTING, f"{name}.csv"), str(out))
+    with open(os.path.join(INVESTING, f"{name}_us_d.csv"), newline="") as f:
+        ref = f.read()
+    assert text == ref
+    with open(out, newline="") as f:
+        assert f.read() == ref
+
+
+def test_load_batch_matches_process_csv(tmp_path):
+    paths = [_csv(tmp_path, 20 + 3 * s, 20 + s) for s in range(5)]
+    series, meta = data.load_batch(paths, "2024-01-15", "intraday_return", device=None, workers=3)
+    for p, (X, Y), m in zip(paths, series, meta):
+        Xr, Yr, dates, mean, std = data.process_csv(p, "2024-01-15", "intraday_return")
+        assert X.shape == Xr.shape and Y.shape == Yr.shape
+        np.testing.assert_array_equal(X.numpy(), Xr.numpy())
+        np.testing.assert_array_equal(Y.numpy(), Yr.numpy())
+        assert (m["mean"], m["std"], m["n"], m["path"]) == (mean, std, len(Xr), p)
+        assert X.is_contiguous() and Y.is_contiguous()
