@@ -28,6 +28,10 @@ try:  # scipy ≥ 1.15: the C port of L-BFGS-B (task codes as int32 pairs)
     AVAILABLE = hasattr(_lbfgsb, "setulb") and isinstance(status_messages, dict)
 except Exception:  # pragma: no cover - older scipy: callers use the threaded driver
     AVAILABLE = False
+if not AVAILABLE:  # pragma: no cover - said once, at import: the fits still run, more slowly
+    import warnings
+    warnings.warn("scipy's L-BFGS-B routine setulb (scipy >= 1.15 layout) is not available: batched fits use the "
+                  "threaded driver (one host thread per fit; same results, several times slower)", RuntimeWarning)
 
 # scipy 1.15 _minimize_lbfgsb defaults
 _DEFAULTS = dict(maxcor=10, ftol=2.2204460492503131e-09, gtol=1e-5, maxfun=15000, maxiter=15000, maxls=20)
