@@ -216,17 +216,35 @@ double band_arg(int kind, double s) {
 
 // band_rmin of problem b at block size bs (64: band_rmin, 16: band_rmin16) from the per-block
 // boxes lo/hi [nvb][D] of its valid rows (blocks of bs rows)
+// The widest band offset (in blocks of bs rows) any routing decision distinguishes: the 64-row
+// paths take p <= band_limit <= Np/256, the band16 path Q <= kBand16MaxQ; a table entry beyond
+// it only has to say "still nonzero" correctly, which a lower bound does.
+static int band_table_cap(const gpx_batch* bt, int bs) {
+  if (bs != kLeaf) return kBand16MaxQ + 1;
+  const char* ep = getenv("GPX_BAND_PMAX");  // (band_limit's override, when it raises the limit)
+  return std::max(bt->Np / kLeaf / 4, ep ? atoi(ep) : 0) + 1;
+}
+
 static void band_tables_lohi(gpx_batch* bt, int b, int bs, const std::vector<double>& lo,
                              const std::vector<double>& hi) {
   const int nb = bt->Np / bs, D = bt->D, n = bt->n[b];
   std::vector<double>& tabv = bs == kLeaf ? bt->band_rmin : bt->band_rmin16;
   double* out = tabv.data() + (size_t)b * GPX_MAX_TERMS * nb;
   std::fill(out, out + (size_t)GPX_MAX_TERMS * nb, INFINITY);
+  int* tail = (bs == kLeaf ? bt->band_tail : bt->band_tail16).data() + (size_t)b * GPX_MAX_TERMS;
+  std::fill(tail, tail + GPX_MAX_TERMS, nb);
   const gpx_kernel_spec& sp = bt->specs[b];
   const int nvb = (n + bs - 1) / bs;  // blocks holding valid rows
+  const int cap = band_table_cap(bt, bs);
   for (int t = 0; t < sp.n_terms; ++t) {
     const int d0 = sp.terms[t].dim_start, dn = sp.terms[t].dim_count;
     double* rt = out + (size_t)t * nb;
+    // one active dimension with the blocks' boxes in increasing order (day offsets): the gap
+    // between blocks k and k − dd is lo[k] − hi[k − dd], nondecreasing in dd for every k, so
+    // rmin is nondecreasing and rmin[cap] bounds every later entry from below
+    bool sorted = dn == 1;
+    for (int k = 1; sorted && k < nvb; ++k) sorted = hi[(size_t)(k - 1) * D + d0] <= lo[(size_t)k * D + d0];
+    const int ddmax = sorted ? std::min(nvb - 1, cap) : nvb - 1;
     double m2 = 0.0;  // max ‖x‖² over the valid rows (active dims), bounded by the boxes
     for (int k = 0; k < nvb; ++k) {
       double s2 = 0.0;
@@ -237,7 +255,7 @@ static void band_tables_lohi(gpx_batch* bt, int b, int bs, const std::vector<dou
       m2 = std::max(m2, s2);
     }
     rt[0] = std::sqrt(m2) * (1.0 + 1e-12);
-    for (int dd = 1; dd < nvb; ++dd) {
+    for (int dd = 1; dd <= ddmax; ++dd) {
       double m = INFINITY;
       for (int k = dd; k < nvb; ++k) {
         double g2 = 0.0;
@@ -251,6 +269,10 @@ static void band_tables_lohi(gpx_batch* bt, int b, int bs, const std::vector<dou
       // the box gap is exact in real arithmetic; shave a relative 1e-12 off for the rounding
       // of the sums above
       rt[dd] = std::sqrt(m) * (1.0 - 1e-12);
+    }
+    if (ddmax < nvb - 1) {
+      for (int dd = ddmax + 1; dd < nvb; ++dd) rt[dd] = rt[ddmax];
+      tail[t] = ddmax;
     }
   }
 }
@@ -301,8 +323,9 @@ static int band_width_bs(const gpx_batch* bt, int b, const double* th, int bs) {
     if (!band_kind(sp.terms[t].kind)) return -1;
   const int nb = bt->Np / bs;
   const double* tab = (bs == kLeaf ? bt->band_rmin : bt->band_rmin16).data() + (size_t)b * GPX_MAX_TERMS * nb;
+  const int* tail = (bs == kLeaf ? bt->band_tail : bt->band_tail16).data() + (size_t)b * GPX_MAX_TERMS;
   const bool prod = sp.n_terms > 1 && sp.combine == GPX_PRODUCT;
-  for (int d = nb - 1; d >= 1; --d) {
+  auto nz_at = [&](int d) {
     bool nz = prod;
     for (int t = 0; t < sp.n_terms; ++t) {
       const double ell = th[sp.terms[t].param_offset];
@@ -315,8 +338,18 @@ static int band_width_bs(const gpx_batch* bt, int b, const double* th, int bs) {
       }
       nz = prod ? (nz && term_nz) : (nz || term_nz);
     }
-    if (nz) return d;
+    return nz;
+  };
+  // beyond the largest tail offset every term's entry repeats, so the scan from the top gives the
+  // same answer as testing that offset once
+  int top = nb - 1, tmax = 0;
+  for (int t = 0; t < sp.n_terms; ++t) tmax = std::max(tmax, tail[t]);
+  if (tmax >= 1 && tmax < nb - 1) {
+    if (nz_at(tmax)) return nb - 1;
+    top = tmax - 1;
   }
+  for (int d = top; d >= 1; --d)
+    if (nz_at(d)) return d;
   return 0;
 }
 
@@ -879,7 +912,11 @@ static int batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, 
   bt->fac_valid.assign(B, 0);
   bt->fac_band.assign(B, 0);
   bt->band_rmin.assign((size_t)B * GPX_MAX_TERMS * (bt->Np / kLeaf), INFINITY);
-  if (bt->Np <= kBand16MaxNp) bt->band_rmin16.assign((size_t)B * GPX_MAX_TERMS * (bt->Np / kBox), INFINITY);
+  bt->band_tail.assign((size_t)B * GPX_MAX_TERMS, bt->Np / kLeaf);
+  if (bt->Np <= kBand16MaxNp) {
+    bt->band_rmin16.assign((size_t)B * GPX_MAX_TERMS * (bt->Np / kBox), INFINITY);
+    bt->band_tail16.assign((size_t)B * GPX_MAX_TERMS, bt->Np / kBox);
+  }
   if (band_shape(bt)) {
     std::vector<double> hx((size_t)B * N_max * D);
     if (hipMemcpy(hx.data(), X, sizeof(double) * hx.size(), hipMemcpyDeviceToHost) != hipSuccess)

@@ -413,16 +413,6 @@ __device__ __forceinline__ void block_store_lds(const double (&v)[16], double* _
 #pragma unroll
   for (int u = 0; u < 16; ++u) s[4 * u * BS] = v[u];
 }
-__device__ __forceinline__ void frag_load_lds(Frag& f, const double* __restrict__ s) {
-  const int t = tid_fresh();
-  s += ((t >> 7) * 32 + ((t & 63) >> 4)) * BS + ((t >> 6) & 1) * 32 + (t & 15);
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) f.c[m][n][r] = s[(m * 16 + 4 * r) * BS + n * 16];
-}
 // the diagonal of a fragment-held block -> global (the selected inverse's diag(K⁻¹), read by
 // band_train_pred_kernel)
 __device__ __forceinline__ void frag_store_diag(const Frag& f, double* __restrict__ g, int ld) {

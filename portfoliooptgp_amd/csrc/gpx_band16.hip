@@ -22,15 +22,17 @@
 //     come out as Pᵀ; the backward sweep loads W_kk and Pᵀ from global memory in the
 //     orientation it needs (a fragment load of a tile or of its transpose costs the same) and
 //     transposes the window's off-diagonal Z tiles through a 2 KiB LDS scratch;
-//   * the 16x16 diagonal Cholesky-and-inverse is the leaf's DPP-broadcast chain (gpx_leaf.h)
-//     on row-layout registers.
+//   * the 16x16 diagonal Cholesky-and-inverse (leaf16m) runs on the matrix cores: four rank-4
+//     steps, each a uniform 4x4 factorisation and two MFMAs (trailing update, L⁻¹ alongside).
 //
 // Inputs / outputs are those of band_fwd1_kernel / band_bwd1_kernel (the host picks this class
 // for problems with p64 <= 2 and Q <= 5): K's band as built with kband = p64max + 1 64-block
-// diagonals (entries in 64-block offset >= kband are read as the exact zeros they are),
-// L (the 16x16 panels P_i = L_{k+i,k}), W (the diagonal blocks W_kk = L_kk⁻¹), z, log L_ii,
-// α, diag(Z) on K's diagonal (band_train_pred_kernel), the per-problem [16] gradient partial
-// row, results[kResBandCheck] = max_j |Σ_i K_ji Z_ij − 1|, info (first failing pivot).
+// diagonals (entries in 64-block offset >= kband are read as the exact zeros they are), z,
+// log L_ii, α, diag(Z) on K's diagonal (band_train_pred_kernel), the per-problem [16] gradient
+// partial row, results[kResBandCheck] = max_j |Σ_i K_ji Z_ij − 1|, info (first failing pivot).
+// The factor itself (W_kk = L_kk⁻¹ and the panels P_i = L_{k+i,k}) goes from the forward to the
+// backward sweep through L's workspace in a private tile layout (frag_store below); the W
+// workspace is not used.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include "gpx_internal.h"
@@ -85,45 +87,30 @@ __device__ __forceinline__ void mms(t4& c, const t4& x, const t4& y) {
   for (int kk = 0; kk < 4; ++kk) c = __builtin_amdgcn_mfma_f64_16x16x4f64(-x[kk], y[kk], c, 0, 0, 0);
 }
 
-// store the transpose of the tile whose fragment is t at g (uniform); lane offset lo = l15·ld + l4
-__device__ __forceinline__ void st_t(const t4& t, double* __restrict__ g, int lo) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) g[lo + 4 * r] = t[r];
-}
-
-// sums over the 4 lanes l4 = 0..3 of a column (lanes l15 + 16·l4: v_permlane32_swap and
-// v_permlane16_swap, no LDS round trip) and over the 16 lanes of a row (DPP row broadcasts)
-__device__ __forceinline__ double xor_lanes(double v, bool sw32) {
+// sums over the 4 lanes l4 = 0..3 of a column (lanes l15 + 16·l4), no LDS round trip: with both
+// operands holding v, v_permlane32_swap leaves [A|A] and [B|B] (A, B: the wave's lower and upper
+// 32 lanes), whose sum is A + B on every lane; v_permlane16_swap does the same for adjacent
+// 16-lane rows. Every lane ends with the same bits (each add is commutative).
+__device__ __forceinline__ double swap_add(double v, bool sw32) {
   const unsigned long long u = __double_as_longlong(v);
   const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
-  const int lane = threadIdx.x & 63;
-  unsigned plo, phi;
-  if (sw32) {
-    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    const bool low = lane < 32;
-    plo = low ? a[1] : a[0];
-    phi = low ? b[1] : b[0];
-  } else {
-    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    const bool even = ((lane >> 4) & 1) == 0;
-    plo = even ? a[1] : a[0];
-    phi = even ? b[1] : b[0];
-  }
-  return __longlong_as_double(((unsigned long long)phi << 32) | plo);
+  const auto a = sw32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                      : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = sw32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                      : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double p = __longlong_as_double(((unsigned long long)b[0] << 32) | a[0]);
+  const double q = __longlong_as_double(((unsigned long long)b[1] << 32) | a[1]);
+  return p + q;
 }
-__device__ __forceinline__ double sum4(double v) {
-  v += xor_lanes(v, true);
-  v += xor_lanes(v, false);
-  return v;
-}
+__device__ __forceinline__ double sum4(double v) { return swap_add(swap_add(v, true), false); }
+// butterfly over the 16 lanes of a row: DPP quad_perm xor 1, xor 2, row_half_mirror, row_mirror
+// (four v_mov_b64_dpp + four adds; every lane ends with the same bits: each add is commutative)
 __device__ __forceinline__ double sum16(double v) {
-  double s[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    s[q] = (bc16(v, 4 * q) + bc16(v, 4 * q + 1)) + (bc16(v, 4 * q + 2) + bc16(v, 4 * q + 3));
-  return (s[0] + s[1]) + (s[2] + s[3]);
+  v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true);
+  v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true);
+  v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, true);
+  v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, true);
+  return v;
 }
 __device__ __forceinline__ double wsum64(double v) {
 #pragma unroll
@@ -146,20 +133,13 @@ __device__ __forceinline__ void tile_glds(const double* __restrict__ g, long lon
   __builtin_amdgcn_global_load_lds(g + (long long)row * ld + col, s, 16, 0, 0);
   __builtin_amdgcn_global_load_lds(g + (long long)(row + 8) * ld + col, s + 128, 16, 0, 0);
 }
-// fragments of an LDS tile (row-major, 16 doubles per row) and of its transpose
-__device__ __forceinline__ t4 lds_n(const double* __restrict__ s, int l15, int l4) {
-  t4 t;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t[r] = s[(4 * r + l4) * 16 + l15];
-  return t;
+// band16's private factor layout (forward sweep -> backward sweep; nothing else reads it): per
+// block step k, Q + 1 tiles of 256 doubles at L + (k·(Q+1) + i)·256 (i = 0: W_kk, i >= 1: P_iᵀ),
+// each stored as its C fragment with a lane's 4 doubles contiguous: a tile is one coalesced 2 KiB
+// store and one coalesced 2 KiB load (two 16-byte accesses per lane), straight into registers
+__device__ __forceinline__ void frag_store(const t4& t, double* __restrict__ g, int lane) {
+  *reinterpret_cast<t4*>(g + 4 * lane) = t;
 }
-__device__ __forceinline__ t4 lds_t(const double* __restrict__ s, int l15, int l4) {
-  t4 t;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t[r] = s[l15 * 16 + 4 * r + l4];
-  return t;
-}
-
 // transpose of a tile through the scratch
 __device__ __forceinline__ t4 tile_transpose(const t4& t, double* __restrict__ sc, int l15, int l4) {
   wsync();
@@ -170,59 +150,6 @@ __device__ __forceinline__ t4 tile_transpose(const t4& t, double* __restrict__ s
 #pragma unroll
   for (int r = 0; r < 4; ++r) o[r] = sc[l15 * kSC + 4 * r + l4];
   return o;
-}
-
-// 16x16 Cholesky-and-inverse of the symmetric tile A (fragment): V = fragment of (L⁻¹)ᵀ, lii =
-// L_{l15,l15}, fail = first pivot that is not > 0 (or −1). The diagonal chain is gpx_leaf.h's
-// (row layout: lane l15 holds row l15; DPP row broadcasts; rsqrt + two Newton steps; the inverse
-// by right-looking substitution, column l15 of L⁻¹ on lane l15).
-__device__ __forceinline__ void leaf16(const t4& A, t4& V, double& lii, int& fail, double* __restrict__ sc,
-                                       int l15, int l4) {
-  wsync();
-#pragma unroll
-  for (int r = 0; r < 4; ++r) sc[(4 * r + l4) * kSC + l15] = A[r];  // A row-major
-  wsync();
-  double rr[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) rr[c] = sc[l15 * kSC + c];  // row l15 of A (its lower part is read)
-  fail = -1;
-  double myinv = 0.0;  // 1/L_{l15,l15}
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const double piv = bc16(rr[j], j);
-    if (!(piv > 0.0) && fail < 0) fail = j;
-    const double inv = rsqrt_nr(piv);
-    const double ljj = piv * inv;
-    myinv = (l15 == j) ? inv : myinv;
-    rr[j] = (l15 > j) ? rr[j] * inv : ((l15 == j) ? ljj : 0.0);
-#pragma unroll
-    for (int k = j + 1; k < 16; ++k) rr[k] = fma(-rr[j], bc16(rr[j], k), rr[k]);
-    __builtin_amdgcn_sched_barrier(0);  // keep the broadcasts of later pivots from being hoisted
-  }
-  double w[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) w[i] = (i == l15) ? 1.0 : 0.0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    w[k] *= bc16(myinv, k);
-    double rk = rr[k];
-    asm volatile("" : "+v"(rk) : "v"(w[k]));
-#pragma unroll
-    for (int i = k + 1; i < 16; ++i) w[i] = fma(-bc16(rk, i), w[k], w[i]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  double d = 0.0;
-#pragma unroll
-  for (int c = 0; c < 16; ++c) d = (c == l15) ? rr[c] : d;
-  lii = d;
-  wsync();
-  if (l4 == 0) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sc[i * kSC + l15] = w[i];  // (L⁻¹)[i][l15], row-major
-  }
-  wsync();
-#pragma unroll
-  for (int r = 0; r < 4; ++r) V[r] = sc[l15 * kSC + 4 * r + l4];  // (L⁻¹)[l15][4r+l4]
 }
 
 // 16x16 Cholesky-and-inverse on the matrix cores: four 4-column steps, each a 4x4 diagonal
@@ -362,13 +289,11 @@ __global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFuse
   const long long ld = a.ld;
   const double* K = a.K + (long long)b * a.sMat;
   double* L = a.L + (long long)b * a.sMat;
-  double* W = a.W + (long long)b * a.sMat;
   double* z = a.z + (long long)b * a.sVec;
   double* ldiag = a.ldiag + (long long)b * a.sVec;
   const double* y = a.Y + (long long)b * a.sY;
   const int n = a.nvalid[b];
   const int lane = threadIdx.x, l15 = lane & 15, l4 = lane >> 4;
-  const int lane_off = l15 * (int)ld + l4;  // this lane's element of a transposed tile store
   constexpr int NW = (Q + 1) * (Q + 2) / 2;
   t4 T[NW];
   double u[Q + 1];
@@ -402,9 +327,11 @@ __global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFuse
     t4 V;
     double lii;
     int fl;
+    double* Lk = L + (long long)k * ((Q + 1) * 256);  // this step's tiles (private layout above)
     {
       t4 Wr;
       leaf16m(T[wid(0, 0)], V, Wr, lii, fl, sc, l15, l4);
+      frag_store(Wr, Lk, lane);  // W_kk
     }
     QP(1);
     if (fl >= 0 && gfail == 0) gfail = k16 + fl + 1;
@@ -430,6 +357,7 @@ __global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFuse
         t4 c = tzero();
         mma(c, V, T[wid(i, 0)]);
         T[wid(i, 0)] = c;
+        frag_store(c, Lk + i * 256, lane);  // P_iᵀ
         double s = 0.0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) s = fma(c[r], zr[r], s);
@@ -444,19 +372,14 @@ __global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFuse
       for (int j = 1; j <= i; ++j)
         if (i <= qk) mms(T[wid(i, j)], T[wid(j, 0)], T[wid(i, 0)]);
     QP(4);
-    // the new row has landed (this also retires the previous step's stores, long done); this
-    // step's outputs go out now, so that the next step's wait does not cover them early:
-    // W_kk (row-major), L_ii, z_k and the panels P_i = L_{k+i,k}
+    // the new row has landed (this also retires this step's tile stores, issued at the leaf and
+    // the panels); L_ii and z_k go out now
     vm_drain();
     wsync();
-    st_t(V, W + (long long)k16 * (ld + 1), lane_off);
     if (l4 == 0) {
       ldiag[k16 + l15] = lii;
       z[k16 + l15] = zp;
     }
-#pragma unroll
-    for (int i = 1; i <= Q; ++i)
-      if (i <= qk) st_t(T[wid(i, 0)], L + (long long)(k16 + 16 * i) * ld + k16, lane_off);
     // move the window down one block; its new row from LDS (fragments of A_{bn, k+1+j}ᵀ, entries
     // in 64-block offset >= 2 as exact zeros, the diagonal tile mirrored from its lower triangle)
 #pragma unroll
@@ -470,11 +393,11 @@ __global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFuse
     for (int j = 0; j <= Q; ++j) {
       t4 t = tzero();
       if (bn < nb) {
-        const int gi = bn * 16 + l15;
+        // (16-row blocks sit inside one 64-block: the 64-block offset is uniform over the tile)
+        const bool zero = (bn >> 2) - ((k + 1 + j) >> 2) >= a.kband;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int cl = 4 * r + l4, gj = (k + 1 + j) * 16 + cl;
-          const bool zero = (gi >> 6) - (gj >> 6) >= a.kband;
+          const int cl = 4 * r + l4;
           const double v = (j == Q && cl > l15) ? snew[j][cl * 16 + l15] : snew[j][l15 * 16 + cl];
           t[r] = zero ? 0.0 : v;
         }
@@ -504,14 +427,18 @@ __global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFuse
 template <int Q, int NT, bool SE1>
 __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
   static_assert(!SE1 || Q <= 4, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 4");
-  extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1))
+  extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1); not SE1)
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
-  __shared__ __attribute__((aligned(16))) double sin_[Q + 1][256];  // next step's W_kk (0), P_i (i), by glds
   // SE1: the K tiles (k+i, k) as built, double-buffered by step parity (the next step's are
   // fetched by glds while this step's are contracted); otherwise the step's Z tiles for the
   // runtime contraction loop
   __shared__ __attribute__((aligned(16))) double sz[SE1 ? 2 * (Q + 1) : Q + 1][256];
-  __shared__ double sal[Q + 1][16];                    // α ring
+  __shared__ double sal[SE1 ? 1 : Q + 1][16];          // α ring (not SE1)
+  // SE1: the α and x values of block m's rows in the contraction's lane order (lane (l15, l4)
+  // takes rows 4r + l4: element of row il at (il & 3)·4 + (il >> 2)), so a lane reads its four
+  // with two ds_read_b128 instead of four strided reads
+  __shared__ __attribute__((aligned(16))) double salT[SE1 ? Q + 1 : 1][16];
+  __shared__ __attribute__((aligned(16))) double sxT[SE1 ? Q + 1 : 1][16];
   __shared__ double scs[Q + 1][16];                    // band check: column sums ring
   __shared__ double sth[GPX_THETA_STRIDE];
   __shared__ double sred[GPX_MAX_TERMS * 3 + 2];
@@ -520,19 +447,15 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
   const long long ld = a.ld;
   double* Kd = a.K + (long long)b * a.sMat;           // diag(Z) goes on K's diagonal
   const double* L = a.L + (long long)b * a.sMat;
-  const double* W = a.W + (long long)b * a.sMat;
   const double* z = a.z + (long long)b * a.sVec;
   double* alpha = a.alpha + (long long)b * a.sVec;
   const double* X = a.X + (long long)b * a.sX;
   const int n = a.nvalid[b], D = a.D, nx = 16 * D;
   const int lane = threadIdx.x, l15 = lane & 15, l4 = lane >> 4;
-  // inputs of a step: W_kk and P_i by glds into sin_, z_k and the block's X rows into registers
+  // inputs of a step: z_k and the block's X rows into registers (and, SE1, the K tiles by glds),
+  // issued at the start of the step before
   auto fetch = [&](int kk, double (&zr)[4], double (&xr)[2]) {
     const int q1 = min(Q, nb - 1 - kk), c16 = kk * 16;
-    tile_glds(W + (long long)c16 * ld + c16, ld, sin_[0], lane);
-#pragma unroll
-    for (int i = 1; i <= Q; ++i)
-      if (i <= q1) tile_glds(L + (long long)(c16 + 16 * i) * ld + c16, ld, sin_[i], lane);
     if constexpr (SE1) {
 #pragma unroll
       for (int i = 0; i <= Q; ++i)
@@ -546,8 +469,20 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
       xr[h] = X[min((long long)c16 * D + e, (long long)n * D - 1)];  // (clamped into the slot's rows)
     }
   };
+  // W_kk and P_iᵀ (the forward sweep's tiles, frag_store layout) straight into registers: two
+  // 16-byte loads per lane and tile, issued once this step's P/G registers are dead (after Z_kk),
+  // so the prefetch needs no LDS and no extra registers
+  auto fetch_f = [&](int kk, t4& Wn, t4 (&Pn)[Q + 1]) {
+    const int q1 = min(Q, nb - 1 - kk);
+    const double* Lk = L + (long long)kk * ((Q + 1) * 256) + 4 * lane;
+    Wn = *reinterpret_cast<const t4*>(Lk);
+#pragma unroll
+    for (int i = 1; i <= Q; ++i) Pn[i] = (i <= q1) ? *reinterpret_cast<const t4*>(Lk + i * 256) : tzero();
+  };
   double zr[4], xr[2];
+  t4 Wn, Pn[Q + 1];
   fetch(nb - 1, zr, xr);
+  fetch_f(nb - 1, Wn, Pn);
   {  // the forward sweep left L_ii: log det's terms (read by the reduce kernel)
     double* ldg = a.ldiag + (long long)b * a.sVec;
     for (int e = lane; e < Np; e += 64) ldg[e] = log(ldg[e]);
@@ -555,7 +490,15 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
   if (lane < GPX_THETA_STRIDE) sth[lane] = a.theta[b * GPX_THETA_STRIDE + lane];
   if (lane < 16) {
 #pragma unroll
-    for (int m = 0; m <= Q; ++m) { sal[m][lane] = 0.0; scs[m][lane] = 0.0; }
+    for (int m = 0; m <= Q; ++m) {
+      scs[m][lane] = 0.0;
+      if constexpr (SE1) {
+        salT[m][lane] = 0.0;
+        sxT[m][lane] = 0.0;
+      } else {
+        sal[m][lane] = 0.0;
+      }
+    }
   }
   vm_drain();
   wsync();
@@ -584,18 +527,26 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
   Q_BEGIN
   for (int k = nb - 1; k >= 0; --k) {
     const int qk = min(Q, nb - 1 - k), k16 = k * 16, cs = k % (Q + 1);
-    // this step's W_kk and P_iᵀ (landed: drained at the end of the previous step)
-    const t4 Wf = lds_n(sin_[0], l15, l4);
+    // this step's W_kk and P_iᵀ (loaded during the previous step)
+    const t4 Wf = Wn;
     t4 P[Q + 1];  // P_iᵀ, then G_i
 #pragma unroll
-    for (int i = 1; i <= Q; ++i) P[i] = (i <= qk) ? lds_t(sin_[i], l15, l4) : tzero();
+    for (int i = 1; i <= Q; ++i) P[i] = Pn[i];
     // X rows of block k -> ring slot cs (scaled by 1/ℓ as GPflow's Stationary.scale when fast)
+    if constexpr (!SE1) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int e = lane + 64 * h;
-      if (e < nx) sx[cs * nx + e] = (k16 + e / D < n) ? xr[h] / xscale : 0.0;
+      for (int h = 0; h < 2; ++h) {
+        const int e = lane + 64 * h;
+        if (e < nx) sx[cs * nx + e] = (k16 + e / D < n) ? xr[h] / xscale : 0.0;
+      }
+      for (int e = lane + 128; e < nx; e += 64) sx[cs * nx + e] = (k16 + e / D < n) ? X[(long long)k16 * D + e] / xscale : 0.0;
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = lane + 64 * h, il = e / D;
+        if (e < nx && e - il * D == fd0) sxT[cs][(il & 3) * 4 + (il >> 2)] = (k16 + il < n) ? xr[h] / xscale : 0.0;
+      }
     }
-    for (int e = lane + 128; e < nx; e += 64) sx[cs * nx + e] = (k16 + e / D < n) ? X[(long long)k16 * D + e] / xscale : 0.0;
     const double zc[4] = {zr[0], zr[1], zr[2], zr[3]};
     lds_drain();
     wsync();
@@ -615,7 +566,12 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
     for (int r = 0; r < 4; ++r) ap = fma(Wf[r], zc[r] - sum16(t[r]), ap);
     ap = sum4(ap);
     al[0] = ap;
-    if (l4 == 0) sal[cs][l15] = ap;
+    if (l4 == 0) {
+      if constexpr (SE1)
+        salT[cs][(l15 & 3) * 4 + (l15 >> 2)] = ap;
+      else
+        sal[cs][l15] = ap;
+    }
     QP(1);
     // G_i = P_i W_kk
 #pragma unroll
@@ -652,6 +608,8 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
 #pragma unroll
     for (int i = 1; i <= Q; ++i)
       if (i <= qk) mms(Zk, P[i], Zn[i]);
+    // the next step's W_kk and P_iᵀ, in flight during the contraction
+    if (k > 0) fetch_f(k - 1, Wn, Pn);
     wsync();
     QP(4);
     // gradient contraction and the band check's K∘Z sums over tile i (0: Z_kk whole, weight 1;
@@ -664,28 +622,30 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
       // K_ij from the built band (the same var·exp(−r²/2) bits the exp would give; entries in
       // 64-block offset >= kband are the exact zeros of the class; the diagonal tile mirrored
       // from its lower triangle): ∂K/∂ℓ = K r²/ℓ, and Σ v ∂K/∂σ² = (Σ v K)/σ² at the end
-      const double xjv = xj[fd0];
+      const double xjv = sxT[cs][(l15 & 3) * 4 + (l15 >> 2)];
 #pragma unroll
       for (int i = 0; i <= Q; ++i) {
         if (i > qk) continue;
         const t4& Zt = (i == 0) ? Zk : Zn[i];
         const int si = (k + i) % (Q + 1);
         const double w = i == 0 ? 1.0 : 2.0;
+        const t4 a4 = *reinterpret_cast<const t4*>(&salT[si][4 * l4]);  // α of rows 4r + l4
+        const t4 x4 = *reinterpret_cast<const t4*>(&sxT[si][4 * l4]);   // x of rows 4r + l4
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int il = 4 * r + l4, gi = (k + i) * 16 + il;
           const double zij = Zt[r];
-          const double ai = sal[si][il];
-          const double r2 = sqdist1(sx[si * nx + il * D + fd0], xjv);
+          const double ai = a4[r];
+          const double r2 = sqdist1(x4[r], xjv);
           const bool up = i == 0 && il < l15;
           const double kraw = sz[(k & 1) * (Q + 1) + i][up ? l15 * 16 + il : il * 16 + l15];
-          const bool zero = (gi >> 6) - (gj >> 6) >= a.kband;
+          const bool zero = ((k + i) >> 2) - (k >> 2) >= a.kband;  // (uniform, see the forward sweep)
           const double v = w * fma(ai, ap, -zij);
           const bool ok = jok && gi < n;
           const bool dg = i == 0 && il == l15;
           const double kij = (zero || !ok) ? 0.0 : kraw;
           const double kg = ok ? (dg ? fvar : kij) : 0.0;  // σ²·g (the noise is not part of ∂K/∂θ)
-          sums[0][0] = fma(v, kg * r2 * finv_ell, sums[0][0]);
+          sums[0][0] = fma(v, kg * r2, sums[0][0]);  // (× 1/ℓ once, at the end)
           sums[0][1] = fma(v, kg, sums[0][1]);
           snoise = (ok && dg) ? snoise + v : snoise;
           const double kz = kij * zij;
@@ -819,7 +779,10 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
   for (int t = 0; t < GPX_MAX_TERMS; ++t)
 #pragma unroll
     for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wsum64(sums[t][q]) : 0.0;
-  if (SE1) vals[1] /= fvar;  // Σ v σ² g -> Σ v ∂K/∂σ²
+  if (SE1) {
+    vals[0] *= finv_ell;  // Σ v K r² -> Σ v ∂K/∂ℓ
+    vals[1] /= fvar;      // Σ v σ² g -> Σ v ∂K/∂σ²
+  }
   vals[GPX_MAX_TERMS * 3] = wsum64(snoise);
   if (lane == 0) {
 #pragma unroll
@@ -851,7 +814,8 @@ static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, int n_ac
                              : max_terms <= 1 ? band16_bwd_kernel<Q, 1, false>
                                               : max_terms == 2 ? band16_bwd_kernel<Q, 2, false>
                                                                : band16_bwd_kernel<Q, GPX_MAX_TERMS, false>;
-  const size_t xs = (size_t)(Q + 1) * 16 * a.D * sizeof(double);
+  const bool se1k = se1 && Q <= 4;
+  const size_t xs = se1k ? 0 : (size_t)(Q + 1) * 16 * a.D * sizeof(double);
   if (ev) {
     hipExtLaunchKernelGGL(band16_fwd_kernel<Q>, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
     hipExtLaunchKernelGGL(bwd, dim3(n_active), dim3(64), xs, s, ev[2], ev[3], 0, a);

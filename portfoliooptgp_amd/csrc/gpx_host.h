@@ -66,6 +66,12 @@ struct gpx_batch {
   // over the term's active dims, [B][GPX_MAX_TERMS][Np/64]; computed when a problem is bound
   std::vector<double> band_rmin;
   std::vector<double> band_rmin16;  // the same per 16-row block, [B][GPX_MAX_TERMS][Np/16] (band16 path)
+  // [B][GPX_MAX_TERMS]: the offset from which a term's table holds one repeated value (a lower
+  // bound: inputs sorted along the term's single dimension make the table nondecreasing, so it is
+  // computed exactly only up to the widest band any path takes and repeated beyond; see
+  // band_tables_lohi), or Np/bs when every entry is exact
+  std::vector<int> band_tail;
+  std::vector<int> band_tail16;
   double* bres = nullptr; size_t bres_cap = 0;  // [B][Np] band-check column sums (per-block path)
   int force_dense = 0;         // re-evaluation of problems whose band check failed
   // pinned staging for gpx_batch_rebind_host, one region per slot ([Nmax*D] X, [Nmax] Y, n and
