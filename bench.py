@@ -216,16 +216,20 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 256)),
                     help="independent series fitted per GPU per step")
-    # band storage (25 MiB per slot) lets 4096 slots stay resident (100 GB of the 288): the
-    # band16 sweeps run one wavefront per problem, so the chip's ~2048 wave places need ~2000
-    # problems in flight (1536 slots: 5370 fits/s, 4096: 5847 at 2 processes, round 3)
-    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 4096)),
+    # band storage (25 MiB per slot) lets 8192 slots stay resident (205 GB of the 288): the
+    # band16 sweeps run one wavefront per problem and each call is a chain of launches (build,
+    # one sweep pair per band width, reduce), so the chip's 2048 two-per-SIMD sweep places stay
+    # filled only with several calls' worth of problems in flight (round 3, profiles/r03_sweeps:
+    # 4096 slots 7872 fits/s, 6144: 8572-8649, 8192: 8695-9925; 9216 thrashed HBM: 3646)
+    ap.add_argument("--width", type=int, default=int(os.environ.get("GPX_BENCH_WIDTH", 8192)),
                     help="resident device slots per GPU (continuous-batching width), split over --procs")
-    ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 2)),
+    ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 1)),
                     help="device batches kept in flight by each host process")
-    # 4 processes x 4 HIP hardware queues: the GPU's queue scheduler time-slices once the
-    # processes' queues exceed ~16 (2 x 8: 6167 fits/s; 3 x 4: 6898; 4 x 4: 7102; round 3)
-    ap.add_argument("--procs", type=int, default=int(os.environ.get("GPX_BENCH_PROCS", 4)),
+    # 8 processes x 2 HIP hardware queues, one device batch of 1024 slots each: the GPU's queue
+    # scheduler time-slices once the processes' queues exceed ~16; 8 host threads keep 8 calls in
+    # flight (8 x 1 batch: 9925 fits/s, 8 x 2: 9074-9599, 10 x 2: 8228, 12 x 2: 7598, 4 x 2 at
+    # 8192 slots: 8695; round 3, profiles/r03_sweeps)
+    ap.add_argument("--procs", type=int, default=int(os.environ.get("GPX_BENCH_PROCS", 8)),
                     help="host processes per GPU (the rank + procs-1 spawned helpers)")
     ap.add_argument("--storage", choices=("band", "dense"), default=os.environ.get("GPX_BENCH_STORAGE", "band"),
                     help="slot workspace: band storage (gpx_batch_create_banded, 25 MiB per slot) or the "
@@ -454,10 +458,9 @@ def secondary_c5(gpu, reps=20):
 
 def main():
     # HIP hardware queues for this process (and the helpers, which inherit the environment), set
-    # before the runtime starts: each process's 2 device batches evaluate on their own streams
-    # (+ the forked p = 2 and fallback streams); over all the GPU's processes the queues stay
-    # within what the queue scheduler maps at once (4 processes x 4)
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPX_HW_QUEUES", "4")
+    # before the runtime starts: over all the GPU's processes the queues stay within what the
+    # queue scheduler maps at once (8 processes x 2)
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPX_HW_QUEUES", "2")
     # driver phase times (host share of the timed region), cheap perf_counter reads
     os.environ.setdefault("GPX_DRIVER_STATS", "1")
     argv = sys.argv[1:]
