@@ -210,9 +210,9 @@ NARROW_FIELDS = ("band_fwd_ms_total", "band_bwd_ms_total", "band_fused_launches"
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 200 timed steps of 256 fits: a timed region of ~10 s (a 1 s region was too short for the
+    # 400 timed steps of 256 fits: a timed region of ~10 s (a 1 s region was too short for the
     # driver's GPU-busy sampler and for a stable figure: runs spread ±8 % at 10 steps)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 256)),
                     help="independent series fitted per GPU per step")
@@ -625,7 +625,9 @@ def main():
     host = []
     for p in parts:
         st = p[4] or {}
-        wait = st.get("device_wait", 0.0)
+        # waiting for the device: the pipelined driver's device_wait, or (one batch per process)
+        # the synchronous device calls, their submit/complete host work included
+        wait = st.get("device_wait", 0.0) + st.get("device_call", 0.0)
         host.append({"proc": p[0], "fits": int(len(p[1])), "busy_s": p[5],
                      "host_share": (p[5] - wait) / p[5] if p[5] > 0 else None,
                      "rounds": st.get("rounds"), "fit_evals": st.get("fit_evals")})

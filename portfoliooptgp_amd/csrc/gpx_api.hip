@@ -523,25 +523,23 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     launch_band_fused(f2, max_terms, r.na - nlo, s2, n1 == 0 ? ev : nullptr);
   }
   if (nlo > 0) {
-    // the band16 class's K band: kband16 64-block diagonals (3 when it holds p = 2 problems)
-    if (n16 > 0 && kband16 != 2) {
-      BuildArgs b16 = ba;
-      b16.band1 = kband16;
-      launch_build(b16, n16, r.s);
-      if (n1 > 0) {
-        BuildArgs b1 = ba;
-        b1.active = r.d_act + n16;
-        b1.band1 = 2;
-        launch_build(b1, n1, r.s);
-      }
-    } else {
-      ba.band1 = 2;
-      launch_build(ba, nlo, r.s);
+    // the p <= 1 class's K band: two 64-block diagonals
+    if (n1 > 0) {
+      BuildArgs b1 = ba;
+      b1.active = r.d_act + n16;
+      b1.band1 = 2;
+      launch_build(b1, n1, r.s);
     }
+    // the band16 class, per width group: K's band as its sweeps read it (the 16-row tiles
+    // (m, m − d), d <= Q), then the sweep pair. kband16 (2, or 3 when the class holds p = 2
+    // problems) still tells the sweeps which entries are exact zeros by the 64-row bound.
     int off = 0;
     for (int g = 0; g < n_g16; ++g) {
+      BuildArgs bg = ba;
+      bg.active = r.d_act + off;
+      launch_band16_build(bg, g16_q[g], g16_n[g], r.s);
       BandFusedArgs f16 = fa;
-      f16.kband = n16 > 0 ? kband16 : 2;
+      f16.kband = kband16;
       f16.active = r.d_act + off;
       launch_band16(f16, g16_q[g], max_terms, se1, g16_n[g], r.s, ev16 ? ev16[g] : nullptr);
       off += g16_n[g];

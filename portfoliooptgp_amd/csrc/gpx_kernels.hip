@@ -44,28 +44,6 @@ __device__ __forceinline__ double wave_sum(double v) {
 // ======================================================================================
 // K build (and cross-covariance Kxs for predict)
 // ======================================================================================
-// value of a single-term isotropic stationary kernel at scaled squared distance r2 = d²/ℓ²
-// (same formulas and 1e-36 clamp as eval_term in gpx_kfun.h)
-template <int KIND>
-__device__ __forceinline__ double stationary_value(double r2, double var) {
-  if constexpr (KIND == GPX_SE) {
-    return var * exp(-0.5 * r2);
-  } else {
-    const double r = sqrt(r2 > 1e-36 ? r2 : 1e-36);
-    if constexpr (KIND == GPX_MATERN12) return var * exp(-r);
-    if constexpr (KIND == GPX_EXPONENTIAL) return var * exp(-0.5 * r);
-    if constexpr (KIND == GPX_MATERN32) {
-      const double s = 1.7320508075688772;
-      return var * ((1.0 + s * r) * exp(-s * r));
-    }
-    if constexpr (KIND == GPX_MATERN52) {
-      const double s = 2.23606797749979;
-      return var * ((1.0 + s * r + (5.0 / 3.0) * r * r) * exp(-s * r));
-    }
-  }
-  return 0.0;
-}
-
 template <int KIND>
 __device__ __forceinline__ void build_stationary(const BuildArgs& a, const DevSpec& spec,
                                                  const double* sth, const double* sxi,

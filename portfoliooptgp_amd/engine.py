@@ -298,11 +298,16 @@ class Engine:
                 f"{[int(info[b]) for b in bad]}): K + noise I is not positive definite", info)
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_predict failed ({rc}): {self.ctx.last_error()}")
-        outs_m = [mean[b, : x.shape[0]] for b, x in zip(act, xs)]
+        rows = act
+        if len(act) < self.B:  # compact copies of the predicted rows (see _predict_train)
+            idx = torch.as_tensor(np.asarray(act, dtype=np.int64), device=dev)
+            mean, var = mean.index_select(0, idx), var.index_select(0, idx)
+            rows = range(len(act))
+        outs_m = [mean[k, : x.shape[0]] for k, x in zip(rows, xs)]
         if full_cov:
-            outs_v = [var[b, : x.shape[0], : x.shape[0]] for b, x in zip(act, xs)]
+            outs_v = [var[k, : x.shape[0], : x.shape[0]] for k, x in zip(rows, xs)]
         else:
-            outs_v = [var[b, : x.shape[0]] for b, x in zip(act, xs)]
+            outs_v = [var[k, : x.shape[0]] for k, x in zip(rows, xs)]
         return outs_m, outs_v, info
 
     def _predict_train(self, act: np.ndarray, theta: np.ndarray, add_noise: bool, column: bool = False):
@@ -327,9 +332,19 @@ class Engine:
                 "positive definite", info)
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_predict_train failed ({rc}): {self.ctx.last_error()}")
+        # the predicted rows only, in a compact copy (same stream): views into the [B, Nmax]
+        # buffers would keep the whole batch's buffers alive as long as any one fit's prediction
+        # is referenced (a long run holds every fit's prediction: 64 MiB per call at B = 1024)
+        if len(act) < self.B:
+            idx = torch.as_tensor(np.asarray(act, dtype=np.int64), device=dev)
+            mean, var = mean.index_select(0, idx), var.index_select(0, idx)
+            rows = range(len(act))
+        else:
+            rows = act
         if column:
             mean, var = mean.unsqueeze(-1), var.unsqueeze(-1)
-        return ([mean[b, : self.n[b]] for b in act], [var[b, : self.n[b]] for b in act], info)
+        return ([mean[k, : self.n[b]] for k, b in zip(rows, act)], [var[k, : self.n[b]] for k, b in zip(rows, act)],
+                info)
 
     def rebind(self, b: int, X, Y, spec: N.GpxKernelSpec) -> None:
         """Load a new problem into slot b (continuous batching). Host inputs are staged in
