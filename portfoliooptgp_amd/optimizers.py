@@ -162,25 +162,41 @@ def _single_thread_blas():
 
 
 class _BlasThreads:
-    """set_num_threads(1) on each BLAS library for the duration (direct calls, not a fresh
-    threadpool_limits scan: this wraps every single-model minimize)."""
+    """set_num_threads(1) on each BLAS library while any fit steps (direct calls, not a fresh
+    threadpool_limits scan: this wraps every single-model minimize). Process-wide and counted:
+    with fits stepping concurrently (threaded driver, user threads) the first context to enter
+    sets one thread and the last to exit restores the previous counts, so one fit finishing
+    does not hand the others a multi-threaded BLAS mid-run."""
+
+    _lock = threading.Lock()
+    _active = 0
+    _prev: list = []
 
     def __init__(self, libs):
         self.libs = libs
 
     def __enter__(self):
-        self.prev = []
-        for lib in self.libs:
-            n = lib.get_num_threads()
-            self.prev.append(n)
-            if n != 1:
-                lib.set_num_threads(1)
+        cls = _BlasThreads
+        with cls._lock:
+            if cls._active == 0:
+                cls._prev = []
+                for lib in self.libs:
+                    n = lib.get_num_threads()
+                    cls._prev.append((lib, n))
+                    if n != 1:
+                        lib.set_num_threads(1)
+            cls._active += 1
         return self
 
     def __exit__(self, *exc):
-        for lib, n in zip(self.libs, self.prev):
-            if n != 1:
-                lib.set_num_threads(n)
+        cls = _BlasThreads
+        with cls._lock:
+            cls._active -= 1
+            if cls._active == 0:
+                for lib, n in cls._prev:
+                    if n != 1:
+                        lib.set_num_threads(n)
+                cls._prev = []
         return False
 
 

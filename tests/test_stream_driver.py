@@ -401,3 +401,28 @@ def test_predict_after_backed_off_line_search_uses_a_fresh_evaluation():
     for r, m, p in zip(res, ms, preds):
         assert float(p[0][0, 0]) == m.kernel.lengthscales.value
         assert m.kernel.lengthscales.unconstrained == r.x[0]
+
+
+def test_blas_thread_limit_is_process_wide_and_counted():
+    """Overlapping single-thread-BLAS contexts (concurrent fits): the limit holds until the
+    last one exits, then the previous count comes back."""
+    from portfoliooptgp_amd.optimizers import _BlasThreads
+
+    class Lib:
+        def __init__(self):
+            self.n = 8
+
+        def get_num_threads(self):
+            return self.n
+
+        def set_num_threads(self, n):
+            self.n = n
+    lib = Lib()
+    a, b = _BlasThreads([lib]), _BlasThreads([lib])
+    a.__enter__()
+    assert lib.n == 1
+    b.__enter__()
+    a.__exit__(None, None, None)
+    assert lib.n == 1          # b still stepping
+    b.__exit__(None, None, None)
+    assert lib.n == 8
