@@ -279,8 +279,11 @@ constexpr __host__ __device__ int wid(int i, int j) { return i * (i + 1) / 2 + j
 //   T_ij −= Q_jᵀ Q_i   (A_{k+i,k+j} −= P_i P_jᵀ), 1 <= j <= i <= Q
 // then the window moves down one block; its new row (block k+Q+1) is loaded during the step.
 // ---------------------------------------------------------------------------------------
+#ifndef GPX_B16_FWD3_WAVES
+#define GPX_B16_FWD3_WAVES 2  // waves per SIMD the Q <= 3 forward sweep is compiled for
+#endif
 template <int Q>
-__global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFusedArgs a) {
+__global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1)) void band16_fwd_kernel(BandFusedArgs a) {
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   __shared__ __attribute__((aligned(16))) double snew[Q + 1][256];  // the entering row, staged by glds
   __shared__ double sv[16];
@@ -357,7 +360,6 @@ __global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFuse
         t4 c = tzero();
         mma(c, V, T[wid(i, 0)]);
         T[wid(i, 0)] = c;
-        frag_store(c, Lk + i * 256, lane);  // P_iᵀ
         double s = 0.0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) s = fma(c[r], zr[r], s);
@@ -372,10 +374,13 @@ __global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFuse
       for (int j = 1; j <= i; ++j)
         if (i <= qk) mms(T[wid(i, j)], T[wid(j, 0)], T[wid(i, 0)]);
     QP(4);
-    // the new row has landed (this also retires this step's tile stores, issued at the leaf and
-    // the panels); L_ii and z_k go out now
+    // the new row has landed (this also retires W_kk's store, issued right after the leaf); the
+    // panels, L_ii and z_k go out now, so that the next step's wait does not cover them early
     vm_drain();
     wsync();
+#pragma unroll
+    for (int i = 1; i <= Q; ++i)
+      if (i <= qk) frag_store(T[wid(i, 0)], Lk + i * 256, lane);  // P_iᵀ
     if (l4 == 0) {
       ldiag[k16 + l15] = lii;
       z[k16 + l15] = zp;
@@ -426,7 +431,7 @@ __global__ __launch_bounds__(64, Q <= 4 ? 2 : 1) void band16_fwd_kernel(BandFuse
 // input column): the contraction is a straight-line loop (contract_block_se1's operations).
 template <int Q, int NT, bool SE1>
 __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
-  static_assert(!SE1 || Q <= 4, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 4");
+  static_assert(!SE1 || Q <= 5, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 5");
   extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1); not SE1)
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   // SE1: the K tiles (k+i, k) as built, double-buffered by step parity (the next step's are
@@ -641,10 +646,12 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
           const double kraw = sz[(k & 1) * (Q + 1) + i][up ? l15 * 16 + il : il * 16 + l15];
           const bool zero = ((k + i) >> 2) - (k >> 2) >= a.kband;  // (uniform, see the forward sweep)
           const double v = w * fma(ai, ap, -zij);
-          const bool ok = jok && gi < n;
+          // rows or columns past n: off the diagonal tile the built band holds exact zeros there
+          // (the padding is the identity), so only the diagonal tile needs the mask
+          const bool ok = i > 0 || (jok && gi < n);
           const bool dg = i == 0 && il == l15;
           const double kij = (zero || !ok) ? 0.0 : kraw;
-          const double kg = ok ? (dg ? fvar : kij) : 0.0;  // σ²·g (the noise is not part of ∂K/∂θ)
+          const double kg = i > 0 ? kij : (ok ? (dg ? fvar : kij) : 0.0);  // σ²·g (the noise is not part of ∂K/∂θ)
           sums[0][0] = fma(v, kg * r2, sums[0][0]);  // (× 1/ℓ once, at the end)
           sums[0][1] = fma(v, kg, sums[0][1]);
           snoise = (ok && dg) ? snoise + v : snoise;
@@ -879,11 +886,11 @@ void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s)
 
 template <int Q>
 static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, int n_active, hipStream_t s, hipEvent_t* ev) {
-  auto bwd = (se1 && Q <= 4) ? band16_bwd_kernel<Q, 1, (Q <= 4)>
+  auto bwd = se1 ? band16_bwd_kernel<Q, 1, true>
                              : max_terms <= 1 ? band16_bwd_kernel<Q, 1, false>
                                               : max_terms == 2 ? band16_bwd_kernel<Q, 2, false>
                                                                : band16_bwd_kernel<Q, GPX_MAX_TERMS, false>;
-  const bool se1k = se1 && Q <= 4;
+  const bool se1k = se1;
   const size_t xs = se1k ? 0 : (size_t)(Q + 1) * 16 * a.D * sizeof(double);
   if (ev) {
     hipExtLaunchKernelGGL(band16_fwd_kernel<Q>, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
