@@ -133,6 +133,17 @@ __device__ __forceinline__ void tile_glds(const double* __restrict__ g, long lon
   __builtin_amdgcn_global_load_lds(g + (long long)row * ld + col, s, 16, 0, 0);
   __builtin_amdgcn_global_load_lds(g + (long long)(row + 8) * ld + col, s + 128, 16, 0, 0);
 }
+// the same copy with the 16-byte column pairs of row r XOR-swizzled by (r >> 1) & 7, so that the
+// forward sweep's transposed fragment reads (lane (l15, l4) reads row l15: sixteen rows 128 B
+// apart, i.e. the same LDS banks) spread over all banks; element (r, c) sits at swz16(r, c)
+__device__ __forceinline__ int swz16(int r, int c) { return r * 16 + ((((c >> 1) ^ (r >> 1)) & 7) << 1) + (c & 1); }
+__device__ __forceinline__ void tile_glds_swz(const double* __restrict__ g, long long ld, double* __restrict__ s,
+                                              int lane) {
+  const int row = lane >> 3, q = lane & 7;
+  __builtin_amdgcn_global_load_lds(g + (long long)row * ld + 2 * (q ^ ((row >> 1) & 7)), s, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(g + (long long)(row + 8) * ld + 2 * (q ^ (((row + 8) >> 1) & 7)), s + 128, 16, 0, 0);
+}
+
 // band16's private factor layout (forward sweep -> backward sweep; nothing else reads it): per
 // block step k, Q + 1 tiles of 256 doubles at L + (k·(Q+1) + i)·256 (i = 0: W_kk, i >= 1: P_iᵀ),
 // each stored as its C fragment with a lane's 4 doubles contiguous: a tile is one coalesced 2 KiB
@@ -317,7 +328,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
     lds_drain();  // the previous step's reads of snew have completed
     if (bn < nb) {
 #pragma unroll
-      for (int j = 0; j <= Q; ++j) tile_glds(K + (long long)(bn * 16) * ld + (k + 1 + j) * 16, ld, snew[j], lane);
+      for (int j = 0; j <= Q; ++j) tile_glds_swz(K + (long long)(bn * 16) * ld + (k + 1 + j) * 16, ld, snew[j], lane);
     }
     double yr[4];
 #pragma unroll
@@ -378,6 +389,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
     // panels, L_ii and z_k go out now, so that the next step's wait does not cover them early
     vm_drain();
     wsync();
+    QP(6);
 #pragma unroll
     for (int i = 1; i <= Q; ++i)
       if (i <= qk) frag_store(T[wid(i, 0)], Lk + i * 256, lane);  // P_iᵀ
@@ -394,6 +406,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
       u[i] = u[i + 1];
     }
     u[Q] = 0.0;
+    QP(7);
 #pragma unroll
     for (int j = 0; j <= Q; ++j) {
       t4 t = tzero();
@@ -403,7 +416,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int cl = 4 * r + l4;
-          const double v = (j == Q && cl > l15) ? snew[j][cl * 16 + l15] : snew[j][l15 * 16 + cl];
+          const double v = (j == Q && cl > l15) ? snew[j][swz16(cl, l15)] : snew[j][swz16(l15, cl)];
           t[r] = zero ? 0.0 : v;
         }
       }

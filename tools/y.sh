@@ -10,3 +10,5 @@ for ell in 1.18 1.6 1.9; do
 done
 timeout -k 10 400 python bench.py --no-cpu-baseline --no-secondary --steps 100 > gpurun_out/${T}_bench.log 2>&1 || { tail -20 gpurun_out/${T}_bench.log; exit 1; }
 python3 -c "import json; d=json.loads(open('gpurun_out/${T}_bench.log').read().strip().splitlines()[-1]); print('fits/s', round(d['value'],1), 'evals/s', round(d['evals_per_s']), 'host_share', [round(h['host_share'],2) for h in d['host']], 'frac', round(d['roofline']['frac'],4), 'chip', round(d['roofline']['chip_frac'],4))"
+timeout -k 10 120 python tools/band16_phases.py 2048 1.18 > gpurun_out/${T}_ph_2048.log 2>&1 || { tail -20 gpurun_out/${T}_ph_2048.log; exit 1; }
+grep -v amdgpu gpurun_out/${T}_ph_2048.log | cut -c1-700
