@@ -126,16 +126,11 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 // wait for this wave's LDS operations
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// async copy of a 16x16 tile (row-major, leading dimension ld) into a 16x16 row-major LDS tile:
-// two 16-byte global_load_lds per lane (8 rows each; LDS destination = base + lane·16 B)
-__device__ __forceinline__ void tile_glds(const double* __restrict__ g, long long ld, double* __restrict__ s, int lane) {
-  const int row = lane >> 3, col = (lane & 7) * 2;
-  __builtin_amdgcn_global_load_lds(g + (long long)row * ld + col, s, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(g + (long long)(row + 8) * ld + col, s + 128, 16, 0, 0);
-}
-// the same copy with the 16-byte column pairs of row r XOR-swizzled by (r >> 1) & 7, so that the
-// forward sweep's transposed fragment reads (lane (l15, l4) reads row l15: sixteen rows 128 B
-// apart, i.e. the same LDS banks) spread over all banks; element (r, c) sits at swz16(r, c)
+// async copy of a 16x16 tile (row-major, leading dimension ld) into a 16x16 LDS tile: two
+// 16-byte global_load_lds per lane (8 rows each; LDS destination = base + lane·16 B), the 16-byte
+// column pairs of row r XOR-swizzled by (r >> 1) & 7 so that transposed fragment reads (lane
+// (l15, l4) reading row l15: sixteen rows 128 B apart, i.e. the same LDS banks) spread over all
+// banks; element (r, c) sits at swz16(r, c)
 __device__ __forceinline__ int swz16(int r, int c) { return r * 16 + ((((c >> 1) ^ (r >> 1)) & 7) << 1) + (c & 1); }
 __device__ __forceinline__ void tile_glds_swz(const double* __restrict__ g, long long ld, double* __restrict__ s,
                                               int lane) {
@@ -477,7 +472,7 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
     if constexpr (SE1) {
 #pragma unroll
       for (int i = 0; i <= Q; ++i)
-        if (i <= q1) tile_glds(Kd + (long long)(c16 + 16 * i) * ld + c16, ld, sz[(kk & 1) * (Q + 1) + i], lane);
+        if (i <= q1) tile_glds_swz(Kd + (long long)(c16 + 16 * i) * ld + c16, ld, sz[(kk & 1) * (Q + 1) + i], lane);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) zr[r] = z[c16 + 4 * r + l4];
@@ -620,14 +615,15 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
       }
     }
     QP(3);
+    // the next step's W_kk and P_iᵀ, in flight during Z_kk and the contraction (issued ahead of
+    // Z_kk's MFMA chain, which holds the wave's issue for ~1k cycles)
+    if (k > 0) fetch_f(k - 1, Wn, Pn);
     // Z_kk = W_kkᵀ W_kk − Σ_i G_iᵀ Z_{k+i,k}
     t4 Zk = tzero();
     mma(Zk, Wf, Wf);
 #pragma unroll
     for (int i = 1; i <= Q; ++i)
       if (i <= qk) mms(Zk, P[i], Zn[i]);
-    // the next step's W_kk and P_iᵀ, in flight during the contraction
-    if (k > 0) fetch_f(k - 1, Wn, Pn);
     wsync();
     QP(4);
     // gradient contraction and the band check's K∘Z sums over tile i (0: Z_kk whole, weight 1;
@@ -656,7 +652,7 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
           const double ai = a4[r];
           const double r2 = sqdist1(x4[r], xjv);
           const bool up = i == 0 && il < l15;
-          const double kraw = sz[(k & 1) * (Q + 1) + i][up ? l15 * 16 + il : il * 16 + l15];
+          const double kraw = sz[(k & 1) * (Q + 1) + i][up ? swz16(l15, il) : swz16(il, l15)];  // (swizzled rows)
           const bool zero = ((k + i) >> 2) - (k >> 2) >= a.kband;  // (uniform, see the forward sweep)
           const double v = w * fma(ai, ap, -zij);
           // rows or columns past n: off the diagonal tile the built band holds exact zeros there
@@ -762,10 +758,12 @@ __global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel
       for (int m = Q - 1; m >= 0; --m)
         if (m < nb) finish(m, R[m]);
     }
+    QP(7);
     // this step's inputs for the next one have landed; this step's outputs go out after the
     // wait (α_k, diag(Z_kk) on K's diagonal for band_train_pred_kernel)
     vm_drain();
     wsync();
+    QP(8);
     if (l4 == 0) alpha[k16 + l15] = ap;
 #pragma unroll
     for (int r = 0; r < 4; ++r)

@@ -22,7 +22,8 @@ from portfoliooptgp_amd.engine import Engine  # noqa: E402
 from portfoliooptgp_amd.kernels import compile_spec  # noqa: E402
 
 NAMES = {0: ["glds + y", "leaf", "W out, z_k", "panels, u", "window update", "new row reads", "drain", "stores, shift"],
-         1: ["loads, frags, glds", "alpha_k", "G", "Z panel", "Z_kk, Z out", "contract", "check, shift"]}
+         1: ["loads, frags, glds", "alpha_k", "G", "Z panel", "Z_kk, Z out", "contract", "stores, shift",
+             "band check", "drain"]}
 
 
 def main():
