@@ -292,7 +292,6 @@ template <int Q>
 __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1)) void band16_fwd_kernel(BandFusedArgs a) {
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   __shared__ __attribute__((aligned(16))) double snew[Q + 1][256];  // the entering row, staged by glds
-  __shared__ double sv[16];
   const int b = a.active[blockIdx.x];
   const int Np = a.Np, nb = Np >> 4;
   const long long ld = a.ld;
@@ -325,39 +324,27 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
 #pragma unroll
       for (int j = 0; j <= Q; ++j) tile_glds_swz(K + (long long)(bn * 16) * ld + (k + 1 + j) * 16, ld, snew[j], lane);
     }
-    double yr[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = k16 + 4 * r + l4;
-      yr[r] = y[min(i, n - 1)];
-      yr[r] = i < n ? yr[r] : 0.0;
-    }
+    // y_k in the row layout of u (lane l15 holds row l15)
+    double yl = y[min(k16 + l15, n - 1)];
+    yl = k16 + l15 < n ? yl : 0.0;
     QP(0);
     t4 V;
     double lii;
     int fl;
     double* Lk = L + (long long)k * ((Q + 1) * 256);  // this step's tiles (private layout above)
+    double zr[4];  // z_k[4r + l4] (the panels' layout), on every lane of the row
     {
       t4 Wr;
       leaf16m(T[wid(0, 0)], V, Wr, lii, fl, sc, l15, l4);
       frag_store(Wr, Lk, lane);  // W_kk
+      QP(1);
+      // z_k = W_kk (y_k + u_k): Wr[r] = W_kk[4r+l4][l15], so each row is a 16-lane sum (DPP
+      // butterfly) of Wr[r]·(y + u)[l15], with y and u already in that lane layout
+      const double yu = yl + u[0];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) zr[r] = sum16(Wr[r] * yu);
     }
-    QP(1);
     if (fl >= 0 && gfail == 0) gfail = k16 + fl + 1;
-    // z_k = W_kk (y_k + u_k): V[r] = W_kk[l15][4r+l4]
-    wsync();
-    if (l4 == 0) sv[l15] = u[0];
-    wsync();
-    double zp = 0.0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) zp = fma(V[r], yr[r] + sv[4 * r + l4], zp);
-    zp = sum4(zp);
-    wsync();
-    if (l4 == 0) sv[l15] = zp;
-    wsync();
-    double zr[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) zr[r] = sv[4 * r + l4];
     QP(2);
     // panels: Q_i = Vᵀ T_i0 (= P_iᵀ), stored as P_i = L_{k+i,k}; u_{k+i} −= P_i z_k
 #pragma unroll
@@ -388,9 +375,10 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
 #pragma unroll
     for (int i = 1; i <= Q; ++i)
       if (i <= qk) frag_store(T[wid(i, 0)], Lk + i * 256, lane);  // P_iᵀ
-    if (l4 == 0) {
-      ldiag[k16 + l15] = lii;
-      z[k16 + l15] = zp;
+    if (l4 == 0) ldiag[k16 + l15] = lii;
+    if (l15 == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) z[k16 + 4 * r + l4] = zr[r];
     }
     // move the window down one block; its new row from LDS (fragments of A_{bn, k+1+j}ᵀ, entries
     // in 64-block offset >= 2 as exact zeros, the diagonal tile mirrored from its lower triangle)
