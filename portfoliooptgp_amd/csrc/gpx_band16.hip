@@ -425,8 +425,11 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
 // ---------------------------------------------------------------------------------------
 // SE1: every problem of the launch is the reference's kernel (one SquaredExponential term on one
 // input column): the contraction is a straight-line loop (contract_block_se1's operations).
+#ifndef GPX_B16_BWD_2W_QMAX
+#define GPX_B16_BWD_2W_QMAX 3  // widest band the SE1 backward sweep is compiled for two waves per SIMD
+#endif
 template <int Q, int NT, bool SE1>
-__global__ __launch_bounds__(64, (Q <= 3 && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
+__global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
   static_assert(!SE1 || Q <= 5, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 5");
   extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1); not SE1)
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
