@@ -56,6 +56,7 @@ N_POINTS = 4096
 NOISE = 1e-5
 MAXITER = 100
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (matrix) datasheet peak, /opt/skills/guides/MI355X_MICROARCH.md
+WAVE_SLOTS = 2048        # band16 sweep places: 256 CUs x 4 SIMDs x 2 waves (one wavefront per problem)
 
 
 def synthetic_series(n: int, seed: int, lengthscale: float = 64.0, n_features: int = 2048,
@@ -204,18 +205,23 @@ SUM_FIELDS = ("contract_ms_total", "contract_launches", "contract_alg_flops", "e
               "shadow_predicts")
 NARROW_FIELDS = ("band_fwd_ms_total", "band_bwd_ms_total", "band_fused_launches", "band_fwd_flops", "band_bwd_flops",
                  "band16_fwd_ms_total", "band16_bwd_ms_total", "band16_launches", "band16_evals", "band16_q_sum",
-                 "band16_fwd_flops", "band16_bwd_flops")
+                 "band16_fwd_flops", "band16_bwd_flops", "band16_wave_ms")
 
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 400 timed steps of 256 fits: a timed region of ~10 s (a 1 s region was too short for the
-    # driver's GPU-busy sampler and for a stable figure: runs spread ±8 % at 10 steps)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 256)),
-                    help="independent series fitted per GPU per step")
+    # a step is 6144 fits per GPU, so the driver's 20 steps (122,880 fits over 8192 slots, each
+    # slot refilled ~15 times) are a steady-state region of several seconds rather than one
+    # fill-and-drain wave (round 3: 256 fits per step, 20 steps = 5120 fits in 8192 slots, a
+    # 0.46 s region whose figure moved ±10 % with the step count)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--fits", type=int, default=int(os.environ.get("GPX_BENCH_FITS", 6144)),
+                    help="independent fits per GPU per step")
+    ap.add_argument("--series", type=int, default=int(os.environ.get("GPX_BENCH_SERIES", 512)),
+                    help="distinct synthetic series per GPU (fits cycle over them; generated on the host "
+                         "before the timed region)")
     # band storage (25 MiB per slot) lets 8192 slots stay resident (205 GB of the 288): the
     # band16 sweeps run one wavefront per problem and each call is a chain of launches (build,
     # one sweep pair per band width, reduce), so the chip's 2048 two-per-SIMD sweep places stay
@@ -260,18 +266,26 @@ class FitWorker:
         self.args, self.w, self.gpu = args, w, gpu
         F = args.fits
         self.F = share(F, P, w)
-        f0 = sum(share(F, P, i) for i in range(w))
+        # distinct series of this process (fits cycle over them: fit f of a step is series
+        # f mod S_w), seeds rank·S + s0 + s
+        S = max(1, min(args.series, F))
+        self.S = share(S, P, w)
+        s0 = sum(share(S, P, i) for i in range(w))
         n = self.n = args.n
         dev = torch.device(f"cuda:{gpu}")
-        data = [synthetic_series(n, rank * F + f0 + f) for f in range(self.F)]
+        data = [synthetic_series(n, rank * S + s0 + s) for s in range(self.S)]
         self.Xd = [torch.as_tensor(x, device=dev) for x, _ in data]  # resident in HBM before timing
         self.Yd = [torch.as_tensor(y, device=dev) for _, y in data]
+        # read-only series: their band-table boxes are computed at the first rebind and reused
+        # (GPX_BOX_CACHE=0 turns that off: every rebind then downloads its boxes)
+        from portfoliooptgp_amd.engine import mark_immutable
+        mark_immutable(*self.Xd)
         W = share(args.width, P, w)
         G = max(1, min(args.groups, W))
         sizes = [share(W, G, g) for g in range(G)]
         spec = compile_spec(gpx.kernels.SquaredExponential(), 1)
         # slot shapes only: every slot is rebound to its fit's series when the fit starts
-        self.engines = [Engine([self.Xd[i % self.F] for i in range(sz)], [self.Yd[i % self.F] for i in range(sz)],
+        self.engines = [Engine([self.Xd[i % self.S] for i in range(sz)], [self.Yd[i % self.S] for i in range(sz)],
                                [spec] * sz, device=gpu, band_storage=args.storage == "band")
                         for sz in sizes]
         self.engines[0].ctx.set_profiling(True)
@@ -282,7 +296,8 @@ class FitWorker:
     def make_model(self, f):
         # GPflow defaults (σ²=1, ℓ=1), σn² = 1e-5 frozen — GPR/model_trainer.py:15-17
         gpx = self.gpx
-        m = gpx.models.GPR(data=(self.Xd[f], self.Yd[f]), kernel=gpx.kernels.SquaredExponential(), device=self.gpu)
+        m = gpx.models.GPR(data=(self.Xd[f % self.S], self.Yd[f % self.S]), kernel=gpx.kernels.SquaredExponential(),
+                           device=self.gpu)
         m.likelihood.variance.assign(NOISE)
         gpx.set_trainable(m.likelihood.variance, False)
         return m
@@ -596,8 +611,14 @@ def main():
         roofline = {
             "kernel": (f"{kname}<Q> (16-row blocks, one wavefront walks a problem's 256 block steps; mean Q {q_mean:.2f})"
                        if b16 else f"{kname} (p<=1 class: one workgroup walks a problem's 64 block steps)"),
-            "bound": "mfma", "achieved": k["achieved"], "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": k["frac"], "traffic": k["traffic"], "traffic_source": k["traffic_source"],
+            # the sweeps are per-wave dependency chains, bounded by latency and by
+            # how many of the chip's wave slots hold a sweep, not by the MFMA or HBM peak: the
+            # MFMA fraction is reported as the contract's roofline, `occupancy` beside it
+            "bound": "latency" if b16 else "mfma", "achieved": k["achieved"], "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": k["frac"], "traffic": k["traffic"], "traffic_source": k["traffic_source"],
+            "occupancy": (tm["band16_wave_ms"] / (WAVE_SLOTS * elapsed * 1e3)) if b16 else None,
+            "occupancy_note": (f"sum over band16 launches of problems x HIP-event launch ms, over {WAVE_SLOTS} wave "
+                               "slots (256 CUs x 4 SIMDs x 2 sweeps per SIMD) x the timed wall ms") if b16 else None,
             "traffic_unit": "bytes/launch", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
             "alg_flops_per_launch": k["alg_flops_per_launch"], "mean_p_blocks": from_p,
             "band16_share_of_band_evals": e16 / max(tm["band_evals"], 1.0), "band16_mean_q": q_mean,

@@ -273,6 +273,9 @@ typedef struct {
   double band16_q_sum;
   double band16_fwd_flops;
   double band16_bwd_flops;
+  /* Σ over band16 launches of (problems in the launch) × (its duration, ms): the wave-ms the
+   * sweeps held (one wavefront per problem); ÷ (wave slots × wall ms) = their occupancy */
+  double band16_wave_ms;
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);

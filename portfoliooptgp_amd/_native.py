@@ -65,7 +65,8 @@ class GpxTiming(ctypes.Structure):
                 ("shadow_predicts", ctypes.c_double), ("band16_fwd_ms_total", ctypes.c_double),
                 ("band16_bwd_ms_total", ctypes.c_double), ("band16_launches", ctypes.c_double),
                 ("band16_evals", ctypes.c_double), ("band16_q_sum", ctypes.c_double),
-                ("band16_fwd_flops", ctypes.c_double), ("band16_bwd_flops", ctypes.c_double)]
+                ("band16_fwd_flops", ctypes.c_double), ("band16_bwd_flops", ctypes.c_double),
+                ("band16_wave_ms", ctypes.c_double)]
 
 
 class GPXError(RuntimeError):

@@ -506,53 +506,71 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   fa.ldiag = bt->ldiag; fa.sVec = Np; fa.X = bt->X; fa.sX = (long long)bt->Nmax * bt->D; fa.D = bt->D;
   fa.specs = bt->d_specs; fa.theta = bt->d_theta; fa.partial = bt->partial; fa.sPartial = bt->partial_stride;
   fa.info = bt->d_info; fa.results = bt->results; fa.Np = Np; fa.ld = mat_ld(bt);
-  hipStream_t sa = bt->aux[0];
-  const bool fork = nlo > 0 && nlo < r.na;
-  if (fork) {
-    (void)hipEventRecord(bt->ev[kEvents - 2], r.s);   // the call's uploads are in
-    (void)hipStreamWaitEvent(sa, bt->ev[kEvents - 2], 0);
-  }
-  if (nlo < r.na) {
-    hipStream_t s2 = fork ? sa : r.s;
-    BuildArgs b2 = ba;
-    b2.active = r.d_act + nlo;
-    b2.band1 = 3;
-    launch_build(b2, r.na - nlo, s2);
-    BandFusedArgs f2 = fa;
-    f2.active = r.d_act + nlo;
-    launch_band_fused(f2, max_terms, r.na - nlo, s2, n1 == 0 ? ev : nullptr);
-  }
-  if (nlo > 0) {
-    // the p <= 1 class's K band: two 64-block diagonals
-    if (n1 > 0) {
-      BuildArgs b1 = ba;
-      b1.active = r.d_act + n16;
-      b1.band1 = 2;
-      launch_build(b1, n1, r.s);
-    }
-    // the band16 class, per width group: K's band as its sweeps read it (the 16-row tiles
-    // (m, m − d), d <= Q), then the sweep pair. kband16 (2, or 3 when the class holds p = 2
-    // problems) still tells the sweeps which entries are exact zeros by the 64-row bound.
+  // The width classes of the call are independent: each class's chain (its K band build, then
+  // its sweeps) is a *lane*, and the lanes run concurrently — the largest on the call's stream,
+  // the others on the batch's auxiliary streams, joined before the reduction. Serialised on one
+  // stream (GPX_BAND_LANES=0, the round-3 order) every class's sweeps — about the same latency
+  // whatever their problem count — followed each other, so a call lasted ~2 sweeps per class
+  // while the small classes held few waves.
+  // Lane kinds: band16 width group g (K's band as its sweeps read it: the 16-row tiles (m, m − d),
+  // d <= Q; kband16 — 2, or 3 when the class holds p = 2 problems — still tells the sweeps which
+  // entries are exact zeros by the 64-row bound), the 64-row p <= 1 class (two 64-block
+  // diagonals), the 64-row p = 2 class (three).
+  struct Lane { int kind, g, n, off; };
+  Lane lanes[kBand16MaxQ + 2];
+  int nl = 0;
+  {
     int off = 0;
     for (int g = 0; g < n_g16; ++g) {
-      BuildArgs bg = ba;
-      bg.active = r.d_act + off;
-      launch_band16_build(bg, g16_q[g], g16_n[g], r.s);
-      BandFusedArgs f16 = fa;
-      f16.kband = kband16;
-      f16.active = r.d_act + off;
-      launch_band16(f16, g16_q[g], max_terms, se1, g16_n[g], r.s, ev16 ? ev16[g] : nullptr);
+      lanes[nl++] = Lane{0, g, g16_n[g], off};
       off += g16_n[g];
     }
-    if (n1 > 0) {
+    if (n1 > 0) lanes[nl++] = Lane{1, 0, n1, n16};
+    if (nlo < r.na) lanes[nl++] = Lane{2, 0, r.na - nlo, nlo};
+  }
+  std::sort(lanes, lanes + nl, [](const Lane& x, const Lane& y) { return x.n > y.n; });
+  static const bool lanes_on = [] {
+    const char* e = getenv("GPX_BAND_LANES");
+    return !(e && atoi(e) == 0);
+  }();
+  const int nstreams = lanes_on ? std::min(nl, 1 + kAux) : 1;
+  auto lane_stream = [&](int i) { return (i % nstreams) == 0 ? r.s : bt->aux[(i % nstreams) - 1]; };
+  if (nstreams > 1) {
+    (void)hipEventRecord(bt->ev[kEvents - 2], r.s);   // the call's uploads are in
+    for (int i = 1; i < nstreams; ++i) (void)hipStreamWaitEvent(bt->aux[i - 1], bt->ev[kEvents - 2], 0);
+  }
+  for (int i = 0; i < nl; ++i) {
+    const Lane& l = lanes[i];
+    hipStream_t ls = lane_stream(i);
+    if (l.kind == 0) {
+      BuildArgs bg = ba;
+      bg.active = r.d_act + l.off;
+      launch_band16_build(bg, g16_q[l.g], l.n, ls);
+      BandFusedArgs f16 = fa;
+      f16.kband = kband16;
+      f16.active = r.d_act + l.off;
+      launch_band16(f16, g16_q[l.g], max_terms, se1, l.n, ls, ev16 ? ev16[l.g] : nullptr);
+    } else if (l.kind == 1) {
+      BuildArgs b1 = ba;
+      b1.active = r.d_act + l.off;
+      b1.band1 = 2;
+      launch_build(b1, l.n, ls);
       BandFusedArgs f1 = fa;
-      f1.active = r.d_act + n16;
-      launch_band_fused1(f1, max_terms, n1, r.s, ev);
+      f1.active = r.d_act + l.off;
+      launch_band_fused1(f1, max_terms, l.n, ls, ev);
+    } else {
+      BuildArgs b2 = ba;
+      b2.active = r.d_act + l.off;
+      b2.band1 = 3;
+      launch_build(b2, l.n, ls);
+      BandFusedArgs f2 = fa;
+      f2.active = r.d_act + l.off;
+      launch_band_fused(f2, max_terms, l.n, ls, n1 == 0 ? ev : nullptr);
     }
   }
-  if (fork) {
-    (void)hipEventRecord(bt->ev[kEvents - 1], sa);
-    (void)hipStreamWaitEvent(r.s, bt->ev[kEvents - 1], 0);
+  for (int i = 1; i < nstreams; ++i) {
+    (void)hipEventRecord(bt->ev[kEvents - 4 - i], bt->aux[i - 1]);
+    (void)hipStreamWaitEvent(r.s, bt->ev[kEvents - 4 - i], 0);
   }
   ReduceArgs ra{};
   ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
@@ -640,9 +658,25 @@ int wait_io(gpx_batch* bt) {
   return GPX_OK;
 }
 
+// An asynchronous predict (predict_impl, `async`) left kernels in flight on bt->io_stream that
+// read the batch's device I/O block, n / specs and the predicted slots' factors. Every later
+// writer of that state on another stream (the uploads and rebind gathers of the next call, and
+// through their order that call's kernels, which overwrite the factors of rebound slots) first
+// waits for those kernels on the device — no host synchronisation. On the same stream the order
+// is already the stream's.
+int fence_io(gpx_batch* bt, hipStream_t s) {
+  if (!bt->io_pending || bt->io_stream == s) return GPX_OK;
+  HIPX(bt->ctx, hipStreamWaitEvent(s, bt->io_ev, 0));
+  return GPX_OK;
+}
+
 int flush_rebinds(gpx_batch* bt, hipStream_t s) {
   if (bt->n_dirty == 0 && bt->pend.empty()) return GPX_OK;
   gpx_ctx* ctx = bt->ctx;
+  {
+    const int e = fence_io(bt, s);
+    if (e != GPX_OK) return e;
+  }
   SubClock fc(bt);
   {
     const int e = wait_io(bt);
@@ -744,6 +778,10 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
   }
   {
     const int e = flush_rebinds(bt, s);
+    if (e != GPX_OK) return e;
+  }
+  {  // (the rebind flush above host-waits for it when it had work; here without rebinds)
+    const int e = fence_io(bt, s);
     if (e != GPX_OK) return e;
   }
   char* hio = bt->h_io;
@@ -1582,6 +1620,7 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
       (void)hipEventElapsedTime(&f1, pe->fq16[g][2], pe->fq16[g][3]);
       bt->timing.band16_fwd_ms_total += f0;
       bt->timing.band16_bwd_ms_total += f1;
+      bt->timing.band16_wave_ms += (double)pe->g16_n[g] * ((double)f0 + (double)f1);
       bt->timing.band16_launches += 1.0;
       bt->timing.band16_evals += pe->g16_n[g];
       bt->timing.band16_q_sum += (double)pe->g16_q[g] * pe->g16_n[g];
@@ -1907,6 +1946,7 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
     if (!bt->io_ev) HIPX(ctx, hipEventCreateWithFlags(&bt->io_ev, hipEventDisableTiming));
     HIPX(ctx, hipEventRecord(bt->io_ev, s));
     bt->io_pending = true;
+    bt->io_stream = s;
     for (int i = 0; i < n_active; ++i) info[active[i]] = 0;
     if (shadow_status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
     return shadow_status;

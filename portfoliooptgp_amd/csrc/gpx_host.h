@@ -104,8 +104,12 @@ struct gpx_batch {
   // a call that returns without synchronising its stream (predict at the training inputs from
   // cached factors) leaves its upload DMA out of h_io in flight: the next writer of the pinned
   // blocks waits on this event first (wait_io)
+  // io_stream is the stream that call ran on: its kernels still read the device side of the
+  // block (active list, θ, n, specs) and the slots' factors, so a writer of those on ANOTHER
+  // stream waits for io_ev on the device first (fence_io)
   hipEvent_t io_ev = nullptr;
   bool io_pending = false;
+  hipStream_t io_stream = nullptr;
   // predict calls upload [active | info | bandp | theta] from their own pinned block, so an
   // asynchronous predict's upload never holds up the next evaluation's (which writes h_io)
   char* h_io_pred = nullptr;
@@ -238,6 +242,7 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
                   hipStream_t s, bool predict_block = false);
 int flush_rebinds(gpx_batch* bt, hipStream_t s);  // pending rebinds -> device (one gather on s)
 int wait_io(gpx_batch* bt);                        // the last asynchronous call's uploads have left h_io
+int fence_io(gpx_batch* bt, hipStream_t s);        // s waits (on the device) for that call's kernels
 int ensure_rebind_meta(gpx_batch* bt);             // pinned n/spec mirrors + dirty flags
 
 }  // namespace gpx

@@ -143,4 +143,7 @@ def load_batch(csv_paths: Sequence[str], train_start_date: str, predict_Y: str =
         series.append((dev[0, off:off + nb].view(nb, 1), dev[1, off:off + nb].view(nb, 1)))
         meta.append(dict(mean=mean, std=std, dates=dates, path=p, n=nb))
         off += nb
+    if pin:  # read-only inputs: their band-table boxes are computed once (engine.mark_immutable)
+        from .engine import mark_immutable
+        mark_immutable(*(t for xy in series for t in xy))
     return series, meta

@@ -7,8 +7,9 @@ predicted_variances), Multi-Input_GPR/Portfolio/portfolio.py:92-165). Here:
 
 * one process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on MI355X,
   "gloo" for CPU tests);
-* fits are assigned to ranks longest-processing-time first on their cost (N³ dense, N·w² on
-  the block-banded path; no communication while fitting);
+* fits are assigned to ranks longest-processing-time first on their cost (device seconds per
+  evaluation on the path the fit takes: (N/16)·(Q+1) on the 16-row band sweeps, N·w² on the 64-row
+  band sweeps, N³ dense; no communication while fitting);
 * every rank fits its shard through the continuous-batching driver and predicts its
   horizon;
 * ONE all_gather of a packed fp64 tensor (θ*, loss*, nfev, mean[H], var[H] per asset) is the
@@ -69,18 +70,64 @@ def band_blocks_estimate(x, lengthscale: float = 1.0, cutoff: float = 38.63) -> 
     return None
 
 
-def fit_cost(n: int, band_blocks: Optional[int] = None) -> float:
-    """Relative cost of one exact-GP fit: O(N³) per evaluation on the dense path, O(N·w²) with
-    w = 64·(p + 1) rows on the block-banded path (band of p blocks)."""
+BAND16_MAX_Q = 5     # widest band of the 16-row sweeps (gpx_host.h kBand16MaxQ)
+BAND16_MAX_D = 8     # input columns they stage per block (kBand16MaxD)
+
+
+def band16_estimate(x, lengthscale: float = 1.0, cutoff: float = 38.63) -> Optional[int]:
+    """Band width Q, in 16-row blocks, that the 16-row sweeps take for a fit on inputs x (the
+    device's band_width16 bound from per-16-row boxes, gpx_api.hip): the smallest Q such that
+    every pair of points more than Q blocks apart is at least ``cutoff`` lengthscales apart.
+    None when that path does not take the series (the 64-row band is wider than 2 blocks, Q > 5,
+    more than 8 input columns, or fewer than 8 64-blocks)."""
+    x = np.asarray(x, dtype=np.float64)
+    x = x.reshape(len(x), -1)
+    p = band_blocks_estimate(x, lengthscale, cutoff)
+    if p is None or p > 2 or x.shape[1] > BAND16_MAX_D:
+        return None
+    n = len(x)
+    nb = (n + 15) // 16
+    lo = np.array([x[k * 16:(k + 1) * 16].min(0) for k in range(nb)])
+    hi = np.array([x[k * 16:(k + 1) * 16].max(0) for k in range(nb)])
+    for q in range(0, min(BAND16_MAX_Q, nb - 1) + 1):
+        ok = True
+        for dd in range(q + 1, min(nb, q + 1 + 2 * BAND16_MAX_Q)):
+            gap = np.maximum(0.0, np.maximum(lo[dd:] - hi[:nb - dd], lo[:nb - dd] - hi[dd:]))
+            if np.sqrt((gap * gap).sum(1)).min() / lengthscale < cutoff:
+                ok = False
+                break
+        if ok:
+            return max(q, 1)
+    return None
+
+
+# Device seconds per evaluation at full-chip throughput, per unit of each path's work model
+# (MI355X, round-3 measurements, DESIGN.md §3d/§4): band16 sweeps ~(N/16)·(Q+1) — a chain of N/16
+# block steps whose cost grows ~linearly in Q+1 (290k / 228k / 183k C2 evaluations/s at Q = 3 /
+# 4 / 5); the 64-row band sweeps N·w², w = 64(p+1) (60k evaluations/s at N = 4096, p = 1); the
+# dense path N³ (832 evaluations/s at N = 4096)
+_K16 = 1.0 / 290e3 / (256 * 4)
+_K64 = 1.0 / 60e3 / (4096 * 128.0 ** 2)
+_KDENSE = 1.0 / 832.0 / 4096.0 ** 3
+
+
+def fit_cost(n: int, band_blocks: Optional[int] = None, band16_q: Optional[int] = None) -> float:
+    """Relative device cost of one exact-GP fit (per evaluation; fits are assumed to take the
+    same number of evaluations), in seconds at full-chip throughput: the 16-row band sweeps
+    (band16_q: Q 16-blocks) ∝ (N/16)·(Q+1); the 64-row band sweeps (band of p
+    64-blocks, §3c) ∝ N·w², w = 64(p+1); the dense path ∝ N³."""
+    if band16_q is not None:
+        return _K16 * (n / 16.0) * (band16_q + 1)
     if band_blocks is None:
-        return float(n) ** 3
+        return _KDENSE * float(n) ** 3
     w = 64.0 * (band_blocks + 1)
-    return float(n) * w * w
+    return _K64 * float(n) * w * w
 
 
 def series_cost(x) -> float:
-    """fit_cost of a series for the default fitter (SE at GPflow's default ℓ = 1)."""
-    return fit_cost(len(x), band_blocks_estimate(x))
+    """fit_cost of a series for the default fitter (SE at GPflow's default ℓ = 1), on the path
+    the device routes it to at that ℓ."""
+    return fit_cost(len(x), band_blocks_estimate(x), band16_estimate(x))
 
 
 def pack_results(indices: Sequence[int], results: Sequence[dict], horizon: int, n_theta: int) -> torch.Tensor:

@@ -70,17 +70,44 @@ def screen_theta(act: np.ndarray, theta: np.ndarray, n_params: np.ndarray, info:
     return np.ascontiguousarray(act[ok])
 
 
-# Per-64-row-block bounding boxes of device-resident series (the band tables' input), kept
-# per series so that rebinding the same series into a slot again (continuous batching refits the
-# same assets step after step) skips the gather's box download and stream synchronise. Keyed by
-# the tensor's identity and its version counter (an in-place write bumps it), holding a
-# reference so the storage cannot be reused under the key.
-_BOX_CACHE: "OrderedDict" = None
-_BOX_CACHE_MAX = 16384
+# Per-16-row-block bounding boxes ([ceil(n/16)][D][2]) of device-resident series (the band
+# tables' input), kept per series so that rebinding the same series into a slot again
+# (continuous batching refits the same assets step after step) skips the gather's box download
+# and stream synchronise. Only series declared immutable take part (mark_immutable: bench.py's
+# resident series, data.load_batch's views): a tensor written through .data, DLPack or native
+# code keeps its version counter, and stale boxes would give band tables that are too narrow.
+# Entries live as long as the tensor (a weakref finalizer drops them), keyed by id() and checked
+# against the tensor's storage pointer, shape and strides.
+_IMMUTABLE = {}   # id(x) -> [weakref(x), (data_ptr, shape, stride), boxes or None]
 
 
-def _box_key(x: torch.Tensor, n: int, D: int):
-    return (x.device.index, x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), n, D)
+def mark_immutable(*tensors) -> None:
+    """Declare device series whose contents will not change while they are in use: their band
+    tables' boxes are computed once and reused by every later rebind of the same tensor.
+    Writing to a marked tensor afterwards is a contract violation (results could be wrong)."""
+    import weakref
+    for x in tensors:
+        if not (isinstance(x, torch.Tensor) and x.is_cuda):
+            continue
+        k = id(x)
+        sig = (x.data_ptr(), tuple(x.shape), tuple(x.stride()))
+        ent = _IMMUTABLE.get(k)
+        if ent is not None and ent[0]() is x and ent[1] == sig:
+            continue
+        _IMMUTABLE[k] = [weakref.ref(x), sig, None]
+        weakref.finalize(x, _IMMUTABLE.pop, k, None)
+
+
+def _immutable_entry(x: torch.Tensor):
+    """The cache entry of a marked tensor whose storage is still the marked one, else None."""
+    if os.environ.get("GPX_BOX_CACHE", "1") == "0":
+        return None
+    ent = _IMMUTABLE.get(id(x))
+    if ent is None or ent[0]() is not x:
+        return None
+    if ent[1] != (x.data_ptr(), tuple(x.shape), tuple(x.stride())):
+        return None
+    return ent
 
 
 class Engine:
@@ -151,19 +178,12 @@ class Engine:
     def _harvest_boxes(self) -> None:
         """After a device call gathered the pending rebinds: cache the boxes of the series that
         were not cached yet (gpx_batch_slot_boxes)."""
-        global _BOX_CACHE
         if not self._box_want:
             return
-        from collections import OrderedDict
-        if _BOX_CACHE is None:
-            _BOX_CACHE = OrderedDict()
-        for b, (key, x) in self._box_want.items():
+        for b, ent in self._box_want.items():
             buf = np.empty(((int(self.n[b]) + 15) // 16) * self.D * 2, dtype=np.float64)  # 16-row boxes
             if self.lib.gpx_batch_slot_boxes(self.handle, int(b), buf.ctypes.data) == N.GPX_OK:
-                _BOX_CACHE[key] = (x, buf)
-                _BOX_CACHE.move_to_end(key)
-                while len(_BOX_CACHE) > _BOX_CACHE_MAX:
-                    _BOX_CACHE.popitem(last=False)
+                ent[2] = buf
         self._box_want.clear()
 
     def lml_grad(self, active: Sequence[int], theta: np.ndarray):
@@ -362,10 +382,9 @@ class Engine:
             x2 = x.reshape(x.shape[0], -1)
             n, D, ny = x2.shape[0], x2.shape[1], y.numel()
             fn = self.lib.gpx_batch_rebind_device
-            key = _box_key(x, n, D) if X.is_contiguous() else None
-            hit = _BOX_CACHE.get(key) if (key is not None and _BOX_CACHE is not None) else None
-            if hit is not None:
-                box = hit[1]
+            ent = _immutable_entry(X) if X.is_contiguous() else None
+            if ent is not None and ent[2] is not None and ent[2].shape[0] == ((n + 15) // 16) * D * 2:
+                box = ent[2]
         else:
             x = np.ascontiguousarray(_host_f64(X))
             y = np.ascontiguousarray(_host_f64(Y)).reshape(-1)
@@ -389,8 +408,8 @@ class Engine:
         self._box_want.pop(b, None)
         if ok_dev:
             self._rebound[b] = (x, y)  # read by the deferred gather
-            if box is None and key is not None:
-                self._box_want[b] = (key, X)
+            if box is None and ent is not None:
+                self._box_want[b] = ent
         else:
             self._rebound.pop(b, None)
 

@@ -742,8 +742,10 @@ class _SteppedDriver:
                 self._run_all()
             # predictions from cached factors return without waiting for the device (in their
             # group stream's order); the caller reads them on its own stream
+            # (every device the groups' engines live on, not only the first group's)
             if self.predict_train and torch.cuda.is_available():
-                torch.cuda.synchronize(self.groups[0][0].device)
+                for dev in sorted({int(e.device) for e, _, _, _ in self.groups}):
+                    torch.cuda.synchronize(dev)
         finally:
             if gc_on:
                 gc.enable()

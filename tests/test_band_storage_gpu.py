@@ -221,9 +221,10 @@ def test_device_rebind_waits_for_the_producer_stream():
 
 
 def test_cached_block_boxes_follow_the_series():
-    """Device rebinds of a series seen before reuse its cached per-block boxes (no box download
-    at the gather, gpx_batch_rebind_device_boxed); an in-place write to the series bumps its
-    version and the boxes are recomputed: results always equal a fresh engine's."""
+    """Device rebinds of a series declared immutable (engine.mark_immutable) reuse its cached
+    per-16-row boxes (no box download at the gather, gpx_batch_rebind_device_boxed); a series
+    that is not declared immutable never does, so an in-place write to it (even one that keeps
+    the version counter, through .data) is seen: results always equal a fresh engine's."""
     from portfoliooptgp_amd import engine as E
     n = 2048
     x, y = O.synthetic_series(n, seed=41)
@@ -238,19 +239,35 @@ def test_cached_block_boxes_follow_the_series():
         return ref.lml_grad([0], th[:1])
 
     l0, g0, _ = fresh(x, y)
+    # not marked: no cache entry, every rebind gathers and downloads its boxes
     eng.rebind(0, xd, yd, spec)
-    eng.lml_grad([0], th)                              # gathers, downloads the boxes, caches them
-    key = E._box_key(xd, n, 1)
-    assert E._BOX_CACHE is not None and key in E._BOX_CACHE
+    assert 0 not in eng._box_want
+    eng.lml_grad([0], th)
+    assert E._immutable_entry(xd) is None
+    # marked: the first gather's boxes are kept, the next rebind of the series is boxed
+    E.mark_immutable(xd)
+    eng.rebind(0, xd, yd, spec)
+    assert 0 in eng._box_want
+    eng.lml_grad([0], th)
+    assert E._immutable_entry(xd)[2] is not None
     eng.rebind(1, xd, yd, spec)                        # cached: boxed rebind
     assert 1 not in eng._box_want
     l1, g1, _ = eng.lml_grad([0, 1], th)
     assert l1[1] == l0[0] and np.array_equal(g1[1, :3], g0[0, :3])
-    # spread the inputs out in place: p = 0 now, and the cached boxes must not be used
-    xd.mul_(50.0)
+    # an unmarked series written in place through .data (version counter unchanged): p = 0 now,
+    # and nothing cached may be used for it
+    xu = torch.as_tensor(x, device="cuda:0")
+    eng.rebind(1, xu, yd, spec)
+    eng.lml_grad([1], th)
+    xu.data.mul_(50.0)
     x50 = x * 50.0
-    eng.rebind(1, xd, yd, spec)
-    assert 1 in eng._box_want
+    eng.rebind(1, xu, yd, spec)
     l2, g2, _ = eng.lml_grad([1], th)
     l3, g3, _ = fresh(x50, y)
     assert l2[1] == l3[0] and np.array_equal(g2[1, :3], g3[0, :3])
+    # the entry goes with the tensor
+    k = id(xd)
+    del xd
+    import gc
+    gc.collect()
+    assert k not in E._IMMUTABLE or E._IMMUTABLE[k][0]() is None

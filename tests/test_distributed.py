@@ -222,19 +222,80 @@ def test_fit_assets_checkpoint_discarded_under_another_fit_configuration(tmp_pat
 
 def test_band_aware_fit_cost_and_shard():
     """LPT costs follow the path a fit takes: a C2-like day-offset series of N = 4096 starts on
-    the banded path (p = 1 block at GPflow's ℓ = 1: N·128² work per evaluation), the same N on
-    normalised inputs runs dense (N³)."""
+    the 16-row band sweeps (Q = 3 16-blocks at GPflow's ℓ = 1: (N/16)·(Q+1) block-step work per
+    evaluation), wider bands on the 64-row sweeps (N·w²), the same N on normalised inputs runs
+    dense (N³); every cost in device seconds per evaluation, so the classes compare."""
     x_days = np.arange(4096.0)
     assert D.band_blocks_estimate(x_days) == 1
     assert D.band_blocks_estimate(x_days / 4096.0) is None        # dense
     assert D.band_blocks_estimate(np.arange(300.0)) is None       # < 8 blocks: dense
     assert D.band_blocks_estimate(np.arange(4096.0), lengthscale=1.72) == 2
-    assert D.series_cost(x_days) == D.fit_cost(4096, 1) == 4096 * 128.0 ** 2
-    assert D.series_cost(x_days / 4096.0) == D.fit_cost(4096) == 4096.0 ** 3
+    assert D.band16_estimate(x_days) == 3
+    assert D.band16_estimate(x_days, lengthscale=1.6) == 4
+    assert D.band16_estimate(x_days, lengthscale=1.72) == 5
+    assert D.band16_estimate(x_days, lengthscale=2.2) is None     # wider than 5 16-blocks
+    assert D.band16_estimate(x_days / 4096.0) is None
+    assert D.series_cost(x_days) == D.fit_cost(4096, 1, 3)
+    assert D.fit_cost(4096, 1, 4) / D.fit_cost(4096, 1, 3) == pytest.approx(5 / 4)
+    assert D.fit_cost(2048, 1, 3) == pytest.approx(D.fit_cost(4096, 1, 3) / 2)
+    assert D.series_cost(x_days / 4096.0) == D.fit_cost(4096) == pytest.approx(1 / 832.0)
     # one dense N=2048 fit outweighs eight banded N=4096 ones: it goes alone
     series = [np.arange(4096.0)] * 8 + [np.arange(2048.0) / 2048.0]
     sh = D.shard_lpt([D.series_cost(x) for x in series], 2)
     assert [8] in sh
+
+
+def _skewed_mix():
+    """Mixed N and band width: day offsets at N = 4096 / 2048 / 1024 with unit spacing (Q = 3)
+    and at 0.7-day spacing (ℓ = 1 spans more points: Q = 4); C3-like."""
+    xs = ([np.arange(4096.0)] * 3 + [np.arange(4096.0) * 0.7] * 2 + [np.arange(2048.0)] * 5
+          + [np.arange(2048.0) * 0.7] * 3 + [np.arange(1024.0)] * 7)
+    return [(x[:, None], np.zeros((len(x), 1))) for x in xs]
+
+
+def _skew_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        series = _skewed_mix()
+        horizons = [np.zeros((2, 1))] * len(series)
+        mine = []
+
+        def fit(ss, hs):   # stand-in fitter: records this rank's shard by series length/spacing
+            out = []
+            for x, _ in ss:
+                mine.append(D.series_cost(x))
+                out.append(dict(loss=float(len(x)), nfev=1, theta=[float(x[1, 0] - x[0, 0]), 1.0],
+                                mean=np.zeros(2), var=np.ones(2)))
+            return out
+        res = D.fit_assets(series, horizons, fit_fn=fit, n_theta=2)
+        q.put((rank, sum(mine), len(mine), sorted(res)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_skewed_mix_balances_band16_costs():
+    """A skewed mix (N = 4096 / 2048 / 1024, bands of Q = 3 and Q = 4 16-blocks) sharded over 2
+    gloo ranks by fit_assets' default band16-aware series_cost: every asset fitted once and
+    gathered on both ranks, and the two ranks' device costs within 10 % (the round-3 64-row cost
+    model, N·(64(p+1))², weighed both band widths alike)."""
+    costs = [D.series_cost(x) for x, _ in _skewed_mix()]
+    assert len(set(np.round(np.array(costs) / costs[-1], 6))) == 5   # five cost classes
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_skew_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    loads = [o[1] for o in outs]
+    assert sum(o[2] for o in outs) == len(costs)
+    assert all(o[3] == list(range(len(costs))) for o in outs)
+    assert max(loads) / min(loads) < 1.10, loads
+    assert sum(loads) == pytest.approx(sum(costs))
 
 
 def _portfolio_worker(rank, world, port, q):
