@@ -122,6 +122,23 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
         t_eval1, t_pred1 = timed(1)
     t_fit = nfev_per_fit * t_eval + t_pred
     t_fit1 = nfev_per_fit * t_eval1 + t_pred1
+    # context, not the baseline: the device's own band algorithm restated on the CPU
+    # (oracle/band_oracle.py, numpy + LAPACK), whole fits (L-BFGS-B + predict) of C2 series run
+    # one per process on every job core, so the GPU/CPU ratio can be split into algorithm and
+    # hardware
+    same_alg = None
+    try:
+        from oracle import band_oracle as BO
+        seeds = list(range(1000, 1000 + 4 * cores))
+        fps, nf_b, s_fit = BO.parallel_fits_per_s(n, seeds, cores, NOISE)
+        same_alg = {"value": fps, "unit": "fits/s", "cores": int(cores), "kind": "port (band algorithm)",
+                    "sample": (f"oracle/band_oracle.py: {len(seeds)} whole C2 fits at N={n} (block-tridiagonal "
+                               "Cholesky + Takahashi selected inverse on the exact-zero band, scipy L-BFGS-B "
+                               f"maxiter 100, predict_f at the training inputs), one per process on {cores} "
+                               "processes, BLAS single-threaded"),
+                    "nfev_mean": nf_b, "seconds_per_fit_1core": s_fit}
+    except Exception as e:  # reported, never fatal
+        same_alg = {"error": f"{type(e).__name__}: {e}"}
     cpu_model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -145,6 +162,7 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
         "cpu_model": cpu_model,
         "host_cpus_visible": aff,
         "cgroup_cpu_quota": quota,
+        "same_algorithm_context": same_alg,
     }
 
 

@@ -1,0 +1,57 @@
+"""The banded CPU restatement (oracle/band_oracle.py: the device's band algorithm on numpy +
+LAPACK, timed by bench.py as the same-algorithm CPU context) against the dense oracle."""
+import numpy as np
+import pytest
+
+from oracle import band_oracle as B
+from oracle import gp_oracle as O
+
+
+@pytest.mark.parametrize("n,ell,var", [(1024, 1.0, 1.0), (1024, 1.6, 0.7), (777, 2.5, 1.3), (300, 1.18, 1.0), (5, 1.0, 1.0)])
+def test_band_eval_matches_dense_oracle(n, ell, var):
+    x, y = O.synthetic_series(n, 3)
+    m = O.OGPR(x, y, O.OSquaredExponential(variance=var, lengthscales=ell), noise_variance=1e-5)
+    l_d, g_d = m.loss_and_grad_u()
+    b = B.OBandGPR(x, y, 1e-5)
+    b.ell, b.var = ell, var
+    l_b, g_b = b.loss_and_grad_u()
+    assert abs(l_b - l_d) <= 1e-9 * abs(l_d)
+    np.testing.assert_allclose(g_b, g_d[:2], rtol=1e-8, atol=1e-8 * np.abs(g_d).max())
+    mf, vf = m.predict_f(x)
+    mb, vb = b.predict_f_train()
+    np.testing.assert_allclose(mb, mf[:, 0], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(vb, vf[:, 0], rtol=1e-8, atol=1e-14)
+
+
+def test_band_eval_noise_gradient():
+    """The noise derivative (trace of ααᵀ − K⁻¹) with the noise trainable."""
+    x, y = O.synthetic_series(512, 5)
+    m = O.OGPR(x, y, O.OSquaredExponential(lengthscales=1.3), noise_variance=1e-3)
+    l_d, g_d = m.loss_and_grad_u()
+    b = B.OBandGPR(x, y, 1e-3, noise_trainable=True)
+    b.ell = 1.3
+    l_b, g_b = b.loss_and_grad_u()
+    assert abs(l_b - l_d) <= 1e-9 * abs(l_d)
+    np.testing.assert_allclose(g_b, g_d, rtol=1e-8)
+
+
+def test_half_band_is_the_underflow_bound():
+    x = np.arange(4096.0)
+    for ell in (1.0, 1.18, 1.72):
+        w = B.se1_half_band(x, ell)
+        a = x / ell
+        r2 = lambda d: -2.0 * a[d] * a[0] + (a[d] * a[d] + a[0] * a[0])
+        assert np.exp(-0.5 * r2(w)) > 0.0 and np.exp(-0.5 * r2(w + 1)) == 0.0
+        assert w == pytest.approx(38.6 * ell, abs=1.5)
+
+
+def test_band_fit_reaches_the_dense_oracle_optimum():
+    """A whole C2-protocol fit (GPR/model_trainer.py:15-20) at N = 512 on the band algorithm
+    reaches the dense oracle's fitted loss (the iterates themselves may part at rounding level)."""
+    x, y = O.synthetic_series(512, 1)
+    fun, u, nfev = B.fit(x, y)
+    m = O.OGPR(x, y, O.OSquaredExponential(), noise_variance=1e-5)
+    m.noise.trainable = False
+    r = O.scipy_minimize(m, 100)
+    assert abs(fun - r.fun) <= 1e-6 * abs(r.fun)
+    assert 3 <= nfev <= 100
