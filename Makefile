@@ -37,6 +37,28 @@ $(PHASES_LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band_phases.o
 phases: $(PHASES_LIB)
 
 clean:
-	rm -f $(CSRC)/*.o $(LIB) $(PHASES_LIB) $(CSMOKE)
+	rm -f $(CSRC)/*.o $(LIB) $(PHASES_LIB) $(CSMOKE) $(HARNESS)
+	rm -rf build/asan
 
-.PHONY: all clean phases
+# host-logic harness (tests/test_host_harness.py): the library's sources compiled with
+# AddressSanitizer + UndefinedBehaviorSanitizer on the HOST code only (-Xarch_host; the gfx950
+# device code is built as usual and never launched: the harness calls pure host functions)
+HARNESS := tests/c/host_harness
+HSRC := $(wildcard $(CSRC)/*.hip)
+HOBJ := $(patsubst $(CSRC)/%.hip,build/asan/%.o,$(HSRC))
+HSAN := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
+  -Xarch_host -fno-omit-frame-pointer -g -O1
+build/asan/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h $(CSRC)/gpx_leaf.h include/gpx.h
+	@mkdir -p build/asan
+	$(HIPCC) --offload-arch=$(ARCH) -std=c++17 -fPIC $(HSAN) -c $< -o $@
+build/asan/gpx_host_math.o: $(CSRC)/gpx_host_math.c include/gpx.h
+	@mkdir -p build/asan
+	gcc -O1 -g -fno-builtin -fno-fast-math -fPIC -std=c11 -fsanitize=address,undefined -c $< -o $@
+build/asan/host_harness.o: tests/c/host_harness.cpp $(CSRC)/gpx_host.h $(CSRC)/gpx_internal.h include/gpx.h
+	@mkdir -p build/asan
+	$(HIPCC) --offload-arch=$(ARCH) -x hip -std=c++17 $(HSAN) -Iinclude -c $< -o $@
+$(HARNESS): build/asan/host_harness.o $(HOBJ) build/asan/gpx_host_math.o
+	$(HIPCC) --offload-arch=$(ARCH) $(HSAN) $^ -o $@
+host-harness: $(HARNESS)
+
+.PHONY: all clean phases host-harness

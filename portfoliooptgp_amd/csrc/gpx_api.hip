@@ -457,6 +457,78 @@ void band_eval(const Run& r, int p, int max_terms) {
   launch_reduce(ra, r.na, r.s);
 }
 
+// Routing of one evaluation call: the block-banded path when K and every ∂K/∂θ vanish exactly
+// beyond a band of p <= band_limit 64-blocks at this θ (gpx_band.hip), the dense recursion
+// otherwise. p <= 2 problems whose band is at most band16_limit 16-blocks take the band16
+// sweeps (grouped by width Q), other p <= 2 problems the 64-row fused sweeps; band storage runs
+// everything else on its dense fallback slots. Pure host logic over the band tables (writes
+// h_bandp; tests/c/host_harness.cpp runs it under ASan/UBSan).
+void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double* theta, Route& rt) {
+  std::vector<int32_t>& order = rt.order;
+  order.clear();
+  order.reserve(n_active);
+  rt.shadow_ids.clear();
+  std::vector<int32_t> band_ids, fused_ids;
+  int pband = 0;
+  int plim = band_limit(bt);
+  if (bt->compact) plim = std::min(plim, kBandStoreP);
+  const char* ef = getenv("GPX_BAND_FUSED");  // 0: p <= 2 problems take the per-block launches too
+  const bool fused_on = !(ef && atoi(ef) == 0);
+  const int q16lim = fused_on ? band16_limit(bt) : -1;
+  std::vector<int32_t> b16_ids[kBand16MaxQ + 1];  // band16 class by width Q (16-blocks)
+  bool b16_p2 = false;                             // ... holding p = 2 problems (K band of 3 diagonals)
+  for (int i = 0; i < n_active; ++i) {
+    const int b = active[i];
+    const double* thb = theta + (size_t)b * GPX_THETA_STRIDE;
+    const int p = plim >= 0 ? band_width(bt, b, thb) : -1;
+    if (p >= 0 && p <= plim) {
+      bt->h_bandp[b] = p;
+      // p <= 2 problems whose band is at most kBand16MaxQ 16-blocks: the band16 sweeps
+      const int q16 = (p <= 2 && q16lim > 0) ? band_width16(bt, b, thb) : -1;
+      if (q16 >= 0 && q16 <= q16lim) {
+        const int Q = std::max(q16, 1);
+        bt->h_bandp[b] = Q;
+        b16_ids[Q].push_back(b);
+        b16_p2 = b16_p2 || p == 2;
+      } else if (fused_on && (p <= 1 || (p == 2 && bt->D <= 12))) {
+        // (the p = 2 sweep holds four 64x64 LDS blocks plus three 64·D X-row slots: <= 160 KiB)
+        fused_ids.push_back(b);
+      } else if (bt->compact) {
+        rt.shadow_ids.push_back(b);  // band storage runs the fused sweeps only
+      } else {
+        band_ids.push_back(b);
+        pband = std::max(pband, p);
+      }
+    } else if (bt->compact) {
+      rt.shadow_ids.push_back(b);    // dense on the fallback slots, at _complete
+    } else {
+      order.push_back(b);
+    }
+  }
+  rt.n16 = 0;
+  for (int q = 1; q <= kBand16MaxQ; ++q) rt.n16 += (int)b16_ids[q].size();
+  rt.n_dense = (int)order.size();
+  rt.n_band = (int)band_ids.size();
+  rt.n_fused = (int)fused_ids.size() + rt.n16;
+  rt.pband = pband;
+  rt.b16_p2 = b16_p2;
+  order.insert(order.end(), band_ids.begin(), band_ids.end());
+  // fused problems: the band16 class first (by width), then p <= 1 (its own two-blocks-per-CU
+  // kernels), then p = 2
+  rt.n_g16 = 0;
+  for (int q = 1; q <= kBand16MaxQ; ++q)
+    if (!b16_ids[q].empty()) {
+      order.insert(order.end(), b16_ids[q].begin(), b16_ids[q].end());
+      rt.g16_q[rt.n_g16] = q;
+      rt.g16_n[rt.n_g16++] = (int)b16_ids[q].size();
+    }
+  rt.n_fused1 = 0;
+  for (int b : fused_ids)
+    if (bt->h_bandp[b] <= 1) order.push_back(b), ++rt.n_fused1;
+  for (int b : fused_ids)
+    if (bt->h_bandp[b] > 1) order.push_back(b);
+}
+
 // Band width <= 2 blocks: the whole sweep per problem in two fused kernels (gpx_band.hip),
 // each problem with its own p (d_bandp); K's band is built for the widest.
 double band_fused_flops(int Np, int p, bool fwd) {
@@ -533,6 +605,12 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     const char* e = getenv("GPX_BAND_LANES");
     return !(e && atoi(e) == 0);
   }();
+  // GPX_B16_INLINE_K=0: the SE1 band16 sweeps read K from a band built by band16_build_kernel
+  // (the round-3 path; same bits) instead of computing their tiles from X
+  static const bool kin = [] {
+    const char* e = getenv("GPX_B16_INLINE_K");
+    return !(e && atoi(e) == 0);
+  }();
   const int nstreams = lanes_on ? std::min(nl, 1 + kAux) : 1;
   auto lane_stream = [&](int i) { return (i % nstreams) == 0 ? r.s : bt->aux[(i % nstreams) - 1]; };
   if (nstreams > 1) {
@@ -543,13 +621,16 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     const Lane& l = lanes[i];
     hipStream_t ls = lane_stream(i);
     if (l.kind == 0) {
-      BuildArgs bg = ba;
-      bg.active = r.d_act + l.off;
-      launch_band16_build(bg, g16_q[l.g], l.n, ls);
+      // SE1 classes compute their K tiles inside the sweeps (band16 KIN): no build launch
+      if (!(se1 && kin)) {
+        BuildArgs bg = ba;
+        bg.active = r.d_act + l.off;
+        launch_band16_build(bg, g16_q[l.g], l.n, ls);
+      }
       BandFusedArgs f16 = fa;
       f16.kband = kband16;
       f16.active = r.d_act + l.off;
-      launch_band16(f16, g16_q[l.g], max_terms, se1, l.n, ls, ev16 ? ev16[l.g] : nullptr);
+      launch_band16(f16, g16_q[l.g], max_terms, se1, kin, l.n, ls, ev16 ? ev16[l.g] : nullptr);
     } else if (l.kind == 1) {
       BuildArgs b1 = ba;
       b1.active = r.d_act + l.off;
@@ -1321,52 +1402,17 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (rc0 != GPX_OK) return rc0;
   }
   sc.lap(0);
-  // Route each problem: the block-banded path when K and every ∂K/∂θ vanish exactly beyond a
-  // band of p <= band_limit 64-blocks at this θ (gpx_band.hip), the dense recursion otherwise.
-  // The device active list is [dense problems | banded problems].
-  std::vector<int32_t> order;
-  order.reserve(n_active);
-  std::vector<int32_t> band_ids, fused_ids, shadow_ids;
-  int pband = 0, pfused = 0;
-  int plim = band_limit(bt);
-  if (bt->compact) plim = std::min(plim, kBandStoreP);
-  const char* ef = getenv("GPX_BAND_FUSED");  // 0: p <= 2 problems take the per-block launches too
-  const bool fused_on = !(ef && atoi(ef) == 0);
-  const int q16lim = fused_on ? band16_limit(bt) : -1;
-  std::vector<int32_t> b16_ids[kBand16MaxQ + 1];  // band16 class by width Q (16-blocks)
-  bool b16_p2 = false;                             // ... holding p = 2 problems (K band of 3 diagonals)
-  for (int i = 0; i < n_active; ++i) {
-    const int b = active[i];
-    const double* thb = theta + (size_t)b * GPX_THETA_STRIDE;
-    const int p = plim >= 0 ? band_width(bt, b, thb) : -1;
-    if (p >= 0 && p <= plim) {
-      bt->h_bandp[b] = p;
-      // p <= 2 problems whose band is at most kBand16MaxQ 16-blocks: the band16 sweeps
-      const int q16 = (p <= 2 && q16lim > 0) ? band_width16(bt, b, thb) : -1;
-      // the p = 2 sweep holds four 64x64 LDS blocks plus three 64·D X-row slots (<= 160 KiB)
-      if (q16 >= 0 && q16 <= q16lim) {
-        const int Q = std::max(q16, 1);
-        bt->h_bandp[b] = Q;
-        b16_ids[Q].push_back(b);
-        b16_p2 = b16_p2 || p == 2;
-      } else if (fused_on && (p <= 1 || (p == 2 && bt->D <= 12))) {
-        fused_ids.push_back(b);
-        pfused = std::max(pfused, p);
-      } else if (bt->compact) {
-        shadow_ids.push_back(b);  // band storage runs the fused sweeps only
-      } else {
-        band_ids.push_back(b);
-        pband = std::max(pband, p);
-      }
-    } else if (bt->compact) {
-      shadow_ids.push_back(b);    // dense on the fallback slots, at _complete
-    } else {
-      order.push_back(b);
-    }
-  }
-  int n16 = 0;
-  for (int q = 1; q <= kBand16MaxQ; ++q) n16 += (int)b16_ids[q].size();
-  const int n_dense = (int)order.size(), n_band = (int)band_ids.size(), n_fused = (int)fused_ids.size() + n16;
+  // Route each problem (route_call: the dense recursion, the per-block banded launches, the
+  // band16 sweeps by width, the 64-row fused sweeps, or the fallback slots of band storage)
+  Route rt;
+  route_call(bt, n_active, active, theta, rt);
+  std::vector<int32_t>& order = rt.order;
+  std::vector<int32_t>& shadow_ids = rt.shadow_ids;
+  const int n_dense = rt.n_dense, n_band = rt.n_band, n_fused = rt.n_fused, n16 = rt.n16;
+  const int pband = rt.pband, n_g16 = rt.n_g16, n_fused1 = rt.n_fused1;
+  const int* g16_q = rt.g16_q;
+  const int* g16_n = rt.g16_n;
+  const bool b16_p2 = rt.b16_p2;
   // the problems launched by this call (band storage: without the shadowed ones)
   n_active = n_dense + n_band + n_fused;
   // band storage: a few fallback problems go out at once on the fallback stream (more than the
@@ -1397,21 +1443,6 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     bt->pending_eval = std::move(pe0);
     return GPX_OK;
   }
-  order.insert(order.end(), band_ids.begin(), band_ids.end());
-  // fused problems: the band16 class first (by width), then p <= 1 (its own two-blocks-per-CU
-  // kernels), then p = 2
-  int g16_q[kBand16MaxQ], g16_n[kBand16MaxQ], n_g16 = 0;
-  for (int q = 1; q <= kBand16MaxQ; ++q)
-    if (!b16_ids[q].empty()) {
-      order.insert(order.end(), b16_ids[q].begin(), b16_ids[q].end());
-      g16_q[n_g16] = q;
-      g16_n[n_g16++] = (int)b16_ids[q].size();
-    }
-  int n_fused1 = 0;
-  for (int b : fused_ids)
-    if (bt->h_bandp[b] <= 1) order.push_back(b), ++n_fused1;
-  for (int b : fused_ids)
-    if (bt->h_bandp[b] > 1) order.push_back(b);
   if (n_band > 0) {
     const int e = ensure(ctx, bt->bres, bt->bres_cap, (size_t)bt->B * bt->Np);
     if (e != GPX_OK) return drop_shadow(e);

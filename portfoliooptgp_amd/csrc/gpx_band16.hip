@@ -275,6 +275,20 @@ __device__ __forceinline__ t4 ktile_t(const double* __restrict__ K, long long ld
 
 constexpr __host__ __device__ int wid(int i, int j) { return i * (i + 1) / 2 + j; }  // lower (i, j), j <= i
 
+// K_ij of the reference's kernel (SE1: one SquaredExponential term on one input column) from the
+// scaled inputs a = x/ℓ, computed where a sweep needs it (KIN) instead of read from a K band that
+// band16_build_kernel wrote: σ²·exp(−½ r²) with GPflow's r² (sqdist1), σn² added on the diagonal,
+// the identity in the padding — the build kernel's operations, so the same bits (sqdist1 is
+// symmetric in its arguments bit for bit, so no tile needs mirroring)
+__device__ __forceinline__ double k_se1(double ai, double aj, bool ok, bool diag, double var, double noise) {
+  if (!ok) return diag ? 1.0 : 0.0;
+  const double v = stationary_value<GPX_SE>(sqdist1(ai, aj), var);
+  return diag ? v + noise : v;
+}
+// index of element il of a 16-row block in the "row-quad" order (il & 3)·4 + (il >> 2): lane
+// (l15, l4) finds the values of rows 4r + l4, r = 0..3, at 4·l4 .. 4·l4 + 3 (two ds_read_b128)
+__device__ __forceinline__ int rq(int il) { return (il & 3) * 4 + (il >> 2); }
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
@@ -288,10 +302,15 @@ constexpr __host__ __device__ int wid(int i, int j) { return i * (i + 1) / 2 + j
 #ifndef GPX_B16_FWD3_WAVES
 #define GPX_B16_FWD3_WAVES 2  // waves per SIMD the Q <= 3 forward sweep is compiled for
 #endif
-template <int Q>
+// KIN (SE1 problems only): the window's K tiles are computed in the sweep from X (k_se1) instead
+// of read from the K band band16_build_kernel wrote — no build launch, and K's band never goes
+// through HBM (2·(Q+1)·16·N doubles less per evaluation); the inputs of the last Q+1 blocks sit
+// scaled (x/ℓ) in a small LDS ring.
+template <int Q, bool KIN>
 __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1)) void band16_fwd_kernel(BandFusedArgs a) {
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
-  __shared__ __attribute__((aligned(16))) double snew[Q + 1][256];  // the entering row, staged by glds
+  __shared__ __attribute__((aligned(16))) double snew[KIN ? 1 : Q + 1][256];  // the entering row, staged by glds
+  __shared__ __attribute__((aligned(16))) double sxa[KIN ? Q + 1 : 1][16];    // KIN: x/ℓ of blocks m, slot m % (Q+1), rq order
   const int b = a.active[blockIdx.x];
   const int Np = a.Np, nb = Np >> 4;
   const long long ld = a.ld;
@@ -303,26 +322,75 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
   const int n = a.nvalid[b];
   const int lane = threadIdx.x, l15 = lane & 15, l4 = lane >> 4;
   constexpr int NW = (Q + 1) * (Q + 2) / 2;
+  // KIN: the SE1 term's column, ℓ, σ², σn²
+  const double* X = a.X + (long long)b * a.sX;
+  int xd0 = 0;
+  double kell = 1.0, kvar = 1.0, knoise = 0.0;
+  if constexpr (KIN) {
+    const gpx_term& tm = a.specs[b].terms[0];
+    const double* th = a.theta + (long long)b * GPX_THETA_STRIDE;
+    xd0 = tm.dim_start;
+    kell = th[tm.param_offset];
+    kvar = th[tm.param_offset + 1];
+    knoise = th[a.specs[b].n_params];
+  }
+  const int D = a.D;
+  auto xval = [&](int g) { return X[(long long)min(g, n - 1) * D + xd0]; };  // (clamped into the slot's rows)
   t4 T[NW];
   double u[Q + 1];
+  if constexpr (KIN) {
+    // blocks 0..Q: the ring and the first window, computed
+    if (l4 == 0) {
 #pragma unroll
-  for (int i = 0; i <= Q; ++i) {
-    u[i] = 0.0;
+      for (int m = 0; m <= Q; ++m) sxa[m][rq(l15)] = m < nb ? xval(m * 16 + l15) / kell : 0.0;
+    }
+    wsync();
 #pragma unroll
-    for (int j = 0; j <= i; ++j) T[wid(i, j)] = (i < nb) ? ktile_t(K, ld, i, j, l15, l4, a.kband) : tzero();
+    for (int i = 0; i <= Q; ++i) {
+      u[i] = 0.0;
+      const double ar = i < nb ? xval(i * 16 + l15) / kell : 0.0;
+      const int gi = i * 16 + l15;
+#pragma unroll
+      for (int j = 0; j <= i; ++j) {
+        t4 t = tzero();
+        if (i < nb) {
+          const t4 ac = *reinterpret_cast<const t4*>(&sxa[j][4 * l4]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int gj = j * 16 + 4 * r + l4;
+            const bool zero = (gi >> 6) - (gj >> 6) >= a.kband;
+            t[r] = zero ? 0.0 : k_se1(ar, ac[r], gi < n && gj < n, gi == gj, kvar, knoise);
+          }
+        }
+        T[wid(i, j)] = t;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i <= Q; ++i) {
+      u[i] = 0.0;
+#pragma unroll
+      for (int j = 0; j <= i; ++j) T[wid(i, j)] = (i < nb) ? ktile_t(K, ld, i, j, l15, l4, a.kband) : tzero();
+    }
   }
   int gfail = 0;
   Q_BEGIN
   for (int k = 0; k < nb; ++k) {
     const int qk = min(Q, nb - 1 - k), k16 = k * 16;
     // the row entering the window after this step (block bn = k+Q+1): global -> LDS, in flight
-    // during the step (the previous step's reads of snew are done: program order + wsync)
+    // during the step (the previous step's reads of snew are done: program order + wsync);
+    // KIN: only its inputs (one value per row, into a register)
     const int bn = k + Q + 1;
-    wsync();
-    lds_drain();  // the previous step's reads of snew have completed
-    if (bn < nb) {
+    double xn = 0.0;
+    if constexpr (KIN) {
+      if (bn < nb) xn = xval(bn * 16 + l15);
+    } else {
+      wsync();
+      lds_drain();  // the previous step's reads of snew have completed
+      if (bn < nb) {
 #pragma unroll
-      for (int j = 0; j <= Q; ++j) tile_glds_swz(K + (long long)(bn * 16) * ld + (k + 1 + j) * 16, ld, snew[j], lane);
+        for (int j = 0; j <= Q; ++j) tile_glds_swz(K + (long long)(bn * 16) * ld + (k + 1 + j) * 16, ld, snew[j], lane);
+      }
     }
     // y_k in the row layout of u (lane l15 holds row l15)
     double yl = y[min(k16 + l15, n - 1)];
@@ -390,20 +458,44 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
     }
     u[Q] = 0.0;
     QP(7);
+    if constexpr (KIN) {
+      // block bn's inputs join the ring (in the slot of block k, whose last reads were at the
+      // previous step's end), then the new row's tiles (bn, k+1+j) from x/ℓ
+      const double ar = xn / kell;
+      if (bn < nb && l4 == 0) sxa[bn % (Q + 1)][rq(l15)] = ar;
+      wsync();
+      const int gi = bn * 16 + l15;
 #pragma unroll
-    for (int j = 0; j <= Q; ++j) {
-      t4 t = tzero();
-      if (bn < nb) {
+      for (int j = 0; j <= Q; ++j) {
+        t4 t = tzero();
+        const int c = k + 1 + j;
         // (16-row blocks sit inside one 64-block: the 64-block offset is uniform over the tile)
-        const bool zero = (bn >> 2) - ((k + 1 + j) >> 2) >= a.kband;
+        if (bn < nb && (bn >> 2) - (c >> 2) < a.kband) {
+          const t4 ac = *reinterpret_cast<const t4*>(&sxa[c % (Q + 1)][4 * l4]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int cl = 4 * r + l4;
-          const double v = (j == Q && cl > l15) ? snew[j][swz16(cl, l15)] : snew[j][swz16(l15, cl)];
-          t[r] = zero ? 0.0 : v;
+          for (int r = 0; r < 4; ++r) {
+            const int gj = c * 16 + 4 * r + l4;
+            t[r] = k_se1(ar, ac[r], gi < n && gj < n, gi == gj, kvar, knoise);
+          }
         }
+        T[wid(Q, j)] = t;
       }
-      T[wid(Q, j)] = t;
+    } else {
+#pragma unroll
+      for (int j = 0; j <= Q; ++j) {
+        t4 t = tzero();
+        if (bn < nb) {
+          // (16-row blocks sit inside one 64-block: the 64-block offset is uniform over the tile)
+          const bool zero = (bn >> 2) - ((k + 1 + j) >> 2) >= a.kband;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int cl = 4 * r + l4;
+            const double v = (j == Q && cl > l15) ? snew[j][swz16(cl, l15)] : snew[j][swz16(l15, cl)];
+            t[r] = zero ? 0.0 : v;
+          }
+        }
+        T[wid(Q, j)] = t;
+      }
     }
     QP(5);
   }
@@ -428,15 +520,18 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
 #ifndef GPX_B16_BWD_2W_QMAX
 #define GPX_B16_BWD_2W_QMAX 3  // widest band the SE1 backward sweep is compiled for two waves per SIMD
 #endif
-template <int Q, int NT, bool SE1>
+// KIN (SE1 only): K_ij computed from the r² the contraction forms anyway (k_se1's operations)
+// instead of fetched from the built K band: no K traffic and no 16 KiB K-tile double buffer.
+template <int Q, int NT, bool SE1, bool KIN>
 __global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
   static_assert(!SE1 || Q <= 5, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 5");
+  static_assert(!KIN || SE1, "inline K tiles: SE1 sweeps only");
   extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1); not SE1)
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   // SE1: the K tiles (k+i, k) as built, double-buffered by step parity (the next step's are
-  // fetched by glds while this step's are contracted); otherwise the step's Z tiles for the
-  // runtime contraction loop
-  __shared__ __attribute__((aligned(16))) double sz[SE1 ? 2 * (Q + 1) : Q + 1][256];
+  // fetched by glds while this step's are contracted; not KIN); otherwise the step's Z tiles
+  // for the runtime contraction loop
+  __shared__ __attribute__((aligned(16))) double sz[SE1 ? (KIN ? 1 : 2 * (Q + 1)) : Q + 1][256];
   __shared__ double sal[SE1 ? 1 : Q + 1][16];          // α ring (not SE1)
   // SE1: the α and x values of block m's rows in the contraction's lane order (lane (l15, l4)
   // takes rows 4r + l4: element of row il at (il & 3)·4 + (il >> 2)), so a lane reads its four
@@ -460,7 +555,7 @@ __global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void
   // issued at the start of the step before
   auto fetch = [&](int kk, double (&zr)[4], double (&xr)[2]) {
     const int q1 = min(Q, nb - 1 - kk), c16 = kk * 16;
-    if constexpr (SE1) {
+    if constexpr (SE1 && !KIN) {
 #pragma unroll
       for (int i = 0; i <= Q; ++i)
         if (i <= q1) tile_glds_swz(Kd + (long long)(c16 + 16 * i) * ld + c16, ld, sz[(kk & 1) * (Q + 1) + i], lane);
@@ -636,20 +731,31 @@ __global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void
         const double w = i == 0 ? 1.0 : 2.0;
         const t4 a4 = *reinterpret_cast<const t4*>(&salT[si][4 * l4]);  // α of rows 4r + l4
         const t4 x4 = *reinterpret_cast<const t4*>(&sxT[si][4 * l4]);   // x of rows 4r + l4
+        const bool zero = ((k + i) >> 2) - (k >> 2) >= a.kband;  // (uniform, see the forward sweep)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int il = 4 * r + l4, gi = (k + i) * 16 + il;
           const double zij = Zt[r];
           const double ai = a4[r];
           const double r2 = sqdist1(x4[r], xjv);
-          const bool up = i == 0 && il < l15;
-          const double kraw = sz[(k & 1) * (Q + 1) + i][up ? swz16(l15, il) : swz16(il, l15)];  // (swizzled rows)
-          const bool zero = ((k + i) >> 2) - (k >> 2) >= a.kband;  // (uniform, see the forward sweep)
+          const bool dg = i == 0 && il == l15;
+          double kraw;
+          if constexpr (KIN) {
+            // (rows past n: the ring holds 0 there and `ok` masks them; off the diagonal tile the
+            // rows past n are exact zeros of K for any finite r², as the built band holds)
+            kraw = 0.0;
+            if (!zero) {
+              const double kv = stationary_value<GPX_SE>(r2, fvar);
+              kraw = dg ? kv + noise : (i > 0 && gi >= n ? 0.0 : kv);
+            }
+          } else {
+            const bool up = i == 0 && il < l15;
+            kraw = sz[(k & 1) * (Q + 1) + i][up ? swz16(l15, il) : swz16(il, l15)];  // (swizzled rows)
+          }
           const double v = w * fma(ai, ap, -zij);
           // rows or columns past n: off the diagonal tile the built band holds exact zeros there
           // (the padding is the identity), so only the diagonal tile needs the mask
           const bool ok = i > 0 || (jok && gi < n);
-          const bool dg = i == 0 && il == l15;
           const double kij = (zero || !ok) ? 0.0 : kraw;
           const double kg = i > 0 ? kij : (ok ? (dg ? fvar : kij) : 0.0);  // σ²·g (the noise is not part of ∂K/∂θ)
           sums[0][0] = fma(v, kg * r2, sums[0][0]);  // (× 1/ℓ once, at the end)
@@ -887,30 +993,32 @@ void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s)
 }
 
 template <int Q>
-static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, int n_active, hipStream_t s, hipEvent_t* ev) {
-  auto bwd = se1 ? band16_bwd_kernel<Q, 1, true>
-                             : max_terms <= 1 ? band16_bwd_kernel<Q, 1, false>
-                                              : max_terms == 2 ? band16_bwd_kernel<Q, 2, false>
-                                                               : band16_bwd_kernel<Q, GPX_MAX_TERMS, false>;
-  const bool se1k = se1;
-  const size_t xs = se1k ? 0 : (size_t)(Q + 1) * 16 * a.D * sizeof(double);
+static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, bool kin, int n_active, hipStream_t s,
+                       hipEvent_t* ev) {
+  kin = kin && se1;
+  auto fwd = kin ? band16_fwd_kernel<Q, true> : band16_fwd_kernel<Q, false>;
+  auto bwd = se1 ? (kin ? band16_bwd_kernel<Q, 1, true, true> : band16_bwd_kernel<Q, 1, true, false>)
+                 : max_terms <= 1 ? band16_bwd_kernel<Q, 1, false, false>
+                                  : max_terms == 2 ? band16_bwd_kernel<Q, 2, false, false>
+                                                   : band16_bwd_kernel<Q, GPX_MAX_TERMS, false, false>;
+  const size_t xs = se1 ? 0 : (size_t)(Q + 1) * 16 * a.D * sizeof(double);
   if (ev) {
-    hipExtLaunchKernelGGL(band16_fwd_kernel<Q>, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
+    hipExtLaunchKernelGGL(fwd, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
     hipExtLaunchKernelGGL(bwd, dim3(n_active), dim3(64), xs, s, ev[2], ev[3], 0, a);
     return;
   }
-  hipLaunchKernelGGL(band16_fwd_kernel<Q>, dim3(n_active), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(fwd, dim3(n_active), dim3(64), 0, s, a);
   hipLaunchKernelGGL(bwd, dim3(n_active), dim3(64), xs, s, a);
 }
 
-void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int n_active, hipStream_t s,
+void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, bool kin, int n_active, hipStream_t s,
                    hipEvent_t* ev) {
   switch (Q) {
-    case 1: launch16_q<1>(a, max_terms, se1, n_active, s, ev); break;
-    case 2: launch16_q<2>(a, max_terms, se1, n_active, s, ev); break;
-    case 3: launch16_q<3>(a, max_terms, se1, n_active, s, ev); break;
-    case 4: launch16_q<4>(a, max_terms, se1, n_active, s, ev); break;
-    default: launch16_q<5>(a, max_terms, se1, n_active, s, ev); break;
+    case 1: launch16_q<1>(a, max_terms, se1, kin, n_active, s, ev); break;
+    case 2: launch16_q<2>(a, max_terms, se1, kin, n_active, s, ev); break;
+    case 3: launch16_q<3>(a, max_terms, se1, kin, n_active, s, ev); break;
+    case 4: launch16_q<4>(a, max_terms, se1, kin, n_active, s, ev); break;
+    default: launch16_q<5>(a, max_terms, se1, kin, n_active, s, ev); break;
   }
 }
 

@@ -231,6 +231,17 @@ int band16_limit(const gpx_batch* bt);  // widest band16 class (16-blocks), -1: 
 bool band_shape(const gpx_batch* bt);  // the banded path handles this batch's padded size
 int band_limit(const gpx_batch* bt);  // largest p the banded path takes (-1: path disabled)
 void band_eval(const Run& r, int p, int max_terms);  // build .. reduce for a banded active set
+// the routing of one evaluation call (gpx_batch_lml_grad_submit), pure host logic: the device
+// active list [dense | per-block band | band16 by width Q | 64-row fused p <= 1 | p = 2], the
+// band-storage fallback problems, the class sizes; writes h_bandp of the routed problems
+struct Route {
+  std::vector<int32_t> order;
+  std::vector<int32_t> shadow_ids;
+  int n_dense = 0, n_band = 0, n_fused = 0, n16 = 0, n_fused1 = 0, pband = 0;
+  int n_g16 = 0, g16_q[kBand16MaxQ] = {}, g16_n[kBand16MaxQ] = {};
+  bool b16_p2 = false;
+};
+void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double* theta, Route& rt);
 // p <= 2: [band16 groups (sizes g16_n, widths g16_q; K band of kband16 64-block diagonals) |
 // p<=1 (n1) | p=2]
 void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int kband16,

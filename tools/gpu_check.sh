@@ -14,3 +14,4 @@ timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 500 python bench.py "$@" > gpurun_out/${TAG}_bench.log 2>&1 \
   || { tail -20 gpurun_out/${TAG}_bench.log; exit 1; }
 tail -1 gpurun_out/${TAG}_bench.log
+python tools/bench_summary.py default gpurun_out/${TAG}_bench.log
