@@ -307,6 +307,12 @@ class FitWorker:
                                [spec] * sz, device=gpu, band_storage=args.storage == "band")
                         for sz in sizes]
         self.engines[0].ctx.set_profiling(True)
+        # GPX_WAVE_TRACE=1: every band16 wavefront's residency (start, end) in the device clock,
+        # merged over the GPU's host processes into an occupancy timeline (wave_trace_summary)
+        self.wtrace = bool(int(os.environ.get("GPX_WAVE_TRACE", "0")))
+        if self.wtrace:
+            for e in self.engines:
+                e.wave_trace(int(os.environ.get("GPX_WAVE_TRACE_CAP", 1 << 21)))
         self.opt = gpx.optimizers.Scipy()
         self.width, self.groups = W, G
         self.traces, self.driver_stats = [], []
@@ -344,7 +350,14 @@ class FitWorker:
     def reset_timing(self):
         for e in self.engines:
             e.reset_timing()
+            if self.wtrace:
+                e.wave_trace_read()  # (discarded: restarts the recording)
         self.driver_stats = []
+
+    def wave_records(self):
+        if not self.wtrace:
+            return None
+        return np.concatenate([e.wave_trace_read() for e in self.engines])
 
     def timing(self):
         tms = [e.last_timing() for e in self.engines]
@@ -372,7 +385,8 @@ def helper_main(w, P, argv, rank, gpu, start, q):
     nfev, summary = wk.run_steps(args.steps)
     torch.cuda.synchronize()
     busy = time.perf_counter() - t0
-    q.put(("done", (w, nfev, summary, wk.timing(), wk.driver_stats[-1] if wk.driver_stats else None, busy)))
+    q.put(("done", (w, nfev, summary, wk.timing(), wk.driver_stats[-1] if wk.driver_stats else None, busy,
+                    wk.wave_records())))
     if os.environ.get("GPX_SUBMIT_STATS"):
         wk.engines.clear()  # destroyed now: the library prints the per-batch submit phases
 
@@ -395,6 +409,40 @@ def collect(q, helpers, kind, timeout):
         assert k == kind, (k, kind)
         got.append(v)
     return got
+
+
+def wave_trace_summary(recs, wall_s, clock_hz=1e8):
+    """Occupancy timeline of the band16 sweeps from every host process's wavefront records
+    (start, end, kind; the device's constant 100 MHz clock, shared by all processes): the mean
+    number of resident sweep wavefronts over the span from the first start to the last end, the
+    share of that span spent at each residency level, and the mean wave durations."""
+    r = np.concatenate([x for x in recs if x is not None and len(x)])
+    if len(r) == 0:
+        return {"records": 0}
+    t0, t1, kind = r[:, 0].astype(np.int64), r[:, 1].astype(np.int64), r[:, 2].astype(np.int64)
+    base = int(t0.min())
+    a, b = t0 - base, t1 - base
+    span = int(b.max())
+    ev_t = np.concatenate([a, b])
+    ev_d = np.concatenate([np.ones_like(a), -np.ones_like(b)])
+    o = np.lexsort((ev_d, ev_t))  # ends before starts at equal times
+    ev_t, ev_d = ev_t[o], ev_d[o]
+    level = np.cumsum(ev_d)
+    dt = np.diff(ev_t, append=ev_t[-1])
+    edges = [0, 256, 512, 1024, 1536, 2048, 1 << 30]
+    share = {f"{edges[i]}-{edges[i + 1] - 1 if edges[i + 1] < (1 << 30) else 'up'}":
+             float(dt[(level >= edges[i]) & (level < edges[i + 1])].sum() / max(span, 1)) for i in range(len(edges) - 1)}
+    fwd, bwd = kind < 16, kind >= 16
+    dur = (b - a) / clock_hz * 1e3
+    return {"records": int(len(r)), "span_s": span / clock_hz, "wall_s": wall_s,
+            "mean_resident_waves": float(((b - a).sum()) / max(span, 1)),
+            "occupancy_2048": float(((b - a).sum()) / max(span, 1) / WAVE_SLOTS),
+            "share_of_span_by_resident_waves": share,
+            "fwd_wave_ms_mean": float(dur[fwd].mean()) if fwd.any() else None,
+            "bwd_wave_ms_mean": float(dur[bwd].mean()) if bwd.any() else None,
+            "q_hist": {int(q): int((kind % 16 == q).sum() // 2) for q in np.unique(kind % 16)},
+            "note": "band16 wavefronts only (s_memrealtime at each wave's start and end); span = first "
+                    "start to last end over all host processes of this GPU"}
 
 
 def secondary_c4(gpu, fits=32):
@@ -552,7 +600,8 @@ def main():
     torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     busy0 = time.perf_counter() - t0
-    parts = [(0, nfev, summary, wk.timing(), wk.driver_stats[-1] if wk.driver_stats else None, busy0)]
+    parts = [(0, nfev, summary, wk.timing(), wk.driver_stats[-1] if wk.driver_stats else None, busy0,
+              wk.wave_records())]
     parts += collect(q, helpers, "done", 1800)  # each sent after synchronising its device work
     parts.sort(key=lambda p: p[0])
     table = np.concatenate([p[2] for p in parts])
@@ -700,6 +749,8 @@ def main():
         "host": host,
         "roofline": roofline,
     }
+    if parts[0][6] is not None:
+        out["wave_trace"] = wave_trace_summary([p[6] for p in parts], elapsed)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, nfev_mean)
     if rank == 0 and world == 1 and not args.no_secondary:

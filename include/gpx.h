@@ -279,6 +279,15 @@ typedef struct {
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);
+/* Diagnostic: per-wavefront residency records of the band16 sweeps (one wavefront walks one
+ * problem), for occupancy timelines across processes sharing a GPU. cap > 0 allocates room for
+ * cap records and turns recording on; 0 frees it and turns it off (both synchronise the device).
+ * Each record is three uint64: start and end in the device's constant 100 MHz clock
+ * (s_memrealtime, one clock for every process on the GPU) and kind = Q (forward sweep) or
+ * 16 + Q (backward sweep). _read synchronises the device, copies up to cap records into out,
+ * sets *n_out and restarts the recording. */
+int gpx_batch_wave_trace(gpx_batch* batch, unsigned int cap);
+int gpx_batch_wave_trace_read(gpx_batch* batch, unsigned long long* out, unsigned int cap, unsigned int* n_out);
 int gpx_set_profiling(gpx_ctx* ctx, int enabled);
 
 /* ---------------------------------------------------------------------------------------

@@ -578,6 +578,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   fa.ldiag = bt->ldiag; fa.sVec = Np; fa.X = bt->X; fa.sX = (long long)bt->Nmax * bt->D; fa.D = bt->D;
   fa.specs = bt->d_specs; fa.theta = bt->d_theta; fa.partial = bt->partial; fa.sPartial = bt->partial_stride;
   fa.info = bt->d_info; fa.results = bt->results; fa.Np = Np; fa.ld = mat_ld(bt);
+  fa.wtrace = bt->d_wtrace; fa.wtrace_n = bt->d_wtrace_n; fa.wtrace_cap = bt->wtrace_cap;
   // The width classes of the call are independent: each class's chain (its K band build, then
   // its sweeps) is a *lane*, and the lanes run concurrently — the largest on the call's stream,
   // the others on the batch's auxiliary streams, joined before the reduction. Serialised on one
@@ -1096,7 +1097,7 @@ int gpx_batch_destroy(gpx_batch* bt) {
   if (bt->compact && bt->Kraw) {  // K/L/W point into the raw allocations (band storage's row offset)
     bt->K = bt->Kraw; bt->L = bt->Lraw; bt->W = bt->Wraw;
   }
-  for (void* p : {(void*)bt->shX, (void*)bt->shY})
+  for (void* p : {(void*)bt->shX, (void*)bt->shY, (void*)bt->d_wtrace, (void*)bt->d_wtrace_n})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
                   (void*)bt->ldiag, (void*)bt->partial, (void*)bt->d_io, (void*)bt->d_n,
@@ -2045,6 +2046,41 @@ int gpx_batch_reset_timing(gpx_batch* bt) {
 int gpx_batch_last_timing(const gpx_batch* bt, gpx_timing* out) {
   if (!bt || !out) return GPX_BAD_ARG;
   *out = bt->timing;
+  return GPX_OK;
+}
+
+// Diagnostic: the band16 sweeps' per-wavefront residency records (BandFusedArgs::wtrace)
+int gpx_batch_wave_trace(gpx_batch* bt, unsigned int cap) {
+  if (!bt) return GPX_BAD_ARG;
+  gpx_ctx* ctx = bt->ctx;
+  HIPX(ctx, hipSetDevice(ctx->device));
+  HIPX(ctx, hipDeviceSynchronize());  // no sweep is writing the old buffer
+  if (bt->d_wtrace) (void)hipFree(bt->d_wtrace);
+  if (bt->d_wtrace_n) (void)hipFree(bt->d_wtrace_n);
+  bt->d_wtrace = nullptr;
+  bt->d_wtrace_n = nullptr;
+  bt->wtrace_cap = 0;
+  if (cap == 0) return GPX_OK;
+  HIPX(ctx, hipMalloc(&bt->d_wtrace, sizeof(unsigned long long) * 3 * (size_t)cap));
+  HIPX(ctx, hipMalloc(&bt->d_wtrace_n, sizeof(unsigned int)));
+  HIPX(ctx, hipMemset(bt->d_wtrace_n, 0, sizeof(unsigned int)));
+  bt->wtrace_cap = cap;
+  return GPX_OK;
+}
+
+int gpx_batch_wave_trace_read(gpx_batch* bt, unsigned long long* out, unsigned int cap, unsigned int* n_out) {
+  if (!bt || !n_out || (cap > 0 && !out)) return GPX_BAD_ARG;
+  gpx_ctx* ctx = bt->ctx;
+  *n_out = 0;
+  if (!bt->d_wtrace) return GPX_OK;
+  HIPX(ctx, hipSetDevice(ctx->device));
+  HIPX(ctx, hipDeviceSynchronize());
+  unsigned int n = 0;
+  HIPX(ctx, hipMemcpy(&n, bt->d_wtrace_n, sizeof(n), hipMemcpyDeviceToHost));
+  n = std::min(n, std::min(cap, bt->wtrace_cap));
+  if (n > 0) HIPX(ctx, hipMemcpy(out, bt->d_wtrace, sizeof(unsigned long long) * 3 * (size_t)n, hipMemcpyDeviceToHost));
+  HIPX(ctx, hipMemset(bt->d_wtrace_n, 0, sizeof(unsigned int)));
+  *n_out = n;
   return GPX_OK;
 }
 

@@ -311,6 +311,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
   __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
   __shared__ __attribute__((aligned(16))) double snew[KIN ? 1 : Q + 1][256];  // the entering row, staged by glds
   __shared__ __attribute__((aligned(16))) double sxa[KIN ? Q + 1 : 1][16];    // KIN: x/ℓ of blocks m, slot m % (Q+1), rq order
+  const unsigned long long wt0 = a.wtrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int b = a.active[blockIdx.x];
   const int Np = a.Np, nb = Np >> 4;
   const long long ld = a.ld;
@@ -501,6 +502,7 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
   }
   Q_END(0);
   if (lane == 0 && gfail > 0 && a.info[b] == 0) a.info[b] = gfail;
+  wave_trace_put(a, wt0, Q);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -541,6 +543,7 @@ __global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void
   __shared__ double scs[Q + 1][16];                    // band check: column sums ring
   __shared__ double sth[GPX_THETA_STRIDE];
   __shared__ double sred[GPX_MAX_TERMS * 3 + 2];
+  const unsigned long long wt0 = a.wtrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int b = a.active[blockIdx.x];
   const int Np = a.Np, nb = Np >> 4;
   const long long ld = a.ld;
@@ -921,6 +924,7 @@ __global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void
     if (slot >= 0) s = sred[slot];
     out[lane] = s;
   }
+  wave_trace_put(a, wt0, 16 + Q);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -130,6 +130,10 @@ struct gpx_batch {
   int* h_info = nullptr;
   gpx_timing timing{};
   double flops_acc = 0.0;
+  // wave residency trace of the band16 sweeps (gpx_batch_wave_trace; off when null)
+  unsigned long long* d_wtrace = nullptr;
+  unsigned int* d_wtrace_n = nullptr;
+  unsigned int wtrace_cap = 0;
   // per-batch auxiliary streams and events (the recursion's T-product forks), so that
   // independent batches of one context can evaluate concurrently on different streams
   int aux_priority = 0;       // priority the aux streams were created with

@@ -162,7 +162,24 @@ struct BandFusedArgs {
   int ld;                                        // leading dimension of K/L/W (Np, or band storage's)
   int kband;                                     // band16: K's band was built with this many 64-block
                                                  // diagonals; entries beyond read as 0 (exact)
+  // wave residency trace (gpx_batch_wave_trace; nullptr: off): each band16 wavefront appends
+  // {start, end, kind} in the device's constant 100 MHz clock (s_memrealtime), kind = Q for the
+  // forward sweep, 16 + Q for the backward
+  unsigned long long* wtrace; unsigned int* wtrace_n; unsigned int wtrace_cap;
 };
+// one wavefront's residency record (lane 0 appends; a vector atomic on the counter)
+__device__ __forceinline__ void wave_trace_put(const BandFusedArgs& a, unsigned long long t0, int kind) {
+  if (a.wtrace == nullptr) return;
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned int i = atomicAdd(a.wtrace_n, 1u);
+    if (i < a.wtrace_cap) {
+      a.wtrace[3ull * i] = t0;
+      a.wtrace[3ull * i + 1] = t1;
+      a.wtrace[3ull * i + 2] = (unsigned long long)kind;
+    }
+  }
+}
 void launch_band_fused(const BandFusedArgs& a, int max_terms, int n_active, hipStream_t s,
                        hipEvent_t* ev = nullptr);  // ev[4]: fwd start/stop, bwd start/stop
 // the same for problems with p <= 1 (two LDS blocks per workgroup: two problems per CU)

@@ -421,6 +421,24 @@ class Engine:
         self.lib.gpx_batch_last_timing(self.handle, ctypes.byref(t))
         return t
 
+    def wave_trace(self, cap: int) -> None:
+        """Diagnostic: record each band16 wavefront's residency (start, end, kind) in the device's
+        100 MHz clock, room for `cap` records (0: off). include/gpx.h gpx_batch_wave_trace."""
+        rc = self.lib.gpx_batch_wave_trace(self.handle, int(cap))
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_batch_wave_trace failed ({rc}): {self.ctx.last_error()}")
+        self._wtrace_cap = int(cap)
+
+    def wave_trace_read(self) -> np.ndarray:
+        """The records since the last read, [n, 3] uint64 (start, end, kind); restarts recording."""
+        cap = getattr(self, "_wtrace_cap", 0)
+        out = np.zeros((max(cap, 1), 3), dtype=np.uint64)
+        n = ctypes.c_uint(0)
+        rc = self.lib.gpx_batch_wave_trace_read(self.handle, out.ctypes.data, cap, ctypes.byref(n))
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_batch_wave_trace_read failed ({rc}): {self.ctx.last_error()}")
+        return out[:n.value]
+
 
 class SVGPEngine:
     """Device state of one SVGP data shard (include/gpx.h gpx_svgp): X [N, D] / Y [N]
