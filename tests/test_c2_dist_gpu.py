@@ -9,7 +9,8 @@ sweeps, Scipy.minimize_stream over a ModelStream in two device groups.
 
 Asserted per seed: loss* within 1e-5 relative of the oracle's fit (SURVEY §8c's bar), θ* within
 1e-4, and the GPU's loss and gradient at its own θ* equal to the CPU restatement's there (loss
-1e-9, gradient 1e-6·max(1, |g|); the CPU side is oracle/band_oracle.py, the band algorithm on
+1e-8 — DESIGN §5's κ-scaled logML bar (1e-9 + 1e-14·κ) at C2's κ ≈ 1e6; observed up to 3e-9 —,
+gradient 1e-6·max(1, |g|); the CPU side is oracle/band_oracle.py, the band algorithm on
 numpy/LAPACK, itself checked against the dense oracle in tests/test_band_oracle.py — the dense
 oracle takes seconds per evaluation at N = 4096). Over the population: the mean number of
 evaluations per fit within ±10 % of the oracle's (fits/s ∝ 1/nfev, so a device that stopped
@@ -72,7 +73,7 @@ def test_c2_fits_in_distribution(golden_dir):
         lb, gb = bm.loss_and_grad_u()
         ea = abs(r.fun - lb) / abs(lb)
         eg = float(np.abs(np.asarray(r.jac) - gb).max() / max(1.0, np.abs(gb).max()))
-        assert ea <= 1e-9, (s, r.fun, lb)
+        assert ea <= 1e-8, (s, r.fun, lb)
         assert eg <= 1e-6, (s, r.jac, gb)
         for k, v in (("loss", el), ("theta", et), ("at_loss", ea), ("at_grad", eg)):
             worst[k] = max(worst[k], v)
