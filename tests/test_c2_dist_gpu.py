@@ -13,9 +13,14 @@ Asserted per seed: loss* within 1e-5 relative of the oracle's fit (SURVEY §8c's
 gradient 1e-6·max(1, |g|); the CPU side is oracle/band_oracle.py, the band algorithm on
 numpy/LAPACK, itself checked against the dense oracle in tests/test_band_oracle.py — the dense
 oracle takes seconds per evaluation at N = 4096). Over the population: the mean number of
-evaluations per fit within ±10 % of the oracle's (fits/s ∝ 1/nfev, so a device that stopped
-early would inflate the headline; individual fits differ — near this flat optimum L-BFGS-B's
-stop test sees 1e-9-level differences of summation order).
+evaluations per fit (fits/s ∝ 1/nfev, so a device that stopped early would inflate the headline).
+
+Individual fits' nfev differ between ANY two correct implementations: near this flat optimum
+L-BFGS-B's stop test reacts to 1e-9-level differences of summation order, and which seeds take
+40+ evaluations instead of ~15 moves between the dense oracle, the band oracle and the device
+(all three on c2_dist_n4096.npz's seeds). So the mean is compared (a) on the dense oracle's 32
+seeds within three standard errors of the difference, and (b) on a 512-seed population fitted
+by the band oracle (c2_dist_band_n4096.npz, standard error 0.36 evaluations) within ±10 %.
 """
 import os
 
@@ -80,6 +85,48 @@ def test_c2_fits_in_distribution(golden_dir):
         nf_gpu.append(int(r.nfev))
         nf_ora.append(int(fx["nfev"][i]))
     mg, mo = float(np.mean(nf_gpu)), float(np.mean(nf_ora))
+    se = float(np.sqrt(np.var(nf_gpu, ddof=1) / len(nf_gpu) + np.var(nf_ora, ddof=1) / len(nf_ora)))
     print(f"C2 in distribution ({len(seeds)} seeds, N={n}): nfev mean GPU {mg:.2f} oracle {mo:.2f} "
-          f"(GPU {nf_gpu}, oracle {nf_ora}); worst rel: {worst}")
+          f"(standard error of the difference {se:.2f}; GPU {nf_gpu}, oracle {nf_ora}); worst rel: {worst}")
+    assert abs(mg - mo) <= 3.0 * se, (mg, mo, se)
+
+
+def _fit_on_device(data, n):
+    def model(i):
+        m = gpx.models.GPR(data=data[i], kernel=K.SquaredExponential())
+        m.likelihood.variance.assign(NOISE)
+        gpx.set_trainable(m.likelihood.variance, False)
+        return m
+
+    models = gpx.optimizers.ModelStream(len(data), model, input_dim=1, max_points=n)
+    spec = compile_spec(K.SquaredExponential(), 1)
+    engines = [Engine([data[g][0]], [data[g][1]], [spec], band_storage=True) for g in range(2)]
+    res, _ = gpx.optimizers.Scipy().minimize_stream(models, width=len(data), engine=engines, groups=2,
+                                                    predict_train=True, options=dict(maxiter=100))
+    return models, res
+
+
+def test_c2_nfev_population_vs_band_oracle(golden_dir):
+    """512 C2 seeds through the bench's path against the band oracle's fits of the same seeds:
+    every fitted loss within 1e-5 and θ* within 1e-4, and the mean evaluations per fit within
+    ±10 % (VERDICT r03 item 5's bar; the population's standard error is ~0.4 evaluations, ~2 %)."""
+    from oracle import gp_oracle as O
+    fx = np.load(os.path.join(golden_dir, "c2_dist_band_n4096.npz"))
+    n = int(fx["n"][0])
+    seeds = [int(s) for s in fx["seeds"]]
+    data = [O.synthetic_series(n, s) for s in seeds]
+    models, res = _fit_on_device(data, n)
+    nf = np.array([r.nfev for r in res], dtype=np.float64)
+    worst_l = worst_t = 0.0
+    for i, (s, r) in enumerate(zip(seeds, res)):
+        theta = np.array([models[i].kernel.lengthscales.value, models[i].kernel.variance.value])
+        el = abs(r.fun - float(fx["loss"][i])) / abs(float(fx["loss"][i]))
+        et = float(np.max(np.abs(theta - fx["theta"][i]) / np.abs(fx["theta"][i])))
+        worst_l, worst_t = max(worst_l, el), max(worst_t, et)
+        assert el <= 1e-5, (s, r.fun, float(fx["loss"][i]))
+        assert et <= 1e-4, (s, theta, fx["theta"][i])
+    mg, mo = float(nf.mean()), float(fx["nfev"].mean())
+    print(f"C2 population ({len(seeds)} seeds): nfev mean GPU {mg:.3f} band oracle {mo:.3f} "
+          f"(GPU > 30: {int((nf > 30).sum())}, oracle > 30: {int((fx['nfev'] > 30).sum())}); "
+          f"worst loss rel {worst_l:.2e}, theta rel {worst_t:.2e}")
     assert abs(mg - mo) <= 0.10 * mo, (mg, mo)
