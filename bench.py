@@ -255,6 +255,11 @@ def parse_args(argv=None):
     # 8192 slots: 8695; round 3, profiles/r03_sweeps)
     ap.add_argument("--procs", type=int, default=int(os.environ.get("GPX_BENCH_PROCS", 8)),
                     help="host processes per GPU (the rank + procs-1 spawned helpers)")
+    # admission control (optimizers.DeviceAdmission): at most this many evaluation calls of the
+    # GPU's host processes on the device at once, so calls complete one after another instead of
+    # all together (0: off)
+    ap.add_argument("--admission", type=int, default=int(os.environ.get("GPX_BENCH_ADMISSION", 0)),
+                    help="device places shared by the GPU's host processes (0: no admission control)")
     ap.add_argument("--storage", choices=("band", "dense"), default=os.environ.get("GPX_BENCH_STORAGE", "band"),
                     help="slot workspace: band storage (gpx_batch_create_banded, 25 MiB per slot) or the "
                          "dense N x N layout (384 MiB per slot)")
@@ -275,13 +280,14 @@ class FitWorker:
     f0 .. f0 + F_w − 1 of the rank's F), its slots (width / procs) in `groups` device batches,
     fitted by one host thread through minimize_stream."""
 
-    def __init__(self, args, w, P, rank, gpu):
+    def __init__(self, args, w, P, rank, gpu, admission=None):
         import torch
         import portfoliooptgp_amd as gpx
         from portfoliooptgp_amd.engine import Engine
         from portfoliooptgp_amd.kernels import compile_spec
         self.torch, self.gpx = torch, gpx
         self.args, self.w, self.gpu = args, w, gpu
+        self.admission = admission
         F = args.fits
         self.F = share(F, P, w)
         # distinct series of this process (fits cycle over them: fit f of a step is series
@@ -336,7 +342,8 @@ class FitWorker:
         models = self.gpx.optimizers.ModelStream(k * F, lambda i: self.make_model(i % F), input_dim=1,
                                                  max_points=self.n, device=self.gpu)
         res, preds = self.opt.minimize_stream(models, width=self.width, engine=self.engines, predict_train=True,
-                                              groups=len(self.engines), options=dict(maxiter=MAXITER))
+                                              groups=len(self.engines), options=dict(maxiter=MAXITER),
+                                              admission=self.admission)
         if getattr(self.opt, "last_trace", None):
             self.traces.append(self.opt.last_trace)
         if getattr(self.opt, "last_stats", None):
@@ -366,7 +373,7 @@ class FitWorker:
         return out
 
 
-def helper_main(w, P, argv, rank, gpu, start, q):
+def helper_main(w, P, argv, rank, gpu, start, q, admission=None):
     """A helper host process (spawned before the rank touched the GPU): warm up, report ready,
     wait for the rank's start signal, fit its slice of the K steps, synchronise, hand back its
     results (the message means its device work is done)."""
@@ -374,7 +381,7 @@ def helper_main(w, P, argv, rank, gpu, start, q):
     args = parse_args(argv)
     import torch
     torch.cuda.set_device(gpu)
-    wk = FitWorker(args, w, P, rank, gpu)
+    wk = FitWorker(args, w, P, rank, gpu, admission)
     if args.warmup > 0:
         wk.run_steps(args.warmup)
     wk.reset_timing()
@@ -568,13 +575,16 @@ def main():
 
     # helper processes first, before anything here touches the GPU (a process that has
     # initialised HIP must not fork/exec)
-    helpers, start, q = [], None, None
+    helpers, start, q, admission = [], None, None, None
     if P > 1:
         import multiprocessing as mp
         ctx = mp.get_context("spawn")
         start = ctx.Event()
         q = ctx.Queue()
-        helpers = [ctx.Process(target=helper_main, args=(w, P, argv, rank, gpu, start, q), daemon=True)
+        # (optimizers.DeviceAdmission's semaphore, made here without importing the package: nothing
+        # may touch the GPU before the helpers are spawned)
+        admission = ctx.BoundedSemaphore(args.admission) if args.admission > 0 else None
+        helpers = [ctx.Process(target=helper_main, args=(w, P, argv, rank, gpu, start, q, admission), daemon=True)
                    for w in range(1, P)]
         for h in helpers:
             h.start()
@@ -594,7 +604,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    wk = FitWorker(args, 0, P, rank, gpu)
+    wk = FitWorker(args, 0, P, rank, gpu, admission)
     if args.warmup > 0:
         wk.run_steps(args.warmup)
     wk.reset_timing()
@@ -749,6 +759,7 @@ def main():
                                "fp64, sigma_n^2=1e-5 fixed, L-BFGS-B maxiter=100 + predict_f(X_train)",
                    "N": n, "fits_per_gpu_per_step": args.fits, "device_slots_per_gpu": args.width,
                    "host_processes_per_gpu": P, "device_batches_per_process": args.groups,
+                   "admission_places": args.admission,
                    "slot_storage": args.storage, "kernel": "SquaredExponential",
                    "parallelism": f"independent fits, {world} rank(s) x 1 GPU x {P} host processes, "
                                   "RCCL all_gather of the per-fit results"},

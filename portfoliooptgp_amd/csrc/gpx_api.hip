@@ -608,9 +608,13 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   }();
   // GPX_B16_INLINE_K=0: the SE1 band16 sweeps read K from a band built by band16_build_kernel
   // (the round-3 path; same bits) instead of computing their tiles from X
-  static const bool kin = [] {
+  // which SE1 band16 sweeps compute their K tiles from X (bit 0: forward, bit 1: backward;
+  // GPX_B16_INLINE_K): a sweep that does not reads the band band16_build_kernel wrote, which
+  // is built whenever the forward sweep needs it (the backward alone computing its tiles still
+  // saves that sweep's K read). Same bits either way.
+  static const int kin = [] {
     const char* e = getenv("GPX_B16_INLINE_K");
-    return !(e && atoi(e) == 0);
+    return e ? (atoi(e) & 3) : 0;
   }();
   const int nstreams = lanes_on ? std::min(nl, 1 + kAux) : 1;
   auto lane_stream = [&](int i) { return (i % nstreams) == 0 ? r.s : bt->aux[(i % nstreams) - 1]; };
@@ -623,7 +627,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     hipStream_t ls = lane_stream(i);
     if (l.kind == 0) {
       // SE1 classes compute their K tiles inside the sweeps (band16 KIN): no build launch
-      if (!(se1 && kin)) {
+      if (!(se1 && (kin & 1) && (kin & 2))) {
         BuildArgs bg = ba;
         bg.active = r.d_act + l.off;
         launch_band16_build(bg, g16_q[l.g], l.n, ls);

@@ -997,11 +997,11 @@ void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s)
 }
 
 template <int Q>
-static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, bool kin, int n_active, hipStream_t s,
+static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, int kin, int n_active, hipStream_t s,
                        hipEvent_t* ev) {
-  kin = kin && se1;
-  auto fwd = kin ? band16_fwd_kernel<Q, true> : band16_fwd_kernel<Q, false>;
-  auto bwd = se1 ? (kin ? band16_bwd_kernel<Q, 1, true, true> : band16_bwd_kernel<Q, 1, true, false>)
+  kin = se1 ? kin : 0;
+  auto fwd = (kin & 1) ? band16_fwd_kernel<Q, true> : band16_fwd_kernel<Q, false>;
+  auto bwd = se1 ? ((kin & 2) ? band16_bwd_kernel<Q, 1, true, true> : band16_bwd_kernel<Q, 1, true, false>)
                  : max_terms <= 1 ? band16_bwd_kernel<Q, 1, false, false>
                                   : max_terms == 2 ? band16_bwd_kernel<Q, 2, false, false>
                                                    : band16_bwd_kernel<Q, GPX_MAX_TERMS, false, false>;
@@ -1015,7 +1015,7 @@ static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, bool kin
   hipLaunchKernelGGL(bwd, dim3(n_active), dim3(64), xs, s, a);
 }
 
-void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, bool kin, int n_active, hipStream_t s,
+void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int kin, int n_active, hipStream_t s,
                    hipEvent_t* ev) {
   switch (Q) {
     case 1: launch16_q<1>(a, max_terms, se1, kin, n_active, s, ev); break;

@@ -300,7 +300,7 @@ class Scipy:
                         device: Optional[int] = None, predict_train: bool = False,
                         engine=None, groups: int = 1,
                         predict_inputs: Optional[Sequence] = None, on_not_pd: str = "raise",
-                        wide_group: bool = False, **scipy_kwargs):
+                        wide_group: bool = False, admission=None, **scipy_kwargs):
         """Continuous batching: fit many models through ``width`` resident device slots.
 
         Every model still runs its own unmodified scipy L-BFGS-B; at most ``width`` are
@@ -318,7 +318,10 @@ class Scipy:
         kernel band is wider than one 64-block (or dense) and the others only narrow ones; a
         fit moves between them (its series rebound, its L-BFGS-B state kept) when its next
         point changes class, so the narrow batches' calls never wait for the slower wide
-        sweeps. Returns (results, predictions|None); models are detached afterwards.
+        sweeps. ``admission``: a DeviceAdmission (or any object with acquire/release) shared
+        by the processes that fit through the same GPU; each evaluation call holds one of its
+        places from just before its submit until its results are back (see DeviceAdmission).
+        Returns (results, predictions|None); models are detached afterwards.
         """
         as_inf = _not_pd_policy(on_not_pd)
         lazy = isinstance(models, ModelStream)
@@ -354,7 +357,8 @@ class Scipy:
         if lbfgsb.supports(method, scipy_kwargs) and not _THREADED:
             drv = _SteppedDriver(models, engines, groups, scipy_kwargs.get("options") or {}, as_inf, D,
                                  predict_train=predict_train or predict_inputs is not None,
-                                 predict_inputs=predict_inputs, width=width, wide_group=wide_group)
+                                 predict_inputs=predict_inputs, width=width, wide_group=wide_group,
+                                 admission=admission)
             drv.run()
             self.last_trace = drv.trace
             self.last_stats = drv.stats
@@ -667,6 +671,34 @@ class _LockstepEvaluator:
                 self._slot_event(i).set()
 
 
+class DeviceAdmission:
+    """Admission control for several host processes that evaluate batches on ONE GPU: at most
+    ``places`` evaluation calls are on the device at a time; a process takes a place just before
+    its submit and gives it back when its results are home (Scipy.minimize_stream(admission=)).
+
+    Why: each process alternates a device call (its ~1000 problems, one wavefront each) and a
+    host phase (its fits' L-BFGS-B steps). The GPU serves concurrent calls interleaved, so
+    calls submitted together also finish together and their processes then step on the host at
+    the same time, leaving the GPU idle ("convoys": the band16 wave trace of round 4 showed
+    fewer than 256 of the 2048 sweep places filled for 30 % of the run). With a few places the
+    device serves the calls nearly first-come first-served: they complete one after another,
+    so the host phases interleave with the other processes' device work.
+
+    Create it in the parent before the helper processes are spawned (a multiprocessing
+    semaphore crosses a spawn only as a Process argument)."""
+
+    def __init__(self, places: int, ctx=None):
+        import multiprocessing as mp
+        self.places = int(places)
+        self._sem = (ctx or mp.get_context("spawn")).BoundedSemaphore(self.places)
+
+    def acquire(self):
+        self._sem.acquire()
+
+    def release(self):
+        self._sem.release()
+
+
 class _SteppedDriver:
     """Single-threaded-per-group fitting with reverse-communication L-BFGS-B (lbfgsb.py).
 
@@ -680,8 +712,9 @@ class _SteppedDriver:
 
     def __init__(self, models, engines, groups: int, options: dict, as_inf: bool, D: int,
                  predict_train: bool = False, predict_inputs=None, width: Optional[int] = None,
-                 fixed: bool = False, wide_group: bool = False):
+                 fixed: bool = False, wide_group: bool = False, admission=None):
         self.models, self.options, self.as_inf, self.D = models, options, as_inf, D
+        self.admission = admission
         self.predict_train, self.predict_inputs, self.fixed = predict_train, predict_inputs, fixed
         G = max(1, groups)
         # group g: rows of its engine (one engine per group, or one engine split row-wise)
@@ -993,9 +1026,18 @@ class _SteppedDriver:
                 # the other's large GEMMs); started in phase they stay in phase
                 self.first_call.wait(timeout=10.0)
                 time.sleep(self.first_call_s * g / G)
+            adm = self.admission
+            if adm is not None:
+                t_a = time.perf_counter()
+                adm.acquire()
+                self._tick("admission_wait", t_a)
             gs.t_call = time.perf_counter()
-            with lock:
-                lml, grad, info = eng.lml_grad(gs.act, gs.theta)
+            try:
+                with lock:
+                    lml, grad, info = eng.lml_grad(gs.act, gs.theta)
+            finally:
+                if adm is not None:
+                    adm.release()
             self._tick("device_call", gs.t_call)
             t_end = time.perf_counter()
             if g == 0 and gs.n_calls == 0:
@@ -1012,12 +1054,23 @@ class _SteppedDriver:
                            for g, (e, rows, lk, stm) in enumerate(self.groups)]
         inflight = []
 
+        adm = self.admission
+
         def submit(gs):
             if not self._prepare(gs):
                 return False
+            if adm is not None:
+                t_a = time.perf_counter()
+                adm.acquire()
+                self._tick("admission_wait", t_a)
             gs.t_call = time.perf_counter()
-            with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():
-                gs.eng.lml_grad_submit(gs.act, gs.theta)
+            try:
+                with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():
+                    gs.eng.lml_grad_submit(gs.act, gs.theta)
+            except BaseException:
+                if adm is not None:
+                    adm.release()
+                raise
             self._tick("submit", gs.t_call)
             return True
 
@@ -1052,7 +1105,11 @@ class _SteppedDriver:
             inflight.remove(gs)
             self._tick("device_wait", t0)
             t1 = time.perf_counter()
-            lml, grad, info = gs.eng.lml_grad_complete()
+            try:
+                lml, grad, info = gs.eng.lml_grad_complete()
+            finally:
+                if adm is not None:
+                    adm.release()
             t_end = time.perf_counter()
             self._tick("complete", t1)
             with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():
