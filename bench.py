@@ -775,6 +775,8 @@ def main():
     }
     if parts[0][6] is not None:
         out["wave_trace"] = wave_trace_summary([p[6] for p in parts], elapsed)
+        if os.environ.get("GPX_WAVE_TRACE_OUT"):  # raw records per host process (tools/wave_overlap.py)
+            np.savez_compressed(os.environ["GPX_WAVE_TRACE_OUT"], **{f"proc{p[0]}": p[6] for p in parts})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, nfev_mean)
     if rank == 0 and world == 1 and not args.no_secondary:
