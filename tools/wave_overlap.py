@@ -20,16 +20,12 @@ ev = np.concatenate(ev)
 ev = ev[np.lexsort((ev[:, 2], ev[:, 0]))]
 t, who, dlt = ev[:, 0], ev[:, 1], ev[:, 2]
 P = len(procs)
-per = np.zeros((len(ev), P), dtype=np.int64)
-cur = np.zeros(P, dtype=np.int64)
-levels = np.empty((len(ev), P), dtype=np.int32)
-for i in range(len(ev)):
-    cur[who[i]] += dlt[i]
-    levels[i] = cur
+nproc = np.zeros(len(ev), dtype=np.int32)
+for k in range(P):
+    nproc += (np.cumsum(np.where(who == k, dlt, 0)) > 0).astype(np.int32)
+tot = np.cumsum(dlt)
 dt = np.diff(t, append=t[-1]).astype(np.float64)
 span = dt.sum()
-nproc = (levels > 0).sum(1)
-tot = levels.sum(1)
 print(f"processes {P}, records {sum(len(d[p]) for p in procs)}, span {span / 1e8:.3f} s")
 for k in range(P + 1):
     sh = dt[nproc == k].sum() / span
