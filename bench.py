@@ -424,6 +424,7 @@ def wave_trace_summary(recs, wall_s, clock_hz=1e8):
     number of resident sweep wavefronts over the span from the first start to the last end, the
     share of that span spent at each residency level, and the mean wave durations."""
     r = np.concatenate([x for x in recs if x is not None and len(x)])
+    r = r[r[:, 2] < 32]  # (kinds >= 32: the library's stream-order markers, tools/call_timeline.py)
     if len(r) == 0:
         return {"records": 0}
     t0, t1, kind = r[:, 0].astype(np.int64), r[:, 1].astype(np.int64), r[:, 2].astype(np.int64)

@@ -557,6 +557,13 @@ double band16_flops(int Np, int Q, bool fwd) {
   return f;
 }
 
+// stream-order markers in the wave trace (diagnostic; no-op unless gpx_batch_wave_trace is on):
+// 38 submit reached the device, 39 rebind gather done, 40 band16 work starts, 43 a lane's K band
+// built, 41 the lanes joined, 42 reduce done, 44 the results' download done
+static void trace_mark(gpx_batch* bt, int kind, hipStream_t s) {
+  if (bt->d_wtrace) launch_wave_marker(bt->d_wtrace, bt->d_wtrace_n, bt->wtrace_cap, kind, s);
+}
+
 void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int kband16,
                      int n1, int max_terms, hipEvent_t* ev, hipEvent_t (*ev16)[4]) {
   // r's active range is [band16 problems (n16, by width group) | p <= 1 problems (n1) | p = 2
@@ -602,6 +609,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     if (nlo < r.na) lanes[nl++] = Lane{2, 0, r.na - nlo, nlo};
   }
   std::sort(lanes, lanes + nl, [](const Lane& x, const Lane& y) { return x.n > y.n; });
+  trace_mark(bt, 40, r.s);
   static const bool lanes_on = [] {
     const char* e = getenv("GPX_BAND_LANES");
     return !(e && atoi(e) == 0);
@@ -631,6 +639,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
         BuildArgs bg = ba;
         bg.active = r.d_act + l.off;
         launch_band16_build(bg, g16_q[l.g], l.n, ls);
+        trace_mark(bt, 43, ls);
       }
       BandFusedArgs f16 = fa;
       f16.kband = kband16;
@@ -658,11 +667,13 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     (void)hipEventRecord(bt->ev[kEvents - 4 - i], bt->aux[i - 1]);
     (void)hipStreamWaitEvent(r.s, bt->ev[kEvents - 4 - i], 0);
   }
+  trace_mark(bt, 41, r.s);
   ReduceArgs ra{};
   ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
   ra.ntiles = 1; ra.z = bt->z; ra.sVec = Np; ra.ldiag = bt->ldiag;
   ra.nvalid = bt->d_n; ra.specs = bt->d_specs; ra.results = bt->results; ra.Np = Np;
   launch_reduce(ra, r.na, r.s);
+  trace_mark(bt, 42, r.s);
 }
 
 // The batch's auxiliary streams (the forked T products of the recursion) take the priority of
@@ -1401,11 +1412,13 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   ++bt->sub_calls;
 
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  trace_mark(bt, 38, s);
   {  // slots rebound since the last call land first: their band tables (from the gather's
      // X boxes) decide the routing below
     const int rc0 = flush_rebinds(bt, s);
     if (rc0 != GPX_OK) return rc0;
   }
+  trace_mark(bt, 39, s);
   sc.lap(0);
   // Route each problem (route_call: the dense recursion, the per-block banded launches, the
   // band16 sweeps by width, the 64-row fused sweeps, or the fallback slots of band storage)
@@ -1594,6 +1607,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   // one DMA into the pinned block: [info | theta (unchanged) | results]
   HIPX(ctx, hipMemcpyAsync(bt->h_io + bt->io_info_off, bt->d_io + bt->io_info_off,
                            bt->io_bytes - bt->io_info_off, hipMemcpyDeviceToHost, s));
+  trace_mark(bt, 44, s);
   sc.lap(4);
   pe->order = std::move(order);
   pe->n_dense = n_dense;

@@ -991,6 +991,20 @@ __global__ __launch_bounds__(256) void band16_build_kernel(BuildArgs a, int Q) {
   for (int q = 0; q < 4; ++q) out[q] = v[q];
 }
 
+// a one-wave kernel that appends a stream-order marker {t, t, kind} to the wave trace: where a
+// call's device work stands when the stream reaches it (kinds >= 32, gpx_api.hip trace_mark)
+__global__ __launch_bounds__(64) void wave_marker_kernel(BandFusedArgs a, int kind) {
+  wave_trace_put(a, __builtin_amdgcn_s_memrealtime(), kind);
+}
+
+void launch_wave_marker(unsigned long long* wt, unsigned int* wn, unsigned int cap, int kind, hipStream_t s) {
+  BandFusedArgs a{};
+  a.wtrace = wt;
+  a.wtrace_n = wn;
+  a.wtrace_cap = cap;
+  hipLaunchKernelGGL(wave_marker_kernel, dim3(1), dim3(64), 0, s, a, kind);
+}
+
 void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s) {
   const int tiles = (a.rows >> 4) * (Q + 1);
   hipLaunchKernelGGL(band16_build_kernel, dim3((tiles + 3) / 4, n_active), dim3(256), 0, s, a, Q);

@@ -190,6 +190,7 @@ void launch_band_fused1(const BandFusedArgs& a, int max_terms, int n_active, hip
 // K's band as the band16 sweeps read it: per 16-row block m the tiles (m, m − d), d = 0..Q,
 // one wavefront per tile (half the entries of the two 64-block diagonals launch_build writes)
 void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s);
+void launch_wave_marker(unsigned long long* wt, unsigned int* wn, unsigned int cap, int kind, hipStream_t s);
 void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int kin, int n_active, hipStream_t s,
                    hipEvent_t* ev = nullptr);
 void launch_band_solve(const BandSolveArgs& a, int n_active, hipStream_t s);

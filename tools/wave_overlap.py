@@ -13,6 +13,7 @@ base = min(int(d[p][:, 0].min()) for p in procs if len(d[p]))
 ev = []
 for k, p in enumerate(procs):
     r = d[p].astype(np.int64)
+    r = r[r[:, 2] < 32]
     a, b = r[:, 0] - base, r[:, 1] - base
     ev.append(np.stack([a, np.full_like(a, k), np.ones_like(a)], 1))
     ev.append(np.stack([b, np.full_like(b, k), -np.ones_like(b)], 1))
