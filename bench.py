@@ -249,6 +249,11 @@ def parse_args(argv=None):
                     help="resident device slots per GPU (continuous-batching width), split over --procs")
     ap.add_argument("--groups", type=int, default=int(os.environ.get("GPX_BENCH_GROUPS", 1)),
                     help="device batches kept in flight by each host process")
+    # a second device batch per process for the slow evaluation classes (Scipy.minimize_stream
+    # wide_group, optimizers._wide_classes): the band16 sweeps wider than GPX_NARROW_Q 16-blocks
+    # and the 64-row sweeps, so the narrow batch's calls never wait for them
+    ap.add_argument("--wide-slots", type=int, default=int(os.environ.get("GPX_BENCH_WIDE", 0)),
+                    help="slots per process of the slow-class device batch, taken from --width (0: one batch)")
     # 8 processes x 2 HIP hardware queues, one device batch of 1024 slots each: the GPU's queue
     # scheduler time-slices once the processes' queues exceed ~16; 8 host threads keep 8 calls in
     # flight (8 x 1 batch: 9925 fits/s, 8 x 2: 9074-9599, 10 x 2: 8228, 12 x 2: 7598, 4 x 2 at
@@ -306,7 +311,12 @@ class FitWorker:
         mark_immutable(*self.Xd)
         W = share(args.width, P, w)
         G = max(1, min(args.groups, W))
-        sizes = [share(W, G, g) for g in range(G)]
+        self.wide = args.wide_slots > 0
+        if self.wide:  # [narrow batch(es) | the slow-class batch]
+            Wn = W - args.wide_slots
+            sizes = [share(Wn, G, g) for g in range(G)] + [args.wide_slots]
+        else:
+            sizes = [share(W, G, g) for g in range(G)]
         spec = compile_spec(gpx.kernels.SquaredExponential(), 1)
         # slot shapes only: every slot is rebound to its fit's series when the fit starts
         self.engines = [Engine([self.Xd[i % self.S] for i in range(sz)], [self.Yd[i % self.S] for i in range(sz)],
@@ -343,7 +353,7 @@ class FitWorker:
                                                  max_points=self.n, device=self.gpu)
         res, preds = self.opt.minimize_stream(models, width=self.width, engine=self.engines, predict_train=True,
                                               groups=len(self.engines), options=dict(maxiter=MAXITER),
-                                              admission=self.admission)
+                                              admission=self.admission, wide_group=self.wide)
         if getattr(self.opt, "last_trace", None):
             self.traces.append(self.opt.last_trace)
         if getattr(self.opt, "last_stats", None):
@@ -760,7 +770,7 @@ def main():
                                "fp64, sigma_n^2=1e-5 fixed, L-BFGS-B maxiter=100 + predict_f(X_train)",
                    "N": n, "fits_per_gpu_per_step": args.fits, "device_slots_per_gpu": args.width,
                    "host_processes_per_gpu": P, "device_batches_per_process": args.groups,
-                   "admission_places": args.admission,
+                   "admission_places": args.admission, "wide_slots_per_process": args.wide_slots,
                    "slot_storage": args.storage, "kernel": "SquaredExponential",
                    "parallelism": f"independent fits, {world} rank(s) x 1 GPU x {P} host processes, "
                                   "RCCL all_gather of the per-fit results"},

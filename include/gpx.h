@@ -197,6 +197,14 @@ int gpx_batch_lml_grad_query(gpx_batch* batch);
  * for the next call's gather). No device work.
  */
 int gpx_batch_band_width(gpx_batch* batch, int n_rows, const int32_t* rows, const double* theta, int32_t* p_out);
+/* The path an evaluation of each row at theta would take, host-side (no device work), as
+ * gpx_batch_lml_grad_submit routes it: 1..15 = the band16 sweeps with a band of that many 16-row
+ * blocks; 16 + p = the 64-row banded path with p 64-blocks in a batch without band16 tables;
+ * 32 + p = the 64-row banded path although the batch has band16 tables (the band is wider than
+ * the band16 sweeps take); -1 = dense (or, band storage, the fallback slots); -2 = not known yet
+ * (a rebind whose gather runs with the next call). Callers that keep several batches use it to
+ * evaluate the slow classes apart from the fast ones (Scipy.minimize_stream wide_group). */
+int gpx_batch_band_class(gpx_batch* batch, int n_rows, const int32_t* rows, const double* theta, int32_t* cls_out);
 
 /*
  * Posterior marginals at Xnew for the active problems: GPflow GPR.predict_f(full_cov=False)

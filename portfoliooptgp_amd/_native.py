@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "gpx_batch_predict", "gpx_batch_predict_full_cov", "gpx_batch_predict_train",
     "gpx_batch_last_timing",
     "gpx_set_profiling", "gpx_batch_reset_timing", "gpx_batch_rebind",
-    "gpx_batch_wave_trace", "gpx_batch_wave_trace_read",
+    "gpx_batch_wave_trace", "gpx_batch_wave_trace_read", "gpx_batch_band_class",
     "gpx_svgp_create", "gpx_svgp_destroy", "gpx_svgp_partials", "gpx_svgp_bind_partials",
     "gpx_svgp_eval_local", "gpx_svgp_eval_finish", "gpx_svgp_elbo_grad", "gpx_svgp_predict",
     "gpx_host_theta_rows", "gpx_host_loss_grad_u",
@@ -164,6 +164,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_slot_boxes.argtypes = [c_void_p, c_int, c_void_p]
         lib.gpx_batch_reset_timing.restype = c_int
         lib.gpx_batch_reset_timing.argtypes = [c_void_p]
+        lib.gpx_batch_band_class.restype = c_int
+        lib.gpx_batch_band_class.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_void_p]
         lib.gpx_batch_wave_trace.restype = c_int
         lib.gpx_batch_wave_trace.argtypes = [c_void_p, ctypes.c_uint]
         lib.gpx_batch_wave_trace_read.restype = c_int

@@ -608,14 +608,19 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     if (n1 > 0) lanes[nl++] = Lane{1, 0, n1, n16};
     if (nlo < r.na) lanes[nl++] = Lane{2, 0, r.na - nlo, nlo};
   }
+  // GPX_LANE_ORDER=1: the small (slow-class) lanes are enqueued first, ahead of the bulk lane,
+  // so their wavefronts reach the dispatcher before the bulk lane's fill the chip
+  static const int lane_order = [] {
+    const char* e = getenv("GPX_LANE_ORDER");
+    return e ? atoi(e) : 0;
+  }();
   std::sort(lanes, lanes + nl, [](const Lane& x, const Lane& y) { return x.n > y.n; });
+  if (lane_order == 1 && nl > 1) std::rotate(lanes, lanes + 1, lanes + nl);  // bulk lane last (on an aux stream)
   trace_mark(bt, 40, r.s);
   static const bool lanes_on = [] {
     const char* e = getenv("GPX_BAND_LANES");
     return !(e && atoi(e) == 0);
   }();
-  // GPX_B16_INLINE_K=0: the SE1 band16 sweeps read K from a band built by band16_build_kernel
-  // (the round-3 path; same bits) instead of computing their tiles from X
   // which SE1 band16 sweeps compute their K tiles from X (bit 0: forward, bit 1: backward;
   // GPX_B16_INLINE_K): a sweep that does not reads the band band16_build_kernel wrote, which
   // is built whenever the forward sweep needs it (the backward alone computing its tiles still
@@ -1784,6 +1789,38 @@ int gpx_batch_band_width(gpx_batch* bt, int n_rows, const int32_t* rows, const d
     }
     const int p = plim >= 0 ? band_width(bt, b, theta + (size_t)b * GPX_THETA_STRIDE) : -1;
     p_out[i] = (p >= 0 && p <= plim) ? p : -1;
+  }
+  return GPX_OK;
+}
+
+int gpx_batch_band_class(gpx_batch* bt, int n_rows, const int32_t* rows, const double* theta, int32_t* cls_out) {
+  if (!bt) return GPX_BAD_ARG;
+  if (n_rows < 0 || (n_rows > 0 && (!rows || !theta || !cls_out)))
+    return fail(bt->ctx, GPX_BAD_ARG, "bad band-class query");
+  const int plim0 = band_limit(bt);
+  const int plim = bt->compact ? std::min(plim0, kBandStoreP) : plim0;
+  const int q16lim = band16_limit(bt);
+  for (int i = 0; i < n_rows; ++i) {
+    const int b = rows[i];
+    if (b < 0 || b >= bt->B) return fail(bt->ctx, GPX_BAD_ARG, "row out of range");
+    bool pending = false;
+    for (const auto& e : bt->pend) pending = pending || e.b == b;
+    if (pending) {
+      cls_out[i] = -2;
+      continue;
+    }
+    const double* thb = theta + (size_t)b * GPX_THETA_STRIDE;
+    const int p = plim >= 0 ? band_width(bt, b, thb) : -1;
+    if (p < 0 || p > plim) {
+      cls_out[i] = -1;
+      continue;
+    }
+    // the same decision as route_call
+    const int q16 = (p <= 2 && q16lim > 0) ? band_width16(bt, b, thb) : -1;
+    if (q16 >= 0 && q16 <= q16lim)
+      cls_out[i] = std::max(q16, 1);
+    else
+      cls_out[i] = (q16lim > 0 ? 32 : 16) + p;
   }
   return GPX_OK;
 }

@@ -929,66 +929,75 @@ __global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void
 
 // ---------------------------------------------------------------------------------------
 // K's band for the band16 sweeps: the 16x16 tiles (m, m − d), d = 0..Q, of every 16-row block m
-// (the diagonal tile whole), one wavefront per tile, lane (r, c4) computing row r, columns
-// 4·c4 .. 4·c4 + 3 — the same values, by the same operations, as build_kernel (inputs scaled by
-// 1/ℓ with one division each for single-term stationary kernels, σn² on the diagonal, the
-// identity in the padding), written to the same band-storage positions.
+// (the diagonal tile whole), lane (r, c4) of a wavefront computing row r, columns 4·c4 .. 4·c4 + 3
+// of a tile — the same values, by the same operations, as build_kernel (inputs scaled by 1/ℓ
+// with one division each for single-term stationary kernels, σn² on the diagonal, the identity in
+// the padding), written to the same band-storage positions. Each wavefront computes kB16Tiles
+// consecutive tiles (one tile per wavefront made a call of ~1000 problems ~1M tiny wavefronts:
+// the dispatch, not the exp work, set the kernel's time, 4-9 ms per call in the round-4 wave
+// trace, and the sweeps of the call waited for it).
 // ---------------------------------------------------------------------------------------
+constexpr int kB16Tiles = 16;
 __global__ __launch_bounds__(256) void band16_build_kernel(BuildArgs a, int Q) {
   const int b = a.active[blockIdx.y];
-  const int nb = a.rows >> 4;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int m = t / (Q + 1), d = t - m * (Q + 1);
-  if (m >= nb || m < d) return;
+  const int nb = a.rows >> 4, ntiles = nb * (Q + 1);
+  const int lane = threadIdx.x & 63;
+  const int t0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kB16Tiles;
+  if (t0 >= ntiles) return;
   const int n = a.nvalid[b], D = a.D;
   const double* X = a.X + (long long)b * a.sX;
   const double* th = a.theta + (long long)b * GPX_THETA_STRIDE;
-  const DevSpec spec = a.specs[b];
+  const DevSpec& spec = a.specs[b];
   const int k0 = spec.terms[0].kind;
   const bool fast = spec.n_terms == 1 && k0 >= GPX_SE && k0 <= GPX_EXPONENTIAL;
   const double noise = th[spec.n_params];
-  const int gi = m * 16 + (lane >> 2), gj0 = (m - d) * 16 + (lane & 3) * 4;
-  double* out = a.out + (long long)b * a.sOut + (long long)gi * a.ldo + gj0;
-  double v[4];
-  if (fast) {
-    const gpx_term& tm = spec.terms[0];
-    const double ell = th[tm.param_offset], var = th[tm.param_offset + 1];
-    const int d0 = tm.dim_start, dn = tm.dim_count;
-    const double* xi = X + (long long)min(gi, n - 1) * D + d0;  // (padding rows: not read)
-    const double xi0 = gi < n ? xi[0] / ell : 0.0;
+  const gpx_term& tm = spec.terms[0];
+  const double ell = th[tm.param_offset], var = th[tm.param_offset + 1];
+  const int d0 = tm.dim_start, dn = tm.dim_count;
+  for (int t = t0; t < min(t0 + kB16Tiles, ntiles); ++t) {
+    const int m = t / (Q + 1), d = t - m * (Q + 1);
+    if (m < d) continue;
+    const int gi = m * 16 + (lane >> 2), gj0 = (m - d) * 16 + (lane & 3) * 4;
+    double* out = a.out + (long long)b * a.sOut + (long long)gi * a.ldo + gj0;
+    double v[4];
+    if (fast) {
+      const double* xi = X + (long long)min(gi, n - 1) * D + d0;  // (padding rows: not read)
+      const double xi0 = gi < n ? xi[0] / ell : 0.0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int gj = gj0 + q;
-      if (gi < n && gj < n) {
-        const double* xj = X + (long long)gj * D + d0;
-        // (x/ℓ by one division per value, as build_kernel stages them)
-        const double r2 = dn == 1 ? sqdist1(xi0, xj[0] / ell) : sqdist_gpflow(xi, xj, dn, ell);
-        switch (k0) {
-          case GPX_SE: v[q] = stationary_value<GPX_SE>(r2, var); break;
-          case GPX_MATERN12: v[q] = stationary_value<GPX_MATERN12>(r2, var); break;
-          case GPX_MATERN32: v[q] = stationary_value<GPX_MATERN32>(r2, var); break;
-          case GPX_MATERN52: v[q] = stationary_value<GPX_MATERN52>(r2, var); break;
-          default: v[q] = stationary_value<GPX_EXPONENTIAL>(r2, var); break;
+      for (int q = 0; q < 4; ++q) {
+        const int gj = gj0 + q;
+        if (gi < n && gj < n) {
+          const double* xj = X + (long long)gj * D + d0;
+          // (x/ℓ by one division per value, as build_kernel stages them)
+          const double r2 = dn == 1 ? sqdist1(xi0, xj[0] / ell) : sqdist_gpflow(xi, xj, dn, ell);
+          switch (k0) {
+            case GPX_SE: v[q] = stationary_value<GPX_SE>(r2, var); break;
+            case GPX_MATERN12: v[q] = stationary_value<GPX_MATERN12>(r2, var); break;
+            case GPX_MATERN32: v[q] = stationary_value<GPX_MATERN32>(r2, var); break;
+            case GPX_MATERN52: v[q] = stationary_value<GPX_MATERN52>(r2, var); break;
+            default: v[q] = stationary_value<GPX_EXPONENTIAL>(r2, var); break;
+          }
+          if (gi == gj) v[q] += noise;
+        } else {
+          v[q] = gi == gj ? 1.0 : 0.0;
         }
-        if (gi == gj) v[q] += noise;
-      } else {
-        v[q] = gi == gj ? 1.0 : 0.0;
       }
-    }
-  } else {
+    } else {
+      const DevSpec sp = spec;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int gj = gj0 + q;
-      if (gi < n && gj < n) {
-        v[q] = eval_k(spec, th, X + (long long)gi * D, X + (long long)gj * D);
-        if (gi == gj) v[q] += noise;
-      } else {
-        v[q] = gi == gj ? 1.0 : 0.0;
+      for (int q = 0; q < 4; ++q) {
+        const int gj = gj0 + q;
+        if (gi < n && gj < n) {
+          v[q] = eval_k(sp, th, X + (long long)gi * D, X + (long long)gj * D);
+          if (gi == gj) v[q] += noise;
+        } else {
+          v[q] = gi == gj ? 1.0 : 0.0;
+        }
       }
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[q] = v[q];
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) out[q] = v[q];
 }
 
 // a one-wave kernel that appends a stream-order marker {t, t, kind} to the wave trace: where a
@@ -1006,8 +1015,8 @@ void launch_wave_marker(unsigned long long* wt, unsigned int* wn, unsigned int c
 }
 
 void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s) {
-  const int tiles = (a.rows >> 4) * (Q + 1);
-  hipLaunchKernelGGL(band16_build_kernel, dim3((tiles + 3) / 4, n_active), dim3(256), 0, s, a, Q);
+  const int tiles = (a.rows >> 4) * (Q + 1), per_wg = 4 * kB16Tiles;
+  hipLaunchKernelGGL(band16_build_kernel, dim3((tiles + per_wg - 1) / per_wg, n_active), dim3(256), 0, s, a, Q);
 }
 
 template <int Q>

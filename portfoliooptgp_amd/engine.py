@@ -255,6 +255,19 @@ class Engine:
             raise N.GPXError(f"gpx_batch_band_width failed ({rc}): {self.ctx.last_error()}")
         return out
 
+    def band_class(self, rows, theta: np.ndarray) -> np.ndarray:
+        """Per row, the path its evaluation at theta would take (include/gpx.h
+        gpx_batch_band_class): 1..15 band16 width Q, 16 + p / 32 + p the 64-row banded path
+        (without / despite band16 tables), -1 dense, -2 not known yet. Host-side."""
+        rows = self._active(rows)
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        out = np.zeros(len(rows), dtype=np.int32)
+        rc = self.lib.gpx_batch_band_class(self.handle, len(rows), rows.ctypes.data, theta.ctypes.data,
+                                           out.ctypes.data)
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_batch_band_class failed ({rc}): {self.ctx.last_error()}")
+        return out
+
     def lml_grad_complete(self):
         act, lml, grad, info = self._submitted
         self._submitted = None

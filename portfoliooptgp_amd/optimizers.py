@@ -753,7 +753,7 @@ class _SteppedDriver:
         # state kept) when its next point changes class and the other side has a free slot, so
         # the narrow batches' calls are not held up by the slower wide sweeps
         self.wide = (wide_group and not fixed and len(self.groups) > 1
-                     and all(hasattr(e, "band_width") for e, _, _, _ in self.groups))
+                     and all(hasattr(e, "band_width") or hasattr(e, "band_class") for e, _, _, _ in self.groups))
         self.moves = 0
 
     def _next(self) -> Optional[int]:
@@ -927,16 +927,39 @@ class _SteppedDriver:
         self._tick("theta", t0)
         return bool(gs.act)
 
+    def _wide_classes(self, gs):
+        """Per active row of the group: True (wide), False (narrow) or None (not known yet).
+        With band16 tables (Engine.band_class) the narrow class is the band16 sweeps of at
+        most GPX_NARROW_Q 16-blocks (default 3: the bulk of C2's evaluations, ~1.3-1.5 ms per
+        sweep); everything slower — the wider band16 sweeps (one wavefront per SIMD), the 64-row
+        sweeps (73 KiB of LDS per workgroup: they wait for whole CUs under a band16 load) and the
+        dense path — is wide, so a call of the narrow batch never waits for it. Without band16
+        tables: band width <= 1 64-block is narrow."""
+        cls_fn = getattr(gs.eng, "band_class", None)
+        if cls_fn is not None:
+            nq = int(os.environ.get("GPX_NARROW_Q", "3"))
+            out = []
+            for c in cls_fn(gs.act, gs.theta):
+                c = int(c)
+                if c == -2:
+                    out.append(None)           # band tables not known yet (a rebind waiting for its gather)
+                elif 1 <= c < 16:
+                    out.append(c > nq)
+                elif 16 <= c < 32:
+                    out.append(c - 16 > 1)     # 64-row band, no band16 tables in this batch
+                else:
+                    out.append(True)           # 64-row band despite band16 tables, or dense
+            return out
+        return [None if p == -2 else (p > 1 or p == -1) for p in gs.eng.band_width(gs.act, gs.theta)]
+
     def _migrate(self, gs) -> bool:
-        """Move the fits whose requested point belongs to the other class (band width <= 1
-        64-block: narrow; wider or dense: wide) to a free slot of a batch of that class. A fit
-        with no free slot on the other side is evaluated where it is. True if any moved."""
-        pw = gs.eng.band_width(gs.act, gs.theta)
+        """Move the fits whose requested point belongs to the other class (_wide_classes) to a
+        free slot of a batch of that class. A fit with no free slot on the other side is
+        evaluated where it is. True if any moved."""
         moved = False
-        for r, p in zip(gs.act, pw):
-            if p == -2:
-                continue  # band tables not known yet (a rebind waiting for its gather)
-            want_wide = p > 1 or p == -1
+        for r, want_wide in zip(gs.act, self._wide_classes(gs)):
+            if want_wide is None:
+                continue
             if want_wide == gs.wide:
                 continue
             if want_wide:

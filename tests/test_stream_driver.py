@@ -426,3 +426,33 @@ def test_blas_thread_limit_is_process_wide_and_counted():
     assert lib.n == 1          # b still stepping
     b.__exit__(None, None, None)
     assert lib.n == 8
+
+
+class ClassFakeEngine(AsyncFakeEngine):
+    """AsyncFakeEngine answering the band-class query (Engine.band_class): band16 width 3
+    below ℓ = 1.5, 5 above (slower: wide at the default GPX_NARROW_Q = 3), and a not-yet-known
+    class (-2) for ℓ in a narrow window, which must leave the fit where it is."""
+
+    def band_class(self, rows, theta):
+        return np.array([-2 if 1.49 < theta[r, 0] <= 1.5 else (5 if theta[r, 0] > 1.5 else 3) for r in rows],
+                        dtype=np.int32)
+
+    def lml_grad(self, rows, theta):
+        self.classes = getattr(self, "classes", []) + [self.band_class(rows, theta)]
+        return super().lml_grad(rows, theta)
+
+
+def test_wide_group_by_band16_class_keeps_trajectories():
+    """The wide batch by band16 class (ClassFakeEngine): fits cross between the narrow and the
+    wide batch with their L-BFGS-B state, and every trajectory is the solo one."""
+    ms = _models(17)
+    ref = [_solo(m) for m in _models(17)]
+    eng = [ClassFakeEngine(4), ClassFakeEngine(4), ClassFakeEngine(3)]
+    res, preds = gpx.optimizers.Scipy().minimize_stream(ms, width=11, engine=eng, groups=3, predict_train=True,
+                                                        wide_group=True)
+    for r, r0, m, p in zip(res, ref, ms, preds):
+        assert r.nfev == r0.nfev
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+        assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
+    wide_pts = np.concatenate(getattr(eng[2], "classes", [np.zeros(0, np.int32)]))
+    assert len(wide_pts) > 0 and (wide_pts == 5).mean() > 0.5
