@@ -463,6 +463,34 @@ void band_eval(const Run& r, int p, int max_terms) {
 // sweeps (grouped by width Q), other p <= 2 problems the 64-row fused sweeps; band storage runs
 // everything else on its dense fallback slots. Pure host logic over the band tables (writes
 // h_bandp; tests/c/host_harness.cpp runs it under ASan/UBSan).
+RouteLimits route_limits(const gpx_batch* bt) {
+  RouteLimits L;
+  L.plim = band_limit(bt);
+  if (bt->compact) L.plim = std::min(L.plim, kBandStoreP);
+  const char* ef = getenv("GPX_BAND_FUSED");  // 0: p <= 2 problems take the per-block launches too
+  L.fused_on = !(ef && atoi(ef) == 0);
+  L.q16lim = L.fused_on ? band16_limit(bt) : -1;
+  return L;
+}
+
+// one problem's path at θ (route_call and gpx_batch_band_class)
+RouteKind route_one(const gpx_batch* bt, int b, const double* thb, const RouteLimits& L, int& w) {
+  const int p = L.plim >= 0 ? band_width(bt, b, thb) : -1;
+  w = p;
+  if (p >= 0 && p <= L.plim) {
+    // p <= 2 problems whose band is at most kBand16MaxQ 16-blocks: the band16 sweeps
+    const int q16 = (p <= 2 && L.q16lim > 0) ? band_width16(bt, b, thb) : -1;
+    if (q16 >= 0 && q16 <= L.q16lim) {
+      w = std::max(q16, 1);
+      return kRouteBand16;
+    }
+    // (the p = 2 sweep holds four 64x64 LDS blocks plus three 64·D X-row slots: <= 160 KiB)
+    if (L.fused_on && (p <= 1 || (p == 2 && bt->D <= 12))) return kRouteFused;
+    return bt->compact ? kRouteShadow : kRouteBand;  // band storage runs the fused sweeps only
+  }
+  return bt->compact ? kRouteShadow : kRouteDense;   // (band storage: dense on the fallback slots)
+}
+
 void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double* theta, Route& rt) {
   std::vector<int32_t>& order = rt.order;
   order.clear();
@@ -470,39 +498,34 @@ void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double
   rt.shadow_ids.clear();
   std::vector<int32_t> band_ids, fused_ids;
   int pband = 0;
-  int plim = band_limit(bt);
-  if (bt->compact) plim = std::min(plim, kBandStoreP);
-  const char* ef = getenv("GPX_BAND_FUSED");  // 0: p <= 2 problems take the per-block launches too
-  const bool fused_on = !(ef && atoi(ef) == 0);
-  const int q16lim = fused_on ? band16_limit(bt) : -1;
+  const RouteLimits L = route_limits(bt);
   std::vector<int32_t> b16_ids[kBand16MaxQ + 1];  // band16 class by width Q (16-blocks)
   bool b16_p2 = false;                             // ... holding p = 2 problems (K band of 3 diagonals)
   for (int i = 0; i < n_active; ++i) {
     const int b = active[i];
     const double* thb = theta + (size_t)b * GPX_THETA_STRIDE;
-    const int p = plim >= 0 ? band_width(bt, b, thb) : -1;
-    if (p >= 0 && p <= plim) {
-      bt->h_bandp[b] = p;
-      // p <= 2 problems whose band is at most kBand16MaxQ 16-blocks: the band16 sweeps
-      const int q16 = (p <= 2 && q16lim > 0) ? band_width16(bt, b, thb) : -1;
-      if (q16 >= 0 && q16 <= q16lim) {
-        const int Q = std::max(q16, 1);
-        bt->h_bandp[b] = Q;
-        b16_ids[Q].push_back(b);
-        b16_p2 = b16_p2 || p == 2;
-      } else if (fused_on && (p <= 1 || (p == 2 && bt->D <= 12))) {
-        // (the p = 2 sweep holds four 64x64 LDS blocks plus three 64·D X-row slots: <= 160 KiB)
+    int w = -1;
+    switch (route_one(bt, b, thb, L, w)) {
+      case kRouteBand16:
+        bt->h_bandp[b] = w;
+        b16_ids[w].push_back(b);
+        b16_p2 = b16_p2 || band_width(bt, b, thb) == 2;
+        break;
+      case kRouteFused:
+        bt->h_bandp[b] = w;
         fused_ids.push_back(b);
-      } else if (bt->compact) {
-        rt.shadow_ids.push_back(b);  // band storage runs the fused sweeps only
-      } else {
+        break;
+      case kRouteBand:
+        bt->h_bandp[b] = w;
         band_ids.push_back(b);
-        pband = std::max(pband, p);
-      }
-    } else if (bt->compact) {
-      rt.shadow_ids.push_back(b);    // dense on the fallback slots, at _complete
-    } else {
-      order.push_back(b);
+        pband = std::max(pband, w);
+        break;
+      case kRouteShadow:
+        if (w >= 0 && w <= L.plim) bt->h_bandp[b] = w;
+        rt.shadow_ids.push_back(b);
+        break;
+      default:
+        order.push_back(b);
     }
   }
   rt.n16 = 0;
@@ -1797,9 +1820,7 @@ int gpx_batch_band_class(gpx_batch* bt, int n_rows, const int32_t* rows, const d
   if (!bt) return GPX_BAD_ARG;
   if (n_rows < 0 || (n_rows > 0 && (!rows || !theta || !cls_out)))
     return fail(bt->ctx, GPX_BAD_ARG, "bad band-class query");
-  const int plim0 = band_limit(bt);
-  const int plim = bt->compact ? std::min(plim0, kBandStoreP) : plim0;
-  const int q16lim = band16_limit(bt);
+  const RouteLimits L = route_limits(bt);
   for (int i = 0; i < n_rows; ++i) {
     const int b = rows[i];
     if (b < 0 || b >= bt->B) return fail(bt->ctx, GPX_BAD_ARG, "row out of range");
@@ -1809,18 +1830,9 @@ int gpx_batch_band_class(gpx_batch* bt, int n_rows, const int32_t* rows, const d
       cls_out[i] = -2;
       continue;
     }
-    const double* thb = theta + (size_t)b * GPX_THETA_STRIDE;
-    const int p = plim >= 0 ? band_width(bt, b, thb) : -1;
-    if (p < 0 || p > plim) {
-      cls_out[i] = -1;
-      continue;
-    }
-    // the same decision as route_call
-    const int q16 = (p <= 2 && q16lim > 0) ? band_width16(bt, b, thb) : -1;
-    if (q16 >= 0 && q16 <= q16lim)
-      cls_out[i] = std::max(q16, 1);
-    else
-      cls_out[i] = (q16lim > 0 ? 32 : 16) + p;
+    int w = -1;
+    const RouteKind k = route_one(bt, b, theta + (size_t)b * GPX_THETA_STRIDE, L, w);
+    cls_out[i] = k == kRouteBand16 ? w : (k == kRouteFused || k == kRouteBand) ? (L.q16lim > 0 ? 32 : 16) + w : -1;
   }
   return GPX_OK;
 }

@@ -246,6 +246,12 @@ struct Route {
   bool b16_p2 = false;
 };
 void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double* theta, Route& rt);
+// the per-call limits of the routing, and one problem's path under them (w: its band width, in
+// 16-blocks for kRouteBand16, in 64-blocks otherwise, -1 when not banded)
+struct RouteLimits { int plim = -1, q16lim = -1; bool fused_on = true; };
+enum RouteKind { kRouteDense, kRouteShadow, kRouteBand, kRouteFused, kRouteBand16 };
+RouteLimits route_limits(const gpx_batch* bt);
+RouteKind route_one(const gpx_batch* bt, int b, const double* theta_row, const RouteLimits& L, int& w);
 // p <= 2: [band16 groups (sizes g16_n, widths g16_q; K band of kband16 64-block diagonals) |
 // p<=1 (n1) | p=2]
 void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int kband16,

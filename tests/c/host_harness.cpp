@@ -264,6 +264,27 @@ int main(int argc, char** argv) {
         CHECK(bandp[b] == p && p <= 2 && ((i < rt.n_fused1) == (p <= 1)), "fused problem %d: p %d bandp %d", b, p,
               bandp[b]);
       }
+      // gpx_batch_band_class (the drivers' class query) agrees with the routing
+      {
+        std::vector<int32_t> cls(active.size());
+        CHECK(gpx_batch_band_class(&bt, (int)active.size(), active.data(), theta.data(), cls.data()) == GPX_OK,
+              "gpx_batch_band_class failed");
+        const int q16lim = route_limits(&bt).q16lim;
+        for (size_t i = 0; i < active.size(); ++i) {
+          const int b = active[i];
+          const auto at = std::find(rt.order.begin(), rt.order.end(), b) - rt.order.begin();
+          const double* th = theta.data() + (size_t)b * GPX_THETA_STRIDE;
+          int want;
+          if (at >= (long)rt.order.size() || at < rt.n_dense) {
+            want = -1;  // dense, or band storage's fallback slots
+          } else if (at < rt.n_dense + rt.n_band || at >= rt.n_dense + rt.n_band + rt.n16) {
+            want = (q16lim > 0 ? 32 : 16) + band_width(&bt, b, th);
+          } else {
+            want = bandp[b];
+          }
+          CHECK(cls[i] == want, "round %d env %d problem %d: band_class %d, routed as %d", round, v, b, cls[i], want);
+        }
+      }
       if (v == 1) CHECK(rt.n16 == 0, "GPX_BAND16=0 still routed %d problems to band16", rt.n16);
       if (v == 3) CHECK(rt.n16 + rt.n_band + rt.n_fused == 0 || bt.compact == 0 ? rt.n_band + rt.n_fused == 0 : true,
                         "GPX_BAND=0 still routed banded problems");
