@@ -652,8 +652,16 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     const char* e = getenv("GPX_B16_INLINE_K");
     return e ? (atoi(e) & 3) : 0;
   }();
-  const int nstreams = lanes_on ? std::min(nl, 1 + kAux) : 1;
-  auto lane_stream = [&](int i) { return (i % nstreams) == 0 ? r.s : bt->aux[(i % nstreams) - 1]; };
+  // GPX_BAND_LANE_STREAMS: streams the lanes are spread over (the bulk lane alone on the call's
+  // stream, the others round-robin on the rest). A process gets GPU_MAX_HW_QUEUES hardware
+  // queues (the bench: 2, so that 8 processes stay within the 16 the GPU maps without
+  // time-slicing) and streams beyond that share queues, where their kernels run in order
+  static const int lane_streams = [] {
+    const char* e = getenv("GPX_BAND_LANE_STREAMS");
+    return e ? std::max(1, atoi(e)) : 1 + kAux;
+  }();
+  const int nstreams = lanes_on ? std::min(std::min(nl, 1 + kAux), lane_streams) : 1;
+  auto lane_stream = [&](int i) { return (i == 0 || nstreams == 1) ? r.s : bt->aux[(i - 1) % (nstreams - 1)]; };
   if (nstreams > 1) {
     (void)hipEventRecord(bt->ev[kEvents - 2], r.s);   // the call's uploads are in
     for (int i = 1; i < nstreams; ++i) (void)hipStreamWaitEvent(bt->aux[i - 1], bt->ev[kEvents - 2], 0);

@@ -306,11 +306,17 @@ __device__ __forceinline__ int rq(int il) { return (il & 3) * 4 + (il >> 2); }
 // of read from the K band band16_build_kernel wrote — no build launch, and K's band never goes
 // through HBM (2·(Q+1)·16·N doubles less per evaluation); the inputs of the last Q+1 blocks sit
 // scaled (x/ℓ) in a small LDS ring.
+// The sweeps are device functions over an LDS block the caller owns, so the forward and backward
+// sweeps of one problem can run in one wavefront (band16_fused_kernel) on one LDS allocation.
 template <int Q, bool KIN>
-__global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1)) void band16_fwd_kernel(BandFusedArgs a) {
-  __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
-  __shared__ __attribute__((aligned(16))) double snew[KIN ? 1 : Q + 1][256];  // the entering row, staged by glds
-  __shared__ __attribute__((aligned(16))) double sxa[KIN ? Q + 1 : 1][16];    // KIN: x/ℓ of blocks m, slot m % (Q+1), rq order
+struct Fwd16 {  // the forward sweep's LDS, in doubles: scratch | the entering row (glds) | x/ℓ ring (KIN)
+  static constexpr int kNew = 16 * kSC, kXa = kNew + (KIN ? 1 : Q + 1) * 256, size = kXa + (KIN ? Q + 1 : 1) * 16;
+};
+template <int Q, bool KIN>
+__device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __restrict__ lds) {
+  double* sc = lds;
+  double(*snew)[256] = reinterpret_cast<double(*)[256]>(lds + Fwd16<Q, KIN>::kNew);  // the entering row, staged by glds
+  double(*sxa)[16] = reinterpret_cast<double(*)[16]>(lds + Fwd16<Q, KIN>::kXa);  // KIN: x/ℓ of blocks m, slot m % (Q+1), rq order
   const unsigned long long wt0 = a.wtrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int b = a.active[blockIdx.x];
   const int Np = a.Np, nb = Np >> 4;
@@ -505,6 +511,12 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
   wave_trace_put(a, wt0, Q);
 }
 
+template <int Q, bool KIN>
+__global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1)) void band16_fwd_kernel(BandFusedArgs a) {
+  __shared__ __attribute__((aligned(16))) double lds[Fwd16<Q, KIN>::size];
+  fwd_sweep<Q, KIN>(a, lds);
+}
+
 // ---------------------------------------------------------------------------------------
 // Backward sweep, k = nb−1 .. 0 (window S_ij = fragment of Z_{k+i,k+j}, 1 <= j <= i <= Q):
 //   α_k = W_kkᵀ (z_k − Σ_i P_iᵀ α_{k+i})
@@ -525,24 +537,38 @@ __global__ __launch_bounds__(64, Q <= 3 ? GPX_B16_FWD3_WAVES : (Q <= 4 ? 2 : 1))
 // KIN (SE1 only): K_ij computed from the r² the contraction forms anyway (k_se1's operations)
 // instead of fetched from the built K band: no K traffic and no 16 KiB K-tile double buffer.
 template <int Q, int NT, bool SE1, bool KIN>
-__global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
-  static_assert(!SE1 || Q <= 5, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 5");
-  static_assert(!KIN || SE1, "inline K tiles: SE1 sweeps only");
-  extern __shared__ double sx[];                       // X ring: [Q+1][16·D] (block m in slot m % (Q+1); not SE1)
-  __shared__ __attribute__((aligned(16))) double sc[16 * kSC];
+struct Bwd16 {  // the backward sweep's LDS, in doubles
+  // scratch [16][kSC] (SE1: θ at [0, 16) before the loop and the final sums at [16, 30) after it)
+  static constexpr int kZ = 16 * kSC;
   // SE1: the K tiles (k+i, k) as built, double-buffered by step parity (the next step's are
   // fetched by glds while this step's are contracted; not KIN); otherwise the step's Z tiles
   // for the runtime contraction loop
-  __shared__ __attribute__((aligned(16))) double sz[SE1 ? (KIN ? 1 : 2 * (Q + 1)) : Q + 1][256];
-  __shared__ double sal[SE1 ? 1 : Q + 1][16];          // α ring (not SE1)
+  static constexpr int nZ = SE1 ? (KIN ? 0 : 2 * (Q + 1)) : Q + 1;
+  static constexpr int kAl = kZ + nZ * 256;                     // α ring (not SE1)
   // SE1: the α and x values of block m's rows in the contraction's lane order (lane (l15, l4)
   // takes rows 4r + l4: element of row il at (il & 3)·4 + (il >> 2)), so a lane reads its four
   // with two ds_read_b128 instead of four strided reads
-  __shared__ __attribute__((aligned(16))) double salT[SE1 ? Q + 1 : 1][16];
-  __shared__ __attribute__((aligned(16))) double sxT[SE1 ? Q + 1 : 1][16];
-  __shared__ double scs[Q + 1][16];                    // band check: column sums ring
-  __shared__ double sth[GPX_THETA_STRIDE];
-  __shared__ double sred[GPX_MAX_TERMS * 3 + 2];
+  static constexpr int kAlT = kAl + (SE1 ? 0 : (Q + 1) * 16);
+  static constexpr int kXT = kAlT + (SE1 ? (Q + 1) * 16 : 0);
+  static constexpr int kCs = kXT + (SE1 ? (Q + 1) * 16 : 0);   // band check: column sums ring
+  static constexpr int kTh = kCs + (Q + 1) * 16;                // θ (not SE1: the term interpreter reads it in the loop)
+  static constexpr int kRed = kTh + (SE1 ? 0 : 16);
+  static constexpr int size = kRed + (SE1 ? 0 : 16);
+};
+template <int Q, int NT, bool SE1, bool KIN>
+__device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __restrict__ lds, double* __restrict__ sx) {
+  static_assert(!SE1 || Q <= 5, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 5");
+  static_assert(!KIN || SE1, "inline K tiles: SE1 sweeps only");
+  using Ly = Bwd16<Q, NT, SE1, KIN>;
+  // sx: X ring [Q+1][16·D] (block m in slot m % (Q+1); not SE1)
+  double* sc = lds;
+  double(*sz)[256] = reinterpret_cast<double(*)[256]>(lds + Ly::kZ);
+  double(*sal)[16] = reinterpret_cast<double(*)[16]>(lds + Ly::kAl);
+  double(*salT)[16] = reinterpret_cast<double(*)[16]>(lds + Ly::kAlT);
+  double(*sxT)[16] = reinterpret_cast<double(*)[16]>(lds + Ly::kXT);
+  double(*scs)[16] = reinterpret_cast<double(*)[16]>(lds + Ly::kCs);
+  double* sth = SE1 ? lds : lds + Ly::kTh;
+  double* sred = SE1 ? lds + 16 : lds + Ly::kRed;
   const unsigned long long wt0 = a.wtrace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int b = a.active[blockIdx.x];
   const int Np = a.Np, nb = Np >> 4;
@@ -927,6 +953,29 @@ __global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void
   wave_trace_put(a, wt0, 16 + Q);
 }
 
+template <int Q, int NT, bool SE1, bool KIN>
+__global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
+  extern __shared__ double sx[];
+  __shared__ __attribute__((aligned(16))) double lds[Bwd16<Q, NT, SE1, KIN>::size];
+  bwd_sweep<Q, NT, SE1, KIN>(a, lds, sx);
+}
+
+// Both sweeps of a problem in one wavefront (SE1 classes): one launch per width class, and each
+// problem's backward sweep starts when its own forward sweep ends instead of when the launch's
+// last one does; the two sweeps share one LDS block.
+template <int Q, bool KIN_F, bool KIN_B>
+__global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX) ? 2 : 1) void band16_fused_kernel(BandFusedArgs a) {
+  constexpr int nf = Fwd16<Q, KIN_F>::size, nbk = Bwd16<Q, 1, true, KIN_B>::size;
+  __shared__ __attribute__((aligned(16))) double lds[nf > nbk ? nf : nbk];
+  fwd_sweep<Q, KIN_F>(a, lds);
+  // the factor tiles, z and L_ii this wavefront stored are read back by it: its stores are
+  // complete and visible to its own loads
+  vm_drain();
+  __threadfence();
+  wsync();
+  bwd_sweep<Q, 1, true, KIN_B>(a, lds, nullptr);
+}
+
 // ---------------------------------------------------------------------------------------
 // K's band for the band16 sweeps: the 16x16 tiles (m, m − d), d = 0..Q, of every 16-row block m
 // (the diagonal tile whole), lane (r, c4) of a wavefront computing row r, columns 4·c4 .. 4·c4 + 3
@@ -1023,6 +1072,23 @@ template <int Q>
 static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, int kin, int n_active, hipStream_t s,
                        hipEvent_t* ev) {
   kin = se1 ? kin : 0;
+  // GPX_B16_FUSED=1: the SE1 classes' sweeps as one fused launch (fwd then bwd per wavefront)
+  static const bool fused = [] {
+    const char* e = getenv("GPX_B16_FUSED");
+    return e && atoi(e) != 0;
+  }();
+  if (se1 && fused) {
+    auto fk = (kin & 1) ? ((kin & 2) ? band16_fused_kernel<Q, true, true> : band16_fused_kernel<Q, true, false>)
+                        : ((kin & 2) ? band16_fused_kernel<Q, false, true> : band16_fused_kernel<Q, false, false>);
+    if (ev) {
+      hipExtLaunchKernelGGL(fk, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
+      (void)hipEventRecord(ev[2], s);  // (the backward sweeps' share is inside ev[0] .. ev[1])
+      (void)hipEventRecord(ev[3], s);
+      return;
+    }
+    hipLaunchKernelGGL(fk, dim3(n_active), dim3(64), 0, s, a);
+    return;
+  }
   auto fwd = (kin & 1) ? band16_fwd_kernel<Q, true> : band16_fwd_kernel<Q, false>;
   auto bwd = se1 ? ((kin & 2) ? band16_bwd_kernel<Q, 1, true, true> : band16_bwd_kernel<Q, 1, true, false>)
                  : max_terms <= 1 ? band16_bwd_kernel<Q, 1, false, false>
