@@ -23,4 +23,10 @@ if w:
 st = d.get("driver_stats_last_call") or {}
 print("   driver:", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()})
 PY
+  # a raw trace: its call timeline here, then the file goes (gpurun copies back <= 64 MiB)
+  tr=$(echo "$kv" | tr ' ' '\n' | sed -n 's/^GPX_WAVE_TRACE_OUT=//p')
+  if [ -n "$tr" ] && [ -f "$tr" ]; then
+    python tools/call_timeline.py "$tr" > "${tr%.npz}_timeline.txt" 2>&1 && sed 's/^/   /' "${tr%.npz}_timeline.txt"
+    [ -n "$KEEP_TRACE" ] || rm -f "$tr"
+  fi
 done
