@@ -755,6 +755,7 @@ class _SteppedDriver:
         self.wide = (wide_group and not fixed and len(self.groups) > 1
                      and all(hasattr(e, "band_width") or hasattr(e, "band_class") for e, _, _, _ in self.groups))
         self.moves = 0
+        self._narrow_q = int(os.environ.get("GPX_NARROW_Q", "3"))
 
     def _next(self) -> Optional[int]:
         with self.qlock:
@@ -937,31 +938,25 @@ class _SteppedDriver:
         tables: band width <= 1 64-block is narrow."""
         cls_fn = getattr(gs.eng, "band_class", None)
         if cls_fn is not None:
-            nq = int(os.environ.get("GPX_NARROW_Q", "3"))
-            out = []
-            for c in cls_fn(gs.act, gs.theta):
-                c = int(c)
-                if c == -2:
-                    out.append(None)           # band tables not known yet (a rebind waiting for its gather)
-                elif 1 <= c < 16:
-                    out.append(c > nq)
-                elif 16 <= c < 32:
-                    out.append(c - 16 > 1)     # 64-row band, no band16 tables in this batch
-                else:
-                    out.append(True)           # 64-row band despite band16 tables, or dense
-            return out
-        return [None if p == -2 else (p > 1 or p == -1) for p in gs.eng.band_width(gs.act, gs.theta)]
+            c = cls_fn(gs.act, gs.theta)
+            nq = self._narrow_q
+            # 1..15 band16 width (wide above nq); 16 + p: 64-row band without band16 tables (wide
+            # above p = 1); 32 + p (64-row band despite band16 tables) and -1 (dense): wide;
+            # -2: band tables not known yet (a rebind waiting for its gather)
+            wide = np.where(c < 16, c > nq, np.where(c < 32, c - 16 > 1, True)) | (c == -1)
+            return wide, c == -2
+        p = gs.eng.band_width(gs.act, gs.theta)
+        return (p > 1) | (p == -1), p == -2
 
     def _migrate(self, gs) -> bool:
         """Move the fits whose requested point belongs to the other class (_wide_classes) to a
         free slot of a batch of that class. A fit with no free slot on the other side is
         evaluated where it is. True if any moved."""
         moved = False
-        for r, want_wide in zip(gs.act, self._wide_classes(gs)):
-            if want_wide is None:
-                continue
-            if want_wide == gs.wide:
-                continue
+        wide, unknown = self._wide_classes(gs)
+        cand = np.nonzero((wide != gs.wide) & ~unknown)[0]
+        for k in cand:
+            r, want_wide = gs.act[k], bool(wide[k])
             if want_wide:
                 tg = self._gss[-1]
             else:
