@@ -252,6 +252,8 @@ def parse_args(argv=None):
     # a second device batch per process for the slow evaluation classes (Scipy.minimize_stream
     # wide_group, optimizers._wide_classes): the band16 sweeps wider than GPX_NARROW_Q 16-blocks
     # and the 64-row sweeps, so the narrow batch's calls never wait for them
+    ap.add_argument("--defer-q", type=int, default=int(os.environ.get("GPX_DEFER_Q", -1)),
+                    help="defer the band16 classes wider than this many 16-blocks and the 64-row sweeps (-1: off)")
     ap.add_argument("--wide-slots", type=int, default=int(os.environ.get("GPX_BENCH_WIDE", 0)),
                     help="slots per process of the slow-class device batch, taken from --width (0: one batch)")
     # 8 processes x 2 HIP hardware queues, one device batch of 1024 slots each: the GPU's queue
@@ -323,6 +325,12 @@ class FitWorker:
                                [spec] * sz, device=gpu, band_storage=args.storage == "band")
                         for sz in sizes]
         self.engines[0].ctx.set_profiling(True)
+        # deferred completion of the slow width classes (Engine.set_deferred): a call completes
+        # when its band16 problems of at most --defer-q 16-blocks are done; the wider ones (and
+        # the 64-row sweeps) come back with a later call
+        if args.defer_q >= 0:
+            for e in self.engines:
+                e.set_deferred(args.defer_q)
         # GPX_WAVE_TRACE=1: every band16 wavefront's residency (start, end) in the device clock,
         # merged over the GPU's host processes into an occupancy timeline (wave_trace_summary)
         self.wtrace = bool(int(os.environ.get("GPX_WAVE_TRACE", "0")))
@@ -534,6 +542,56 @@ def secondary_c4(gpu, fits=32, kind="m52"):
                 "bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / FP64_PEAK_TFLOPS, "avg_launch_ms": c_ms / max(c_l, 1.0), "launches": c_l,
                 "alg_flops_per_launch": c_f / max(c_l, 1.0)}}
+
+
+def secondary_c3(gpu, n=2048, series=20, share=3, reps=3):
+    """Config C3 (BASELINE.json configs[2]): the per-asset batch, `series` synthetic series x
+    N = 2048 (SE, GPflow defaults, σn² = 1e-5 fixed, maxiter 100, predict_f at the training
+    inputs), fitted on one GPU; and `share` = ceil(20 / 8) series, the largest per-GPU share when
+    the 20 are sharded over 8 GPUs (distributed.shard_lpt; the all_gather after it is a few
+    KB). wall(20) / wall(3) bounds the 8-GPU strong-scaling speed-up of this batch: each GPU's
+    fits run concurrently, so the batch takes about as long as its slowest fit's chain of
+    evaluations either way. Median of `reps` runs each."""
+    import torch
+    import portfoliooptgp_amd as gpx
+    from portfoliooptgp_amd.engine import Engine
+    from portfoliooptgp_amd.kernels import compile_spec
+    dev = f"cuda:{gpu}"
+    data = [synthetic_series(n, s) for s in range(series)]
+    data = [(torch.as_tensor(x, device=dev), torch.as_tensor(y, device=dev)) for x, y in data]
+    spec = compile_spec(gpx.kernels.SquaredExponential(), 1)
+
+    def model(i):
+        m = gpx.models.GPR(data=data[i], kernel=gpx.kernels.SquaredExponential(), device=gpu)
+        m.likelihood.variance.assign(NOISE)
+        gpx.set_trainable(m.likelihood.variance, False)
+        return m
+
+    def run(k):
+        eng = Engine([d[0] for d in data[:k]], [d[1] for d in data[:k]], [spec] * k, device=gpu, band_storage=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res, _ = gpx.optimizers.Scipy().minimize_stream([model(i) for i in range(k)], width=k, engine=eng,
+                                                        predict_train=True, options=dict(maxiter=MAXITER))
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, res
+
+    run(share)  # warm-up
+    w_all = sorted(run(series)[0] for _ in range(reps))[reps // 2]
+    t_share, res_share = [], None
+    for _ in range(reps):
+        t, res_share = run(share)
+        t_share.append(t)
+    w_share = sorted(t_share)[reps // 2]
+    return {"config": "C3", "workload": f"{series} synthetic series x N={n}, SE, fp64, sigma_n^2=1e-5 fixed, "
+            "L-BFGS-B maxiter=100 + predict_f(X_train), band-storage slots, one GPU",
+            "wall_s_all_series_1gpu": w_all, "fits_per_s_1gpu": series / w_all,
+            "wall_s_per_gpu_share_at_8gpus": w_share, "share_series": share,
+            "nfev_of_share": [int(r.nfev) for r in res_share],
+            "ratio_wall_all_over_share": w_all / w_share,
+            "note": "an upper bound on the 8-GPU speed-up of this batch (the ranks' shares run concurrently); "
+                    "each fit is a chain of ~20 dependent evaluations of ~1.5 ms, so a GPU holding 3 fits takes "
+                    "about as long as one holding 20"}
 
 
 def secondary_c5(gpu, reps=20):
@@ -771,6 +829,7 @@ def main():
                    "N": n, "fits_per_gpu_per_step": args.fits, "device_slots_per_gpu": args.width,
                    "host_processes_per_gpu": P, "device_batches_per_process": args.groups,
                    "admission_places": args.admission, "wide_slots_per_process": args.wide_slots,
+                   "deferred_above_q": args.defer_q,
                    "slot_storage": args.storage, "kernel": "SquaredExponential",
                    "parallelism": f"independent fits, {world} rank(s) x 1 GPU x {P} host processes, "
                                   "RCCL all_gather of the per-fit results"},
@@ -791,7 +850,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, nfev_mean)
     if rank == 0 and world == 1 and not args.no_secondary:
-        for name, fn in (("secondary_c4_dense", lambda: secondary_c4(gpu)),
+        for name, fn in (("secondary_c3_batch", lambda: secondary_c3(gpu)),
+                         ("secondary_c4_dense", lambda: secondary_c4(gpu)),
                          ("secondary_c4_expxexp", lambda: secondary_c4(gpu, kind="expxexp")),
                          ("secondary_c5_svgp", lambda: secondary_c5(gpu))):
             try:

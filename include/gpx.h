@@ -62,6 +62,9 @@ extern "C" {
 #define GPX_NOT_PD 1
 #define GPX_BAD_ARG 2
 #define GPX_HIP_ERROR 3
+/* info[b] of a problem whose evaluation was deferred (gpx_batch_set_deferred): its result comes
+ * with a later gpx_batch_lml_grad_complete or gpx_batch_deferred_wait */
+#define GPX_INFO_DEFERRED (-1000)
 
 #define GPX_MAX_TERMS 4
 #define GPX_THETA_STRIDE 16 /* kernel params + 1 noise slot, per problem */
@@ -205,6 +208,20 @@ int gpx_batch_band_width(gpx_batch* batch, int n_rows, const int32_t* rows, cons
  * (a rebind whose gather runs with the next call). Callers that keep several batches use it to
  * evaluate the slow classes apart from the fast ones (Scipy.minimize_stream wide_group). */
 int gpx_batch_band_class(gpx_batch* batch, int n_rows, const int32_t* rows, const double* theta, int32_t* cls_out);
+/* Deferred completion of the slow evaluation classes. With q >= 0, the problems of a call whose
+ * evaluation takes the band16 sweeps wider than q 16-row blocks, or the 64-row banded sweeps,
+ * run on a stream of their own and gpx_batch_lml_grad_complete returns without waiting for them:
+ * it reports info[b] = GPX_INFO_DEFERRED for those rows, and delivers (lml, grad, info) of
+ * deferred rows of earlier calls whose work has finished by then (rows of neither kind are not
+ * written). A deferred row may not be evaluated, predicted or rebound until it is delivered;
+ * gpx_batch_deferred_wait blocks until every deferred row is delivered (into its arrays). The
+ * call's other problems never wait for the slow classes, whose sweeps (one wavefront per SIMD,
+ * or 73 KiB of LDS per workgroup) start late under a full band16 load. Same results, bit for
+ * bit, as without deferral. q < 0 turns it off (the default). */
+int gpx_batch_set_deferred(gpx_batch* batch, int q);
+int gpx_batch_deferred_wait(gpx_batch* batch, double* lml, double* grad, int32_t* info);
+/* rows with a deferred evaluation in flight: writes up to cap slot indices, returns the count */
+int gpx_batch_deferred_rows(const gpx_batch* batch, int32_t* rows, int cap);
 
 /*
  * Posterior marginals at Xnew for the active problems: GPflow GPR.predict_f(full_cov=False)

@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "gpx_batch_last_timing",
     "gpx_set_profiling", "gpx_batch_reset_timing", "gpx_batch_rebind",
     "gpx_batch_wave_trace", "gpx_batch_wave_trace_read", "gpx_batch_band_class",
+    "gpx_batch_set_deferred", "gpx_batch_deferred_wait", "gpx_batch_deferred_rows",
     "gpx_svgp_create", "gpx_svgp_destroy", "gpx_svgp_partials", "gpx_svgp_bind_partials",
     "gpx_svgp_eval_local", "gpx_svgp_eval_finish", "gpx_svgp_elbo_grad", "gpx_svgp_predict",
     "gpx_host_theta_rows", "gpx_host_loss_grad_u",
@@ -75,6 +76,8 @@ class GPXError(RuntimeError):
 
 
 INFO_BAD_THETA = -1  # info code of a problem whose θ was screened out on the host
+INFO_DEFERRED = -1000  # GPX_INFO_DEFERRED: the problem's result comes with a later complete
+INFO_UNSET = -2000  # (Python side) a row the last complete did not report on
 
 
 class InvalidParameterError(GPXError):
@@ -164,6 +167,12 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_slot_boxes.argtypes = [c_void_p, c_int, c_void_p]
         lib.gpx_batch_reset_timing.restype = c_int
         lib.gpx_batch_reset_timing.argtypes = [c_void_p]
+        lib.gpx_batch_set_deferred.restype = c_int
+        lib.gpx_batch_set_deferred.argtypes = [c_void_p, c_int]
+        lib.gpx_batch_deferred_wait.restype = c_int
+        lib.gpx_batch_deferred_wait.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.gpx_batch_deferred_rows.restype = c_int
+        lib.gpx_batch_deferred_rows.argtypes = [c_void_p, c_void_p, c_int]
         lib.gpx_batch_band_class.restype = c_int
         lib.gpx_batch_band_class.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_void_p]
         lib.gpx_batch_wave_trace.restype = c_int

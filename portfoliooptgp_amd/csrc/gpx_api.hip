@@ -598,16 +598,17 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   // K's band is built per class on that class's stream (2 block diagonals for p <= 1, 3 for
   // p = 2), so the p <= 1 build does not pay for the wider class and the two overlap
   BuildArgs ba{};
-  ba.active = r.d_act; ba.specs = bt->d_specs; ba.theta = bt->d_theta; ba.nvalid = bt->d_n;
+  ba.active = r.d_act; ba.specs = bt->d_specs; ba.theta = r.theta ? r.theta : bt->d_theta; ba.nvalid = bt->d_n;
   ba.X = bt->X; ba.sX = (long long)bt->Nmax * bt->D; ba.X2 = bt->X; ba.sX2 = ba.sX; ba.D = bt->D;
   ba.m2 = 0; ba.out = bt->K; ba.sOut = st; ba.ldo = mat_ld(bt); ba.rows = ba.cols = Np;
   ba.symmetric = 1;
   BandFusedArgs fa{};
-  fa.active = r.d_act; fa.bandp = bt->d_bandp; fa.K = bt->K; fa.L = bt->L; fa.W = bt->W; fa.sMat = st;
+  fa.active = r.d_act; fa.bandp = r.bandp ? r.bandp : bt->d_bandp; fa.K = bt->K; fa.L = bt->L; fa.W = bt->W; fa.sMat = st;
   fa.Y = bt->Y; fa.sY = bt->Nmax; fa.nvalid = bt->d_n; fa.z = bt->z; fa.alpha = bt->alpha;
   fa.ldiag = bt->ldiag; fa.sVec = Np; fa.X = bt->X; fa.sX = (long long)bt->Nmax * bt->D; fa.D = bt->D;
-  fa.specs = bt->d_specs; fa.theta = bt->d_theta; fa.partial = bt->partial; fa.sPartial = bt->partial_stride;
-  fa.info = bt->d_info; fa.results = bt->results; fa.Np = Np; fa.ld = mat_ld(bt);
+  fa.specs = bt->d_specs; fa.theta = r.theta ? r.theta : bt->d_theta; fa.partial = bt->partial;
+  fa.sPartial = bt->partial_stride;
+  fa.info = r.info ? r.info : bt->d_info; fa.results = bt->results; fa.Np = Np; fa.ld = mat_ld(bt);
   fa.wtrace = bt->d_wtrace; fa.wtrace_n = bt->d_wtrace_n; fa.wtrace_cap = bt->wtrace_cap;
   // The width classes of the call are independent: each class's chain (its K band build, then
   // its sweeps) is a *lane*, and the lanes run concurrently — the largest on the call's stream,
@@ -660,7 +661,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     const char* e = getenv("GPX_BAND_LANE_STREAMS");
     return e ? std::max(1, atoi(e)) : 1 + kAux;
   }();
-  const int nstreams = lanes_on ? std::min(std::min(nl, 1 + kAux), lane_streams) : 1;
+  const int nstreams = (lanes_on && !r.one_stream) ? std::min(std::min(nl, 1 + kAux), lane_streams) : 1;
   auto lane_stream = [&](int i) { return (i == 0 || nstreams == 1) ? r.s : bt->aux[(i - 1) % (nstreams - 1)]; };
   if (nstreams > 1) {
     (void)hipEventRecord(bt->ev[kEvents - 2], r.s);   // the call's uploads are in
@@ -917,6 +918,9 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
     const int e = fence_io(bt, s);
     if (e != GPX_OK) return e;
   }
+  // a deferred slow part copies the active list, θ and band widths it runs on out of the I/O
+  // block on its own stream: this upload may overwrite them only after those copies
+  if (bt->slow_in_armed) HIPX(bt->ctx, hipStreamWaitEvent(s, bt->slow_in, 0));
   char* hio = bt->h_io;
   if (predict_block) {  // (the last asynchronous predict's upload out of it has completed)
     const int e = wait_io(bt);
@@ -1137,6 +1141,17 @@ int gpx_batch_destroy(gpx_batch* bt) {
             "download=%.3f complete_sync=%.3f (flush: wait_io=%.3f box_sync=%.3f over %lld syncs) s\n", bt->B,
             bt->sub_calls, bt->sub_s[0], bt->sub_s[1], bt->sub_s[2], bt->sub_s[3], bt->sub_s[4], bt->sub_s[5],
             bt->sub_s[6], bt->sub_s[7], bt->box_syncs);
+  if (bt->slow_s) {  // deferred slow parts still read and write the buffers below
+    (void)hipStreamSynchronize(bt->slow_s);
+    bt->slow_out.clear();
+    bt->slow_pool.clear();
+    (void)hipStreamDestroy(bt->slow_s);
+    for (hipEvent_t e : {bt->slow_in, bt->slow_up})
+      if (e) (void)hipEventDestroy(e);
+    for (void* q : {(void*)bt->d_slow_act, (void*)bt->d_slow_theta, (void*)bt->d_slow_bandp, (void*)bt->d_slow_info,
+                    (void*)bt->d_slow_res, (void*)bt->d_slow_info_c})
+      if (q) (void)hipFree(q);
+  }
   if (bt->shadow) gpx_batch_destroy(bt->shadow);  // waits for its own submitted evaluation
   if (bt->shadow_s) (void)hipStreamDestroy(bt->shadow_s);
   if (bt->shadow_ev) (void)hipEventDestroy(bt->shadow_ev);
@@ -1191,6 +1206,8 @@ static int check_rebind(gpx_batch* bt, int b, int n, const gpx_kernel_spec* spec
         tm.dim_start + tm.dim_count > bt->D || tm.param_offset < 0 || tm.param_offset + np > sp.n_params)
       return fail(ctx, GPX_BAD_ARG, "bad kernel term");
   }
+  if (!bt->deferred.empty() && b >= 0 && b < bt->B && bt->deferred[b])
+    return fail(ctx, GPX_BAD_ARG, "slot has a deferred evaluation in flight (gpx_batch_deferred_wait)");
   return GPX_OK;
 }
 
@@ -1434,6 +1451,199 @@ static int shadow_collect(gpx_batch* bt, const std::vector<int32_t>& ids, double
   return status;
 }
 
+// ---- deferred completion of the slow classes (gpx_batch_set_deferred) ----
+static int slow_setup(gpx_batch* bt) {
+  gpx_ctx* ctx = bt->ctx;
+  if (bt->slow_s) return GPX_OK;
+  HIPX(ctx, hipStreamCreateWithFlags(&bt->slow_s, hipStreamNonBlocking));
+  HIPX(ctx, hipEventCreateWithFlags(&bt->slow_in, hipEventDisableTiming));
+  HIPX(ctx, hipEventCreateWithFlags(&bt->slow_up, hipEventDisableTiming));
+  const size_t B = bt->B;
+  HIPX(ctx, hipMalloc(&bt->d_slow_act, sizeof(int) * B));
+  HIPX(ctx, hipMalloc(&bt->d_slow_theta, sizeof(double) * B * GPX_THETA_STRIDE));
+  HIPX(ctx, hipMalloc(&bt->d_slow_bandp, sizeof(int) * B));
+  HIPX(ctx, hipMalloc(&bt->d_slow_info, sizeof(int) * B));
+  HIPX(ctx, hipMalloc(&bt->d_slow_res, sizeof(double) * B * kResStride));
+  HIPX(ctx, hipMalloc(&bt->d_slow_info_c, sizeof(int) * B));
+  return GPX_OK;
+}
+
+// The slow part of a call: problems order[off .. off + n) of the uploaded active list (band16
+// groups q/cnt, then the 64-row sweeps' p <= 1 problems (n1) and p = 2 ones), on slow_s, from
+// copies of the active list / θ / widths so the next call's upload cannot change them under it
+static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off, int n, int n_g16, const int* q,
+                       const int* cnt, int n16, int n1, bool se1, int kband16, int max_terms, const double* theta) {
+  gpx_ctx* ctx = bt->ctx;
+  {
+    const int e = slow_setup(bt);
+    if (e != GPX_OK) return e;
+  }
+  std::unique_ptr<gpx_batch::SlowRec> rec;
+  if (!bt->slow_pool.empty()) {
+    rec = std::move(bt->slow_pool.back());
+    bt->slow_pool.pop_back();
+  } else {
+    rec.reset(new gpx_batch::SlowRec());
+    HIPX(ctx, hipEventCreateWithFlags(&rec->done, hipEventDisableTiming));
+    HIPX(ctx, hipHostMalloc(&rec->h_res, sizeof(double) * bt->B * kResStride));
+    HIPX(ctx, hipHostMalloc(&rec->h_info, sizeof(int) * bt->B));
+  }
+  rec->ids.assign(ids, ids + n);
+  rec->theta.assign(theta, theta + (size_t)bt->B * GPX_THETA_STRIDE);
+  rec->clear_events();
+  rec->n_g16 = n_g16;
+  for (int g = 0; g < n_g16; ++g) {
+    rec->g16_q[g] = q[g];
+    rec->g16_n[g] = cnt[g];
+  }
+  rec->p64.clear();
+  hipStream_t ss = bt->slow_s;
+  HIPX(ctx, hipEventRecord(bt->slow_up, s));
+  HIPX(ctx, hipStreamWaitEvent(ss, bt->slow_up, 0));
+  HIPX(ctx, hipMemcpyAsync(bt->d_slow_act, bt->d_active + off, sizeof(int) * n, hipMemcpyDeviceToDevice, ss));
+  HIPX(ctx, hipMemcpyAsync(bt->d_slow_theta, bt->d_theta, sizeof(double) * bt->B * GPX_THETA_STRIDE,
+                           hipMemcpyDeviceToDevice, ss));
+  HIPX(ctx, hipMemcpyAsync(bt->d_slow_bandp, bt->d_bandp, sizeof(int) * bt->B, hipMemcpyDeviceToDevice, ss));
+  HIPX(ctx, hipMemsetAsync(bt->d_slow_info, 0, sizeof(int) * bt->B, ss));
+  HIPX(ctx, hipEventRecord(bt->slow_in, ss));
+  bt->slow_in_armed = true;
+  const bool fused64 = n > n16;
+  if (ctx->profiling) {
+    for (int g = 0; g < n_g16; ++g)
+      for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&rec->fq16[g][e]));
+    if (fused64) {
+      for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&rec->fq[e]));
+      // (the timed 64-row pair is the p <= 1 class's when there is one, else the p = 2 class's)
+      const int t0 = n16, t1 = n1 > 0 ? n16 + n1 : n;
+      for (int i = t0; i < t1; ++i) rec->p64.push_back(bt->h_bandp[ids[i]]);
+    }
+  }
+  Run r{bt, bt->d_slow_act, n, ss};
+  r.theta = bt->d_slow_theta;
+  r.bandp = bt->d_slow_bandp;
+  r.info = bt->d_slow_info;
+  r.one_stream = true;
+  band_fused_eval(r, n16, n_g16, q, cnt, se1, kband16, n1, max_terms, (ctx->profiling && fused64) ? rec->fq : nullptr,
+                  ctx->profiling ? rec->fq16 : nullptr);
+  launch_slow_gather(bt->d_slow_act, n, bt->results, kResStride, bt->d_slow_res, bt->d_slow_info, bt->d_slow_info_c, ss);
+  HIPX(ctx, hipMemcpyAsync(rec->h_res, bt->d_slow_res, sizeof(double) * n * kResStride, hipMemcpyDeviceToHost, ss));
+  HIPX(ctx, hipMemcpyAsync(rec->h_info, bt->d_slow_info_c, sizeof(int) * n, hipMemcpyDeviceToHost, ss));
+  HIPX(ctx, hipEventRecord(rec->done, ss));
+  HIPX(ctx, hipGetLastError());
+  if (bt->deferred.size() != (size_t)bt->B) bt->deferred.assign(bt->B, 0);
+  for (int i = 0; i < n; ++i) {
+    bt->deferred[ids[i]] = 1;
+    bt->fac_valid[ids[i]] = 0;
+  }
+  bt->slow_out.push_back(std::move(rec));
+  return GPX_OK;
+}
+
+// A finished slow part's results into the caller's arrays, as _complete reports its own rows
+// (band-check failures re-evaluated densely here)
+static int deliver_slow(gpx_batch* bt, gpx_batch::SlowRec& rec, double* lml, double* grad, int32_t* info) {
+  gpx_ctx* ctx = bt->ctx;
+  const char* et = getenv("GPX_BAND_TOL");
+  const double band_tol = et ? atof(et) : 1e-6;
+  int status = GPX_OK;
+  std::vector<int32_t> redo;
+  const int n = (int)rec.ids.size();
+  for (int i = 0; i < n; ++i) {
+    const int b = rec.ids[i];
+    bt->deferred[b] = 0;
+    const double* res = rec.h_res + (size_t)i * kResStride;
+    info[b] = rec.h_info[i];
+    const int np = bt->specs[b].n_params;
+    if (info[b] == 0 && !(res[kResBandCheck] <= band_tol)) {
+      redo.push_back(b);
+      continue;
+    }
+    if (info[b] != 0) {
+      status = GPX_NOT_PD;
+      lml[b] = NAN;
+      for (int p = 0; p <= np; ++p) grad[(size_t)b * GPX_THETA_STRIDE + p] = NAN;
+      bt->fac_valid[b] = 0;
+      continue;
+    }
+    lml[b] = res[0];
+    for (int p = 0; p <= np; ++p) grad[(size_t)b * GPX_THETA_STRIDE + p] = res[1 + p];
+    std::memcpy(&bt->fac_theta[(size_t)b * GPX_THETA_STRIDE], rec.theta.data() + (size_t)b * GPX_THETA_STRIDE,
+                sizeof(double) * GPX_THETA_STRIDE);
+    bt->fac_valid[b] = 1;
+    bt->fac_band[b] = 1;
+  }
+  if (ctx->profiling) {
+    bt->timing.band_evals += n;
+    bt->timing.evals += n;
+    for (int g = 0; g < rec.n_g16; ++g) {
+      float f0 = 0.f, f1 = 0.f;
+      (void)hipEventElapsedTime(&f0, rec.fq16[g][0], rec.fq16[g][1]);
+      (void)hipEventElapsedTime(&f1, rec.fq16[g][2], rec.fq16[g][3]);
+      bt->timing.band16_fwd_ms_total += f0;
+      bt->timing.band16_bwd_ms_total += f1;
+      bt->timing.band16_wave_ms += (double)rec.g16_n[g] * ((double)f0 + (double)f1);
+      bt->timing.band16_launches += 1.0;
+      bt->timing.band16_evals += rec.g16_n[g];
+      bt->timing.band16_q_sum += (double)rec.g16_q[g] * rec.g16_n[g];
+      bt->timing.band16_fwd_flops += rec.g16_n[g] * band16_flops(bt->Np, rec.g16_q[g], true);
+      bt->timing.band16_bwd_flops += rec.g16_n[g] * band16_flops(bt->Np, rec.g16_q[g], false);
+      bt->timing.band_p_sum += rec.g16_n[g];
+    }
+    if (rec.fq[0]) {
+      float f0 = 0.f, f1 = 0.f;
+      (void)hipEventElapsedTime(&f0, rec.fq[0], rec.fq[1]);
+      (void)hipEventElapsedTime(&f1, rec.fq[2], rec.fq[3]);
+      bt->timing.band_fwd_ms_total += f0;
+      bt->timing.band_bwd_ms_total += f1;
+      bt->timing.band_fused_launches += 1.0;
+      for (int pb : rec.p64) {
+        bt->timing.band_fwd_flops += band_fused_flops(bt->Np, pb, true);
+        bt->timing.band_bwd_flops += band_fused_flops(bt->Np, pb, false);
+        bt->timing.band_p_sum += pb;
+      }
+    }
+  }
+  if (!redo.empty()) {
+    if (ctx->profiling) bt->timing.band_fallbacks += (double)redo.size();
+    int rc2;
+    if (bt->compact) {
+      rc2 = shadow_lml_grad(bt, redo, rec.theta.data(), lml, grad, info, bt->slow_s);
+    } else {
+      bt->force_dense = 1;
+      rc2 = gpx_batch_lml_grad(bt, (int)redo.size(), redo.data(), rec.theta.data(), lml, grad, info, bt->slow_s);
+      bt->force_dense = 0;
+    }
+    if (rc2 != GPX_OK && rc2 != GPX_NOT_PD) return rc2;
+    if (rc2 == GPX_NOT_PD) status = GPX_NOT_PD;
+  }
+  return status;
+}
+
+// every slow part that has finished (block: all of them, waiting), oldest first
+static int deliver_ready(gpx_batch* bt, double* lml, double* grad, int32_t* info, bool block) {
+  gpx_ctx* ctx = bt->ctx;
+  int status = GPX_OK;
+  while (!bt->slow_out.empty()) {
+    gpx_batch::SlowRec& rec = *bt->slow_out.front();
+    if (block) {
+      HIPX(ctx, hipEventSynchronize(rec.done));
+    } else {
+      const hipError_t e = hipEventQuery(rec.done);
+      if (e == hipErrorNotReady) break;
+      if (e != hipSuccess) return fail(ctx, GPX_HIP_ERROR, std::string("hipEventQuery: ") + hipGetErrorString(e));
+    }
+    std::unique_ptr<gpx_batch::SlowRec> done = std::move(bt->slow_out.front());
+    bt->slow_out.erase(bt->slow_out.begin());
+    const int rc = deliver_slow(bt, *done, lml, grad, info);
+    done->clear_events();
+    bt->slow_pool.push_back(std::move(done));
+    if (rc != GPX_OK && rc != GPX_NOT_PD) return rc;
+    if (rc == GPX_NOT_PD) status = GPX_NOT_PD;
+  }
+  if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
+  return status;
+}
+
 int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                               void* stream) {
   if (!bt) return GPX_BAD_ARG;
@@ -1443,6 +1653,10 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     const int e = check_active_theta(bt, n_active, active, theta);
     if (e != GPX_OK) return e;
   }
+  if (!bt->deferred.empty())
+    for (int i = 0; i < n_active; ++i)
+      if (bt->deferred[active[i]])
+        return fail(ctx, GPX_BAD_ARG, "a problem of the call has a deferred evaluation in flight");
   HIPX(ctx, hipSetDevice(ctx->device));
   SubClock sc(bt);
   ++bt->sub_calls;
@@ -1611,7 +1825,36 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     band_eval(Run{bt, bt->d_active + n_dense, n_band, s}, pband, max_terms);
   }
   hipEvent_t* fqe = pe->fq;
-  if (n_fused > 0) {
+  // deferred completion: the slow classes (band16 wider than defer_q, then the 64-row sweeps) are
+  // the tail of the fused range; they go out as a slow part and this call completes without them
+  int n_slow = 0, n_g16_run = n_g16, n16_run = n16, n_fused1_run = n_fused1;
+  if (bt->defer_q >= 0 && n_fused > 0) {
+    int k = 0, nb16 = 0;
+    while (k < n_g16 && g16_q[k] <= bt->defer_q) nb16 += g16_n[k++];
+    if (n_fused > nb16 && n_dense + n_band + nb16 > 0) {  // (a call of slow problems only just runs)
+      n_slow = n_fused - nb16;
+      n_g16_run = k;
+      n16_run = nb16;
+      n_fused1_run = 0;
+    }
+  }
+  const int n_fused_run = n_fused - n_slow;
+  if (n_slow > 0) {
+    int max_terms = 1;
+    bool se1s = true;
+    const int off = n_active - n_slow;
+    for (int i = off; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
+    for (int i = off; i < off + (n16 - n16_run); ++i) {
+      const gpx_kernel_spec& sp = bt->specs[order[i]];
+      se1s = se1s && sp.n_terms == 1 && sp.terms[0].kind == GPX_SE && sp.terms[0].dim_count == 1;
+    }
+    const int rcs = submit_slow(bt, s, order.data() + off, off, n_slow, n_g16 - n_g16_run, g16_q + n_g16_run,
+                                g16_n + n_g16_run, n16 - n16_run, n_fused1, se1s, b16_p2 ? 3 : 2, max_terms, theta);
+    if (rcs != GPX_OK) return drop_shadow(rcs);
+  }
+  if (n_fused_run > 0) {
+    const int n_fused = n_fused_run, n16 = n16_run, n_g16 = n_g16_run, n_fused1 = n_fused1_run;
+    const int n_active = n_dense + n_band + n_fused;
     int max_terms = 1;
     for (int i = n_dense + n_band; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
     const bool old_fused = n_fused > n16;  // the 64-row fused kernels run too
@@ -1645,11 +1888,16 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
                            bt->io_bytes - bt->io_info_off, hipMemcpyDeviceToHost, s));
   trace_mark(bt, 44, s);
   sc.lap(4);
+  if (n_slow > 0) {  // the call's own problems: [dense | band | bulk band16]
+    pe->deferred_ids.assign(order.end() - n_slow, order.end());
+    order.resize(order.size() - n_slow);
+    pe->n_active = n_active - n_slow;
+  }
   pe->order = std::move(order);
   pe->n_dense = n_dense;
   pe->n_band = n_band;
-  pe->n_fused = n_fused;
-  pe->n_fused1 = n_fused1;
+  pe->n_fused = n_fused_run;
+  pe->n_fused1 = n_fused1_run;
   pe->shadow_ids = std::move(shadow_ids);
   pe->shadow_async = shadow_async;
   bt->pending_eval = std::move(pe);
@@ -1762,6 +2010,16 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
     bt->fac_valid[b] = 1;
     bt->fac_band[b] = i >= n_dense;
   }
+  for (int b : pe->deferred_ids) {  // (their results come with a later _complete / deferred_wait)
+    info[b] = GPX_INFO_DEFERRED;
+    lml[b] = NAN;
+    for (int p = 0; p <= bt->specs[b].n_params; ++p) grad[(size_t)b * GPX_THETA_STRIDE + p] = NAN;
+  }
+  if (!bt->slow_out.empty()) {  // earlier calls' slow parts that have finished by now
+    const int rcd = deliver_ready(bt, lml, grad, info, false);
+    if (rcd != GPX_OK && rcd != GPX_NOT_PD) return rcd;
+    if (rcd == GPX_NOT_PD) status = GPX_NOT_PD;
+  }
   if (status == GPX_NOT_PD) last_error_slot() = "K + noise*I is not positive definite for some problem";
   if (bt->compact) {
     // band storage: the problems routed dense and those whose band check failed run on the
@@ -1865,6 +2123,10 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
     return fail(ctx, GPX_BAD_ARG, "bad predict args");
   if (!train && ((long long)M + 63) / 64 * 64 > kGemmMaxLd)
     return fail(ctx, GPX_BAD_ARG, "too many prediction points for one call (kGemmMaxLd): split Xnew");
+  if (!bt->deferred.empty() && active)
+    for (int i = 0; i < n_active; ++i)
+      if (active[i] >= 0 && active[i] < bt->B && bt->deferred[active[i]])
+        return fail(ctx, GPX_BAD_ARG, "a problem has a deferred evaluation in flight");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   // band storage: only predict at the training inputs from a cached banded factor at exactly
@@ -2122,6 +2384,33 @@ int gpx_batch_last_timing(const gpx_batch* bt, gpx_timing* out) {
   if (!bt || !out) return GPX_BAD_ARG;
   *out = bt->timing;
   return GPX_OK;
+}
+
+int gpx_batch_set_deferred(gpx_batch* bt, int q) {
+  if (!bt) return GPX_BAD_ARG;
+  if (q < 0 && !bt->slow_out.empty())
+    return fail(bt->ctx, GPX_BAD_ARG, "deferred evaluations in flight (gpx_batch_deferred_wait first)");
+  bt->defer_q = q < 0 ? -1 : q;
+  if (bt->deferred.size() != (size_t)bt->B) bt->deferred.assign(bt->B, 0);
+  return GPX_OK;
+}
+
+int gpx_batch_deferred_wait(gpx_batch* bt, double* lml, double* grad, int32_t* info) {
+  if (!bt) return GPX_BAD_ARG;
+  if (!lml || !grad || !info) return fail(bt->ctx, GPX_BAD_ARG, "null output");
+  HIPX(bt->ctx, hipSetDevice(bt->ctx->device));
+  return deliver_ready(bt, lml, grad, info, true);
+}
+
+int gpx_batch_deferred_rows(const gpx_batch* bt, int32_t* rows, int cap) {
+  if (!bt) return 0;
+  int n = 0;
+  for (const auto& r : bt->slow_out)
+    for (int b : r->ids) {
+      if (rows && n < cap) rows[n] = b;
+      ++n;
+    }
+  return n;
 }
 
 // Diagnostic: the band16 sweeps' per-wavefront residency records (BandFusedArgs::wtrace)

@@ -130,6 +130,25 @@ struct gpx_batch {
   int* h_info = nullptr;
   gpx_timing timing{};
   double flops_acc = 0.0;
+  // deferred completion of the slow width classes (gpx_batch_set_deferred): the band16 classes
+  // wider than defer_q 16-blocks and the 64-row sweeps of a call run on slow_s from copies of
+  // the call's active list / θ / widths (d_slow_*), and their results come back with a later
+  // _complete (or gpx_batch_deferred_wait); the call itself completes with the rest
+  int defer_q = -1;
+  hipStream_t slow_s = nullptr;
+  hipEvent_t slow_in = nullptr;       // the latest slow part's copies are done (the next upload waits)
+  hipEvent_t slow_up = nullptr;       // the call's upload (and rebind gather) are in: the slow part may start
+  bool slow_in_armed = false;
+  int* d_slow_act = nullptr;
+  double* d_slow_theta = nullptr;
+  int* d_slow_bandp = nullptr;
+  int* d_slow_info = nullptr;
+  double* d_slow_res = nullptr;       // the slow problems' result rows, gathered for one download
+  int* d_slow_info_c = nullptr;
+  struct SlowRec;
+  std::vector<std::unique_ptr<SlowRec>> slow_out;   // in flight, oldest first
+  std::vector<std::unique_ptr<SlowRec>> slow_pool;  // delivered, reused (pinned buffers)
+  std::vector<char> deferred;         // [B]: the slot's evaluation is in flight in a slow part
   // wave residency trace of the band16 sweeps (gpx_batch_wave_trace; off when null)
   unsigned long long* d_wtrace = nullptr;
   unsigned int* d_wtrace_n = nullptr;
@@ -186,6 +205,12 @@ struct Run {
   hipStream_t s;
   bool dag = false;  // run the T products of the top recursion levels on the aux streams
   int* next_event = nullptr;
+  // the deferred (slow-class) part of a call reads its own copies of the call's θ rows and band
+  // widths and writes its own info block, and keeps all its lanes on its one stream
+  const double* theta = nullptr;
+  const int* bandp = nullptr;
+  int* info = nullptr;
+  bool one_stream = false;
 };
 
 struct PhaseTimer {
@@ -268,6 +293,33 @@ int ensure_rebind_meta(gpx_batch* bt);             // pinned n/spec mirrors + di
 
 }  // namespace gpx
 
+// A deferred slow part (gpx_batch_set_deferred) between its submit and its delivery
+struct gpx_batch::SlowRec {
+  std::vector<int32_t> ids;           // its problems, in launch order
+  std::vector<double> theta;          // the call's θ rows (B × GPX_THETA_STRIDE)
+  hipEvent_t done = nullptr;          // its results are in h_res / h_info
+  double* h_res = nullptr;            // pinned [B][kResStride] (the first ids.size() rows used)
+  int* h_info = nullptr;              // pinned [B]
+  // profiling: its band16 groups and 64-row sweep pair, as PendingEval records them
+  int n_g16 = 0, g16_q[gpx::kBand16MaxQ] = {}, g16_n[gpx::kBand16MaxQ] = {};
+  hipEvent_t fq16[gpx::kBand16MaxQ][4] = {};
+  hipEvent_t fq[4] = {};
+  std::vector<int> p64;               // band widths of the timed 64-row launch pair's problems
+  void clear_events() {
+    for (auto& g : fq16)
+      for (auto& x : g)
+        if (x) (void)hipEventDestroy(x), x = nullptr;
+    for (auto& x : fq)
+      if (x) (void)hipEventDestroy(x), x = nullptr;
+  }
+  ~SlowRec() {
+    clear_events();
+    if (done) (void)hipEventDestroy(done);
+    if (h_res) (void)hipHostFree(h_res);
+    if (h_info) (void)hipHostFree(h_info);
+  }
+};
+
 // State of a submitted evaluation between gpx_batch_lml_grad_submit and _complete: the
 // routing, a copy of θ (the factor cache records it), and the timing events
 struct gpx_batch::PendingEval {
@@ -275,6 +327,7 @@ struct gpx_batch::PendingEval {
   int n_active = 0, n_dense = 0, n_band = 0, n_fused = 0, n_fused1 = 0, ng = 0;
   std::vector<int32_t> order;
   std::vector<int32_t> shadow_ids;  // band storage: problems evaluated on the dense shadow
+  std::vector<int32_t> deferred_ids;  // problems of the call whose results come later (slow part)
   bool shadow_async = false;         // shadow_ids were submitted on bt->shadow_s by _submit
   std::vector<double> theta;
   std::unique_ptr<gpx::PhaseTimer> total, ct, bp;

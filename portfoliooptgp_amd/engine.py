@@ -195,7 +195,7 @@ class Engine:
         assert theta.shape == (self.B, N.GPX_THETA_STRIDE)
         lml = np.full(self.B, np.nan)
         grad = np.full((self.B, N.GPX_THETA_STRIDE), np.nan)
-        info = np.zeros(self.B, dtype=np.int32)
+        info = np.full(self.B, N.INFO_UNSET if self.deferral >= 0 else 0, dtype=np.int32)
         act = screen_theta(act, theta, self.n_params, info)
         if len(act) == 0:
             return lml, grad, info
@@ -220,7 +220,9 @@ class Engine:
         assert theta.shape == (self.B, N.GPX_THETA_STRIDE)
         lml = np.full(self.B, np.nan)
         grad = np.full((self.B, N.GPX_THETA_STRIDE), np.nan)
-        info = np.zeros(self.B, dtype=np.int32)
+        # (with deferral a complete reports on the call's rows and on earlier deferred rows it
+        # delivers; every other row keeps INFO_UNSET)
+        info = np.full(self.B, N.INFO_UNSET if self.deferral >= 0 else 0, dtype=np.int32)
         act = screen_theta(act, theta, self.n_params, info)
         self._submitted = (act, lml, grad, info)
         if len(act) == 0:
@@ -254,6 +256,30 @@ class Engine:
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_band_width failed ({rc}): {self.ctx.last_error()}")
         return out
+
+    deferral = -1
+
+    def set_deferred(self, q: int) -> None:
+        """Deferred completion of the slow evaluation classes (include/gpx.h
+        gpx_batch_set_deferred): the problems of a call that take the band16 sweeps wider than q
+        16-blocks or the 64-row sweeps come back from a later lml_grad_complete (info
+        INFO_DEFERRED until then); q < 0 turns it off."""
+        rc = self.lib.gpx_batch_set_deferred(self.handle, int(q))
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_batch_set_deferred failed ({rc}): {self.ctx.last_error()}")
+        self.deferral = int(q) if q >= 0 else -1
+
+    def deferred_wait(self):
+        """Every deferred row's result (blocking): (lml, grad, info) with info INFO_UNSET on the
+        rows not delivered here."""
+        lml = np.full(self.B, np.nan)
+        grad = np.full((self.B, N.GPX_THETA_STRIDE), np.nan)
+        info = np.full(self.B, N.INFO_UNSET, dtype=np.int32)
+        rc = self.lib.gpx_batch_deferred_wait(self.handle, lml.ctypes.data, grad.ctypes.data, info.ctypes.data)
+        if rc not in (N.GPX_OK, N.GPX_NOT_PD):
+            raise N.GPXError(f"gpx_batch_deferred_wait failed ({rc}): {self.ctx.last_error()}")
+        self.eval_count += int(((info != N.INFO_UNSET) & (info != N.INFO_DEFERRED)).sum())
+        return lml, grad, info
 
     def band_class(self, rows, theta: np.ndarray) -> np.ndarray:
         """Per row, the path its evaluation at theta would take (include/gpx.h

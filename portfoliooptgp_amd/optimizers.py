@@ -873,6 +873,10 @@ class _SteppedDriver:
                         except BaseException as e:
                             drv.errors[r] = e
             self.theta = drv._theta_of(eng)
+            # rows whose evaluation the engine deferred (info INFO_DEFERRED, Engine.set_deferred):
+            # row -> (P, the requested point, layout columns), stepped when a later complete
+            # (or a drain) delivers their result
+            self.pending = {}
             self.wide = drv.wide and g == len(drv.groups) - 1
             self.n_calls = 0
             self.act = self.packs = None
@@ -907,7 +911,7 @@ class _SteppedDriver:
         # θ rows of every requested point in one native call per variable layout (the same
         # libm softplus as Parameter.value, so the values are those of the per-model path)
         for moved in (False, True):
-            gs.act = sorted(active)
+            gs.act = sorted(r for r in active if r not in gs.pending) if gs.pending else sorted(active)
             layouts = {}
             for r in gs.act:
                 layouts.setdefault(active[r]["key"], []).append(r)
@@ -990,32 +994,21 @@ class _SteppedDriver:
             lib.gpx_host_loss_grad_u(len(rs), P, U.ctypes.data, R.ctypes.data, cols.ctypes.data,
                                      lml.ctypes.data, grad.ctypes.data, loss.ctypes.data, gu.ctypes.data)
             for k, r in enumerate(rs):
-                s = active[r]
-                if s.get("reeval") is not None:
-                    # the extra evaluation at the result's x (its factor serves the predict)
-                    done.append((r, info[r] == 0))
+                if info[r] == N.INFO_DEFERRED:
+                    gs.pending[r] = (P, U[k].copy(), cols)
                     continue
-                s["last_u"] = U[k]
-                try:
-                    if info[r] != 0:
-                        if info[r] == N.INFO_BAD_THETA:
-                            err = N.InvalidParameterError(
-                                f"model {s['i']}: hyperparameters out of (0, inf): {gs.theta[r, :eng.n_params[r] + 1]}")
-                        else:
-                            err = N.NotPositiveDefiniteError(
-                                f"Cholesky decomposition was not successful (model {s['i']}, pivot "
-                                f"{int(info[r])}): K + noise I is not positive definite", info[r])
-                        if not self.as_inf:
-                            raise err
-                        s["st"].tell(float("inf"), np.zeros(P))
-                    else:
-                        s["st"].tell(float(loss[k]), gu[k])
-                except BaseException as e:
-                    self.errors[s["i"]] = e
-                    done.append((r, False))
-                    continue
-                if s["st"].done:
-                    done.append((r, True))
+                self._take(gs, r, P, U[k], loss[k], gu[k], info[r], done)
+        if gs.pending:
+            # deferred rows of earlier calls that this complete (or drain) delivered
+            got = [r for r in gs.pending if info[r] != N.INFO_UNSET and info[r] != N.INFO_DEFERRED]
+            for r in got:
+                P, u, cols = gs.pending.pop(r)
+                loss = np.empty(1)
+                gu = np.empty((1, P))
+                R = np.array([r], dtype=np.int32)
+                lib.gpx_host_loss_grad_u(1, P, u.ctypes.data, R.ctypes.data, cols.ctypes.data, lml.ctypes.data,
+                                         grad.ctypes.data, loss.ctypes.data, gu.ctypes.data)
+                self._take(gs, r, P, u, loss[0], gu[0], info[r], done)
         self._tick("steps", t0)
         t_steps = clk()
         held = self._finish(eng, gs.lock, active, done)
@@ -1032,11 +1025,51 @@ class _SteppedDriver:
             if not self.fixed:
                 gs.free.append(r)
 
+    def _take(self, gs, r, P, u, loss, gu, inf, done):
+        """One fit's (loss, grad) at its requested point u: the L-BFGS-B step, or its failure;
+        appends (row, ok) to done when the fit is finished."""
+        s = gs.active[r]
+        if s.get("reeval") is not None:
+            # the extra evaluation at the result's x (its factor serves the predict)
+            done.append((r, inf == 0))
+            return
+        s["last_u"] = u
+        try:
+            if inf != 0:
+                if inf == N.INFO_BAD_THETA:
+                    err = N.InvalidParameterError(
+                        f"model {s['i']}: hyperparameters out of (0, inf): {gs.theta[r, :gs.eng.n_params[r] + 1]}")
+                else:
+                    err = N.NotPositiveDefiniteError(
+                        f"Cholesky decomposition was not successful (model {s['i']}, pivot "
+                        f"{int(inf)}): K + noise I is not positive definite", inf)
+                if not self.as_inf:
+                    raise err
+                s["st"].tell(float("inf"), np.zeros(P))
+            else:
+                s["st"].tell(float(loss), gu)
+        except BaseException as e:
+            self.errors[s["i"]] = e
+            done.append((r, False))
+            return
+        if s["st"].done:
+            done.append((r, True))
+
+    def _drain(self, gs) -> None:
+        """Wait for the group's deferred evaluations and step their fits (nothing else to run)."""
+        with gs.lock:
+            lml, grad, info = gs.eng.deferred_wait()
+        gs.packs = []
+        self._consume(gs, lml, grad, info, time.perf_counter())
+
     def _loop(self, g: int, eng, rows, lock):
         G = len(self.groups)
         gs = self._Group(self, g, eng, rows, lock, None)
         while True:
             if not self._prepare(gs):
+                if gs.pending:
+                    self._drain(gs)
+                    continue
                 return
             if g > 0 and gs.n_calls == 0 and G > 1:
                 # stagger: start g/G of a group-0 call after group 0's first call returns, so the
@@ -1102,6 +1135,16 @@ class _SteppedDriver:
         for gs in gss:
             if submit(gs):
                 inflight.append(gs)
+
+        def drain_idle():
+            # a group with nothing left to submit but deferred rows in flight: wait for them
+            for x in gss:
+                while x not in inflight and x.pending:
+                    with torch.cuda.stream(x.stream) if x.stream is not None else contextlib.nullcontext():
+                        self._drain(x)
+                        if submit(x):
+                            inflight.append(x)
+        drain_idle()
         while inflight:
             # complete whichever batch finishes first (the wide batch's calls are longer)
             t0 = time.perf_counter()
@@ -1136,6 +1179,7 @@ class _SteppedDriver:
                     inflight.append(gs)
             if self.wide:
                 submit_idle()
+            drain_idle()
 
     def _finish(self, eng, lock, active, done):
         """Results of the finished fits and their predictions. Returns the rows held back for

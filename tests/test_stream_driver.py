@@ -456,3 +456,76 @@ def test_wide_group_by_band16_class_keeps_trajectories():
         assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
     wide_pts = np.concatenate(getattr(eng[2], "classes", [np.zeros(0, np.int32)]))
     assert len(wide_pts) > 0 and (wide_pts == 5).mean() > 0.5
+
+
+class DeferringFakeEngine(FakeEngine):
+    """FakeEngine with deferred completion (Engine.set_deferred): a row whose requested
+    lengthscale exceeds 1.5 comes back INFO_DEFERRED and is delivered by the NEXT complete (or by
+    deferred_wait); a deferred row may not be submitted or rebound before its delivery."""
+
+    deferral = 3
+
+    def __init__(self, B):
+        super().__init__(B)
+        self._late = {}      # row -> (lml, grad row) of a deferred evaluation
+        self._sub = None
+        self.deferred_total = 0
+
+    def rebind(self, b, X, Y, spec):
+        assert b not in self._late, "rebind of a row with a deferred evaluation"
+        super().rebind(b, X, Y, spec)
+
+    def lml_grad_submit(self, rows, theta):
+        rows = list(rows)
+        assert self._sub is None and not (set(rows) & set(self._late)), "a deferred row was submitted again"
+        th = np.array(theta, copy=True)
+        self._sub = (rows, th, FakeEngine.lml_grad(self, rows, th))
+
+    def lml_grad_ready(self):
+        return True
+
+    def lml_grad_complete(self):
+        (rows, th, (lml, grad, _)), self._sub = self._sub, None
+        info = np.full(self.B, N.INFO_UNSET, dtype=np.int32)
+        for r, (l, g) in self._late.items():  # the last call's deferred rows arrive now
+            lml[r], grad[r], info[r] = l, g, 0
+        self._late = {}
+        for r in rows:
+            if th[r, 0] > 1.5:
+                self._late[r] = (lml[r], grad[r].copy())
+                lml[r], grad[r], info[r] = np.nan, np.nan, N.INFO_DEFERRED
+                self.deferred_total += 1
+            else:
+                info[r] = 0
+        return lml, grad, info
+
+    def lml_grad(self, rows, theta):
+        self.lml_grad_submit(rows, theta)
+        return self.lml_grad_complete()
+
+    def deferred_wait(self):
+        lml = np.full(self.B, np.nan)
+        grad = np.full((self.B, N.GPX_THETA_STRIDE), np.nan)
+        info = np.full(self.B, N.INFO_UNSET, dtype=np.int32)
+        for r, (l, g) in self._late.items():
+            lml[r], grad[r], info[r] = l, g, 0
+        self._late = {}
+        return lml, grad, info
+
+
+@pytest.mark.parametrize("engines", [1, 2])
+def test_deferred_rows_keep_trajectories(engines):
+    """Rows deferred by the engine (results one call later, drained at the end) are stepped when
+    they arrive: every fit's trajectory and prediction is the solo one, each fit is evaluated
+    exactly nfev times, and the deferral did happen."""
+    ms = _models(17)
+    ref = [_solo(m) for m in _models(17)]
+    eng = [DeferringFakeEngine(5) for _ in range(engines)]
+    res, preds = gpx.optimizers.Scipy().minimize_stream(ms, width=5 * engines, engine=eng if engines > 1 else eng[0],
+                                                        groups=engines, predict_train=True)
+    for r, r0, m, p in zip(res, ref, ms, preds):
+        assert r.nfev == r0.nfev
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+        assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
+    assert sum(sum(e.calls) for e in eng) == sum(r.nfev for r in res)
+    assert sum(e.deferred_total for e in eng) > 0
