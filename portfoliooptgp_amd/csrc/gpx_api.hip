@@ -620,17 +620,26 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   // d <= Q; kband16 — 2, or 3 when the class holds p = 2 problems — still tells the sweeps which
   // entries are exact zeros by the 64-row bound), the 64-row p <= 1 class (two 64-block
   // diagonals), the 64-row p = 2 class (three).
-  struct Lane { int kind, g, n, off; };
+  struct Lane { int kind, g, n, off, g_end; };
   Lane lanes[kBand16MaxQ + 2];
   int nl = 0;
   {
     int off = 0;
     for (int g = 0; g < n_g16; ++g) {
-      lanes[nl++] = Lane{0, g, g16_n[g], off};
+      // (r.wide_from: the SE1 groups of width 4 and 5 as one lane, one band16_wide_kernel launch)
+      if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= 5 && nl > 0 &&
+          lanes[nl - 1].kind == 3) {
+        lanes[nl - 1].n += g16_n[g];
+        lanes[nl - 1].g_end = g + 1;
+      } else if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= 5) {
+        lanes[nl++] = Lane{3, g, g16_n[g], off, g + 1};
+      } else {
+        lanes[nl++] = Lane{0, g, g16_n[g], off, g + 1};
+      }
       off += g16_n[g];
     }
-    if (n1 > 0) lanes[nl++] = Lane{1, 0, n1, n16};
-    if (nlo < r.na) lanes[nl++] = Lane{2, 0, r.na - nlo, nlo};
+    if (n1 > 0) lanes[nl++] = Lane{1, 0, n1, n16, 0};
+    if (nlo < r.na) lanes[nl++] = Lane{2, 0, r.na - nlo, nlo, 0};
   }
   // GPX_LANE_ORDER=1: the small (slow-class) lanes are enqueued first, ahead of the bulk lane,
   // so their wavefronts reach the dispatcher before the bulk lane's fill the chip
@@ -682,6 +691,26 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       f16.kband = kband16;
       f16.active = r.d_act + l.off;
       launch_band16(f16, g16_q[l.g], max_terms, se1, kin, l.n, ls, ev16 ? ev16[l.g] : nullptr);
+    } else if (l.kind == 3) {
+      // the wide SE1 groups: their K bands (unless computed in the sweeps), then one launch
+      int goff = l.off;
+      for (int g = l.g; g < l.g_end; ++g) {
+        if (!((kin & 1) && (kin & 2))) {
+          BuildArgs bg = ba;
+          bg.active = r.d_act + goff;
+          launch_band16_build(bg, g16_q[g], g16_n[g], ls);
+        }
+        goff += g16_n[g];
+      }
+      BandFusedArgs f16 = fa;
+      f16.kband = kband16;
+      f16.active = r.d_act + l.off;
+      if (ev16)
+        for (int g = l.g + 1; g < l.g_end; ++g) (void)hipEventRecord(ev16[g][0], ls);
+      launch_band16_wide(f16, kin, l.n, ls, ev16 ? ev16[l.g] : nullptr);
+      if (ev16)
+        for (int g = l.g + 1; g < l.g_end; ++g)
+          for (int e = 1; e < 4; ++e) (void)hipEventRecord(ev16[g][e], ls);
     } else if (l.kind == 1) {
       BuildArgs b1 = ba;
       b1.active = r.d_act + l.off;
@@ -1141,12 +1170,13 @@ int gpx_batch_destroy(gpx_batch* bt) {
             "download=%.3f complete_sync=%.3f (flush: wait_io=%.3f box_sync=%.3f over %lld syncs) s\n", bt->B,
             bt->sub_calls, bt->sub_s[0], bt->sub_s[1], bt->sub_s[2], bt->sub_s[3], bt->sub_s[4], bt->sub_s[5],
             bt->sub_s[6], bt->sub_s[7], bt->box_syncs);
-  if (bt->slow_s) {  // deferred slow parts still read and write the buffers below
-    (void)hipStreamSynchronize(bt->slow_s);
+  if (!bt->slow_out.empty() || bt->slow_s || bt->d_slow_res) {  // deferred slow parts use the buffers below
+    for (auto& r : bt->slow_out) (void)hipEventSynchronize(r->done);
+    if (bt->slow_s) (void)hipStreamSynchronize(bt->slow_s);
     bt->slow_out.clear();
     bt->slow_pool.clear();
-    (void)hipStreamDestroy(bt->slow_s);
-    for (hipEvent_t e : {bt->slow_in, bt->slow_up})
+    if (bt->slow_s) (void)hipStreamDestroy(bt->slow_s);
+    for (hipEvent_t e : {bt->slow_in, bt->slow_up, bt->bulk_ev})
       if (e) (void)hipEventDestroy(e);
     for (void* q : {(void*)bt->d_slow_act, (void*)bt->d_slow_theta, (void*)bt->d_slow_bandp, (void*)bt->d_slow_info,
                     (void*)bt->d_slow_res, (void*)bt->d_slow_info_c})
@@ -1452,19 +1482,35 @@ static int shadow_collect(gpx_batch* bt, const std::vector<int32_t>& ids, double
 }
 
 // ---- deferred completion of the slow classes (gpx_batch_set_deferred) ----
+// GPX_DEFER_STREAM=1: the slow part runs on a stream of its own, from copies of the call's
+// inputs; by default it follows the call's own work on the call's stream, after the call's
+// download (the call completes at an event there). A process gets few hardware queues (the
+// bench: 2), and a second stream shares one with the first, so its kernels run in order with
+// them anyway; on one stream the slow part delays only the next call, which waits for the host
+// to step the fits first.
+static bool defer_own_stream() {
+  static const bool on = [] {
+    const char* e = getenv("GPX_DEFER_STREAM");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 static int slow_setup(gpx_batch* bt) {
   gpx_ctx* ctx = bt->ctx;
-  if (bt->slow_s) return GPX_OK;
+  const size_t B = bt->B;
+  if (!bt->d_slow_res) {
+    HIPX(ctx, hipMalloc(&bt->d_slow_res, sizeof(double) * B * kResStride));
+    HIPX(ctx, hipMalloc(&bt->d_slow_info_c, sizeof(int) * B));
+  }
+  if (!defer_own_stream() || bt->slow_s) return GPX_OK;
   HIPX(ctx, hipStreamCreateWithFlags(&bt->slow_s, hipStreamNonBlocking));
   HIPX(ctx, hipEventCreateWithFlags(&bt->slow_in, hipEventDisableTiming));
   HIPX(ctx, hipEventCreateWithFlags(&bt->slow_up, hipEventDisableTiming));
-  const size_t B = bt->B;
   HIPX(ctx, hipMalloc(&bt->d_slow_act, sizeof(int) * B));
   HIPX(ctx, hipMalloc(&bt->d_slow_theta, sizeof(double) * B * GPX_THETA_STRIDE));
   HIPX(ctx, hipMalloc(&bt->d_slow_bandp, sizeof(int) * B));
   HIPX(ctx, hipMalloc(&bt->d_slow_info, sizeof(int) * B));
-  HIPX(ctx, hipMalloc(&bt->d_slow_res, sizeof(double) * B * kResStride));
-  HIPX(ctx, hipMalloc(&bt->d_slow_info_c, sizeof(int) * B));
   return GPX_OK;
 }
 
@@ -1497,16 +1543,19 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
     rec->g16_n[g] = cnt[g];
   }
   rec->p64.clear();
-  hipStream_t ss = bt->slow_s;
-  HIPX(ctx, hipEventRecord(bt->slow_up, s));
-  HIPX(ctx, hipStreamWaitEvent(ss, bt->slow_up, 0));
-  HIPX(ctx, hipMemcpyAsync(bt->d_slow_act, bt->d_active + off, sizeof(int) * n, hipMemcpyDeviceToDevice, ss));
-  HIPX(ctx, hipMemcpyAsync(bt->d_slow_theta, bt->d_theta, sizeof(double) * bt->B * GPX_THETA_STRIDE,
-                           hipMemcpyDeviceToDevice, ss));
-  HIPX(ctx, hipMemcpyAsync(bt->d_slow_bandp, bt->d_bandp, sizeof(int) * bt->B, hipMemcpyDeviceToDevice, ss));
-  HIPX(ctx, hipMemsetAsync(bt->d_slow_info, 0, sizeof(int) * bt->B, ss));
-  HIPX(ctx, hipEventRecord(bt->slow_in, ss));
-  bt->slow_in_armed = true;
+  const bool own = defer_own_stream();
+  hipStream_t ss = own ? bt->slow_s : s;
+  if (own) {
+    HIPX(ctx, hipEventRecord(bt->slow_up, s));
+    HIPX(ctx, hipStreamWaitEvent(ss, bt->slow_up, 0));
+    HIPX(ctx, hipMemcpyAsync(bt->d_slow_act, bt->d_active + off, sizeof(int) * n, hipMemcpyDeviceToDevice, ss));
+    HIPX(ctx, hipMemcpyAsync(bt->d_slow_theta, bt->d_theta, sizeof(double) * bt->B * GPX_THETA_STRIDE,
+                             hipMemcpyDeviceToDevice, ss));
+    HIPX(ctx, hipMemcpyAsync(bt->d_slow_bandp, bt->d_bandp, sizeof(int) * bt->B, hipMemcpyDeviceToDevice, ss));
+    HIPX(ctx, hipMemsetAsync(bt->d_slow_info, 0, sizeof(int) * bt->B, ss));
+    HIPX(ctx, hipEventRecord(bt->slow_in, ss));
+    bt->slow_in_armed = true;
+  }
   const bool fused64 = n > n16;
   if (ctx->profiling) {
     for (int g = 0; g < n_g16; ++g)
@@ -1518,14 +1567,20 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
       for (int i = t0; i < t1; ++i) rec->p64.push_back(bt->h_bandp[ids[i]]);
     }
   }
-  Run r{bt, bt->d_slow_act, n, ss};
-  r.theta = bt->d_slow_theta;
-  r.bandp = bt->d_slow_bandp;
-  r.info = bt->d_slow_info;
+  // (on the call's stream, after its download: the next call's upload follows this part in the
+  // stream's order, so the part reads the call's own active list, θ and widths in place)
+  Run r{bt, own ? bt->d_slow_act : bt->d_active + off, n, ss};
+  if (own) {
+    r.theta = bt->d_slow_theta;
+    r.bandp = bt->d_slow_bandp;
+    r.info = bt->d_slow_info;
+  }
   r.one_stream = true;
+  r.wide_from = 1;  // the part's band16 classes as one launch (band16_wide_kernel)
   band_fused_eval(r, n16, n_g16, q, cnt, se1, kband16, n1, max_terms, (ctx->profiling && fused64) ? rec->fq : nullptr,
                   ctx->profiling ? rec->fq16 : nullptr);
-  launch_slow_gather(bt->d_slow_act, n, bt->results, kResStride, bt->d_slow_res, bt->d_slow_info, bt->d_slow_info_c, ss);
+  launch_slow_gather(r.d_act, n, bt->results, kResStride, bt->d_slow_res, own ? bt->d_slow_info : bt->d_info,
+                     bt->d_slow_info_c, ss);
   HIPX(ctx, hipMemcpyAsync(rec->h_res, bt->d_slow_res, sizeof(double) * n * kResStride, hipMemcpyDeviceToHost, ss));
   HIPX(ctx, hipMemcpyAsync(rec->h_info, bt->d_slow_info_c, sizeof(int) * n, hipMemcpyDeviceToHost, ss));
   HIPX(ctx, hipEventRecord(rec->done, ss));
@@ -1607,10 +1662,11 @@ static int deliver_slow(gpx_batch* bt, gpx_batch::SlowRec& rec, double* lml, dou
     if (ctx->profiling) bt->timing.band_fallbacks += (double)redo.size();
     int rc2;
     if (bt->compact) {
-      rc2 = shadow_lml_grad(bt, redo, rec.theta.data(), lml, grad, info, bt->slow_s);
+      rc2 = shadow_lml_grad(bt, redo, rec.theta.data(), lml, grad, info, bt->slow_s ? bt->slow_s : ctx->stream);
     } else {
       bt->force_dense = 1;
-      rc2 = gpx_batch_lml_grad(bt, (int)redo.size(), redo.data(), rec.theta.data(), lml, grad, info, bt->slow_s);
+      rc2 = gpx_batch_lml_grad(bt, (int)redo.size(), redo.data(), rec.theta.data(), lml, grad, info,
+                               bt->slow_s ? bt->slow_s : ctx->stream);
       bt->force_dense = 0;
     }
     if (rc2 != GPX_OK && rc2 != GPX_NOT_PD) return rc2;
@@ -1828,6 +1884,8 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   // deferred completion: the slow classes (band16 wider than defer_q, then the 64-row sweeps) are
   // the tail of the fused range; they go out as a slow part and this call completes without them
   int n_slow = 0, n_g16_run = n_g16, n16_run = n16, n_fused1_run = n_fused1;
+  struct SlowArgs { int off, n_g16, g0, n16, n1; bool se1; int max_terms; };
+  SlowArgs slow_args{-1, 0, 0, 0, 0, true, 1};
   if (bt->defer_q >= 0 && n_fused > 0) {
     int k = 0, nb16 = 0;
     while (k < n_g16 && g16_q[k] <= bt->defer_q) nb16 += g16_n[k++];
@@ -1848,9 +1906,13 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
       const gpx_kernel_spec& sp = bt->specs[order[i]];
       se1s = se1s && sp.n_terms == 1 && sp.terms[0].kind == GPX_SE && sp.terms[0].dim_count == 1;
     }
-    const int rcs = submit_slow(bt, s, order.data() + off, off, n_slow, n_g16 - n_g16_run, g16_q + n_g16_run,
-                                g16_n + n_g16_run, n16 - n16_run, n_fused1, se1s, b16_p2 ? 3 : 2, max_terms, theta);
-    if (rcs != GPX_OK) return drop_shadow(rcs);
+    if (defer_own_stream()) {
+      const int rcs = submit_slow(bt, s, order.data() + off, off, n_slow, n_g16 - n_g16_run, g16_q + n_g16_run,
+                                  g16_n + n_g16_run, n16 - n16_run, n_fused1, se1s, b16_p2 ? 3 : 2, max_terms, theta);
+      if (rcs != GPX_OK) return drop_shadow(rcs);
+    } else {
+      slow_args = SlowArgs{off, n_g16 - n_g16_run, n_g16_run, n16 - n16_run, n_fused1, se1s, max_terms};
+    }
   }
   if (n_fused_run > 0) {
     const int n_fused = n_fused_run, n16 = n16_run, n_g16 = n_g16_run, n_fused1 = n_fused1_run;
@@ -1887,6 +1949,16 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   HIPX(ctx, hipMemcpyAsync(bt->h_io + bt->io_info_off, bt->d_io + bt->io_info_off,
                            bt->io_bytes - bt->io_info_off, hipMemcpyDeviceToHost, s));
   trace_mark(bt, 44, s);
+  if (slow_args.off >= 0) {
+    // the call completes here; its slow part follows on the same stream
+    if (!bt->bulk_ev) HIPX(ctx, hipEventCreateWithFlags(&bt->bulk_ev, hipEventDisableTiming));
+    HIPX(ctx, hipEventRecord(bt->bulk_ev, s));
+    pe->bulk_done = bt->bulk_ev;
+    const SlowArgs& a = slow_args;
+    const int rcs = submit_slow(bt, s, order.data() + a.off, a.off, n_slow, a.n_g16, g16_q + a.g0, g16_n + a.g0, a.n16,
+                                a.n1, a.se1, b16_p2 ? 3 : 2, a.max_terms, theta);
+    if (rcs != GPX_OK) return drop_shadow(rcs);
+  }
   sc.lap(4);
   if (n_slow > 0) {  // the call's own problems: [dense | band | bulk band16]
     pe->deferred_ids.assign(order.end() - n_slow, order.end());
@@ -1913,7 +1985,10 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = pe->s;
   SubClock sc(bt);
-  HIPX(ctx, hipStreamSynchronize(s));
+  if (pe->bulk_done)  // (a slow part follows the call on its stream)
+    HIPX(ctx, hipEventSynchronize(pe->bulk_done));
+  else
+    HIPX(ctx, hipStreamSynchronize(s));
   sc.lap(5);
   const int n_active = pe->n_active, n_dense = pe->n_dense, n_band = pe->n_band, n_fused = pe->n_fused;
   const int n_fused1 = pe->n_fused1, ng = pe->ng;
@@ -2056,7 +2131,8 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
 int gpx_batch_lml_grad_query(gpx_batch* bt) {
   if (!bt) return GPX_BAD_ARG;
   if (!bt->pending_eval) return 1;
-  hipError_t e = hipStreamQuery(bt->pending_eval->s);
+  hipError_t e = bt->pending_eval->bulk_done ? hipEventQuery(bt->pending_eval->bulk_done)
+                                              : hipStreamQuery(bt->pending_eval->s);
   if (e == hipSuccess && bt->pending_eval->shadow_async) e = hipStreamQuery(bt->shadow_s);
   if (e == hipSuccess) return 1;
   if (e == hipErrorNotReady) return 0;

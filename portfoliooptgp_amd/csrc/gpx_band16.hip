@@ -1088,6 +1088,43 @@ void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s)
   hipLaunchKernelGGL(band16_build_kernel, dim3((tiles + per_wg - 1) / per_wg, n_active), dim3(256), 0, s, a, Q);
 }
 
+// The wide classes (Q = 4, 5: one wavefront per SIMD either way) of a call as ONE launch, each
+// wavefront running both sweeps of its problem at its own width (bandp): a single launch instead
+// of a build / forward / backward chain per class, so a call's few wide problems cost one wave
+// latency instead of one per class. SE1 problems only.
+template <int Q, bool KF, bool KB>
+__device__ __forceinline__ void fused_sweeps(const BandFusedArgs& a, double* __restrict__ lds) {
+  fwd_sweep<Q, KF>(a, lds);
+  vm_drain();
+  __threadfence();
+  wsync();
+  bwd_sweep<Q, 1, true, KB>(a, lds, nullptr);
+}
+template <bool KF, bool KB>
+__global__ __launch_bounds__(64, 1) void band16_wide_kernel(BandFusedArgs a) {
+  constexpr int f4 = Fwd16<4, KF>::size, b4 = Bwd16<4, 1, true, KB>::size;
+  constexpr int f5 = Fwd16<5, KF>::size, b5 = Bwd16<5, 1, true, KB>::size;
+  constexpr int n4 = f4 > b4 ? f4 : b4, n5 = f5 > b5 ? f5 : b5;
+  __shared__ __attribute__((aligned(16))) double lds[n4 > n5 ? n4 : n5];
+  const int Q = a.bandp[a.active[blockIdx.x]];
+  if (Q == 5)
+    fused_sweeps<5, KF, KB>(a, lds);
+  else
+    fused_sweeps<4, KF, KB>(a, lds);
+}
+
+void launch_band16_wide(const BandFusedArgs& a, int kin, int n_active, hipStream_t s, hipEvent_t* ev) {
+  auto k = (kin & 1) ? ((kin & 2) ? band16_wide_kernel<true, true> : band16_wide_kernel<true, false>)
+                     : ((kin & 2) ? band16_wide_kernel<false, true> : band16_wide_kernel<false, false>);
+  if (ev) {
+    hipExtLaunchKernelGGL(k, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
+    (void)hipEventRecord(ev[2], s);
+    (void)hipEventRecord(ev[3], s);
+    return;
+  }
+  hipLaunchKernelGGL(k, dim3(n_active), dim3(64), 0, s, a);
+}
+
 template <int Q>
 static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, int kin, int n_active, hipStream_t s,
                        hipEvent_t* ev) {

@@ -138,6 +138,7 @@ struct gpx_batch {
   hipStream_t slow_s = nullptr;
   hipEvent_t slow_in = nullptr;       // the latest slow part's copies are done (the next upload waits)
   hipEvent_t slow_up = nullptr;       // the call's upload (and rebind gather) are in: the slow part may start
+  hipEvent_t bulk_ev = nullptr;       // same-stream deferral: the call's own results are downloaded
   bool slow_in_armed = false;
   int* d_slow_act = nullptr;
   double* d_slow_theta = nullptr;
@@ -211,6 +212,7 @@ struct Run {
   const int* bandp = nullptr;
   int* info = nullptr;
   bool one_stream = false;
+  int wide_from = 0;  // > 0: the band16 groups of at least this width run as ONE launch (band16_wide_kernel)
 };
 
 struct PhaseTimer {
@@ -328,6 +330,7 @@ struct gpx_batch::PendingEval {
   std::vector<int32_t> order;
   std::vector<int32_t> shadow_ids;  // band storage: problems evaluated on the dense shadow
   std::vector<int32_t> deferred_ids;  // problems of the call whose results come later (slow part)
+  hipEvent_t bulk_done = nullptr;     // (not owned) the call's results are in h_io; a slow part may follow
   bool shadow_async = false;         // shadow_ids were submitted on bt->shadow_s by _submit
   std::vector<double> theta;
   std::unique_ptr<gpx::PhaseTimer> total, ct, bp;
