@@ -9,7 +9,8 @@ i=0
 for kv in "$@"; do
   i=$((i + 1))
   log="gpurun_out/${TAG}_${i}.log"
-  env $kv timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary > "$log" 2>&1 \
+  echo "# env: $kv" > "$log"
+  env $kv timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary >> "$log" 2>&1 \
     || { echo "[$kv] failed"; tail -20 "$log"; exit 1; }
   python tools/bench_summary.py "$kv" "$log"
   python - "$log" <<'PY'
