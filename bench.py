@@ -170,11 +170,15 @@ def band_traffic(kernel_key, problems_per_launch):
     """HBM bytes per launch of the banded roofline kernel from the committed PMC summary of
     THAT kernel (profiles/<round>_band*_traffic.json whose "kernel" names kernel_key, written by
     tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE passes): bytes per problem x
-    the launch's problem count. None when absent."""
+    the launch's problem count. None when absent. The summaries of the inline-K sweeps
+    (GPX_B16_INLINE_K=3: no K band through HBM) are named *_kin3_*, and used only on that path."""
     import glob
     root = os.path.dirname(os.path.abspath(__file__))
+    kin3 = (int(os.environ.get("GPX_B16_INLINE_K", "0") or 0) & 3) == 3
     files = []
     for f in sorted(glob.glob(os.path.join(root, "profiles", "*_band*traffic.json"))):
+        if ("_kin3_" in os.path.basename(f)) != kin3:
+            continue
         d = json.load(open(f))
         if any(kernel_key in k for k in d.get("kernel", [])):
             files.append((f, d))

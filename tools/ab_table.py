@@ -1,18 +1,26 @@
 """Markdown table of bench A/B runs (gpurun_out/<tag>_<i>.log from tools/ab_env.sh, which also
-prints the environment of each run): python tools/ab_table.py LOG_GLOB ... > profiles/r04_ab.md"""
+prints the environment of each run): python tools/ab_table.py [--env MAP.json] LOG_GLOB ... >
+profiles/r04_ab.md. MAP.json = {"<tag>_<i>": "VAR=VALUE ..."} labels logs written without their
+"# env:" line."""
 import glob
 import json
 import sys
 
+args = sys.argv[1:]
+envmap = {}
+if args[:1] == ["--env"]:
+    envmap = json.load(open(args[1]))
+    args = args[2:]
 rows = []
-for pat in sys.argv[1:]:
+for pat in args:
     for f in sorted(glob.glob(pat)):
         try:
             lines = open(f).read().strip().splitlines()
             d = json.loads(lines[-1])
         except Exception:
             continue
-        env = lines[0][len("# env: "):] if lines[0].startswith("# env: ") else ""
+        env = next((l[len("# env: "):] for l in lines if l.startswith("# env: ")), "")
+        env = env or envmap.get(f.rsplit("/", 1)[-1][:-len(".log")], "")
         c = d.get("config", {})
         w = d.get("wave_trace") or {}
         st = d.get("driver_stats_last_call") or {}

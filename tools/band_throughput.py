@@ -4,6 +4,7 @@ evaluated back to back on their own streams (submit all, complete all) for `reps
 Prints evaluations/s, the fused sweeps' average launch times and the chip's block-product rate.
 
 usage: python tools/band_throughput.py [--b 384] [--g 4] [--reps 20] [--ell 1.18]
+       [--ells 1.18:0.89,1.6:0.05,1.9:0.06]   (a mix of width classes: ℓ:share, spread over every batch)
 """
 import argparse
 import json
@@ -28,6 +29,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--ell", type=float, default=1.18)
     ap.add_argument("--series", type=int, default=64, help="distinct series (cycled over the slots)")
+    ap.add_argument("--ells", default="", help="ℓ:share,... (a class mix; overrides --ell)")
     a = ap.parse_args()
     n = 4096
     data = [synthetic_series(n, s) for s in range(a.series)]
@@ -41,6 +43,12 @@ def main():
     streams = [torch.cuda.Stream() for _ in engs]
     th = np.ones((a.b, 16))
     th[:, :3] = [a.ell, 1.0, 1e-5]
+    if a.ells:
+        mix = [tuple(map(float, t.split(":"))) for t in a.ells.split(",")]
+        w = np.array([m[1] for m in mix]) / sum(m[1] for m in mix)
+        cnt = np.floor(w * a.b).astype(int)
+        cnt[0] += a.b - cnt.sum()
+        th[:, 0] = np.repeat([m[0] for m in mix], cnt)
     act = list(range(a.b))
 
     def rnd():
@@ -62,7 +70,7 @@ def main():
     evals = sum(t.band_evals for t in tms)
     fl = lambda f: sum(getattr(t, f) for t in tms)  # noqa: E731
     per_eval = band_problem_flops(n, 1, True) + band_problem_flops(n, 1, False)
-    out = {"B": a.b, "G": a.g, "reps": a.reps, "ell": a.ell, "evals_per_s": evals / dt,
+    out = {"B": a.b, "G": a.g, "reps": a.reps, "ell": a.ells or a.ell, "evals_per_s": evals / dt,
            "ms_per_round": dt / a.reps * 1e3, "band_evals": evals,
            "fwd1_avg_ms": fl("band_fwd_ms_total") / max(fl("band_fused_launches"), 1),
            "bwd1_avg_ms": fl("band_bwd_ms_total") / max(fl("band_fused_launches"), 1),
