@@ -1575,7 +1575,13 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
     r.bandp = bt->d_slow_bandp;
     r.info = bt->d_slow_info;
   }
-  r.one_stream = true;
+  // GPX_DEFER_LANES=1: the part's lanes (the wide band16 launch; the 64-row sweeps) on the
+  // batch's lane streams, joined on ss, instead of one after another on ss
+  static const bool lanes = [] {
+    const char* e = getenv("GPX_DEFER_LANES");
+    return e && atoi(e) != 0;
+  }();
+  r.one_stream = !lanes;
   r.wide_from = 1;  // the part's band16 classes as one launch (band16_wide_kernel)
   band_fused_eval(r, n16, n_g16, q, cnt, se1, kband16, n1, max_terms, (ctx->profiling && fused64) ? rec->fq : nullptr,
                   ctx->profiling ? rec->fq16 : nullptr);

@@ -81,10 +81,10 @@ __device__ __forceinline__ void mma(t4& c, const t4& x, const t4& y) {
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) c = __builtin_amdgcn_mfma_f64_16x16x4f64(x[kk], y[kk], c, 0, 0, 0);
 }
-// c −= Xᵀ·Y
+// c −= Xᵀ·Y (blgp = 1 on an f64 MFMA is its neg modifier on A: −X exactly, no sign-flip VALU op)
 __device__ __forceinline__ void mms(t4& c, const t4& x, const t4& y) {
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) c = __builtin_amdgcn_mfma_f64_16x16x4f64(-x[kk], y[kk], c, 0, 0, 0);
+  for (int kk = 0; kk < 4; ++kk) c = __builtin_amdgcn_mfma_f64_16x16x4f64(x[kk], y[kk], c, 0, 0, 1);
 }
 
 // sums over the 4 lanes l4 = 0..3 of a column (lanes l15 + 16·l4), no LDS round trip: with both
@@ -191,7 +191,7 @@ __device__ __forceinline__ void leaf16m(t4 A, t4& V, t4& Wr, double& lii, int& f
 #pragma unroll
       for (int c = 0; c <= a; ++c) d[a][c] = sm[(4 * jb + a) * 4 + c];  // (same address on every lane)
     // 4x4 Cholesky L_d and its inverse Li (uniform)
-    double l[4][4], iv[4], li[4][4];
+    double l[4][4], iv[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
 #pragma unroll
@@ -208,29 +208,21 @@ __device__ __forceinline__ void leaf16m(t4 A, t4& V, t4& Wr, double& lii, int& f
       iv[a] = rsqrt_nr(pv);
       l[a][a] = pv * iv[a];
     }
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      li[a][a] = iv[a];
-#pragma unroll
-      for (int c = a - 1; c >= 0; --c) {  // li[a][c] = −iv[a] Σ_{e=c}^{a−1} l[a][e] li[e][c]
-        double t = 0.0;
-#pragma unroll
-        for (int e = c; e < a; ++e) t = fma(l[a][e], li[e][c], t);
-        li[a][c] = -iv[a] * t;
-      }
-    }
     if ((l15 >> 2) == jb) {
       const int a = l15 & 3;
       lii = a == 0 ? l[0][0] : a == 1 ? l[1][1] : a == 2 ? l[2][2] : l[3][3];
     }
-    // panel column block jb of L: rows below the block m·Li_dᵀ, rows of the block L_d, above 0
-    double lrow[4];  // Li[l4][c] (0 for c > l4)
+    // panel column block jb of L: rows below the block m·Li_dᵀ, rows of the block L_d, above 0.
+    // lrow = row l4 of Li = L_d⁻¹ (0 for c > l4), by substitution along the row (Li·L_d = I:
+    // Li[a][c] = −iv[c] Σ_{e=c+1}^{a} Li[a][e] l[e][c]), each lane its own row: no 4x4 inverse
+    double lrow[4];
+    lrow[3] = l4 == 3 ? iv[3] : 0.0;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      double v = 0.0;
+    for (int c = 2; c >= 0; --c) {
+      double t = lrow[c + 1] * l[c + 1][c];
 #pragma unroll
-      for (int a = c; a < 4; ++a) v = (l4 == a) ? li[a][c] : v;
-      lrow[c] = v;
+      for (int e = c + 2; e < 4; ++e) t = fma(lrow[e], l[e][c], t);
+      lrow[c] = l4 == c ? iv[c] : (l4 > c ? -iv[c] * t : 0.0);
     }
     double xb = 0.0;
 #pragma unroll
@@ -238,13 +230,13 @@ __device__ __forceinline__ void leaf16m(t4 A, t4& V, t4& Wr, double& lii, int& f
     // rows below the block only: the update of the block's own rows and columns (L_d L_dᵀ) is
     // never read again, so the block rows of the panel are left at 0
     xb = l15 - 4 * jb >= 4 ? xb : 0.0;
-    A = __builtin_amdgcn_mfma_f64_16x16x4f64(-xb, xb, A, 0, 0, 0);  // trailing update (rank 4)
+    A = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, A, 0, 0, 1);  // trailing update (rank 4)
     // block row jb of L⁻¹: Li · (its current rows), then the rows below
     double wn = 0.0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) wn = fma(lrow[c], wv[c], wn);
     Wr[jb] = wn;
-    Wr = __builtin_amdgcn_mfma_f64_16x16x4f64(-xb, wn, Wr, 0, 0, 0);
+    Wr = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, wn, Wr, 0, 0, 1);
   }
   // V = fragment of (L⁻¹)ᵀ
   wsync();
@@ -382,19 +374,23 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
   }
   int gfail = 0;
   Q_BEGIN
-  for (int k = 0; k < nb; ++k) {
-    const int qk = min(Q, nb - 1 - k), k16 = k * 16;
+  // one block step; qkc = the window rows below the diagonal block (Q but in the last Q steps),
+  // fullc: a new row enters (all but the last Q + 1 steps). The steps with both constant run
+  // as a loop of their own, free of the edge conditions and their branches
+  auto step = [&](const int k, const auto qkc, const auto fullc) __attribute__((always_inline)) {
+    const int qk = qkc, k16 = k * 16;
     // the row entering the window after this step (block bn = k+Q+1): global -> LDS, in flight
     // during the step (the previous step's reads of snew are done: program order + wsync);
     // KIN: only its inputs (one value per row, into a register)
     const int bn = k + Q + 1;
+    const bool newrow = decltype(fullc)::value || bn < nb;
     double xn = 0.0;
     if constexpr (KIN) {
-      if (bn < nb) xn = xval(bn * 16 + l15);
+      if (newrow) xn = xval(bn * 16 + l15);
     } else {
       wsync();
       lds_drain();  // the previous step's reads of snew have completed
-      if (bn < nb) {
+      if (newrow) {
 #pragma unroll
         for (int j = 0; j <= Q; ++j) tile_glds_swz(K + (long long)(bn * 16) * ld + (k + 1 + j) * 16, ld, snew[j], lane);
       }
@@ -469,7 +465,7 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
       // block bn's inputs join the ring (in the slot of block k, whose last reads were at the
       // previous step's end), then the new row's tiles (bn, k+1+j) from x/ℓ
       const double ar = xn / kell;
-      if (bn < nb && l4 == 0) sxa[bn % (Q + 1)][rq(l15)] = ar;
+      if (newrow && l4 == 0) sxa[bn % (Q + 1)][rq(l15)] = ar;
       wsync();
       const int gi = bn * 16 + l15;
 #pragma unroll
@@ -477,7 +473,7 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
         t4 t = tzero();
         const int c = k + 1 + j;
         // (16-row blocks sit inside one 64-block: the 64-block offset is uniform over the tile)
-        if (bn < nb && (bn >> 2) - (c >> 2) < a.kband) {
+        if (newrow && (bn >> 2) - (c >> 2) < a.kband) {
           const t4 ac = *reinterpret_cast<const t4*>(&sxa[c % (Q + 1)][4 * l4]);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -491,7 +487,7 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
 #pragma unroll
       for (int j = 0; j <= Q; ++j) {
         t4 t = tzero();
-        if (bn < nb) {
+        if (newrow) {
           // (16-row blocks sit inside one 64-block: the 64-block offset is uniform over the tile)
           const bool zero = (bn >> 2) - ((k + 1 + j) >> 2) >= a.kband;
 #pragma unroll
@@ -505,7 +501,12 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
       }
     }
     QP(5);
-  }
+  };
+  int k = 0;
+  // (not the two-wave Q = 4 sweep: its two copies of the step no longer fit 256 registers)
+  if constexpr (Q != 4)
+    for (; k < nb - Q - 1; ++k) step(k, std::integral_constant<int, Q>{}, std::true_type{});
+  for (; k < nb; ++k) step(k, min(Q, nb - 1 - k), std::false_type{});
   Q_END(0);
   if (lane == 0 && gfail > 0 && a.info[b] == 0) a.info[b] = gfail;
   wave_trace_put(a, wt0, Q);
@@ -682,13 +683,14 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
     if (k > 0) fetch(k - 1, zr, xr);
     QP(0);
     // α_k = W_kkᵀ (z_k − Σ_i P_iᵀ α_{k+i})
+    // (no edge conditions in this step's products: the window's tiles beyond the last block
+    // are exact zeros — P_i past qk is loaded as 0, so G_i, Z_{k+i,k} and every S tile that
+    // reaches past the matrix stay 0 — and adding their zero products leaves every value as is)
     double t[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int i = 1; i <= Q; ++i)
-      if (i <= qk) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) t[r] = fma(P[i][r], al[i], t[r]);
-      }
+      for (int r = 0; r < 4; ++r) t[r] = fma(P[i][r], al[i], t[r]);
     double ap = 0.0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) ap = fma(Wf[r], zc[r] - sum16(t[r]), ap);
@@ -703,29 +705,24 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
     QP(1);
     // G_i = P_i W_kk
 #pragma unroll
-    for (int i = 1; i <= Q; ++i)
-      if (i <= qk) {
-        t4 g = tzero();
-        mma(g, P[i], Wf);
-        P[i] = g;
-      }
+    for (int i = 1; i <= Q; ++i) {
+      t4 g = tzero();
+      mma(g, P[i], Wf);
+      P[i] = g;
+    }
     QP(2);
     // Z_{k+i,k} = −Σ_j Z_{k+i,k+j} G_j
     t4 Zn[Q + 1];
 #pragma unroll
     for (int i = 1; i <= Q; ++i) {
       Zn[i] = tzero();
-      if (i <= qk) {
 #pragma unroll
-        for (int j = 1; j <= Q; ++j) {
-          if (j <= qk) {
-            if (j >= i) {
-              mms(Zn[i], S[wid(j - 1, i - 1)], P[j]);
-            } else {
-              const t4 tt = tile_transpose(S[wid(i - 1, j - 1)], sc, l15, l4);
-              mms(Zn[i], tt, P[j]);
-            }
-          }
+      for (int j = 1; j <= Q; ++j) {
+        if (j >= i) {
+          mms(Zn[i], S[wid(j - 1, i - 1)], P[j]);
+        } else {
+          const t4 tt = tile_transpose(S[wid(i - 1, j - 1)], sc, l15, l4);
+          mms(Zn[i], tt, P[j]);
         }
       }
     }
@@ -737,8 +734,7 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
     t4 Zk = tzero();
     mma(Zk, Wf, Wf);
 #pragma unroll
-    for (int i = 1; i <= Q; ++i)
-      if (i <= qk) mms(Zk, P[i], Zn[i]);
+    for (int i = 1; i <= Q; ++i) mms(Zk, P[i], Zn[i]);
     wsync();
     QP(4);
     // gradient contraction and the band check's K∘Z sums over tile i (0: Z_kk whole, weight 1;
@@ -752,6 +748,7 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
       // 64-block offset >= kband are the exact zeros of the class; the diagonal tile mirrored
       // from its lower triangle): ∂K/∂ℓ = K r²/ℓ, and Σ v ∂K/∂σ² = (Σ v K)/σ² at the end
       const double xjv = sxT[cs][(l15 & 3) * 4 + (l15 >> 2)];
+      const double m2xj = -2.0 * xjv, xj2 = xjv * xjv;
 #pragma unroll
       for (int i = 0; i <= Q; ++i) {
         if (i > qk) continue;
@@ -766,7 +763,7 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
           const int il = 4 * r + l4, gi = (k + i) * 16 + il;
           const double zij = Zt[r];
           const double ai = a4[r];
-          const double r2 = sqdist1(x4[r], xjv);
+          const double r2 = sqdist1_b(x4[r], m2xj, xj2);
           const bool dg = i == 0 && il == l15;
           double kraw;
           if constexpr (KIN) {

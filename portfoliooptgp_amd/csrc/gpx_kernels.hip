@@ -324,7 +324,7 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
       for (int kk = 0; kk < 4; ++kk) {
         const double av = sS[li + l15 * 17 + 4 * kk + l4];
         const double bv = sS[lk + l15 * 17 + 4 * kk + l4];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 1);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) sS[ob + (l4 + 4 * u) * 17 + l15] = acc[u];
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const double av = sS[di + l15 * 17 + 4 * kk + l4];   // D_i[row][k']
-          wv[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, t[kk], wv[h], 0, 0, 0);
+          wv[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, t[kk], wv[h], 0, 0, 1);
         }
       }
     }

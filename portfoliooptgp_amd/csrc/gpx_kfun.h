@@ -46,6 +46,12 @@ __device__ __forceinline__ double sqdist1(double a, double b) {
 #pragma clang fp contract(off)
   return -2.0 * (a * b) + (a * a + b * b);
 }
+// sqdist1(a, b) from b's −2b and b², computed once per column: the same bits (a·(−2b) is
+// −2·(a·b) exactly, a power-of-two scaling commuting with the rounding)
+__device__ __forceinline__ double sqdist1_b(double a, double m2b, double b2) {
+#pragma clang fp contract(off)
+  return a * m2b + (a * a + b2);
+}
 // raw inputs: scale by 1/ℓ (a division, as Stationary.scale) on the fly
 __device__ __forceinline__ double sqdist_gpflow(const double* __restrict__ xi, const double* __restrict__ xj,
                                                 int dn, double ell) {

@@ -147,7 +147,7 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
     for (int kk = 0; kk < 4; ++kk) {
       const double av = sA[(ri + l15) * S + c0 + 4 * kk + l4];
       const double bv = sA[(rk + l15) * S + c0 + 4 * kk + l4];
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 1);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) sA[(ri + l4 + 4 * u) * S + rk + l15] = acc[u];
@@ -216,7 +216,7 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const double av = sW[(i * 16 + l15) * S + i * 16 + 4 * kk + l4];     // D_i[row][k']
-        wv = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, t[kk], wv, 0, 0, 0);  // T[k'][col]
+        wv = __builtin_amdgcn_mfma_f64_16x16x4f64(av, t[kk], wv, 0, 0, 1);  // T[k'][col]
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) sW[(i * 16 + l4 + 4 * q) * S + j * 16 + l15] = wv[q];

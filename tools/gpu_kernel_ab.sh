@@ -20,4 +20,5 @@ for lib in "$OLD" portfoliooptgp_amd/libgpx.so; do
     echo "$lib $e $(tail -1 gpurun_out/${TAG}_tp.tmp)" | tee -a gpurun_out/${TAG}_throughput.txt
   done
 done
-bash tools/ab_env.sh $TAG "GPX_LIB=$OLD GPX_DEFER_Q=-1" "GPX_DEFER_Q=-1" "GPX_LIB=$OLD GPX_DEFER_Q=3" "GPX_DEFER_Q=3"
+bash tools/ab_env.sh $TAG "GPX_LIB=$OLD GPX_DEFER_Q=-1" "GPX_DEFER_Q=-1" "GPX_LIB=$OLD GPX_DEFER_Q=3" "GPX_DEFER_Q=3" \
+  "GPX_DEFER_Q=-1 GPX_B16_INLINE_K=3" "GPX_DEFER_Q=3 GPX_B16_INLINE_K=3" "GPX_DEFER_Q=3 GPX_DEFER_LANES=1"

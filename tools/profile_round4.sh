@@ -6,14 +6,16 @@
 #      processes, which must not start under the profiler) -> per-kernel summary + trace check
 #   3. --pmc FETCH_SIZE, 4. --pmc WRITE_SIZE (separate passes) -> HBM bytes per problem of the
 #      band16 sweeps, for the K-band path (default) and the inline-K path (GPX_B16_INLINE_K=3)
-# usage: tools/profile_round4.sh TAG
+# usage: [SKIP_BENCH=1] tools/profile_round4.sh TAG
 set -e
 TAG=${1:-r04}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-timeout -k 10 600 python3 "$ROOT/bench.py" > "$OUT/bench.log" 2>&1
-tail -1 "$OUT/bench.log" | cut -c1-300
+if [ -z "$SKIP_BENCH" ]; then  # (SKIP_BENCH=1: the caller has just run the default bench line)
+  timeout -k 10 600 python3 "$ROOT/bench.py" > "$OUT/bench.log" 2>&1
+  tail -1 "$OUT/bench.log" | cut -c1-300
+fi
 GPX_WAVE_TRACE=1 GPX_WAVE_TRACE_OUT="$OUT/wave_trace.npz" timeout -k 10 300 python3 "$ROOT/bench.py" \
   --no-cpu-baseline --no-secondary > "$OUT/wave_bench.log" 2>&1
 python3 "$ROOT/tools/call_timeline.py" "$OUT/wave_trace.npz" > "$OUT/call_timeline.txt"
