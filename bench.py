@@ -174,7 +174,7 @@ def band_traffic(kernel_key, problems_per_launch):
     (GPX_B16_INLINE_K=3: no K band through HBM) are named *_kin3_*, and used only on that path."""
     import glob
     root = os.path.dirname(os.path.abspath(__file__))
-    kin3 = (int(os.environ.get("GPX_B16_INLINE_K", "0") or 0) & 3) == 3
+    kin3 = (int(os.environ.get("GPX_B16_INLINE_K", "3") or 0) & 3) == 3  # (the library's default: 3)
     files = []
     for f in sorted(glob.glob(os.path.join(root, "profiles", "*_band*traffic.json"))):
         if ("_kin3_" in os.path.basename(f)) != kin3:
@@ -256,7 +256,7 @@ def parse_args(argv=None):
     # a second device batch per process for the slow evaluation classes (Scipy.minimize_stream
     # wide_group, optimizers._wide_classes): the band16 sweeps wider than GPX_NARROW_Q 16-blocks
     # and the 64-row sweeps, so the narrow batch's calls never wait for them
-    ap.add_argument("--defer-q", type=int, default=int(os.environ.get("GPX_DEFER_Q", -1)),
+    ap.add_argument("--defer-q", type=int, default=int(os.environ.get("GPX_DEFER_Q", 3)),
                     help="defer the band16 classes wider than this many 16-blocks and the 64-row sweeps (-1: off)")
     ap.add_argument("--wide-slots", type=int, default=int(os.environ.get("GPX_BENCH_WIDE", 0)),
                     help="slots per process of the slow-class device batch, taken from --width (0: one batch)")

@@ -660,7 +660,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   // saves that sweep's K read). Same bits either way.
   static const int kin = [] {
     const char* e = getenv("GPX_B16_INLINE_K");
-    return e ? (atoi(e) & 3) : 0;
+    return e ? (atoi(e) & 3) : 3;  // default: both (round 4: +4-7 % on the C2 bench, K's band never in HBM)
   }();
   // GPX_BAND_LANE_STREAMS: streams the lanes are spread over (the bulk lane alone on the call's
   // stream, the others round-robin on the rest). A process gets GPU_MAX_HW_QUEUES hardware

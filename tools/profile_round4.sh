@@ -5,7 +5,7 @@
 #   2. rocprofv3 --kernel-trace --stats of one host process (the bench's helpers are spawned
 #      processes, which must not start under the profiler) -> per-kernel summary + trace check
 #   3. --pmc FETCH_SIZE, 4. --pmc WRITE_SIZE (separate passes) -> HBM bytes per problem of the
-#      band16 sweeps, for the K-band path (default) and the inline-K path (GPX_B16_INLINE_K=3)
+#      band16 sweeps, for the K-band path (GPX_B16_INLINE_K=0) and the inline-K path (3, the default)
 # usage: [SKIP_BENCH=1] tools/profile_round4.sh TAG
 set -e
 TAG=${1:-r04}
