@@ -227,7 +227,8 @@ SUM_FIELDS = ("contract_ms_total", "contract_launches", "contract_alg_flops", "e
               "shadow_predicts")
 NARROW_FIELDS = ("band_fwd_ms_total", "band_bwd_ms_total", "band_fused_launches", "band_fwd_flops", "band_bwd_flops",
                  "band16_fwd_ms_total", "band16_bwd_ms_total", "band16_launches", "band16_evals", "band16_q_sum",
-                 "band16_fwd_flops", "band16_bwd_flops", "band16_wave_ms")
+                 "band16_fwd_flops", "band16_bwd_flops", "band16_wave_ms", "band16_wide_ms_total",
+                 "band16_wide_launches", "band16_wide_flops", "band16_wide_evals")
 
 
 def parse_args(argv=None):
@@ -744,7 +745,10 @@ def main():
     for key, ms, fl, la in (("band16_fwd_kernel", tm["band16_fwd_ms_total"], tm["band16_fwd_flops"], tm["band16_launches"]),
                             ("band16_bwd_kernel", tm["band16_bwd_ms_total"], tm["band16_bwd_flops"], tm["band16_launches"]),
                             ("band_fwd1_kernel", tm["band_fwd_ms_total"], tm["band_fwd_flops"], tm["band_fused_launches"]),
-                            ("band_bwd1_kernel<1>", tm["band_bwd_ms_total"], tm["band_bwd_flops"], tm["band_fused_launches"])):
+                            ("band_bwd1_kernel<1>", tm["band_bwd_ms_total"], tm["band_bwd_flops"], tm["band_fused_launches"]),
+                            # the deferred part's Q = 4/5 classes, both sweeps per wavefront, one launch
+                            ("band16_wide_kernel", tm["band16_wide_ms_total"], tm["band16_wide_flops"],
+                             tm["band16_wide_launches"])):
         b_ms = ms / max(la, 1.0)
         b_fl = fl / max(la, 1.0)
         ach = b_fl / (b_ms * 1e-3) / 1e12 if b_ms > 0 else 0.0
@@ -754,8 +758,9 @@ def main():
     q_mean = tm["band16_q_sum"] / max(e16, 1.0)
     for key in ("band16_fwd_kernel", "band16_bwd_kernel"):
         k = sweeps[key]
-        ppl = e16 / max(k["launches"], 1.0)  # problems per launch
+        ppl = (e16 - tm["band16_wide_evals"]) / max(k["launches"], 1.0)  # problems per launch
         k["traffic"], k["traffic_source"] = band_traffic(key, ppl) if ppl > 0 else (None, None)
+    sweeps["band16_wide_kernel"]["traffic"], sweeps["band16_wide_kernel"]["traffic_source"] = None, None
     for key, fwd in (("band_fwd1_kernel", True), ("band_bwd1_kernel<1>", False)):
         k = sweeps[key]
         ppl = k["alg_flops_per_launch"] / band_problem_flops(n, 1, fwd)
@@ -765,7 +770,8 @@ def main():
     # tile products + the 64-row sweeps' block products) / wall time
     # (the 64-row sweeps' flops are those of their timed launch pairs: the p <= 1 class's when the
     # call has one, else the p = 2 class's)
-    chip_fl = tm["band16_fwd_flops"] + tm["band16_bwd_flops"] + tm["band_fwd_flops"] + tm["band_bwd_flops"]
+    chip_fl = (tm["band16_fwd_flops"] + tm["band16_bwd_flops"] + tm["band16_wide_flops"] + tm["band_fwd_flops"]
+               + tm["band_bwd_flops"])
     chip_ach = chip_fl / elapsed / 1e12
     kname = max(sweeps, key=lambda k: sweeps[k]["ms_total"])
     if sweeps[kname]["ms_total"] > tm["contract_ms_total"]:

@@ -301,6 +301,10 @@ typedef struct {
   /* Σ over band16 launches of (problems in the launch) × (its duration, ms): the wave-ms the
    * sweeps held (one wavefront per problem); ÷ (wave slots × wall ms) = their occupancy */
   double band16_wave_ms;
+  /* the deferred part's wide launches (band16_wide_kernel: the Q = 4 and 5 classes of a call, both
+   * sweeps per wavefront): their durations, count, MFMA flops and problems — kept out of the
+   * band16 forward/backward launch figures above (which count the per-class launches only) */
+  double band16_wide_ms_total, band16_wide_launches, band16_wide_flops, band16_wide_evals;
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);

@@ -68,7 +68,9 @@ class GpxTiming(ctypes.Structure):
                 ("band16_bwd_ms_total", ctypes.c_double), ("band16_launches", ctypes.c_double),
                 ("band16_evals", ctypes.c_double), ("band16_q_sum", ctypes.c_double),
                 ("band16_fwd_flops", ctypes.c_double), ("band16_bwd_flops", ctypes.c_double),
-                ("band16_wave_ms", ctypes.c_double)]
+                ("band16_wave_ms", ctypes.c_double), ("band16_wide_ms_total", ctypes.c_double),
+                ("band16_wide_launches", ctypes.c_double), ("band16_wide_flops", ctypes.c_double),
+                ("band16_wide_evals", ctypes.c_double)]
 
 
 class GPXError(RuntimeError):

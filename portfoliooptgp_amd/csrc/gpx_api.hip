@@ -662,6 +662,13 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     const char* e = getenv("GPX_B16_INLINE_K");
     return e ? (atoi(e) & 3) : 3;  // default: both (round 4: +4-7 % on the C2 bench, K's band never in HBM)
   }();
+  // the same for the wide launch (the Q = 4, 5 classes of a deferred part, one wavefront per SIMD:
+  // there the exp on each sweep's chain costs more than a build launch; GPX_B16_INLINE_K_WIDE,
+  // default: as GPX_B16_INLINE_K)
+  static const int kin_wide = [] {
+    const char* e = getenv("GPX_B16_INLINE_K_WIDE");
+    return e ? (atoi(e) & 3) : kin;
+  }();
   // GPX_BAND_LANE_STREAMS: streams the lanes are spread over (the bulk lane alone on the call's
   // stream, the others round-robin on the rest). A process gets GPU_MAX_HW_QUEUES hardware
   // queues (the bench: 2, so that 8 processes stay within the 16 the GPU maps without
@@ -695,7 +702,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       // the wide SE1 groups: their K bands (unless computed in the sweeps), then one launch
       int goff = l.off;
       for (int g = l.g; g < l.g_end; ++g) {
-        if (!((kin & 1) && (kin & 2))) {
+        if (!((kin_wide & 1) && (kin_wide & 2))) {
           BuildArgs bg = ba;
           bg.active = r.d_act + goff;
           launch_band16_build(bg, g16_q[g], g16_n[g], ls);
@@ -707,7 +714,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       f16.active = r.d_act + l.off;
       if (ev16)
         for (int g = l.g + 1; g < l.g_end; ++g) (void)hipEventRecord(ev16[g][0], ls);
-      launch_band16_wide(f16, kin, l.n, ls, ev16 ? ev16[l.g] : nullptr);
+      launch_band16_wide(f16, kin_wide, l.n, ls, ev16 ? ev16[l.g] : nullptr);
       if (ev16)
         for (int g = l.g + 1; g < l.g_end; ++g)
           for (int e = 1; e < 4; ++e) (void)hipEventRecord(ev16[g][e], ls);
@@ -1538,6 +1545,7 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
   rec->theta.assign(theta, theta + (size_t)bt->B * GPX_THETA_STRIDE);
   rec->clear_events();
   rec->n_g16 = n_g16;
+  rec->se1 = se1;
   for (int g = 0; g < n_g16; ++g) {
     rec->g16_q[g] = q[g];
     rec->g16_n[g] = cnt[g];
@@ -1636,19 +1644,35 @@ static int deliver_slow(gpx_batch* bt, gpx_batch::SlowRec& rec, double* lml, dou
   if (ctx->profiling) {
     bt->timing.band_evals += n;
     bt->timing.evals += n;
+    bool wide_seen = false;
     for (int g = 0; g < rec.n_g16; ++g) {
       float f0 = 0.f, f1 = 0.f;
       (void)hipEventElapsedTime(&f0, rec.fq16[g][0], rec.fq16[g][1]);
       (void)hipEventElapsedTime(&f1, rec.fq16[g][2], rec.fq16[g][3]);
-      bt->timing.band16_fwd_ms_total += f0;
-      bt->timing.band16_bwd_ms_total += f1;
-      bt->timing.band16_wave_ms += (double)rec.g16_n[g] * ((double)f0 + (double)f1);
-      bt->timing.band16_launches += 1.0;
-      bt->timing.band16_evals += rec.g16_n[g];
-      bt->timing.band16_q_sum += (double)rec.g16_q[g] * rec.g16_n[g];
-      bt->timing.band16_fwd_flops += rec.g16_n[g] * band16_flops(bt->Np, rec.g16_q[g], true);
-      bt->timing.band16_bwd_flops += rec.g16_n[g] * band16_flops(bt->Np, rec.g16_q[g], false);
-      bt->timing.band_p_sum += rec.g16_n[g];
+      const int n = rec.g16_n[g], q = rec.g16_q[g];
+      const double fl = n * (band16_flops(bt->Np, q, true) + band16_flops(bt->Np, q, false));
+      if (rec.se1 && q >= 4 && q <= 5) {
+        // the wide launch (band_fused_eval's kind-3 lane): every one of its groups' events spans
+        // the one kernel, so it is counted once, apart from the per-class launches
+        if (!wide_seen) {
+          bt->timing.band16_wide_ms_total += f0;
+          bt->timing.band16_wide_launches += 1.0;
+          wide_seen = true;
+        }
+        bt->timing.band16_wide_flops += fl;
+        bt->timing.band16_wide_evals += n;
+        bt->timing.band16_wave_ms += (double)n * (double)f0;
+      } else {
+        bt->timing.band16_fwd_ms_total += f0;
+        bt->timing.band16_bwd_ms_total += f1;
+        bt->timing.band16_wave_ms += (double)n * ((double)f0 + (double)f1);
+        bt->timing.band16_launches += 1.0;
+        bt->timing.band16_fwd_flops += n * band16_flops(bt->Np, q, true);
+        bt->timing.band16_bwd_flops += n * band16_flops(bt->Np, q, false);
+      }
+      bt->timing.band16_evals += n;
+      bt->timing.band16_q_sum += (double)q * n;
+      bt->timing.band_p_sum += n;
     }
     if (rec.fq[0]) {
       float f0 = 0.f, f1 = 0.f;

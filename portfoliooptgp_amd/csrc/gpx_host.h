@@ -304,6 +304,7 @@ struct gpx_batch::SlowRec {
   int* h_info = nullptr;              // pinned [B]
   // profiling: its band16 groups and 64-row sweep pair, as PendingEval records them
   int n_g16 = 0, g16_q[gpx::kBand16MaxQ] = {}, g16_n[gpx::kBand16MaxQ] = {};
+  bool se1 = false;                   // (its Q = 4, 5 groups ran as one band16_wide_kernel launch)
   hipEvent_t fq16[gpx::kBand16MaxQ][4] = {};
   hipEvent_t fq[4] = {};
   std::vector<int> p64;               // band widths of the timed 64-row launch pair's problems

@@ -58,18 +58,22 @@ np.savez({path!r}, **out)
 """
 
 
-def _run(kin, path):
+def _run(kin, path, wide=None):
     env = dict(os.environ, GPX_B16_INLINE_K=str(kin))
+    env.pop("GPX_B16_INLINE_K_WIDE", None)
+    if wide is not None:
+        env["GPX_B16_INLINE_K_WIDE"] = str(wide)
     code = CHILD.format(root=ROOT, path=path)
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     return np.load(path)
 
 
-@pytest.mark.parametrize("kin", [1, 2, 3])
-def test_inline_k_bit_identical(tmp_path, kin):
+@pytest.mark.parametrize("kin,wide", [(1, None), (2, None), (3, None), (3, 0)])
+def test_inline_k_bit_identical(tmp_path, kin, wide):
+    """(wide: GPX_B16_INLINE_K_WIDE, the setting of the deferred part's wide launch)"""
     ref = _run(0, str(tmp_path / "k0.npz"))
-    got = _run(kin, str(tmp_path / f"k{kin}.npz"))
+    got = _run(kin, str(tmp_path / f"k{kin}.npz"), wide)
     q = ref["q"]
     assert set(int(c) for c in q) >= {1, 2, 3, 4, 5}, q  # every band16 width present
     for key in ("lml-1", "grad-1", "info-1", "lml3", "grad3", "info3", "mean", "var"):
