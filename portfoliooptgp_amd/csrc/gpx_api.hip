@@ -802,6 +802,14 @@ static bool submit_stats_on() {
   }();
   return on;
 }
+void print_submit_stats(const gpx_batch* bt) {
+  fprintf(stderr, "[gpx submit stats] batch B=%d calls=%lld flush=%.3f route=%.3f upload=%.3f launch=%.3f "
+          "download=%.3f complete_sync=%.3f (flush: wait_io=%.3f box_sync=%.3f over %lld syncs) "
+          "predict=%.3f (io wait %.3f, shadow slots %.3f, %.0f shadow predicts) s\n", bt->B,
+          bt->sub_calls, bt->sub_s[0], bt->sub_s[1], bt->sub_s[2], bt->sub_s[3], bt->sub_s[4], bt->sub_s[5],
+          bt->sub_s[6], bt->sub_s[7], bt->box_syncs, bt->sub_s[8], bt->sub_s[9], bt->sub_s[10],
+          bt->timing.shadow_predicts);
+}
 struct SubClock {
   gpx_batch* bt;
   bool on;
@@ -959,7 +967,9 @@ int upload_common(gpx_batch* bt, int n_active, const int32_t* active, const doub
   if (bt->slow_in_armed) HIPX(bt->ctx, hipStreamWaitEvent(s, bt->slow_in, 0));
   char* hio = bt->h_io;
   if (predict_block) {  // (the last asynchronous predict's upload out of it has completed)
+    SubClock pc(bt);
     const int e = wait_io(bt);
+    pc.lap(9);
     if (e != GPX_OK) return e;
     if (!bt->h_io_pred) HIPX(ctx, hipHostMalloc(&bt->h_io_pred, bt->io_bytes, hipHostMallocNonCoherent));
     hio = bt->h_io_pred;
@@ -1172,11 +1182,7 @@ int gpx_batch_destroy(gpx_batch* bt) {
     (void)hipStreamSynchronize(bt->pending_eval->s);
     bt->pending_eval.reset();
   }
-  if (submit_stats_on() && bt->sub_calls > 0)
-    fprintf(stderr, "[gpx submit stats] batch B=%d calls=%lld flush=%.3f route=%.3f upload=%.3f launch=%.3f "
-            "download=%.3f complete_sync=%.3f (flush: wait_io=%.3f box_sync=%.3f over %lld syncs) s\n", bt->B,
-            bt->sub_calls, bt->sub_s[0], bt->sub_s[1], bt->sub_s[2], bt->sub_s[3], bt->sub_s[4], bt->sub_s[5],
-            bt->sub_s[6], bt->sub_s[7], bt->box_syncs);
+  if (submit_stats_on() && bt->sub_calls > 0) print_submit_stats(bt);
   if (!bt->slow_out.empty() || bt->slow_s || bt->d_slow_res) {  // deferred slow parts use the buffers below
     for (auto& r : bt->slow_out) (void)hipEventSynchronize(r->done);
     if (bt->slow_s) (void)hipStreamSynchronize(bt->slow_s);
@@ -1489,16 +1495,15 @@ static int shadow_collect(gpx_batch* bt, const std::vector<int32_t>& ids, double
 }
 
 // ---- deferred completion of the slow classes (gpx_batch_set_deferred) ----
-// GPX_DEFER_STREAM=1: the slow part runs on a stream of its own, from copies of the call's
-// inputs; by default it follows the call's own work on the call's stream, after the call's
-// download (the call completes at an event there). A process gets few hardware queues (the
-// bench: 2), and a second stream shares one with the first, so its kernels run in order with
-// them anyway; on one stream the slow part delays only the next call, which waits for the host
-// to step the fits first.
+// By default the slow part runs on a stream of its own, from copies of the call's inputs, so the
+// next call's work does not queue behind it (the C2 bench: +14-18 % over the same-stream variant
+// once the driver's calls are on a stream of their own). GPX_DEFER_STREAM=0: it
+// follows the call's own work on the call's stream, after the call's download (the call
+// completes at an event there), and delays the next call.
 static bool defer_own_stream() {
   static const bool on = [] {
     const char* e = getenv("GPX_DEFER_STREAM");
-    return e && atoi(e) != 0;
+    return !(e && atoi(e) == 0);
   }();
   return on;
 }
@@ -1746,6 +1751,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   HIPX(ctx, hipSetDevice(ctx->device));
   SubClock sc(bt);
   ++bt->sub_calls;
+  if (submit_stats_on() && bt->sub_calls % 256 == 0) print_submit_stats(bt);  // (runs that never destroy it)
 
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   trace_mark(bt, 38, s);
@@ -2235,6 +2241,11 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
         return fail(ctx, GPX_BAD_ARG, "a problem has a deferred evaluation in flight");
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  SubClock pclk(bt);
+  struct PredLap {  // (GPX_SUBMIT_STATS: the call's host time, whatever path it returns by)
+    SubClock& c;
+    ~PredLap() { c.lap(8); }
+  } plap{pclk};
   // band storage: only predict at the training inputs from a cached banded factor at exactly
   // this θ stays here; every other problem is predicted on the dense fallback slots, one by one
   std::vector<int32_t> keep;
@@ -2274,6 +2285,11 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
       bt->timing.shadow_predicts += 1;
       info[b] = inf[0];
       if (rc == GPX_NOT_PD) shadow_status = GPX_NOT_PD;
+    }
+    if (n_active > (int)keep.size()) {
+      SubClock sc2(bt);
+      sc2.t = pclk.t;
+      sc2.lap(10);  // (from the call's start: the shadow slots' synchronous predicts)
     }
     if (keep.empty()) return shadow_status;
     active = keep.data();

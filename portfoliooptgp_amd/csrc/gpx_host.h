@@ -166,7 +166,7 @@ struct gpx_batch {
   hipEvent_t fork = nullptr, join[kGroups] = {};
   // GPX_SUBMIT_STATS=1: host wall seconds of gpx_batch_lml_grad_submit's phases (rebind flush,
   // routing, upload, launches, download enqueue) and of _complete's wait, printed at destroy
-  double sub_s[8] = {};
+  double sub_s[12] = {};  // (GPX_SUBMIT_STATS: 0-7 the submit phases, 8-10 predict: total, its I/O wait, shadow slots)
   long long sub_calls = 0, box_syncs = 0;
 };
 

@@ -727,7 +727,11 @@ class _SteppedDriver:
         else:
             e = engines[0]
             lock = threading.Lock()
-            self.groups = [(e, list(range(g, e.B, G)), lock, _new_stream(e.device) if G > 1 else None)
+            # (a stream of its own for one group too: on the caller's default stream a predict is
+            # synchronous — gpx_batch_predict_train returns early only on an explicit stream — and
+            # with deferred slow parts in the stream that wait is the slow part's whole duration)
+            own = G > 1 or os.environ.get("GPX_DRIVER_CALLER_STREAM", "0") != "1"
+            self.groups = [(e, list(range(g, e.B, G)), lock, _new_stream(e.device) if own else None)
                            for g in range(G)]
         if width is not None:  # at most `width` slots in total, dealt round-robin over groups
             keep = [[] for _ in self.groups]

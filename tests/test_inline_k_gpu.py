@@ -58,22 +58,26 @@ np.savez({path!r}, **out)
 """
 
 
-def _run(kin, path, wide=None):
+def _run(kin, path, wide=None, extra=None):
     env = dict(os.environ, GPX_B16_INLINE_K=str(kin))
-    env.pop("GPX_B16_INLINE_K_WIDE", None)
+    for k in ("GPX_B16_INLINE_K_WIDE", "GPX_DEFER_STREAM"):
+        env.pop(k, None)
     if wide is not None:
         env["GPX_B16_INLINE_K_WIDE"] = str(wide)
+    env.update(extra or {})
     code = CHILD.format(root=ROOT, path=path)
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     return np.load(path)
 
 
-@pytest.mark.parametrize("kin,wide", [(1, None), (2, None), (3, None), (3, 0)])
-def test_inline_k_bit_identical(tmp_path, kin, wide):
-    """(wide: GPX_B16_INLINE_K_WIDE, the setting of the deferred part's wide launch)"""
+@pytest.mark.parametrize("kin,wide,extra", [(1, None, None), (2, None, None), (3, None, None), (3, 0, None),
+                                            (3, None, {"GPX_DEFER_STREAM": "0"})])
+def test_inline_k_bit_identical(tmp_path, kin, wide, extra):
+    """(wide: GPX_B16_INLINE_K_WIDE, the setting of the deferred part's wide launch; extra: the
+    deferred part on the call's own stream instead of a stream of its own)"""
     ref = _run(0, str(tmp_path / "k0.npz"))
-    got = _run(kin, str(tmp_path / f"k{kin}.npz"), wide)
+    got = _run(kin, str(tmp_path / f"k{kin}.npz"), wide, extra)
     q = ref["q"]
     assert set(int(c) for c in q) >= {1, 2, 3, 4, 5}, q  # every band16 width present
     for key in ("lml-1", "grad-1", "info-1", "lml3", "grad3", "info3", "mean", "var"):
