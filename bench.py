@@ -760,7 +760,9 @@ def main():
         k = sweeps[key]
         ppl = (e16 - tm["band16_wide_evals"]) / max(k["launches"], 1.0)  # problems per launch
         k["traffic"], k["traffic_source"] = band_traffic(key, ppl) if ppl > 0 else (None, None)
-    sweeps["band16_wide_kernel"]["traffic"], sweeps["band16_wide_kernel"]["traffic_source"] = None, None
+    k = sweeps["band16_wide_kernel"]
+    ppl = tm["band16_wide_evals"] / max(k["launches"], 1.0)
+    k["traffic"], k["traffic_source"] = band_traffic("band16_wide_kernel", ppl) if ppl > 0 else (None, None)
     for key, fwd in (("band_fwd1_kernel", True), ("band_bwd1_kernel<1>", False)):
         k = sweeps[key]
         ppl = k["alg_flops_per_launch"] / band_problem_flops(n, 1, fwd)
@@ -778,7 +780,9 @@ def main():
         k = sweeps[kname]
         b16 = kname.startswith("band16")
         roofline = {
-            "kernel": (f"{kname}<Q> (16-row blocks, one wavefront walks a problem's 256 block steps; mean Q {q_mean:.2f})"
+            "kernel": ("band16_wide_kernel (the deferred Q = 4, 5 classes: one wavefront walks a problem's 256 block "
+                       "steps forward, then back)" if kname == "band16_wide_kernel" else
+                       f"{kname}<Q> (16-row blocks, one wavefront walks a problem's 256 block steps; mean Q {q_mean:.2f})"
                        if b16 else f"{kname} (p<=1 class: one workgroup walks a problem's 64 block steps)"),
             # the sweeps are per-wave dependency chains, bounded by latency and by
             # how many of the chip's wave slots hold a sweep, not by the MFMA or HBM peak: the

@@ -18,8 +18,8 @@ def is_contract(name: str) -> bool:
 
 def matcher(bench_kernel: str):
     """Trace-name predicate for the kernel a bench line's roofline names."""
-    for tag in ("band16_bwd_kernel", "band16_fwd_kernel", "band_bwd1_kernel", "band_fwd1_kernel", "band_bwd_kernel",
-                "band_fwd_kernel"):
+    for tag in ("band16_bwd_kernel", "band16_fwd_kernel", "band16_wide_kernel", "band_bwd1_kernel", "band_fwd1_kernel",
+                "band_bwd_kernel", "band_fwd_kernel"):
         if bench_kernel.startswith(tag):
             return lambda name, tag=tag: tag + "<" in name or tag + "(" in name
     return is_contract
