@@ -655,9 +655,9 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     return !(e && atoi(e) == 0);
   }();
   // which SE1 band16 sweeps compute their K tiles from X (bit 0: forward, bit 1: backward;
-  // GPX_B16_INLINE_K): a sweep that does not reads the band band16_build_kernel wrote, which
-  // is built whenever the forward sweep needs it (the backward alone computing its tiles still
-  // saves that sweep's K read). Same bits either way.
+  // GPX_B16_INLINE_K): a sweep that does not reads K's band — written by band16_build_kernel
+  // when the forward reads it too, by the forward itself when only the backward reads it (1:
+  // each K tile's exp once, the band through HBM once each way). Same bits every way.
   static const int kin = [] {
     const char* e = getenv("GPX_B16_INLINE_K");
     return e ? (atoi(e) & 3) : 3;  // default: both (round 4: +4-7 % on the C2 bench, K's band never in HBM)
@@ -687,8 +687,9 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     const Lane& l = lanes[i];
     hipStream_t ls = lane_stream(i);
     if (l.kind == 0) {
-      // SE1 classes compute their K tiles inside the sweeps (band16 KIN): no build launch
-      if (!(se1 && (kin & 1) && (kin & 2))) {
+      // SE1 classes compute their K tiles inside the sweeps (band16 KIN): no build launch (a
+      // forward computing them while the backward reads the band writes the band itself)
+      if (!(se1 && (kin & 1))) {
         BuildArgs bg = ba;
         bg.active = r.d_act + l.off;
         launch_band16_build(bg, g16_q[l.g], l.n, ls);
@@ -697,12 +698,13 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       BandFusedArgs f16 = fa;
       f16.kband = kband16;
       f16.active = r.d_act + l.off;
+      f16.kstore = se1 && (kin & 1) && !(kin & 2);
       launch_band16(f16, g16_q[l.g], max_terms, se1, kin, l.n, ls, ev16 ? ev16[l.g] : nullptr);
     } else if (l.kind == 3) {
       // the wide SE1 groups: their K bands (unless computed in the sweeps), then one launch
       int goff = l.off;
       for (int g = l.g; g < l.g_end; ++g) {
-        if (!((kin_wide & 1) && (kin_wide & 2))) {
+        if (!(kin_wide & 1)) {
           BuildArgs bg = ba;
           bg.active = r.d_act + goff;
           launch_band16_build(bg, g16_q[g], g16_n[g], ls);
@@ -712,6 +714,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       BandFusedArgs f16 = fa;
       f16.kband = kband16;
       f16.active = r.d_act + l.off;
+      f16.kstore = (kin_wide & 1) && !(kin_wide & 2);
       if (ev16)
         for (int g = l.g + 1; g < l.g_end; ++g) (void)hipEventRecord(ev16[g][0], ls);
       launch_band16_wide(f16, kin_wide, l.n, ls, ev16 ? ev16[l.g] : nullptr);

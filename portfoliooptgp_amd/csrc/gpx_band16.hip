@@ -40,6 +40,13 @@
 
 namespace gpx {
 
+// (external linkage: the compiler may not fold the loads into literals, see ExpC below)
+__device__ unsigned long long g_exp_c[16] = {
+    0x3ff71547652b82feull, 0xbfe62e42fefa39efull, 0xbc7abc9e3b39803full, 0x3e5ade156a5dcb37ull,
+    0x3e928af3fca7ab0cull, 0x3ec71dee623fde64ull, 0x3efa01997c89e6b0ull, 0x3f2a01a014761f6eull,
+    0x3f56c16c1852b7b0ull, 0x3f81111111122322ull, 0x3fa55555555502a1ull, 0x3fc5555555555511ull,
+    0x3fe000000000000bull, 0x4090000000000000ull /* 1024 */, 0xc090cc0000000000ull /* -1075 */, 0ull};
+
 // Phase timing (diagnostic build only, -DGPX_BAND_PHASES: libgpx_phases.so, tools/band16_phases.py):
 // each wave adds the shader-clock cycles of its steps' phases into g_b16_phase[kernel][phase]
 // ([kernel][15] counts waves).
@@ -267,15 +274,59 @@ __device__ __forceinline__ t4 ktile_t(const double* __restrict__ K, long long ld
 
 constexpr __host__ __device__ int wid(int i, int j) { return i * (i + 1) / 2 + j; }  // lower (i, j), j <= i
 
+// exp(x) as the device library computes it (the sequence of the gfx950 __ocml_exp_f64 code: a
+// rndne(x·log2 e) reduction in two fma steps, a degree-12 polynomial, ldexp, the overflow and
+// underflow selects — the same operations on the same constants, so the same bits), with the
+// constants read from a device array: uniform loads, so they sit in scalar registers and every
+// polynomial step is one v_fma_f64 with a scalar operand. The library's own exp is compiled
+// with literal constants and v_fmac, whose accumulator must be a fresh vector copy of each
+// constant: 14 v_mov_b64 per exp inside the sweeps' loops (tests/test_inline_k_gpu.py checks the
+// bits against the build kernel's exp).
+struct ExpC {
+  double c[15];
+  __device__ __forceinline__ void load() {
+#pragma unroll
+    for (int i = 0; i < 15; ++i) c[i] = __longlong_as_double((long long)g_exp_c[i]);
+  }
+  __device__ __forceinline__ double exp(double x) const {
+    const double k = __builtin_rint(x * c[0]);
+    double r = __builtin_fma(k, c[1], x);
+    r = __builtin_fma(k, c[2], r);
+    double p = __builtin_fma(r, c[3], c[4]);
+#pragma unroll
+    for (int i = 5; i <= 12; ++i) p = __builtin_fma(r, p, c[i]);
+    p = __builtin_fma(r, p, 1.0);
+    p = __builtin_fma(r, p, 1.0);
+    double e = __builtin_amdgcn_ldexp(p, (int)k);
+    e = !(x > c[13]) ? e : __builtin_inf();  // (NaN passes through both selects, as in the library)
+    return !(x < c[14]) ? e : 0.0;
+  }
+};
+// the library's own exp (for the sweeps whose registers leave no room for ExpC)
+struct ExpLib {
+  __device__ __forceinline__ void load() {}
+  __device__ __forceinline__ double exp(double x) const { return ::exp(x); }
+};
+
 // K_ij of the reference's kernel (SE1: one SquaredExponential term on one input column) from the
 // scaled inputs a = x/ℓ, computed where a sweep needs it (KIN) instead of read from a K band that
 // band16_build_kernel wrote: σ²·exp(−½ r²) with GPflow's r² (sqdist1), σn² added on the diagonal,
 // the identity in the padding — the build kernel's operations, so the same bits (sqdist1 is
 // symmetric in its arguments bit for bit, so no tile needs mirroring)
-__device__ __forceinline__ double k_se1(double ai, double aj, bool ok, bool diag, double var, double noise) {
+template <class EXP>
+__device__ __forceinline__ double k_se1(double ai, double aj, bool ok, bool diag, double var, double noise,
+                                       const EXP& E) {
   if (!ok) return diag ? 1.0 : 0.0;
-  const double v = stationary_value<GPX_SE>(sqdist1(ai, aj), var);
+  const double v = var * E.exp(-0.5 * sqdist1(ai, aj));  // (stationary_value<GPX_SE>'s operations)
   return diag ? v + noise : v;
+}
+// a tile in fragment-of-transpose layout (t[r] = A[bi·16 + l15][bj·16 + 4r + l4], as ktile_t reads
+// it) into the row-major band where band16_build_kernel would have written it
+__device__ __forceinline__ void ktile_store(double* __restrict__ K, long long ld, int bi, int bj, const t4& t, int l15,
+                                            int l4) {
+  double* p = K + (long long)(bi * 16 + l15) * ld + bj * 16 + l4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[4 * r] = t[r];
 }
 // index of element il of a 16-row block in the "row-quad" order (il & 3)·4 + (il >> 2): lane
 // (l15, l4) finds the values of rows 4r + l4, r = 0..3, at 4·l4 .. 4·l4 + 3 (two ds_read_b128)
@@ -304,7 +355,9 @@ template <int Q, bool KIN>
 struct Fwd16 {  // the forward sweep's LDS, in doubles: scratch | the entering row (glds) | x/ℓ ring (KIN)
   static constexpr int kNew = 16 * kSC, kXa = kNew + (KIN ? 1 : Q + 1) * 256, size = kXa + (KIN ? Q + 1 : 1) * 16;
 };
-template <int Q, bool KIN>
+// XC: K's tiles (KIN) through ExpC (scalar-register constants) when Q <= 3; the fused kernels,
+// whose backward sweep shares the registers, use the library's exp
+template <int Q, bool KIN, bool XC = true>
 __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __restrict__ lds) {
   double* sc = lds;
   double(*snew)[256] = reinterpret_cast<double(*)[256]>(lds + Fwd16<Q, KIN>::kNew);  // the entering row, staged by glds
@@ -313,10 +366,11 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
   const int b = a.active[blockIdx.x];
   const int Np = a.Np, nb = Np >> 4;
   const long long ld = a.ld;
-  const double* K = a.K + (long long)b * a.sMat;
+  double* K = a.K + (long long)b * a.sMat;  // (KIN with kstore: written, otherwise read)
   double* L = a.L + (long long)b * a.sMat;
   double* z = a.z + (long long)b * a.sVec;
   double* ldiag = a.ldiag + (long long)b * a.sVec;
+  const bool kst = KIN && a.kstore;
   const double* y = a.Y + (long long)b * a.sY;
   const int n = a.nvalid[b];
   const int lane = threadIdx.x, l15 = lane & 15, l4 = lane >> 4;
@@ -325,7 +379,9 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
   const double* X = a.X + (long long)b * a.sX;
   int xd0 = 0;
   double kell = 1.0, kvar = 1.0, knoise = 0.0;
+  std::conditional_t<(XC && Q <= 3), ExpC, ExpLib> E;  // (Q >= 4: no scalar registers to spare)
   if constexpr (KIN) {
+    E.load();
     const gpx_term& tm = a.specs[b].terms[0];
     const double* th = a.theta + (long long)b * GPX_THETA_STRIDE;
     xd0 = tm.dim_start;
@@ -358,8 +414,9 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
           for (int r = 0; r < 4; ++r) {
             const int gj = j * 16 + 4 * r + l4;
             const bool zero = (gi >> 6) - (gj >> 6) >= a.kband;
-            t[r] = zero ? 0.0 : k_se1(ar, ac[r], gi < n && gj < n, gi == gj, kvar, knoise);
+            t[r] = zero ? 0.0 : k_se1(ar, ac[r], gi < n && gj < n, gi == gj, kvar, knoise, E);
           }
+          if (kst) ktile_store(K, ld, i, j, t, l15, l4);
         }
         T[wid(i, j)] = t;
       }
@@ -478,8 +535,9 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int gj = c * 16 + 4 * r + l4;
-            t[r] = k_se1(ar, ac[r], gi < n && gj < n, gi == gj, kvar, knoise);
+            t[r] = k_se1(ar, ac[r], gi < n && gj < n, gi == gj, kvar, knoise, E);
           }
+          if (kst) ktile_store(K, ld, bn, c, t, l15, l4);
         }
         T[wid(Q, j)] = t;
       }
@@ -771,6 +829,8 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
             // rows past n are exact zeros of K for any finite r², as the built band holds)
             kraw = 0.0;
             if (!zero) {
+              // (the library's exp here: the backward sweep has no scalar registers to spare for
+              // ExpC's constants — with them it spills)
               const double kv = stationary_value<GPX_SE>(r2, fvar);
               kraw = dg ? kv + noise : (i > 0 && gi >= n ? 0.0 : kv);
             }
@@ -964,7 +1024,7 @@ template <int Q, bool KIN_F, bool KIN_B>
 __global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX) ? 2 : 1) void band16_fused_kernel(BandFusedArgs a) {
   constexpr int nf = Fwd16<Q, KIN_F>::size, nbk = Bwd16<Q, 1, true, KIN_B>::size;
   __shared__ __attribute__((aligned(16))) double lds[nf > nbk ? nf : nbk];
-  fwd_sweep<Q, KIN_F>(a, lds);
+  fwd_sweep<Q, KIN_F, false>(a, lds);
   // the factor tiles, z and L_ii this wavefront stored are read back by it: its stores are
   // complete and visible to its own loads
   vm_drain();
@@ -1091,7 +1151,7 @@ void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s)
 // latency instead of one per class. SE1 problems only.
 template <int Q, bool KF, bool KB>
 __device__ __forceinline__ void fused_sweeps(const BandFusedArgs& a, double* __restrict__ lds) {
-  fwd_sweep<Q, KF>(a, lds);
+  fwd_sweep<Q, KF, false>(a, lds);
   vm_drain();
   __threadfence();
   wsync();

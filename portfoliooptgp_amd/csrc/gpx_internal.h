@@ -162,6 +162,8 @@ struct BandFusedArgs {
   int ld;                                        // leading dimension of K/L/W (Np, or band storage's)
   int kband;                                     // band16: K's band was built with this many 64-block
                                                  // diagonals; entries beyond read as 0 (exact)
+  int kstore;                                    // band16 SE1, forward computing K's tiles (KIN): it
+                                                 // also writes them into K's band for the backward
   // wave residency trace (gpx_batch_wave_trace; nullptr: off): each band16 wavefront appends
   // {start, end, kind} in the device's constant 100 MHz clock (s_memrealtime), kind = Q for the
   // forward sweep, 16 + Q for the backward
