@@ -313,11 +313,12 @@ struct ExpLib {
 // band16_build_kernel wrote: σ²·exp(−½ r²) with GPflow's r² (sqdist1), σn² added on the diagonal,
 // the identity in the padding — the build kernel's operations, so the same bits (sqdist1 is
 // symmetric in its arguments bit for bit, so no tile needs mirroring)
+// (the row's −2a_i and a_i² formed once per row: sqdist1_b, the same bits as sqdist1(a_i, a_j))
 template <class EXP>
-__device__ __forceinline__ double k_se1(double ai, double aj, bool ok, bool diag, double var, double noise,
-                                       const EXP& E) {
+__device__ __forceinline__ double k_se1(double m2ai, double ai2, double aj, bool ok, bool diag, double var,
+                                       double noise, const EXP& E) {
   if (!ok) return diag ? 1.0 : 0.0;
-  const double v = var * E.exp(-0.5 * sqdist1(ai, aj));  // (stationary_value<GPX_SE>'s operations)
+  const double v = var * E.exp(-0.5 * sqdist1_b(aj, m2ai, ai2));  // (stationary_value<GPX_SE>'s operations)
   return diag ? v + noise : v;
 }
 // a tile in fragment-of-transpose layout (t[r] = A[bi·16 + l15][bj·16 + 4r + l4], as ktile_t reads
@@ -414,7 +415,7 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
           for (int r = 0; r < 4; ++r) {
             const int gj = j * 16 + 4 * r + l4;
             const bool zero = (gi >> 6) - (gj >> 6) >= a.kband;
-            t[r] = zero ? 0.0 : k_se1(ar, ac[r], gi < n && gj < n, gi == gj, kvar, knoise, E);
+            t[r] = zero ? 0.0 : k_se1(-2.0 * ar, ar * ar, ac[r], gi < n && gj < n, gi == gj, kvar, knoise, E);
           }
           if (kst) ktile_store(K, ld, i, j, t, l15, l4);
         }
@@ -521,7 +522,7 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
     if constexpr (KIN) {
       // block bn's inputs join the ring (in the slot of block k, whose last reads were at the
       // previous step's end), then the new row's tiles (bn, k+1+j) from x/ℓ
-      const double ar = xn / kell;
+      const double ar = xn / kell, m2ar = -2.0 * ar, ar2 = ar * ar;
       if (newrow && l4 == 0) sxa[bn % (Q + 1)][rq(l15)] = ar;
       wsync();
       const int gi = bn * 16 + l15;
@@ -535,7 +536,7 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int gj = c * 16 + 4 * r + l4;
-            t[r] = k_se1(ar, ac[r], gi < n && gj < n, gi == gj, kvar, knoise, E);
+            t[r] = k_se1(m2ar, ar2, ac[r], gi < n && gj < n, gi == gj, kvar, knoise, E);
           }
           if (kst) ktile_store(K, ld, bn, c, t, l15, l4);
         }
