@@ -1519,7 +1519,19 @@ static int slow_setup(gpx_batch* bt) {
     HIPX(ctx, hipMalloc(&bt->d_slow_info_c, sizeof(int) * B));
   }
   if (!defer_own_stream() || bt->slow_s) return GPX_OK;
-  HIPX(ctx, hipStreamCreateWithFlags(&bt->slow_s, hipStreamNonBlocking));
+  // GPX_SLOW_PRIORITY: the slow stream at the device's lowest (-1) or highest (1) stream priority
+  // (streams of another priority take hardware queues of their own); 0 / unset: the default
+  static const int prio = [] {
+    const char* e = getenv("GPX_SLOW_PRIORITY");
+    return e ? atoi(e) : 0;
+  }();
+  if (prio != 0) {
+    int least = 0, greatest = 0;
+    HIPX(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPX(ctx, hipStreamCreateWithPriority(&bt->slow_s, hipStreamNonBlocking, prio > 0 ? greatest : least));
+  } else {
+    HIPX(ctx, hipStreamCreateWithFlags(&bt->slow_s, hipStreamNonBlocking));
+  }
   HIPX(ctx, hipEventCreateWithFlags(&bt->slow_in, hipEventDisableTiming));
   HIPX(ctx, hipEventCreateWithFlags(&bt->slow_up, hipEventDisableTiming));
   HIPX(ctx, hipMalloc(&bt->d_slow_act, sizeof(int) * B));
