@@ -40,12 +40,6 @@
 
 namespace gpx {
 
-// (external linkage: the compiler may not fold the loads into literals, see ExpC below)
-__device__ unsigned long long g_exp_c[16] = {
-    0x3ff71547652b82feull, 0xbfe62e42fefa39efull, 0xbc7abc9e3b39803full, 0x3e5ade156a5dcb37ull,
-    0x3e928af3fca7ab0cull, 0x3ec71dee623fde64ull, 0x3efa01997c89e6b0ull, 0x3f2a01a014761f6eull,
-    0x3f56c16c1852b7b0ull, 0x3f81111111122322ull, 0x3fa55555555502a1ull, 0x3fc5555555555511ull,
-    0x3fe000000000000bull, 0x4090000000000000ull /* 1024 */, 0xc090cc0000000000ull /* -1075 */, 0ull};
 
 // Phase timing (diagnostic build only, -DGPX_BAND_PHASES: libgpx_phases.so, tools/band16_phases.py):
 // each wave adds the shader-clock cycles of its steps' phases into g_b16_phase[kernel][phase]
@@ -274,38 +268,47 @@ __device__ __forceinline__ t4 ktile_t(const double* __restrict__ K, long long ld
 
 constexpr __host__ __device__ int wid(int i, int j) { return i * (i + 1) / 2 + j; }  // lower (i, j), j <= i
 
-// exp(x) as the device library computes it (the sequence of the gfx950 __ocml_exp_f64 code: a
-// rndne(x·log2 e) reduction in two fma steps, a degree-12 polynomial, ldexp, the overflow and
-// underflow selects — the same operations on the same constants, so the same bits), with the
-// constants read from a device array: uniform loads, so they sit in scalar registers and every
-// polynomial step is one v_fma_f64 with a scalar operand. The library's own exp is compiled
-// with literal constants and v_fmac, whose accumulator must be a fresh vector copy of each
-// constant: 14 v_mov_b64 per exp inside the sweeps' loops (tests/test_inline_k_gpu.py checks the
-// bits against the build kernel's exp).
-struct ExpC {
-  double c[15];
-  __device__ __forceinline__ void load() {
+// Four exps in lockstep, as the device library computes exp (the sequence of the gfx950
+// __ocml_exp_f64 code: a rndne(x·log2 e) reduction in two fma steps, a degree-12 polynomial,
+// ldexp, the overflow and underflow selects — the same operations on the same constants, so the
+// same bits; tests/test_inline_k_gpu.py checks them against the build kernel's exp). The library's
+// exp alone is compiled with literal constants and v_fmac, whose accumulator must be a fresh
+// vector copy of each constant: 14 v_mov_b64 per exp inside the sweeps' loops (≈ 230 per step).
+// Four at a time, each constant is put in a register once for the four.
+__device__ __forceinline__ void exp4(const double (&x)[4], double (&e)[4]) {
+  constexpr double c[13] = {0x1.71547652b82fep+0, -0x1.62e42fefa39efp-1, -0x1.abc9e3b39803fp-56,
+                            0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22, 0x1.71dee623fde64p-19,
+                            0x1.a01997c89e6b0p-16, 0x1.a01a014761f6ep-13, 0x1.6c16c1852b7b0p-10,
+                            0x1.1111111122322p-7, 0x1.55555555502a1p-5, 0x1.5555555555511p-3,
+                            0x1.000000000000bp-1};
+  double k[4], r[4], p[4];
 #pragma unroll
-    for (int i = 0; i < 15; ++i) c[i] = __longlong_as_double((long long)g_exp_c[i]);
+  for (int q = 0; q < 4; ++q) {
+    k[q] = __builtin_rint(x[q] * c[0]);
+    r[q] = __builtin_fma(k[q], c[1], x[q]);
   }
-  __device__ __forceinline__ double exp(double x) const {
-    const double k = __builtin_rint(x * c[0]);
-    double r = __builtin_fma(k, c[1], x);
-    r = __builtin_fma(k, c[2], r);
-    double p = __builtin_fma(r, c[3], c[4]);
 #pragma unroll
-    for (int i = 5; i <= 12; ++i) p = __builtin_fma(r, p, c[i]);
-    p = __builtin_fma(r, p, 1.0);
-    p = __builtin_fma(r, p, 1.0);
-    double e = __builtin_amdgcn_ldexp(p, (int)k);
-    e = !(x > c[13]) ? e : __builtin_inf();  // (NaN passes through both selects, as in the library)
-    return !(x < c[14]) ? e : 0.0;
+  for (int q = 0; q < 4; ++q) r[q] = __builtin_fma(k[q], c[2], r[q]);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p[q] = __builtin_fma(r[q], c[3], c[4]);
+#pragma unroll
+  for (int i = 5; i <= 12; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p[q] = __builtin_fma(r[q], p[q], c[i]);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    p[q] = __builtin_fma(r[q], p[q], 1.0);
+    p[q] = __builtin_fma(r[q], p[q], 1.0);
+    double v = __builtin_amdgcn_ldexp(p[q], (int)k[q]);
+    v = !(x[q] > 1024.0) ? v : __builtin_inf();
+    e[q] = !(x[q] < -1075.0) ? v : 0.0;
   }
-};
-// the library's own exp (for the sweeps whose registers leave no room for ExpC)
+}
+// the K tiles' exp: one at a time (the library's), or a tile's four together (exp4)
 struct ExpLib {
   __device__ __forceinline__ void load() {}
   __device__ __forceinline__ double exp(double x) const { return ::exp(x); }
+  __device__ __forceinline__ void exp4(const double (&x)[4], double (&e)[4]) const { gpx::exp4(x, e); }
 };
 
 // K_ij of the reference's kernel (SE1: one SquaredExponential term on one input column) from the
@@ -356,9 +359,7 @@ template <int Q, bool KIN>
 struct Fwd16 {  // the forward sweep's LDS, in doubles: scratch | the entering row (glds) | x/ℓ ring (KIN)
   static constexpr int kNew = 16 * kSC, kXa = kNew + (KIN ? 1 : Q + 1) * 256, size = kXa + (KIN ? Q + 1 : 1) * 16;
 };
-// XC: K's tiles (KIN) through ExpC (scalar-register constants) when Q <= 3; the fused kernels,
-// whose backward sweep shares the registers, use the library's exp
-template <int Q, bool KIN, bool XC = true>
+template <int Q, bool KIN>
 __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __restrict__ lds) {
   double* sc = lds;
   double(*snew)[256] = reinterpret_cast<double(*)[256]>(lds + Fwd16<Q, KIN>::kNew);  // the entering row, staged by glds
@@ -380,7 +381,7 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
   const double* X = a.X + (long long)b * a.sX;
   int xd0 = 0;
   double kell = 1.0, kvar = 1.0, knoise = 0.0;
-  std::conditional_t<(XC && Q <= 3), ExpC, ExpLib> E;  // (Q >= 4: no scalar registers to spare)
+  ExpLib E;
   if constexpr (KIN) {
     E.load();
     const gpx_term& tm = a.specs[b].terms[0];
@@ -533,10 +534,16 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
         // (16-row blocks sit inside one 64-block: the 64-block offset is uniform over the tile)
         if (newrow && (bn >> 2) - (c >> 2) < a.kband) {
           const t4 ac = *reinterpret_cast<const t4*>(&sxa[c % (Q + 1)][4 * l4]);
+          // the tile's four exps together (k_se1's operations, element by element)
+          double xe[4], ev[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xe[r] = -0.5 * sqdist1_b(ac[r], m2ar, ar2);
+          E.exp4(xe, ev);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int gj = c * 16 + 4 * r + l4;
-            t[r] = k_se1(m2ar, ar2, ac[r], gi < n && gj < n, gi == gj, kvar, knoise, E);
+            const double v = kvar * ev[r];
+            t[r] = !(gi < n && gj < n) ? (gi == gj ? 1.0 : 0.0) : (gi == gj ? v + knoise : v);
           }
           if (kst) ktile_store(K, ld, bn, c, t, l15, l4);
         }
@@ -817,12 +824,23 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
         const t4 a4 = *reinterpret_cast<const t4*>(&salT[si][4 * l4]);  // α of rows 4r + l4
         const t4 x4 = *reinterpret_cast<const t4*>(&sxT[si][4 * l4]);   // x of rows 4r + l4
         const bool zero = ((k + i) >> 2) - (k >> 2) >= a.kband;  // (uniform, see the forward sweep)
+        double r2v[4], kexp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) r2v[r] = sqdist1_b(x4[r], m2xj, xj2);
+        if constexpr (KIN) {
+          if (!zero) {
+            double xe[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xe[r] = -0.5 * r2v[r];
+            exp4(xe, kexp);
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int il = 4 * r + l4, gi = (k + i) * 16 + il;
           const double zij = Zt[r];
           const double ai = a4[r];
-          const double r2 = sqdist1_b(x4[r], m2xj, xj2);
+          const double r2 = r2v[r];
           const bool dg = i == 0 && il == l15;
           double kraw;
           if constexpr (KIN) {
@@ -830,9 +848,7 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
             // rows past n are exact zeros of K for any finite r², as the built band holds)
             kraw = 0.0;
             if (!zero) {
-              // (the library's exp here: the backward sweep has no scalar registers to spare for
-              // ExpC's constants — with them it spills)
-              const double kv = stationary_value<GPX_SE>(r2, fvar);
+              const double kv = fvar * kexp[r];  // (stationary_value<GPX_SE>'s operations)
               kraw = dg ? kv + noise : (i > 0 && gi >= n ? 0.0 : kv);
             }
           } else {
@@ -1025,7 +1041,7 @@ template <int Q, bool KIN_F, bool KIN_B>
 __global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX) ? 2 : 1) void band16_fused_kernel(BandFusedArgs a) {
   constexpr int nf = Fwd16<Q, KIN_F>::size, nbk = Bwd16<Q, 1, true, KIN_B>::size;
   __shared__ __attribute__((aligned(16))) double lds[nf > nbk ? nf : nbk];
-  fwd_sweep<Q, KIN_F, false>(a, lds);
+  fwd_sweep<Q, KIN_F>(a, lds);
   // the factor tiles, z and L_ii this wavefront stored are read back by it: its stores are
   // complete and visible to its own loads
   vm_drain();
@@ -1152,7 +1168,7 @@ void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s)
 // latency instead of one per class. SE1 problems only.
 template <int Q, bool KF, bool KB>
 __device__ __forceinline__ void fused_sweeps(const BandFusedArgs& a, double* __restrict__ lds) {
-  fwd_sweep<Q, KF, false>(a, lds);
+  fwd_sweep<Q, KF>(a, lds);
   vm_drain();
   __threadfence();
   wsync();
