@@ -75,10 +75,12 @@ def test_two_wave_sweeps_fit_256_registers(kernels, q):
 
 
 def test_bench_sweeps_do_not_spill(kernels):
-    """Every sweep a C2 (SE1) evaluation can launch: band16 fwd/bwd/fused for Q = 1..5 with the
-    K band read (KIN = 0) — the bench's default — the wide (Q = 4/5) kernel, and the build."""
-    pats = [r"band16_fwd_kernelILi[1-5]ELb0E", r"band16_bwd_kernelILi[1-5]ELi1ELb1ELb0E",
-            r"band16_fused_kernelILi[1-5]ELb0ELb0E", r"band16_wide_kernel", r"band16_build_kernel"]
+    """Every sweep a C2 (SE1) evaluation can launch: band16 fwd/bwd for Q = 1..5 with K's tiles
+    computed in the sweeps (the default) or read from the K band, the fused sweeps, the wide
+    (Q = 4/5, deferred) kernel, and the build."""
+    pats = [r"band16_fwd_kernelILi[1-5]ELb[01]E", r"band16_bwd_kernelILi[1-5]ELi1ELb1ELb[01]E",
+            r"band16_fused_kernelILi[1-5]ELb0ELb0E", r"band16_fused_kernelILi[1-5]ELb1ELb1E",
+            r"band16_wide_kernel", r"band16_build_kernel"]
     for p in pats:
         for name, (v, a, scratch) in _find(kernels, p).items():
             assert scratch == 0, (name, v, a, scratch)
