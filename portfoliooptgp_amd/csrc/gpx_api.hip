@@ -1610,7 +1610,13 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
     return e && atoi(e) != 0;
   }();
   r.one_stream = !lanes;
-  r.wide_from = 1;  // the part's band16 classes as one launch (band16_wide_kernel)
+  // the part's band16 classes as one launch (band16_wide_kernel), or (GPX_DEFER_WIDE=0) one
+  // forward and one backward launch per class, each at its own occupancy
+  static const bool wide = [] {
+    const char* e = getenv("GPX_DEFER_WIDE");
+    return !(e && atoi(e) == 0);
+  }();
+  r.wide_from = wide ? 1 : 0;
   band_fused_eval(r, n16, n_g16, q, cnt, se1, kband16, n1, max_terms, (ctx->profiling && fused64) ? rec->fq : nullptr,
                   ctx->profiling ? rec->fq16 : nullptr);
   launch_slow_gather(r.d_act, n, bt->results, kResStride, bt->d_slow_res, own ? bt->d_slow_info : bt->d_info,
