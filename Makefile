@@ -9,14 +9,14 @@ CSMOKE := tests/c/gpx_c_smoke
 
 all: $(LIB) $(CSMOKE)
 
-$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h $(CSRC)/gpx_leaf.h include/gpx.h
+$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h $(CSRC)/gpx_leaf.h $(CSRC)/gpx_b16core.h include/gpx.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 # host helpers of the L-BFGS-B driver: plain gcc, libm calls as Python's math module makes them
 $(CSRC)/gpx_host_math.o: $(CSRC)/gpx_host_math.c include/gpx.h
 	gcc -O2 -fno-builtin -fno-fast-math -fPIC -std=c11 -Wall -c $< -o $@
 
-$(LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band.o $(CSRC)/gpx_band16.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
+$(LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band.o $(CSRC)/gpx_band16.o $(CSRC)/gpx_bcr.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-soname,libgpx.so $^ -o $@
 
 # plain-C consumer of the C ABI (gcc, HIP runtime API only), run by tests/test_c_abi_gpu.py
@@ -32,7 +32,7 @@ $(CSRC)/gpx_band_phases.o: $(CSRC)/gpx_band.hip $(CSRC)/gpx_internal.h $(CSRC)/g
 	$(HIPCC) $(HIPFLAGS) -DGPX_BAND_PHASES -c $< -o $@
 $(CSRC)/gpx_band16_phases.o: $(CSRC)/gpx_band16.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_leaf.h $(CSRC)/gpx_kfun.h
 	$(HIPCC) $(HIPFLAGS) -DGPX_BAND_PHASES -c $< -o $@
-$(PHASES_LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band_phases.o $(CSRC)/gpx_band16_phases.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
+$(PHASES_LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band_phases.o $(CSRC)/gpx_band16_phases.o $(CSRC)/gpx_bcr.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-soname,libgpx_phases.so $^ -o $@
 phases: $(PHASES_LIB)
 
@@ -48,7 +48,7 @@ HSRC := $(wildcard $(CSRC)/*.hip)
 HOBJ := $(patsubst $(CSRC)/%.hip,build/asan/%.o,$(HSRC))
 HSAN := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
   -Xarch_host -fno-omit-frame-pointer -g -O1
-build/asan/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h $(CSRC)/gpx_leaf.h include/gpx.h
+build/asan/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h $(CSRC)/gpx_leaf.h $(CSRC)/gpx_b16core.h include/gpx.h
 	@mkdir -p build/asan
 	$(HIPCC) --offload-arch=$(ARCH) -std=c++17 -fPIC $(HSAN) -c $< -o $@
 build/asan/gpx_host_math.o: $(CSRC)/gpx_host_math.c include/gpx.h

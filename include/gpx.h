@@ -305,6 +305,9 @@ typedef struct {
    * sweeps per wavefront): their durations, count, MFMA flops and problems — kept out of the
    * band16 forward/backward launch figures above (which count the per-class launches only) */
   double band16_wide_ms_total, band16_wide_launches, band16_wide_flops, band16_wide_evals;
+  /* block cyclic reduction (calls with at most GPX_BCR_MAX band16 problems): the device time of
+   * the reduction chains (forward and backward levels, contraction), chains, problem-evaluations */
+  double bcr_ms_total, bcr_calls, bcr_evals;
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);

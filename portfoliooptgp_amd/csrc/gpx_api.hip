@@ -580,6 +580,13 @@ double band16_flops(int Np, int Q, bool fwd) {
   return f;
 }
 
+// the most band16 problems a call may hold for them to take the block-cyclic-reduction path
+// (gpx_bcr.hip) instead of the one-wavefront sweeps (GPX_BCR_MAX; 0 turns it off)
+static int bcr_max_problems() {
+  const char* e = getenv("GPX_BCR_MAX");  // (read per call: a process can compare the paths)
+  return e ? atoi(e) : 32;
+}
+
 // stream-order markers in the wave trace (diagnostic; no-op unless gpx_batch_wave_trace is on):
 // 38 submit reached the device, 39 rebind gather done, 40 band16 work starts, 43 a lane's K band
 // built, 41 the lanes joined, 42 reduce done, 44 the results' download done
@@ -625,7 +632,12 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   int nl = 0;
   {
     int off = 0;
-    for (int g = 0; g < n_g16; ++g) {
+    // (r.bcr_q: the band16 problems as ONE block-cyclic-reduction chain, gpx_bcr.hip)
+    if (r.bcr_q > 0 && n16 > 0) {
+      lanes[nl++] = Lane{4, 0, n16, 0, n_g16};
+      off = n16;
+    }
+    for (int g = 0; g < n_g16 && r.bcr_q == 0; ++g) {
       // (r.wide_from: the SE1 groups of width 4 and 5 as one lane, one band16_wide_kernel launch)
       if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= 5 && nl > 0 &&
           lanes[nl - 1].kind == 3) {
@@ -721,6 +733,17 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       if (ev16)
         for (int g = l.g + 1; g < l.g_end; ++g)
           for (int e = 1; e < 4; ++e) (void)hipEventRecord(ev16[g][e], ls);
+    } else if (l.kind == 4) {
+      BcrArgs ca{};
+      ca.active = r.d_act + l.off; ca.specs = bt->d_specs; ca.theta = fa.theta; ca.nvalid = bt->d_n;
+      ca.X = bt->X; ca.sX = (long long)bt->Nmax * bt->D; ca.D = bt->D; ca.Y = bt->Y; ca.sY = bt->Nmax;
+      ca.ws = bt->bcr_ws; ca.sWs = bcr_ws_doubles(r.bcr_q, bt->Nmax); ca.info = fa.info;
+      ca.z = bt->z; ca.ldiag = bt->ldiag; ca.alpha = bt->alpha; ca.sVec = Np; ca.Np = Np;
+      ca.Kd = bt->K; ca.sMat = st; ca.ld = mat_ld(bt);
+      ca.partial = bt->partial; ca.sPartial = bt->partial_stride; ca.results = bt->results;
+      if (bt->ctx->profiling && bt->bcr_ev[0]) (void)hipEventRecord(bt->bcr_ev[0], ls);
+      launch_bcr(ca, r.bcr_q, max_terms, l.n, bt->Nmax, ls);
+      if (bt->ctx->profiling && bt->bcr_ev[1]) (void)hipEventRecord(bt->bcr_ev[1], ls);
     } else if (l.kind == 1) {
       BuildArgs b1 = ba;
       b1.active = r.d_act + l.off;
@@ -1214,8 +1237,10 @@ int gpx_batch_destroy(gpx_batch* bt) {
   for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
                   (void*)bt->ldiag, (void*)bt->partial, (void*)bt->d_io, (void*)bt->d_n,
                   (void*)bt->d_specs, (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw,
-                  (void*)bt->bres})
+                  (void*)bt->bres, (void*)bt->bcr_ws})
     if (p) (void)hipFree(p);
+  for (hipEvent_t e : bt->bcr_ev)
+    if (e) (void)hipEventDestroy(e);
   if (bt->h_io) (void)hipHostFree(bt->h_io);
   if (bt->h_io_pred) (void)hipHostFree(bt->h_io_pred);
   if (bt->h_stage) (void)hipHostFree(bt->h_stage);
@@ -1794,6 +1819,11 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   const int* g16_q = rt.g16_q;
   const int* g16_n = rt.g16_n;
   const bool b16_p2 = rt.b16_p2;
+  // a call with few band16 problems takes them by block cyclic reduction (gpx_bcr.hip): the
+  // one-wavefront sweeps' N/16-step chain would be the whole call's latency
+  int bcr_q = 0;
+  if (n16 > 0 && n16 <= bcr_max_problems())
+    for (int g = 0; g < n_g16; ++g) bcr_q = std::max(bcr_q, g16_q[g]);
   // the problems launched by this call (band storage: without the shadowed ones)
   n_active = n_dense + n_band + n_fused;
   // band storage: a few fallback problems go out at once on the fallback stream (more than the
@@ -1827,6 +1857,12 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   if (n_band > 0) {
     const int e = ensure(ctx, bt->bres, bt->bres_cap, (size_t)bt->B * bt->Np);
     if (e != GPX_OK) return drop_shadow(e);
+  }
+  if (bcr_q > 0) {
+    const int e = ensure(ctx, bt->bcr_ws, bt->bcr_ws_cap, (size_t)n16 * (size_t)bcr_ws_doubles(bcr_q, bt->Nmax));
+    if (e != GPX_OK) return drop_shadow(e);
+    if (ctx->profiling && !bt->bcr_ev[0])
+      for (auto& e2 : bt->bcr_ev) HIPX(ctx, hipEventCreate(&e2));
   }
   sc.lap(1);
   int rc = upload_common(bt, n_active, order.data(), theta, s);
@@ -1943,7 +1979,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   int n_slow = 0, n_g16_run = n_g16, n16_run = n16, n_fused1_run = n_fused1;
   struct SlowArgs { int off, n_g16, g0, n16, n1; bool se1; int max_terms; };
   SlowArgs slow_args{-1, 0, 0, 0, 0, true, 1};
-  if (bt->defer_q >= 0 && n_fused > 0) {
+  if (bt->defer_q >= 0 && n_fused > 0 && bcr_q == 0) {
     int k = 0, nb16 = 0;
     while (k < n_g16 && g16_q[k] <= bt->defer_q) nb16 += g16_n[k++];
     if (n_fused > nb16 && n_dense + n_band + nb16 > 0) {  // (a call of slow problems only just runs)
@@ -1980,8 +2016,9 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (ctx->profiling && old_fused)
       for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&fqe[e]));
     pe->n_band16 = n16;
-    pe->n_g16 = n_g16;
-    for (int g = 0; g < n_g16; ++g) {
+    pe->n_g16 = bcr_q > 0 ? 0 : n_g16;
+    pe->n_bcr = bcr_q > 0 ? n16 : 0;
+    for (int g = 0; g < pe->n_g16; ++g) {
       pe->g16_q[g] = g16_q[g];
       pe->g16_n[g] = g16_n[g];
       if (ctx->profiling)
@@ -1994,7 +2031,9 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
       const gpx_kernel_spec& sp = bt->specs[order[i]];
       se1 = se1 && sp.n_terms == 1 && sp.terms[0].kind == GPX_SE && sp.terms[0].dim_count == 1;
     }
-    band_fused_eval(Run{bt, bt->d_active + n_dense + n_band, n_fused, s}, n16, n_g16, g16_q, g16_n, se1,
+    Run rf{bt, bt->d_active + n_dense + n_band, n_fused, s};
+    rf.bcr_q = bcr_q;
+    band_fused_eval(rf, n16, n_g16, g16_q, g16_n, se1,
                     b16_p2 ? 3 : 2, n_fused1,
                     max_terms, (ctx->profiling && old_fused) ? fqe : nullptr, ctx->profiling ? pe->fq16 : nullptr);
   }
@@ -2079,6 +2118,13 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
       bt->timing.band_evals += n_band + n_fused;
       for (int i = n_dense; i < n_active; ++i)
         bt->timing.band_p_sum += (i >= n_dense + n_band && i < n_dense + n_band + pe->n_band16) ? 1 : bt->h_bandp[order[i]];
+    }
+    if (pe->n_bcr > 0 && bt->bcr_ev[0]) {
+      float fb = 0.f;
+      (void)hipEventElapsedTime(&fb, bt->bcr_ev[0], bt->bcr_ev[1]);
+      bt->timing.bcr_ms_total += fb;
+      bt->timing.bcr_calls += 1.0;
+      bt->timing.bcr_evals += pe->n_bcr;
     }
     for (int g = 0; g < pe->n_g16; ++g) {
       float f0 = 0.f, f1 = 0.f;

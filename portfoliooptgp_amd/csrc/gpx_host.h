@@ -73,6 +73,9 @@ struct gpx_batch {
   std::vector<int> band_tail;
   std::vector<int> band_tail16;
   double* bres = nullptr; size_t bres_cap = 0;  // [B][Np] band-check column sums (per-block path)
+  // block-cyclic-reduction workspace (gpx_bcr.hip: calls with few band16 problems), grow-only
+  double* bcr_ws = nullptr; size_t bcr_ws_cap = 0;
+  hipEvent_t bcr_ev[2] = {};       // profiling: the last call's reduction chain, start / end
   int force_dense = 0;         // re-evaluation of problems whose band check failed
   // pinned staging for gpx_batch_rebind_host, one region per slot ([Nmax*D] X, [Nmax] Y, n and
   // the spec): a slot's previous copies have completed before it is rebound (every evaluation
@@ -213,6 +216,7 @@ struct Run {
   int* info = nullptr;
   bool one_stream = false;
   int wide_from = 0;  // > 0: the band16 groups of at least this width run as ONE launch (band16_wide_kernel)
+  int bcr_q = 0;      // > 0: the band16 problems run as block cyclic reduction with blocks of 16·bcr_q rows
 };
 
 struct PhaseTimer {
@@ -343,6 +347,7 @@ struct gpx_batch::PendingEval {
   int n_band16 = 0;
   int g16_q[gpx::kBand16MaxQ] = {}, g16_n[gpx::kBand16MaxQ] = {}, n_g16 = 0;
   hipEvent_t fq16[gpx::kBand16MaxQ][4] = {};
+  int n_bcr = 0;                      // problems of the call on the block-cyclic-reduction path (bcr_ev timed)
   ~PendingEval() {
     for (auto x : kev)
       if (x) (void)hipEventDestroy(x);

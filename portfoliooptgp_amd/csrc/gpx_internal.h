@@ -199,6 +199,38 @@ void launch_slow_gather(const int* act, int n, const double* res, int stride, do
                         int* info_out, hipStream_t s);
 void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int kin, int n_active, hipStream_t s,
                    hipEvent_t* ev = nullptr);
+// ---- block cyclic reduction over the band (gpx_bcr.hip): calls with few problems -------------
+// per-problem workspace, nbm blocks of bs = 16Q rows: the blocks A (then Z_XX), C (the coupling
+// with the left neighbour: E, then Z), the neighbours' updates ΔL / ΔR, the factor W_X, P_Iᵀ,
+// P_Kᵀ; the vectors y, the y updates, z, α; per block a [16] gradient row and a check maximum
+struct BcrLayout {
+  long long A, C, DL, DR, Wm, PI, PK, y, dyL, dyR, z, al, part, chk, ctr, total;
+  __host__ __device__ BcrLayout(int bs, int nbm) {
+    const long long M = (long long)bs * bs * nbm, V = (long long)bs * nbm;
+    A = 0; C = M; DL = 2 * M; DR = 3 * M; Wm = 4 * M; PI = 5 * M; PK = 6 * M;
+    y = 7 * M; dyL = y + V; dyR = dyL + V; z = dyR + V; al = z + V;
+    part = al + V; chk = part + (long long)GPX_THETA_STRIDE * nbm; ctr = chk + nbm; total = ctr + 1;
+  }
+};
+struct BcrArgs {
+  const int* active;                 // the class's problems (workspace index = position here)
+  const DevSpec* specs; const double* theta; const int* nvalid;
+  const double* X; long long sX; int D;
+  const double* Y; long long sY;
+  double* ws; long long sWs;         // per-problem workspace (bcr_ws_doubles)
+  int nbm, bs;                       // blocks per problem in the layout, block rows (set by the launcher)
+  int* info;
+  double* z; double* ldiag; double* alpha; long long sVec; int Np;   // the reduce kernel's inputs, α
+  double* Kd; long long sMat; int ld;                                 // diag(Z) onto K's diagonal
+  double* partial; long long sPartial;                                // the [16] gradient row (tile 0)
+  double* results;                                                    // [kResBandCheck]
+  int level;
+};
+long long bcr_ws_doubles(int Q, int Nmax);
+// the whole evaluation of np problems of band width <= Q 16-blocks (Q <= 5): forward levels,
+// backward levels, contraction, per-problem finish; the reduce kernel follows (launch_reduce)
+void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStream_t s);
+
 void launch_band_solve(const BandSolveArgs& a, int n_active, hipStream_t s);
 void launch_band_transpose(const BandTransposeArgs& a, int q, int n_active, hipStream_t s);
 void launch_band_contract(const BandContractArgs& a, int max_terms, int n_active, hipStream_t s);

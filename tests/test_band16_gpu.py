@@ -22,6 +22,14 @@ from tests.test_gpu_parity import check_grad, check_loss, check_mean, check_var,
 K = gpx.kernels
 
 
+@pytest.fixture(autouse=True)
+def _band16_sweeps(monkeypatch):
+    """These tests are about the one-wavefront band16 sweeps: keep their small calls off the
+    block-cyclic-reduction path (gpx_bcr.hip, tests/test_bcr_gpu.py), which takes calls of at most
+    GPX_BCR_MAX band16 problems by default."""
+    monkeypatch.setenv("GPX_BCR_MAX", "0")
+
+
 def _no16():
     return _Env("GPX_BAND16", "0")
 

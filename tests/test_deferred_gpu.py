@@ -14,6 +14,14 @@ from portfoliooptgp_amd.kernels import compile_spec  # noqa: E402
 from oracle import gp_oracle as O  # noqa: E402
 
 K = gpx.kernels
+
+
+@pytest.fixture(autouse=True)
+def _band16_sweeps(monkeypatch):
+    """These tests are about the one-wavefront band16 sweeps: keep their small calls off the
+    block-cyclic-reduction path (gpx_bcr.hip, tests/test_bcr_gpu.py), which takes calls of at most
+    GPX_BCR_MAX band16 problems by default."""
+    monkeypatch.setenv("GPX_BCR_MAX", "0")
 # ℓ on unit-spaced day offsets -> band16 width Q (38.6 ℓ rows): 1.18 -> 3, 1.6 -> 4, 1.9 -> 5;
 # 2.3 -> 89 rows: the 64-row sweeps (p = 2)
 ELLS = [1.18, 1.6, 1.18, 1.9, 2.3, 1.0, 1.6, 1.9, 1.18]

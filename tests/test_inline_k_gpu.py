@@ -59,7 +59,7 @@ np.savez({path!r}, **out)
 
 
 def _run(kin, path, wide=None, extra=None):
-    env = dict(os.environ, GPX_B16_INLINE_K=str(kin))
+    env = dict(os.environ, GPX_B16_INLINE_K=str(kin), GPX_BCR_MAX="0")  # (the band16 sweeps, not gpx_bcr)
     for k in ("GPX_B16_INLINE_K_WIDE", "GPX_DEFER_STREAM"):
         env.pop(k, None)
     if wide is not None:
