@@ -32,7 +32,9 @@ $(CSRC)/gpx_band_phases.o: $(CSRC)/gpx_band.hip $(CSRC)/gpx_internal.h $(CSRC)/g
 	$(HIPCC) $(HIPFLAGS) -DGPX_BAND_PHASES -c $< -o $@
 $(CSRC)/gpx_band16_phases.o: $(CSRC)/gpx_band16.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_leaf.h $(CSRC)/gpx_kfun.h
 	$(HIPCC) $(HIPFLAGS) -DGPX_BAND_PHASES -c $< -o $@
-$(PHASES_LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band_phases.o $(CSRC)/gpx_band16_phases.o $(CSRC)/gpx_bcr.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
+$(CSRC)/gpx_bcr_phases.o: $(CSRC)/gpx_bcr.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_b16core.h $(CSRC)/gpx_kfun.h
+	$(HIPCC) $(HIPFLAGS) -DGPX_BCR_PHASES -c $< -o $@
+$(PHASES_LIB): $(CSRC)/gpx_kernels.o $(CSRC)/gpx_api.o $(CSRC)/gpx_band_phases.o $(CSRC)/gpx_band16_phases.o $(CSRC)/gpx_bcr_phases.o $(CSRC)/gpx_svgp_kernels.o $(CSRC)/gpx_svgp.o $(CSRC)/gpx_host_math.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-soname,libgpx_phases.so $^ -o $@
 phases: $(PHASES_LIB)
 

@@ -214,7 +214,8 @@ int gpx_batch_band_class(gpx_batch* batch, int n_rows, const int32_t* rows, cons
  * it reports info[b] = GPX_INFO_DEFERRED for those rows, and delivers (lml, grad, info) of
  * deferred rows of earlier calls whose work has finished by then (rows of neither kind are not
  * written). A deferred row may not be evaluated, predicted or rebound until it is delivered;
- * gpx_batch_deferred_wait blocks until every deferred row is delivered (into its arrays). The
+ * gpx_batch_deferred_wait blocks until every deferred row is delivered (into its arrays; it is
+ * refused, GPX_BAD_ARG, while an evaluation is submitted on the batch and not completed). The
  * call's other problems never wait for the slow classes, whose sweeps (one wavefront per SIMD,
  * or 73 KiB of LDS per workgroup) start late under a full band16 load. Same results, bit for
  * bit, as without deferral. q < 0 turns it off (the default). */

@@ -1543,6 +1543,7 @@ static int slow_setup(gpx_batch* bt) {
     HIPX(ctx, hipMalloc(&bt->d_slow_res, sizeof(double) * B * kResStride));
     HIPX(ctx, hipMalloc(&bt->d_slow_info_c, sizeof(int) * B));
   }
+  if (!bt->slow_in) HIPX(ctx, hipEventCreateWithFlags(&bt->slow_in, hipEventDisableTiming));
   if (!defer_own_stream() || bt->slow_s) return GPX_OK;
   // GPX_SLOW_PRIORITY: the slow stream at the device's lowest (-1) or highest (1) stream priority
   // (streams of another priority take hardware queues of their own); 0 / unset: the default
@@ -1557,7 +1558,6 @@ static int slow_setup(gpx_batch* bt) {
   } else {
     HIPX(ctx, hipStreamCreateWithFlags(&bt->slow_s, hipStreamNonBlocking));
   }
-  HIPX(ctx, hipEventCreateWithFlags(&bt->slow_in, hipEventDisableTiming));
   HIPX(ctx, hipEventCreateWithFlags(&bt->slow_up, hipEventDisableTiming));
   HIPX(ctx, hipMalloc(&bt->d_slow_act, sizeof(int) * B));
   HIPX(ctx, hipMalloc(&bt->d_slow_theta, sizeof(double) * B * GPX_THETA_STRIDE));
@@ -1649,6 +1649,12 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
   HIPX(ctx, hipMemcpyAsync(rec->h_res, bt->d_slow_res, sizeof(double) * n * kResStride, hipMemcpyDeviceToHost, ss));
   HIPX(ctx, hipMemcpyAsync(rec->h_info, bt->d_slow_info_c, sizeof(int) * n, hipMemcpyDeviceToHost, ss));
   HIPX(ctx, hipEventRecord(rec->done, ss));
+  if (!own) {
+    // same-stream mode reads the call's active list, θ, widths and info in place: the next
+    // upload into them (from any stream) waits for the part to finish (upload_common)
+    HIPX(ctx, hipEventRecord(bt->slow_in, ss));
+    bt->slow_in_armed = true;
+  }
   HIPX(ctx, hipGetLastError());
   if (bt->deferred.size() != (size_t)bt->B) bt->deferred.assign(bt->B, 0);
   for (int i = 0; i < n; ++i) {
@@ -1672,12 +1678,12 @@ static int deliver_slow(gpx_batch* bt, gpx_batch::SlowRec& rec, double* lml, dou
     const int b = rec.ids[i];
     bt->deferred[b] = 0;
     const double* res = rec.h_res + (size_t)i * kResStride;
-    info[b] = rec.h_info[i];
     const int np = bt->specs[b].n_params;
-    if (info[b] == 0 && !(res[kResBandCheck] <= band_tol)) {
-      redo.push_back(b);
+    if (rec.h_info[i] == 0 && !(res[kResBandCheck] <= band_tol)) {
+      redo.push_back(b);  // (its info is written by the dense re-evaluation, once that succeeds)
       continue;
     }
+    info[b] = rec.h_info[i];
     if (info[b] != 0) {
       status = GPX_NOT_PD;
       lml[b] = NAN;
@@ -2587,6 +2593,11 @@ int gpx_batch_set_deferred(gpx_batch* bt, int q) {
 int gpx_batch_deferred_wait(gpx_batch* bt, double* lml, double* grad, int32_t* info) {
   if (!bt) return GPX_BAD_ARG;
   if (!lml || !grad || !info) return fail(bt->ctx, GPX_BAD_ARG, "null output");
+  // a delivered row whose band check failed is re-evaluated densely through this batch (or its
+  // fallback slots), which an evaluation still submitted on it would refuse: refuse before any
+  // slow part is taken off the queue, so nothing is lost
+  if (bt->pending_eval)
+    return fail(bt->ctx, GPX_BAD_ARG, "an evaluation is submitted on this batch: complete it before deferred_wait");
   HIPX(bt->ctx, hipSetDevice(bt->ctx->device));
   return deliver_ready(bt, lml, grad, info, true);
 }

@@ -46,6 +46,36 @@
 
 namespace gpx {
 
+// Phase timing (diagnostic build only, -DGPX_BCR_PHASES: libgpx_phases.so, tools/bcr_phases.py):
+// thread 0 of each workgroup adds the shader-clock cycles of its phases into
+// g_bcr_phase[kernel][level][phase] ([..][..][15] counts workgroups); kernel 0 = forward levels,
+// 1 = backward levels, 2 = contraction (level 0)
+#ifdef GPX_BCR_PHASES
+__device__ unsigned long long g_bcr_phase[3][16][16];
+#define BP_BEGIN unsigned long long bp_t = __builtin_amdgcn_s_memtime(), bp_acc[8] = {};
+#define BP(i)                                                          \
+  do {                                                                 \
+    const unsigned long long bp_n = __builtin_amdgcn_s_memtime();      \
+    bp_acc[i] += bp_n - bp_t;                                          \
+    bp_t = bp_n;                                                       \
+  } while (0)
+#define BP_END(kid, lev)                                                             \
+  do {                                                                               \
+    if (threadIdx.x == 0) {                                                          \
+      for (int bp_i = 0; bp_i < 8; ++bp_i) atomicAdd(&g_bcr_phase[kid][lev][bp_i], bp_acc[bp_i]); \
+      atomicAdd(&g_bcr_phase[kid][lev][15], 1ull);                                   \
+    }                                                                                \
+  } while (0)
+#else
+#define BP_BEGIN
+#define BP(i) \
+  do {        \
+  } while (0)
+#define BP_END(kid, lev) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace {
 
 template <int Q>
@@ -171,6 +201,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
   const int m = lvl_m(n0, l), top = lvl_top(n0);
   const int j = blockIdx.x;
   if (l > top || j >= m) return;
+  BP_BEGIN
   const bool is_top = l == top;
   const bool elim = is_top || (j & 1);
   const int X = j << l, h = l > 0 ? 1 << (l - 1) : 0;
@@ -254,6 +285,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
   }
   if (!elim) return;
   __syncthreads();
+  BP(0);
   // right-hand sides, tile column w of each: R1 = E_XI, R2 = E_KXᵀ, R3 = I, RY = y (wave Q−1, column 0)
   t4 R1[Q], R2[Q], R3[Q], RY[Q];
   const double* CX = ws + Lw.C + (long long)X * BB;
@@ -290,6 +322,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
       __syncthreads();
     }
   }
+  BP(1);
   // right-looking Cholesky of A_X over its tile columns, with the right-hand sides
 #pragma unroll
   for (int t = 0; t < Q; ++t) {
@@ -351,6 +384,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
     }
     __syncthreads();
   }
+  BP(2);
   // the factor for the backward levels: W_X (lower tiles), P_Iᵀ, P_Kᵀ, z_X
   double* Wg = ws + Lw.Wm + (long long)X * BB;
   double* PIg = ws + Lw.PI + (long long)X * BB;
@@ -379,6 +413,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
       }
   }
   __syncthreads();
+  BP(3);
   // the neighbours' updates (column w of each; the Δ's lower tiles only)
   if (hasI) {
     double* dLo = ws + Lw.DL + (long long)X * BB;
@@ -422,6 +457,8 @@ __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
     s = sum4(s);
     if (l4 == 0) ws[Lw.dyR + (long long)X * bs + 16 * w + l15] = s;
   }
+  BP(4);
+  BP_END(0, l);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -461,6 +498,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_bwd_kernel(BcrArgs a) {
   }
   const int I = X - (1 << l), K = X + (1 << l);
   const bool hasI = !is_top, hasK = !is_top && K < n0;
+  BP_BEGIN
   const BcrLayout Lw(bs, a.nbm);
   double* ws = a.ws + (long long)p * a.sWs;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
@@ -497,6 +535,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_bwd_kernel(BcrArgs a) {
     }
   }
   __syncthreads();
+  BP(0);
   // α_X
   for (int i = tid; i < bs; i += NT) {
     double t = sz[i];
@@ -512,6 +551,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_bwd_kernel(BcrArgs a) {
     for (int r = i; r < bs; ++r) v = fma(s0[r * rs + i], st[r], v);
     al[(long long)X * bs + i] = v;
   }
+  BP(1);
   // G_I, G_K (column w) and row w of W_Xᵀ W_X
   t4 GI[Q], GK[Q], Zr[Q];
 #pragma unroll
@@ -528,6 +568,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_bwd_kernel(BcrArgs a) {
       if (mm >= k) mma(Zr[k], Wm, fr(s0, rs, mm, k, l15, l4));
     }
   }
+  BP(2);
   double* ZC = ws + Lw.C;
   __syncthreads();
   if (!is_top) {
@@ -550,6 +591,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_bwd_kernel(BcrArgs a) {
       s2[r * rs + c] = v2[k];
     }
     __syncthreads();
+    BP(3);
     t4 ZIX[Q], ZKX[Q];
 #pragma unroll
     for (int i = 0; i < Q; ++i) {
@@ -566,6 +608,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_bwd_kernel(BcrArgs a) {
       }
     }
     __syncthreads();
+    BP(4);
     double* ZCX = ZC + (long long)X * BB;
     double* ZCK = ZC + (long long)K * BB;
 #pragma unroll
@@ -589,6 +632,8 @@ __global__ __launch_bounds__(64 * Q) void bcr_bwd_kernel(BcrArgs a) {
   double* ZX = ws + Lw.A + (long long)X * BB;
 #pragma unroll
   for (int i = 0; i < Q; ++i) fst(ZX, bs, w, i, Zr[i], l15, l4);
+  BP(6);
+  BP_END(1, l);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -612,6 +657,7 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
   const int p = blockIdx.y, b = a.active[p];
   const int n = a.nvalid[b], n0 = (n + bs - 1) / bs, J = blockIdx.x;
   if (J >= n0) return;
+  BP_BEGIN
   const BcrLayout Lw(bs, a.nbm);
   const double* ws = a.ws + (long long)p * a.sWs;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -628,6 +674,7 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
   const double* ZCJ1 = ws + Lw.C + (long long)(J + 1) * BB;  // Z_{J+1,J} (J + 1 < n0)
   if (k1.on) stage_scaled(sx, Xb, D, n, k1, bs, J - 1, J, J + 1 < n0 ? J + 1 : -1, tid, 256);
   __syncthreads();
+  BP(0);
   double sums[NTm][3];
 #pragma unroll
   for (int t = 0; t < NTm; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
@@ -703,6 +750,7 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
     for (int v = 0; v < NV; ++v) sred[wave][v] = vals[v];
   }
   __syncthreads();
+  BP(1);
   double* part = const_cast<double*>(ws) + Lw.part + (long long)J * GPX_THETA_STRIDE;
   if (tid < GPX_THETA_STRIDE) {
     int slot = -1;
@@ -737,6 +785,8 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
   if (lane == 0) smax[wave] = res;
   __syncthreads();
   if (tid == 0) const_cast<double*>(ws)[Lw.chk + J] = fmax(fmax(smax[0], smax[1]), fmax(smax[2], smax[3]));
+  BP(2);
+  BP_END(2, 0);
 }
 
 // per problem: the [16] gradient row (Σ over blocks, in a fixed order) for the reduce kernel, the
@@ -813,3 +863,15 @@ void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStr
 }
 
 }  // namespace gpx
+
+#ifdef GPX_BCR_PHASES
+// out[3*16*16] <- g_bcr_phase; reset != 0 zeroes it afterwards. Diagnostic build only.
+extern "C" int gpx_debug_bcr_phases(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gpx::g_bcr_phase), sizeof(gpx::g_bcr_phase)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long zero[3][16][16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gpx::g_bcr_phase), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

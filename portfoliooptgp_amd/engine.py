@@ -186,10 +186,13 @@ class Engine:
                 ent[2] = buf
         self._box_want.clear()
 
-    def lml_grad(self, active: Sequence[int], theta: np.ndarray):
+    def lml_grad(self, active: Sequence[int], theta: np.ndarray, wait_deferred: bool = True):
         """logML [B], ∂logML/∂θ [B, 16], info [B] for the active rows (others untouched).
         info[b] > 0: the LAPACK-style failing pivot; info[b] == INFO_BAD_THETA: θ of problem b
-        is not finite and > 0, so b was left out of the device call (the others still run)."""
+        is not finite and > 0, so b was left out of the device call (the others still run).
+        With deferral on (set_deferred), the rows of this call that the library deferred are
+        waited for and merged in (wait_deferred, for callers that read info != 0 as a failure);
+        the stepped driver passes wait_deferred=False and steps them when they arrive."""
         act = self._active(active)
         theta = np.ascontiguousarray(theta, dtype=np.float64)
         assert theta.shape == (self.B, N.GPX_THETA_STRIDE)
@@ -208,8 +211,19 @@ class Engine:
         self._harvest_boxes()
         if rc not in (N.GPX_OK, N.GPX_NOT_PD):
             raise N.GPXError(f"gpx_batch_lml_grad failed ({rc}): {self.ctx.last_error()}")
-        self.eval_count += len(act)
+        self.eval_count += self._count_reported(info) if self.deferral >= 0 else len(act)
+        if wait_deferred and self.deferral >= 0 and (info[act] == N.INFO_DEFERRED).any():
+            l2, g2, i2 = self.deferred_wait()
+            got = (i2 != N.INFO_UNSET) & (i2 != N.INFO_DEFERRED)
+            lml[got], grad[got], info[got] = l2[got], g2[got], i2[got]
         return lml, grad, info
+
+    @staticmethod
+    def _count_reported(info: np.ndarray) -> int:
+        """Problem-evaluations a deferral-mode complete reported: the call's own rows that were not
+        deferred and the earlier deferred rows it delivered (each evaluation counted once,
+        whichever call delivers it)."""
+        return int(((info != N.INFO_UNSET) & (info != N.INFO_DEFERRED) & (info != N.INFO_BAD_THETA)).sum())
 
     def lml_grad_submit(self, active: Sequence[int], theta: np.ndarray):
         """First half of lml_grad: enqueue the evaluation on the current stream and return at
@@ -278,7 +292,7 @@ class Engine:
         rc = self.lib.gpx_batch_deferred_wait(self.handle, lml.ctypes.data, grad.ctypes.data, info.ctypes.data)
         if rc not in (N.GPX_OK, N.GPX_NOT_PD):
             raise N.GPXError(f"gpx_batch_deferred_wait failed ({rc}): {self.ctx.last_error()}")
-        self.eval_count += int(((info != N.INFO_UNSET) & (info != N.INFO_DEFERRED)).sum())
+        self.eval_count += self._count_reported(info)
         return lml, grad, info
 
     def band_class(self, rows, theta: np.ndarray) -> np.ndarray:
@@ -304,7 +318,7 @@ class Engine:
                                                   info.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
         if rc not in (N.GPX_OK, N.GPX_NOT_PD):
             raise N.GPXError(f"gpx_batch_lml_grad_complete failed ({rc}): {self.ctx.last_error()}")
-        self.eval_count += len(act)
+        self.eval_count += self._count_reported(info) if self.deferral >= 0 else len(act)
         return lml, grad, info
 
     def predict(self, active: Sequence[int], theta: np.ndarray, Xnew: Sequence, add_noise: bool,

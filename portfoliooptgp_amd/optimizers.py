@@ -684,11 +684,16 @@ class DeviceAdmission:
     device serves the calls nearly first-come first-served: they complete one after another,
     so the host phases interleave with the other processes' device work.
 
+    A pipelined driver (several device batches from one host thread) holds ONE place while any
+    of its calls is in flight, so a process never waits for a place while holding one.
+
     Create it in the parent before the helper processes are spawned (a multiprocessing
     semaphore crosses a spawn only as a Process argument)."""
 
     def __init__(self, places: int, ctx=None):
         import multiprocessing as mp
+        if int(places) < 1:
+            raise ValueError("DeviceAdmission needs at least one place")
         self.places = int(places)
         self._sem = (ctx or mp.get_context("spawn")).BoundedSemaphore(self.places)
 
@@ -1089,7 +1094,7 @@ class _SteppedDriver:
             gs.t_call = time.perf_counter()
             try:
                 with lock:
-                    lml, grad, info = eng.lml_grad(gs.act, gs.theta)
+                    lml, grad, info = eng.lml_grad(gs.act, gs.theta, wait_deferred=False)
             finally:
                 if adm is not None:
                     adm.release()
@@ -1109,22 +1114,35 @@ class _SteppedDriver:
                            for g, (e, rows, lk, stm) in enumerate(self.groups)]
         inflight = []
 
+        # admission: this pipeline holds at most ONE place, from the submit that finds nothing of
+        # it in flight to the complete that leaves nothing in flight — a place per group would let
+        # one thread wait on the semaphore while holding places that only its own completes give
+        # back (places < groups across the processes: every process waits for ever)
         adm = self.admission
+        held = [False]
+
+        def take():
+            if adm is not None and not held[0]:
+                t_a = time.perf_counter()
+                adm.acquire()
+                held[0] = True
+                self._tick("admission_wait", t_a)
+
+        def give():
+            if adm is not None and held[0] and not inflight:
+                adm.release()
+                held[0] = False
 
         def submit(gs):
             if not self._prepare(gs):
                 return False
-            if adm is not None:
-                t_a = time.perf_counter()
-                adm.acquire()
-                self._tick("admission_wait", t_a)
+            take()
             gs.t_call = time.perf_counter()
             try:
                 with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():
                     gs.eng.lml_grad_submit(gs.act, gs.theta)
             except BaseException:
-                if adm is not None:
-                    adm.release()
+                give()
                 raise
             self._tick("submit", gs.t_call)
             return True
@@ -1173,8 +1191,7 @@ class _SteppedDriver:
             try:
                 lml, grad, info = gs.eng.lml_grad_complete()
             finally:
-                if adm is not None:
-                    adm.release()
+                give()
             t_end = time.perf_counter()
             self._tick("complete", t1)
             with torch.cuda.stream(gs.stream) if gs.stream is not None else contextlib.nullcontext():

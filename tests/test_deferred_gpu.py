@@ -115,3 +115,45 @@ def test_deferred_fits_equal_undeferred_fits():
         assert a.nfev == b.nfev and np.array_equal(a.x, b.x) and a.fun == b.fun
         assert np.array_equal(pa[0].cpu().numpy(), pb[0].cpu().numpy())
         assert np.array_equal(pa[1].cpu().numpy(), pb[1].cpu().numpy())
+
+
+def test_deferred_redo_path_and_wait_while_submitted():
+    """a deferred row whose band check fails is re-evaluated densely when it is
+    delivered (here every check fails: GPX_BAND_TOL=1e-30), with the results of the undeferred
+    call at the same tolerance; deferred_wait is refused while an evaluation is submitted (the
+    re-evaluation would need the batch), and works once it is completed."""
+    import os
+    n = 2048
+    data = [O.synthetic_series(n, s) for s in range(len(ELLS))]
+    th = _theta(ELLS)
+    act = list(range(len(ELLS)))
+    prev = os.environ.get("GPX_BAND_TOL")
+    os.environ["GPX_BAND_TOL"] = "1e-30"
+    try:
+        ref = _engine(n, data, None)
+        l0, g0, i0 = ref.lml_grad(act, th)
+        assert not i0.any()
+        eng = _engine(n, data, 3)
+        eng.lml_grad_submit(act, th)
+        l1, g1, i1 = eng.lml_grad_complete()
+        pend = [b for b in act if i1[b] == N.INFO_DEFERRED]
+        assert pend
+        fast = [b for b in act if b not in pend]
+        eng.lml_grad_submit(fast, th)
+        with pytest.raises(N.GPXError):
+            eng.deferred_wait()
+        l2, g2, i2 = eng.lml_grad_complete()
+        for b in pend:  # delivered by the complete (its slow part had finished) or still in flight
+            if i2[b] == 0:
+                l1[b], g1[b], i1[b] = l2[b], g2[b], 0
+        l3, g3, i3 = eng.deferred_wait()
+        for b in pend:
+            if i3[b] != N.INFO_UNSET:
+                l1[b], g1[b], i1[b] = l3[b], g3[b], i3[b]
+        for b in act:
+            assert i1[b] == 0 and l1[b] == l0[b] and np.array_equal(g1[b, :3], g0[b, :3]), (b, i1[b])
+    finally:
+        if prev is None:
+            os.environ.pop("GPX_BAND_TOL", None)
+        else:
+            os.environ["GPX_BAND_TOL"] = prev

@@ -24,7 +24,7 @@ class FakeEngine:
         y = np.asarray(Y, dtype=np.float64).reshape(-1)
         self.target[b] = [1.0 + abs(y.mean()) * 3.0, 0.5 + y.std()]
 
-    def lml_grad(self, rows, theta):
+    def lml_grad(self, rows, theta, wait_deferred=True):
         self.calls.append(len(rows))
         lml = np.full(self.B, np.nan)
         grad = np.full((self.B, N.GPX_THETA_STRIDE), np.nan)
@@ -88,7 +88,7 @@ def test_stream_equals_solo(width, groups, engines):
 class NotPDEngine(FakeEngine):
     """As FakeEngine, but K + σn²I 'fails to factor' once the lengthscale passes 2.5."""
 
-    def lml_grad(self, rows, theta):
+    def lml_grad(self, rows, theta, wait_deferred=True):
         lml, grad, info = super().lml_grad(rows, theta)
         for r in rows:
             if theta[r, 0] > 2.5:
@@ -117,7 +117,7 @@ class BadThetaEngine(FakeEngine):
     """As FakeEngine, but the lengthscale counts as out of (0, ∞) once it passes 2.5 (the
     device engine's host-side screen marks such rows INFO_BAD_THETA and skips them)."""
 
-    def lml_grad(self, rows, theta):
+    def lml_grad(self, rows, theta, wait_deferred=True):
         lml, grad, info = super().lml_grad(rows, theta)
         for r in rows:
             if theta[r, 0] > 2.5:
@@ -260,7 +260,7 @@ class BandFakeEngine(AsyncFakeEngine):
     def band_width(self, rows, theta):
         return np.array([2 if theta[r, 0] > 1.5 else 1 for r in rows], dtype=np.int32)
 
-    def lml_grad(self, rows, theta):
+    def lml_grad(self, rows, theta, wait_deferred=True):
         self.classes = getattr(self, "classes", []) + [self.band_width(rows, theta)]
         return super().lml_grad(rows, theta)
 
@@ -371,7 +371,7 @@ class CachedPredictEngine(FakeEngine):
         self.last_theta = {}
         self.uncached = 0
 
-    def lml_grad(self, rows, theta):
+    def lml_grad(self, rows, theta, wait_deferred=True):
         lml, grad, info = super().lml_grad(rows, theta)
         for r in rows:
             lml[r] += 1e-7 * np.sin(1e9 * theta[r, 0])     # rounding-level roughness
@@ -437,7 +437,7 @@ class ClassFakeEngine(AsyncFakeEngine):
         return np.array([-2 if 1.49 < theta[r, 0] <= 1.5 else (5 if theta[r, 0] > 1.5 else 3) for r in rows],
                         dtype=np.int32)
 
-    def lml_grad(self, rows, theta):
+    def lml_grad(self, rows, theta, wait_deferred=True):
         self.classes = getattr(self, "classes", []) + [self.band_class(rows, theta)]
         return super().lml_grad(rows, theta)
 
@@ -499,7 +499,7 @@ class DeferringFakeEngine(FakeEngine):
                 info[r] = 0
         return lml, grad, info
 
-    def lml_grad(self, rows, theta):
+    def lml_grad(self, rows, theta, wait_deferred=True):
         self.lml_grad_submit(rows, theta)
         return self.lml_grad_complete()
 
@@ -529,3 +529,39 @@ def test_deferred_rows_keep_trajectories(engines):
         assert float(p[0][0, 0]) == pytest.approx(m.kernel.lengthscales.value)
     assert sum(sum(e.calls) for e in eng) == sum(r.nfev for r in res)
     assert sum(e.deferred_total for e in eng) > 0
+
+
+class _CountingAdmission:
+    """DeviceAdmission's interface over a plain semaphore, counting the places held at once; a
+    blocking acquire that cannot be served fails the test instead of hanging it."""
+
+    def __init__(self, places):
+        import threading
+        self.places, self.held, self.peak = places, 0, 0
+        self._sem = threading.BoundedSemaphore(places)
+
+    def acquire(self):
+        assert self._sem.acquire(timeout=5.0), "admission deadlock: no place came back"
+        self.held += 1
+        self.peak = max(self.peak, self.held)
+
+    def release(self):
+        self.held -= 1
+        self._sem.release()
+
+
+@pytest.mark.parametrize("places,engines", [(1, 2), (1, 3), (2, 3)])
+def test_admission_one_place_per_pipeline(places, engines):
+    """A pipelined driver (one host thread, several device batches) with fewer admission places
+    than batches: it holds one place while any of its calls is in flight (a place per
+    group deadlocked), and the fits keep their solo trajectories."""
+    ms = _models(9)
+    ref = [_solo(m) for m in _models(9)]
+    eng = [AsyncFakeEngine(2) for _ in range(engines)]
+    adm = _CountingAdmission(places)
+    res, _ = gpx.optimizers.Scipy().minimize_stream(ms, width=2 * engines, engine=eng, groups=engines,
+                                                    admission=adm)
+    for r, r0 in zip(res, ref):
+        assert r.nfev == r0.nfev
+        np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+    assert adm.peak == 1 and adm.held == 0
