@@ -225,7 +225,8 @@ def contract_traffic(n, flops_per_launch):
 SUM_FIELDS = ("contract_ms_total", "contract_launches", "contract_alg_flops", "eval_ms_total", "evals",
               "band_ms_total", "band_calls", "band_evals", "band_p_sum", "band_fallbacks", "shadow_evals",
               "shadow_predicts")
-NARROW_FIELDS = ("band_fwd_ms_total", "band_bwd_ms_total", "band_fused_launches", "band_fwd_flops", "band_bwd_flops",
+NARROW_FIELDS = ("band_fwd_ms_total", "band_bwd_ms_total", "band_fused_launches", "band_fused_p2_launches",
+                 "band_fwd_flops", "band_bwd_flops",
                  "band16_fwd_ms_total", "band16_bwd_ms_total", "band16_launches", "band16_evals", "band16_q_sum",
                  "band16_fwd_flops", "band16_bwd_flops", "band16_wave_ms", "band16_wide_ms_total",
                  "band16_wide_launches", "band16_wide_flops", "band16_wide_evals")
@@ -594,9 +595,83 @@ def secondary_c3(gpu, n=2048, series=20, share=3, reps=3):
             "wall_s_per_gpu_share_at_8gpus": w_share, "share_series": share,
             "nfev_of_share": [int(r.nfev) for r in res_share],
             "ratio_wall_all_over_share": w_all / w_share,
-            "note": "an upper bound on the 8-GPU speed-up of this batch (the ranks' shares run concurrently); "
-                    "each fit is a chain of ~20 dependent evaluations of ~1.5 ms, so a GPU holding 3 fits takes "
-                    "about as long as one holding 20"}
+            "note": "calls of at most GPX_BCR_MAX (32) problems take the block-cyclic-reduction path (DESIGN.md "
+                    "§3f); wall(20) / wall(share) is an upper bound on the 8-GPU speed-up of this batch (the ranks' "
+                    "shares run concurrently): each fit is a chain of ~20 dependent evaluations"}
+
+
+def secondary_solo(gpu, n=N_POINTS, seeds=(0, 1, 2), reps=3):
+    """The reference's own call pattern: ONE exact GPR fit at a time, as GPR/model_trainer.py:15-20
+    runs it inside its kernel loop — models.GPR from GPflow's defaults, Scipy().minimize
+    (maxiter=100), predict_f at the training inputs — on the C2 series (N = 4096, SE, sigma_n^2 =
+    1e-5 fixed). A call of one problem takes the block-cyclic-reduction path; the
+    one-wavefront band16 sweeps (GPX_BCR_MAX=0) are timed beside it on the same fits. Median wall
+    time of `reps` fits per seed (after a warm-up fit), and the device time of one evaluation's
+    reduction chain (HIP events, profiling on, a separate pass)."""
+    import torch
+    import portfoliooptgp_amd as gpx
+    from portfoliooptgp_amd import _native as N
+    from portfoliooptgp_amd.engine import solo_engine
+
+    def fit(x, y):
+        m = gpx.models.GPR(data=(x, y), kernel=gpx.kernels.SquaredExponential(), device=gpu)
+        m.likelihood.variance.assign(NOISE)
+        gpx.set_trainable(m.likelihood.variance, False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables, options=dict(maxiter=MAXITER))
+        m.predict_f(x)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, int(r.nfev), float(r.fun), m
+
+    out = {"config": "C2, one fit at a time", "workload": f"synthetic 1-D series, N={n}, SE, fp64, sigma_n^2=1e-5 "
+           "fixed, models.GPR + Scipy().minimize(maxiter=100) + predict_f(X_train), one GPR per call (the "
+           "reference's GPR/model_trainer.py:15-20 loop)", "seeds": list(seeds)}
+    prev = os.environ.get("GPX_BCR_MAX")
+    try:
+        for mode, cap in (("bcr", prev), ("band16_sweeps", "0")):
+            if cap is None:
+                os.environ.pop("GPX_BCR_MAX", None)
+            else:
+                os.environ["GPX_BCR_MAX"] = cap
+            walls, nfevs, funs = [], [], []
+            for s in seeds:
+                x, y = synthetic_series(n, s)
+                fit(x, y)  # warm-up: engine creation, first gather
+                w = []
+                for _ in range(reps):
+                    t, nf, fun, _m = fit(x, y)
+                    w.append(t)
+                walls.append(sorted(w)[reps // 2])
+                nfevs.append(nf)
+                funs.append(fun)
+            out[mode] = {"fit_ms_per_seed": [1e3 * v for v in walls], "fit_ms_median": 1e3 * sorted(walls)[len(walls) // 2],
+                         "nfev": nfevs, "loss": funs}
+        if prev is None:
+            os.environ.pop("GPX_BCR_MAX", None)
+        else:
+            os.environ["GPX_BCR_MAX"] = prev
+        # one evaluation's device chain on the reduction path (profiling on: HIP events around it)
+        x, y = synthetic_series(n, seeds[0])
+        _, _, _, m = fit(x, y)
+        ctx = N.Context.get(gpu)
+        ctx.set_profiling(True)
+        eng = solo_engine(m)
+        m.loss_and_grad_unconstrained()
+        eng.reset_timing()
+        for _ in range(20):
+            m.loss_and_grad_unconstrained()
+        t = eng.last_timing()
+        ctx.set_profiling(False)
+        out["bcr_chain_ms_per_eval"] = t.bcr_ms_total / max(t.bcr_calls, 1.0)
+        out["device_ms_per_eval"] = t.eval_ms_total / max(t.evals, 1.0)
+    finally:
+        if prev is None:
+            os.environ.pop("GPX_BCR_MAX", None)
+        else:
+            os.environ["GPX_BCR_MAX"] = prev
+    out["speedup_vs_band16_sweeps"] = out["band16_sweeps"]["fit_ms_median"] / out["bcr"]["fit_ms_median"]
+    return out
 
 
 def secondary_c5(gpu, reps=20):
@@ -742,10 +817,16 @@ def main():
     #     launch's HIP-event duration
     #   64-row fused sweeps (the wider bands): the 64^3 block products (leaf 2/3 of one)
     sweeps = {}
+    # the 64-row pairs' kernels by the name rocprof records: band_fwd1_kernel / band_bwd1_kernel<1> (the
+    # p <= 1 class) or band_fwd_kernel / band_bwd_kernel<1> (the p = 2 class, two 64-blocks per step)
+    p2 = tm["band_fused_p2_launches"]
+    f64n, b64n = (("band_fwd_kernel", "band_bwd_kernel<1>") if p2 >= tm["band_fused_launches"] > 0 else
+                  ("band_fwd1_kernel", "band_bwd1_kernel<1>") if p2 == 0 else
+                  ("band_fwd1_kernel+band_fwd_kernel", "band_bwd1_kernel<1>+band_bwd_kernel<1>"))
     for key, ms, fl, la in (("band16_fwd_kernel", tm["band16_fwd_ms_total"], tm["band16_fwd_flops"], tm["band16_launches"]),
                             ("band16_bwd_kernel", tm["band16_bwd_ms_total"], tm["band16_bwd_flops"], tm["band16_launches"]),
-                            ("band_fwd1_kernel", tm["band_fwd_ms_total"], tm["band_fwd_flops"], tm["band_fused_launches"]),
-                            ("band_bwd1_kernel<1>", tm["band_bwd_ms_total"], tm["band_bwd_flops"], tm["band_fused_launches"]),
+                            (f64n, tm["band_fwd_ms_total"], tm["band_fwd_flops"], tm["band_fused_launches"]),
+                            (b64n, tm["band_bwd_ms_total"], tm["band_bwd_flops"], tm["band_fused_launches"]),
                             # the deferred part's Q = 4/5 classes, both sweeps per wavefront, one launch
                             ("band16_wide_kernel", tm["band16_wide_ms_total"], tm["band16_wide_flops"],
                              tm["band16_wide_launches"])):
@@ -763,10 +844,12 @@ def main():
     k = sweeps["band16_wide_kernel"]
     ppl = tm["band16_wide_evals"] / max(k["launches"], 1.0)
     k["traffic"], k["traffic_source"] = band_traffic("band16_wide_kernel", ppl) if ppl > 0 else (None, None)
-    for key, fwd in (("band_fwd1_kernel", True), ("band_bwd1_kernel<1>", False)):
+    for key, fwd in ((f64n, True), (b64n, False)):
         k = sweeps[key]
-        ppl = k["alg_flops_per_launch"] / band_problem_flops(n, 1, fwd)
-        k["traffic"], k["traffic_source"] = band_traffic(key.split("<")[0], ppl) if ppl > 0 else (None, None)
+        pw = 2 if p2 >= tm["band_fused_launches"] > 0 else 1
+        ppl = k["alg_flops_per_launch"] / band_problem_flops(n, pw, fwd)
+        tkey = ("band_fwd1_kernel" if fwd else "band_bwd1_kernel")  # (the committed traffic passes: the p <= 1 pair)
+        k["traffic"], k["traffic_source"] = band_traffic(tkey, ppl) if (ppl > 0 and pw == 1) else (None, None)
     from_p = tm["band_p_sum"] / max(tm["band_evals"], 1.0)
     # the whole chip over the timed region: the MFMA flops of every banded evaluation (band16
     # tile products + the 64-row sweeps' block products) / wall time
@@ -864,7 +947,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, nfev_mean)
     if rank == 0 and world == 1 and not args.no_secondary:
-        for name, fn in (("secondary_c3_batch", lambda: secondary_c3(gpu)),
+        for name, fn in (("secondary_solo", lambda: secondary_solo(gpu)),
+                         ("secondary_c3_batch", lambda: secondary_c3(gpu)),
                          ("secondary_c4_dense", lambda: secondary_c4(gpu)),
                          ("secondary_c4_expxexp", lambda: secondary_c4(gpu, kind="expxexp")),
                          ("secondary_c5_svgp", lambda: secondary_c5(gpu))):

@@ -309,6 +309,9 @@ typedef struct {
   /* block cyclic reduction (calls with at most GPX_BCR_MAX band16 problems): the device time of
    * the reduction chains (forward and backward levels, contraction), chains, problem-evaluations */
   double bcr_ms_total, bcr_calls, bcr_evals;
+  /* of band_fused_launches: the timed 64-row launch pairs that were the p = 2 class's
+   * (band_fwd_kernel / band_bwd_kernel) rather than the p <= 1 class's (band_fwd1_kernel / band_bwd1_kernel) */
+  double band_fused_p2_launches;
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);

@@ -632,10 +632,11 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   int nl = 0;
   {
     int off = 0;
-    // (r.bcr_q: the band16 problems as ONE block-cyclic-reduction chain, gpx_bcr.hip)
-    if (r.bcr_q > 0 && n16 > 0) {
-      lanes[nl++] = Lane{4, 0, n16, 0, n_g16};
-      off = n16;
+    // (r.bcr_q: each band16 width group as a block-cyclic-reduction chain of its own width,
+    // gpx_bcr.hip: a problem's arithmetic depends on its own width only, not on the call's mix)
+    for (int g = 0; g < n_g16 && r.bcr_q > 0; ++g) {
+      lanes[nl++] = Lane{4, g, g16_n[g], off, g + 1};
+      off += g16_n[g];
     }
     for (int g = 0; g < n_g16 && r.bcr_q == 0; ++g) {
       // (r.wide_from: the SE1 groups of width 4 and 5 as one lane, one band16_wide_kernel launch)
@@ -691,6 +692,8 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   }();
   const int nstreams = (lanes_on && !r.one_stream) ? std::min(std::min(nl, 1 + kAux), lane_streams) : 1;
   auto lane_stream = [&](int i) { return (i == 0 || nstreams == 1) ? r.s : bt->aux[(i - 1) % (nstreams - 1)]; };
+  const bool bcr_timed = r.bcr_q > 0 && bt->ctx->profiling && bt->bcr_ev[0];
+  if (bcr_timed) (void)hipEventRecord(bt->bcr_ev[0], r.s);
   if (nstreams > 1) {
     (void)hipEventRecord(bt->ev[kEvents - 2], r.s);   // the call's uploads are in
     for (int i = 1; i < nstreams; ++i) (void)hipStreamWaitEvent(bt->aux[i - 1], bt->ev[kEvents - 2], 0);
@@ -737,13 +740,13 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       BcrArgs ca{};
       ca.active = r.d_act + l.off; ca.specs = bt->d_specs; ca.theta = fa.theta; ca.nvalid = bt->d_n;
       ca.X = bt->X; ca.sX = (long long)bt->Nmax * bt->D; ca.D = bt->D; ca.Y = bt->Y; ca.sY = bt->Nmax;
-      ca.ws = bt->bcr_ws; ca.sWs = bcr_ws_doubles(r.bcr_q, bt->Nmax); ca.info = fa.info;
+      // (workspace: every problem of the call at its position, in slots of the widest layout)
+      ca.sWs = bcr_ws_doubles(kBand16MaxQ, bt->Nmax);
+      ca.ws = bt->bcr_ws + (size_t)l.off * (size_t)ca.sWs; ca.info = fa.info;
       ca.z = bt->z; ca.ldiag = bt->ldiag; ca.alpha = bt->alpha; ca.sVec = Np; ca.Np = Np;
       ca.Kd = bt->K; ca.sMat = st; ca.ld = mat_ld(bt);
       ca.partial = bt->partial; ca.sPartial = bt->partial_stride; ca.results = bt->results;
-      if (bt->ctx->profiling && bt->bcr_ev[0]) (void)hipEventRecord(bt->bcr_ev[0], ls);
-      launch_bcr(ca, r.bcr_q, max_terms, l.n, bt->Nmax, ls);
-      if (bt->ctx->profiling && bt->bcr_ev[1]) (void)hipEventRecord(bt->bcr_ev[1], ls);
+      launch_bcr(ca, g16_q[l.g], max_terms, l.n, bt->Nmax, ls);
     } else if (l.kind == 1) {
       BuildArgs b1 = ba;
       b1.active = r.d_act + l.off;
@@ -766,6 +769,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     (void)hipEventRecord(bt->ev[kEvents - 4 - i], bt->aux[i - 1]);
     (void)hipStreamWaitEvent(r.s, bt->ev[kEvents - 4 - i], 0);
   }
+  if (bcr_timed) (void)hipEventRecord(bt->bcr_ev[1], r.s);
   trace_mark(bt, 41, r.s);
   ReduceArgs ra{};
   ra.active = r.d_act; ra.partial = bt->partial; ra.sPartial = bt->partial_stride;
@@ -1738,6 +1742,9 @@ static int deliver_slow(gpx_batch* bt, gpx_batch::SlowRec& rec, double* lml, dou
       bt->timing.band_fwd_ms_total += f0;
       bt->timing.band_bwd_ms_total += f1;
       bt->timing.band_fused_launches += 1.0;
+      bool p2 = !rec.p64.empty();
+      for (int pb : rec.p64) p2 = p2 && pb == 2;
+      if (p2) bt->timing.band_fused_p2_launches += 1.0;
       for (int pb : rec.p64) {
         bt->timing.band_fwd_flops += band_fused_flops(bt->Np, pb, true);
         bt->timing.band_bwd_flops += band_fused_flops(bt->Np, pb, false);
@@ -1827,9 +1834,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   const bool b16_p2 = rt.b16_p2;
   // a call with few band16 problems takes them by block cyclic reduction (gpx_bcr.hip): the
   // one-wavefront sweeps' N/16-step chain would be the whole call's latency
-  int bcr_q = 0;
-  if (n16 > 0 && n16 <= bcr_max_problems())
-    for (int g = 0; g < n_g16; ++g) bcr_q = std::max(bcr_q, g16_q[g]);
+  const int bcr_q = (n16 > 0 && n16 <= bcr_max_problems()) ? 1 : 0;
   // the problems launched by this call (band storage: without the shadowed ones)
   n_active = n_dense + n_band + n_fused;
   // band storage: a few fallback problems go out at once on the fallback stream (more than the
@@ -1865,7 +1870,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (e != GPX_OK) return drop_shadow(e);
   }
   if (bcr_q > 0) {
-    const int e = ensure(ctx, bt->bcr_ws, bt->bcr_ws_cap, (size_t)n16 * (size_t)bcr_ws_doubles(bcr_q, bt->Nmax));
+    const int e = ensure(ctx, bt->bcr_ws, bt->bcr_ws_cap, (size_t)n16 * (size_t)bcr_ws_doubles(kBand16MaxQ, bt->Nmax));
     if (e != GPX_OK) return drop_shadow(e);
     if (ctx->profiling && !bt->bcr_ev[0])
       for (auto& e2 : bt->bcr_ev) HIPX(ctx, hipEventCreate(&e2));
@@ -2152,6 +2157,7 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
       bt->timing.band_fwd_ms_total += f0;
       bt->timing.band_bwd_ms_total += f1;
       bt->timing.band_fused_launches += 1.0;
+      if (n_fused1 == 0) bt->timing.band_fused_p2_launches += 1.0;
       // the timed launch pair is the p <= 1 class's when there is one, else the p = 2 class's
       const int t0 = n_dense + n_band + pe->n_band16, t1 = n_fused1 > 0 ? t0 + n_fused1 : n_active;
       for (int i = t0; i < t1; ++i) {

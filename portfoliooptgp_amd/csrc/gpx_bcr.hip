@@ -176,6 +176,58 @@ __device__ __forceinline__ void stage_scaled(double* __restrict__ sx, const doub
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
+// The level-0 blocks from the inputs (grid: blocks J x 2 parts x problems, 256 threads):
+// part 0 the lower tiles of A_J = K_JJ + σn²I (the identity in the padding) and y_J, part 1 the
+// coupling C_J = K_{J,J−1}. Single-term stationary kernels from rows scaled once by 1/ℓ (KSt1).
+// ---------------------------------------------------------------------------------------
+template <int Q>
+__global__ __launch_bounds__(256) void bcr_build_kernel(BcrArgs a) {
+  constexpr int bs = Bcr<Q>::bs, BB = Bcr<Q>::BB;
+  __shared__ double sx[2 * bs * kXs];  // x/ℓ of blocks J−1 (slot 0) and J (slot 1)
+  const int p = blockIdx.z, b = a.active[p], part = blockIdx.y;
+  const int n = a.nvalid[b], n0 = (n + bs - 1) / bs, J = blockIdx.x;
+  if (J >= n0 || (part == 1 && J == 0)) return;
+  const BcrLayout Lw(bs, a.nbm);
+  double* ws = a.ws + (long long)p * a.sWs;
+  const int tid = threadIdx.x;
+  const DevSpec spec = a.specs[b];
+  const double* th = a.theta + (long long)b * GPX_THETA_STRIDE;
+  const double noise = th[spec.n_params];
+  const double* Xb = a.X + (long long)b * a.sX;
+  const int D = a.D;
+  const KSt1 k1 = kst1(spec, th);
+  if (k1.on) {
+    for (int e = tid; e < 2 * bs * k1.dn; e += 256) {
+      const int slot = e / (bs * k1.dn), rem = e - slot * bs * k1.dn, r = rem / k1.dn, d = rem - r * k1.dn;
+      const int g = (J - 1 + slot) * bs + r;
+      if (g >= 0) sx[(slot * bs + r) * kXs + d] = g < n ? Xb[(long long)g * D + k1.d0 + d] / k1.ell : 0.0;
+    }
+    __syncthreads();
+  }
+  double* out = ws + (part == 0 ? Lw.A : Lw.C) + (long long)J * BB;
+  const int c0 = (part == 0 ? J : J - 1) * bs;
+  for (int e = tid; e < BB; e += 256) {
+    const int r = e / bs, c = e - r * bs;
+    if (part == 0 && (r >> 4) < (c >> 4)) continue;
+    const int gi = J * bs + r, gj = c0 + c;
+    double v;
+    if (gi >= n || gj >= n) {
+      v = gi == gj ? 1.0 : 0.0;
+    } else if (k1.on) {
+      v = k1.val(sqdist_scaled(sx + (bs + r) * kXs, sx + ((part == 0 ? bs : 0) + c) * kXs, k1.dn));
+      if (gi == gj) v += noise;
+    } else {
+      v = kval(spec, th, noise, Xb, D, n, gi, gj);
+    }
+    out[e] = v;
+  }
+  if (part == 0 && tid < bs) {
+    const int g = J * bs + tid;
+    ws[Lw.y + g] = g < n ? a.Y[(long long)b * a.sY + g] : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Forward level l (grid: node positions j < m_l x problems). Odd j (and the top node): eliminate
 // node X = j·2^l with neighbours I = X − 2^l, K = X + 2^l (if K < n0):
 //   A_X (+ the level l−1 updates still pending on it) into LDS; right-hand sides
@@ -184,73 +236,42 @@ __device__ __forceinline__ void stage_scaled(double* __restrict__ sx, const doub
 //   applied to the right-hand sides as it goes: afterwards they hold P_Iᵀ = L⁻¹E_XI, P_Kᵀ, W_X,
 //   z_X; then ΔA_I = P_I P_Iᵀ, ΔA_K = P_K P_Kᵀ (lower tiles), E_KI = −P_K P_Iᵀ (-> C[K]) and the
 //   y updates P_I z_X, P_K z_X.
-// Even j: the node survives; at level 0 its A and y are built from the inputs, at level l > 0
-// the updates of its two level l−1 neighbours are applied in place.
+// Even j: the node survives; at level l > 0 the updates of its two level l−1 neighbours are
+// applied in place (the level-0 blocks come from bcr_build_kernel).
 // ---------------------------------------------------------------------------------------
 template <int Q>
 __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
   constexpr int bs = Bcr<Q>::bs, rs = Bcr<Q>::rs, BB = Bcr<Q>::BB, NT = 64 * Q, PER = BB / NT;
-  __shared__ __attribute__((aligned(16))) double lds[2 * Bcr<Q>::mat + bs + 16 * kSC + 3 * bs * kXs];
+  __shared__ __attribute__((aligned(16))) double lds[2 * Bcr<Q>::mat + bs + 16 * kSC];
   double* sA = lds;                    // A_X -> L (W_tt on the diagonal) during the sweep, then P_Iᵀ
   double* sB = lds + Bcr<Q>::mat;      // P_Kᵀ
   double* sz = lds + 2 * Bcr<Q>::mat;  // y_X, then z_X
   double* sc = sz + bs;                // leaf16m's scratch
-  double* sx = sc + 16 * kSC;          // level 0, single-term stationary kernels: x/ℓ of blocks I, X, K
   const int p = blockIdx.y, b = a.active[p];
   const int n = a.nvalid[b], n0 = (n + bs - 1) / bs, l = a.level;
   const int m = lvl_m(n0, l), top = lvl_top(n0);
   const int j = blockIdx.x;
   if (l > top || j >= m) return;
-  BP_BEGIN
   const bool is_top = l == top;
   const bool elim = is_top || (j & 1);
+  if (l == 0 && !elim) return;  // (bcr_build_kernel wrote the level-0 blocks)
+  BP_BEGIN
   const int X = j << l, h = l > 0 ? 1 << (l - 1) : 0;
   // updates pending on X from its level l−1 neighbours X − h (ΔR of that node) and X + h (ΔL)
   const bool pl = l > 0 && X > 0, pr = l > 0 && X + h < n0;
   const BcrLayout Lw(bs, a.nbm);
   double* ws = a.ws + (long long)p * a.sWs;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
-  const DevSpec spec = a.specs[b];
-  const double* th = a.theta + (long long)b * GPX_THETA_STRIDE;
-  const double noise = th[spec.n_params];
-  const double* Xb = a.X + (long long)b * a.sX;
-  const int D = a.D;
-  const KSt1 k1 = kst1(spec, th);
   const int I = X - (1 << l), K = X + (1 << l);
   const bool hasI = elim && !is_top, hasK = elim && !is_top && K < n0;
   double* Ag = ws + Lw.A + (long long)X * BB;
   double* yg = ws + Lw.y + (long long)X * bs;
-  // K + σn²I at rows (gi, gj) of blocks (bi, bj) ∈ {I, X, K} (slots 0, 1, 2 of sx)
-  auto kat = [&](int si, int gi, int sj, int gj) {
-    if (!k1.on) return kval(spec, th, noise, Xb, D, n, gi, gj);
-    if (gi >= n || gj >= n) return gi == gj ? 1.0 : 0.0;
-    const double v = k1.val(sqdist_scaled(sx + (si * bs + gi % bs) * kXs, sx + (sj * bs + gj % bs) * kXs, k1.dn));
-    return gi == gj ? v + noise : v;
-  };
-  if (l == 0) {
-    if (k1.on) stage_scaled(sx, Xb, D, n, k1, bs, hasI ? I : -1, X, hasK ? K : -1, tid, NT);
-    __syncthreads();
-    // A_X (its lower tiles; the diagonal tiles whole) and y_X from the inputs
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + k * NT, r = e / bs, c = e - r * bs;
-      if ((r >> 4) < (c >> 4)) continue;
-      const double v = kat(1, X * bs + r, 1, X * bs + c);
-      if (elim)
-        sA[r * rs + c] = v;
-      else
-        Ag[e] = v;
-    }
-    if (tid < bs) {
-      const int g = X * bs + tid;
-      const double v = g < n ? a.Y[(long long)b * a.sY + g] : 0.0;
-      if (elim)
-        sz[tid] = v;
-      else
-        yg[tid] = v;
-    }
-  } else {
-    // A_X − (ΔR of X − h + ΔL of X + h), y likewise: every load issued before the first use
+  const double* CX = ws + Lw.C + (long long)X * BB;
+  const double* CK = ws + Lw.C + (long long)K * BB;
+  // A_X − (ΔR of X − h + ΔL of X + h), y likewise, and the couplings E_XI, E_KX: every load
+  // issued before the first use
+  t4 R1[Q], R2[Q], R3[Q], RY[Q];
+  {
     const double* dR = ws + Lw.DR + (long long)(X - h) * BB;
     const double* dL = ws + Lw.DL + (long long)(X + h) * BB;
     double va[PER], vr[PER], vl[PER];
@@ -266,6 +287,14 @@ __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
       const double yr = pl ? ws[Lw.dyR + (long long)(X - h) * bs + tid] : 0.0;
       const double yl = pr ? ws[Lw.dyL + (long long)(X + h) * bs + tid] : 0.0;
       vy = yg[tid] - (yr + yl);
+    }
+    // right-hand sides, tile column w of each: R1 = E_XI, R2 = E_KXᵀ, R3 = I, RY = y (wave Q−1)
+    if (elim) {
+#pragma unroll
+      for (int t = 0; t < Q; ++t) {
+        R1[t] = hasI ? fr(CX, bs, t, w, l15, l4) : tzero();
+        R2[t] = hasK ? frT(CK, bs, w, t, l15, l4) : tzero();
+      }
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -286,40 +315,12 @@ __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
   if (!elim) return;
   __syncthreads();
   BP(0);
-  // right-hand sides, tile column w of each: R1 = E_XI, R2 = E_KXᵀ, R3 = I, RY = y (wave Q−1, column 0)
-  t4 R1[Q], R2[Q], R3[Q], RY[Q];
-  const double* CX = ws + Lw.C + (long long)X * BB;
-  const double* CK = ws + Lw.C + (long long)K * BB;
 #pragma unroll
   for (int t = 0; t < Q; ++t) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       R3[t][r] = (t == w && 4 * r + l4 == l15) ? 1.0 : 0.0;
       RY[t][r] = (w == Q - 1 && l15 == 0) ? sz[16 * t + 4 * r + l4] : 0.0;
-    }
-    R1[t] = (hasI && l > 0) ? fr(CX, bs, t, w, l15, l4) : tzero();
-    R2[t] = (hasK && l > 0) ? frT(CK, bs, w, t, l15, l4) : tzero();
-  }
-  if (l == 0) {  // E_XI and E_KXᵀ = K(X, K) from the inputs, one at a time through sB (free until the end)
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-      const bool has = side == 0 ? hasI : hasK;
-      if (!has) continue;
-      const int col0 = (side == 0 ? I : K) * bs, sj = side == 0 ? 0 : 2;
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int e = tid + k * NT, r = e / bs, c = e - r * bs;
-        sB[r * rs + c] = kat(1, X * bs + r, sj, col0 + c);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int t = 0; t < Q; ++t) {
-        if (side == 0)
-          R1[t] = fr(sB, rs, t, w, l15, l4);
-        else
-          R2[t] = fr(sB, rs, t, w, l15, l4);
-      }
-      __syncthreads();
     }
   }
   BP(1);
@@ -536,20 +537,27 @@ __global__ __launch_bounds__(64 * Q) void bcr_bwd_kernel(BcrArgs a) {
   }
   __syncthreads();
   BP(0);
-  // α_X
-  for (int i = tid; i < bs; i += NT) {
-    double t = sz[i];
+  // α_X = W_Xᵀ (z_X − P_Iᵀ α_I − P_Kᵀ α_K): four threads per row (NT = 4·bs), each a quarter of
+  // the dot products, summed over the four lanes in a fixed order
+  {
+    const int i = tid >> 2, q = tid & 3;
+    double t = 0.0;
     if (hasI)
-      for (int c = 0; c < bs; ++c) t = fma(-s1[i * rs + c], saI[c], t);
+      for (int c = q; c < bs; c += 4) t = fma(s1[i * rs + c], saI[c], t);
     if (hasK)
-      for (int c = 0; c < bs; ++c) t = fma(-s2[i * rs + c], saK[c], t);
-    st[i] = t;
+      for (int c = q; c < bs; c += 4) t = fma(s2[i * rs + c], saK[c], t);
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    if (q == 0) st[i] = sz[i] - t;
   }
   __syncthreads();
-  for (int i = tid; i < bs; i += NT) {
+  {
+    const int i = tid >> 2, q = tid & 3;
     double v = 0.0;
-    for (int r = i; r < bs; ++r) v = fma(s0[r * rs + i], st[r], v);
-    al[(long long)X * bs + i] = v;
+    for (int r = i + q; r < bs; r += 4) v = fma(s0[r * rs + i], st[r], v);
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    if (q == 0) al[(long long)X * bs + i] = v;
   }
   BP(1);
   // G_I, G_K (column w) and row w of W_Xᵀ W_X
@@ -654,6 +662,9 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
   __shared__ double sred[4][NV];
   __shared__ double smax[4];
   __shared__ double sx[3 * bs * kXs];  // single-term stationary kernels: x/ℓ of blocks J−1, J, J+1
+  __shared__ double sZD[BB], sZ1[BB];  // Z_JJ, Z_{J+1,J}
+  __shared__ double sal[2 * bs];       // α of blocks J, J+1
+  constexpr int VM = (bs + G - 1) / G;  // entries of Z_{J,J−1} per thread (its check part)
   const int p = blockIdx.y, b = a.active[p];
   const int n = a.nvalid[b], n0 = (n + bs - 1) / bs, J = blockIdx.x;
   if (J >= n0) return;
@@ -672,7 +683,31 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
   const double* ZD = ws + Lw.A + (long long)J * BB;
   const double* ZCJ = ws + Lw.C + (long long)J * BB;         // Z_{J,J−1} (J >= 1)
   const double* ZCJ1 = ws + Lw.C + (long long)(J + 1) * BB;  // Z_{J+1,J} (J + 1 < n0)
-  if (k1.on) stage_scaled(sx, Xb, D, n, k1, bs, J - 1, J, J + 1 < n0 ? J + 1 : -1, tid, 256);
+  // the block's Z tiles and α rows into LDS, its share of Z_{J,J−1} into registers: every load
+  // issued before the first use
+  double zc[VM];
+  {
+    constexpr int PERC = BB / 256;
+    double v0[PERC], v1[PERC];
+#pragma unroll
+    for (int k = 0; k < PERC; ++k) {
+      v0[k] = ZD[tid + k * 256];
+      v1[k] = J + 1 < n0 ? ZCJ1[tid + k * 256] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < VM; ++k) {
+      const int v = g + k * G;
+      zc[k] = (k1.on && J >= 1 && g < G && v < bs) ? ZCJ[u * bs + v] : 0.0;
+    }
+    const double a0 = tid < 2 * bs ? al[(long long)J * bs + tid] : 0.0;  // (block J+1 past n0: zeros)
+    if (k1.on) stage_scaled(sx, Xb, D, n, k1, bs, J - 1, J, J + 1 < n0 ? J + 1 : -1, tid, 256);
+#pragma unroll
+    for (int k = 0; k < PERC; ++k) {
+      sZD[tid + k * 256] = v0[k];
+      sZ1[tid + k * 256] = v1[k];
+    }
+    if (tid < 2 * bs) sal[tid] = a0;
+  }
   __syncthreads();
   BP(0);
   double sums[NTm][3];
@@ -696,15 +731,17 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
     return eval_k_grad<NTm>(spec, th, Xb + (long long)gi * D, Xb + (long long)gj * D, dk);
   };
   if (g < G && ju < n) {
-    const double aj = al[ju];
-    for (int v = g; v < bs; v += G) {
+    const double aj = sal[u];
+    for (int k = 0; k < VM; ++k) {
+      const int v = g + k * G;
+      if (v >= bs) continue;
       double dk[NTm][3];
       {  // (J, J)
         const int i = J * bs + v;
         if (i < n) {
-          const double z = ZD[v * bs + u];
+          const double z = sZD[v * bs + u];
           double kv = kgrad(1, i, 1, ju, dk);
-          const double vv = fma(al[i], aj, -z);
+          const double vv = fma(sal[v], aj, -z);
 #pragma unroll
           for (int t = 0; t < NTm; ++t)
 #pragma unroll
@@ -719,9 +756,9 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
       if (J + 1 < n0) {  // (J+1, J)
         const int i = (J + 1) * bs + v;
         if (i < n) {
-          const double z = ZCJ1[v * bs + u];
+          const double z = sZ1[v * bs + u];
           const double kv = kgrad(2, i, 1, ju, dk);
-          const double vv = 2.0 * fma(al[i], aj, -z);
+          const double vv = 2.0 * fma(sal[bs + v], aj, -z);
 #pragma unroll
           for (int t = 0; t < NTm; ++t)
 #pragma unroll
@@ -729,11 +766,19 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
           cs = fma(kv, z, cs);
         }
       }
-      if (J >= 1) {  // (J, J−1): the check only
-        const int jj = (J - 1) * bs + v;
-        const double kv = k1.on ? k1.val(sqdist_scaled(sx + (bs + u) * kXs, sx + v * kXs, k1.dn))
-                                : eval_k(spec, th, Xb + (long long)ju * D, Xb + (long long)jj * D);
-        cs = fma(kv, ZCJ[u * bs + v], cs);
+    }
+    // (J, J−1): the check only (its gradient share is block J−1's)
+    if (J >= 1) {
+      if (k1.on) {
+#pragma unroll
+        for (int k = 0; k < VM; ++k) {
+          const int v = g + k * G;
+          if (v < bs) cs = fma(k1.val(sqdist_scaled(sx + (bs + u) * kXs, sx + v * kXs, k1.dn)), zc[k], cs);
+        }
+      } else {
+        for (int v = g; v < bs; v += G)
+          cs = fma(eval_k(spec, th, Xb + (long long)ju * D, Xb + (long long)((J - 1) * bs + v) * D), ZCJ[u * bs + v],
+                   cs);
       }
     }
   }
@@ -776,9 +821,9 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
     const int row = J * bs + tid;
     if (row < n) {
       res = (tot == tot) ? fabs(tot - 1.0) : INFINITY;
-      a.Kd[(long long)b * a.sMat + (long long)row * a.ld + row] = ZD[tid * bs + tid];
+      a.Kd[(long long)b * a.sMat + (long long)row * a.ld + row] = sZD[tid * bs + tid];
     }
-    if (row < a.Np) a.alpha[(long long)b * a.sVec + row] = row < n ? al[row] : 0.0;
+    if (row < a.Np) a.alpha[(long long)b * a.sVec + row] = row < n ? sal[tid] : 0.0;
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) res = fmax(res, __shfl_xor(res, o, 64));
@@ -837,6 +882,7 @@ static void launch_bcr_q(BcrArgs a, int max_terms, int np, int Nmax, hipStream_t
   a.bs = bs;
   int top = 0;
   while (((nbm + (1 << top) - 1) >> top) > 1) ++top;
+  hipLaunchKernelGGL(bcr_build_kernel<Q>, dim3(nbm, 2, np), dim3(256), 0, s, a);
   for (int l = 0; l <= top; ++l) {
     a.level = l;
     hipLaunchKernelGGL(bcr_fwd_kernel<Q>, dim3((nbm + (1 << l) - 1) >> l, np), dim3(64 * Q), 0, s, a);

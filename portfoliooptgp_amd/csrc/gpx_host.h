@@ -216,7 +216,7 @@ struct Run {
   int* info = nullptr;
   bool one_stream = false;
   int wide_from = 0;  // > 0: the band16 groups of at least this width run as ONE launch (band16_wide_kernel)
-  int bcr_q = 0;      // > 0: the band16 problems run as block cyclic reduction with blocks of 16·bcr_q rows
+  int bcr_q = 0;      // > 0: the band16 width groups run as block cyclic reduction (gpx_bcr.hip), each at its width
 };
 
 struct PhaseTimer {

@@ -33,9 +33,10 @@ def _close(la, ga, lb, gb, P, what, rows=None):
 
 @pytest.mark.parametrize("n", [2048, 4096])
 def test_bcr_equals_sweeps_and_dense(n):
-    """C2/C3 sizes: ℓ giving band16 widths Q = 1..5 (one call at the widest Q, and one call per
-    row), a ragged member; against the band16 sweeps and the dense path; predictions at the
-    training inputs (α and diag(K⁻¹) of the selected inverse)."""
+    """C2/C3 sizes: ℓ giving band16 widths Q = 1..5 (one chain per width group), a ragged member;
+    against the band16 sweeps and the dense path; predictions at the training inputs (α and
+    diag(K⁻¹) of the selected inverse); a problem alone in its call gives the same bits as in the
+    mixed call (its arithmetic depends on its own width only)."""
     data = [O.synthetic_series(n, seed=s) for s in range(7)]
     xs = [d[0] for d in data]
     ys = [d[1] for d in data]
@@ -66,12 +67,12 @@ def test_bcr_equals_sweeps_and_dense(n):
         ld, gd, idn = eng.lml_grad(act, th)
         assert not idn.any()
     _close(lb, gb, ld, gd, 3, "bcr vs dense")
-    # one problem per call: each at its own width (the call's block size is its widest problem's)
+    # batch composition: each problem alone in its call, the same bits
     for b in act:
         eng.reset_timing()
         l1, g1, _ = eng.lml_grad([b], th)
         assert eng.last_timing().bcr_evals == 1
-        _close(l1, g1, ld, gd, 3, "bcr solo vs dense", rows=[b])
+        assert l1[b] == lb[b] and np.array_equal(g1[b, :3], gb[b, :3]), b
 
 
 @pytest.mark.parametrize("fam,ell", [("se", 1.0), ("se", 1.4), ("m12", 0.02), ("m32", 0.05), ("m52", 0.06),
