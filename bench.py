@@ -939,6 +939,11 @@ def main():
                       "problems_per_call": tm["band_evals"] / max(tm["band_calls"], 1.0)},
         "host": host,
         "roofline": roofline,
+        "box_cache": {"note": "the timed fits cycle over 512 resident series (12 fits each per step), marked immutable: "
+                              "a rebind reuses the series' band boxes. Fresh series pay the box download and one stream "
+                              "synchronise per call: GPX_BOX_CACHE=0 on the same box, 13431 vs 14192 fits/s (-5.3 %, "
+                              "profiles/r05_ab.md)", "fresh_series_fits_per_s_same_box": 13431.2,
+                      "cached_fits_per_s_same_box": 14191.8},
     }
     if parts[0][6] is not None:
         out["wave_trace"] = wave_trace_summary([p[6] for p in parts], elapsed)
