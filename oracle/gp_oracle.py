@@ -482,7 +482,19 @@ class OGPR:
             p.set_u(float(v))
 
     def _Ky(self):
-        K = self.kernel.K(self.X)
+        """K + σn²I; a NOT_PD outcome (np.linalg.LinAlgError, as the Cholesky would give) where it
+        cannot be formed: a hyperparameter outside (0, inf) — e.g. a Periodic period or lengthscale
+        driven to 0 by a chaotic L-BFGS-B path, where sin(π·Δ/p)/ℓ is 0/0 — or a non-finite entry.
+        The device reports the same points as not positive definite (its pivot test !(p > 0) fails on
+        NaN) or as out-of-domain hyperparameters (InvalidParameterError); GPflow's fit raises out of
+        Scipy.minimize there (GPR/model_trainer.py:18-19 catches nothing)."""
+        for prm in self.kernel.params() + [self.noise]:
+            if not (np.isfinite(prm.value) and prm.value > 0.0):
+                raise np.linalg.LinAlgError(f"hyperparameter {prm.name}={prm.value} outside (0, inf): not positive definite")
+        with np.errstate(all="ignore"):
+            K = self.kernel.K(self.X)
+        if not np.all(np.isfinite(K)):
+            raise np.linalg.LinAlgError("K has non-finite entries: not positive definite")
         return K + self.noise.value * np.eye(K.shape[0])
 
     def log_marginal_likelihood(self) -> float:
@@ -511,7 +523,10 @@ class OGPR:
         Wm = np.outer(alpha, alpha) - Kinv
         grads = []
         kparams = self.kernel.params()
-        dks = self.kernel.dK(self.X)
+        # (at a degenerate θ — ℓ ~ 1e-300 after a chaotic path — a ∂K/∂θ entry can be 0·inf = NaN:
+        # reported as such, the caller compares the finite components)
+        with np.errstate(all="ignore"):
+            dks = self.kernel.dK(self.X)
         for p, dk in zip(kparams, dks):
             if p.trainable:
                 grads.append(0.5 * float(np.sum(Wm * dk)) * p.dtheta_du())
@@ -547,7 +562,9 @@ class OGPR:
         lml = -0.5 * (z @ z) - np.sum(np.log(np.diag(L))) - ld(0.5) * n * ld(LOG2PI)
         Wm = np.outer(alpha, alpha) - Kinv
         grads = []
-        for p, dk in zip(self.kernel.params(), self.kernel.dK(self.X)):
+        with np.errstate(all="ignore"):
+            dks = self.kernel.dK(self.X)
+        for p, dk in zip(self.kernel.params(), dks):
             if p.trainable:
                 grads.append(float(ld(0.5) * np.sum(Wm * dk.astype(ld))) * p.dtheta_du())
         if self.noise.trainable:
