@@ -188,6 +188,25 @@ def band_traffic(kernel_key, problems_per_launch):
     return d["hbm_bytes_per_problem"] * problems_per_launch, os.path.relpath(f, root)
 
 
+def trace_check(kernel_key):
+    """The committed rocprofv3 check of the roofline kernel's launch time in the headline layout
+    (profiles/<round>_trace_multi.json, tools/trace_multi.py via tools/profile_round5.sh: 8
+    concurrent traced instances): trace average vs the instances' HIP events and vs that round's
+    default bench line. None when absent."""
+    import glob
+    root = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(root, "profiles", "*_trace_multi.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel_key)
+    if k is None:
+        return None
+    return {"source": os.path.relpath(files[-1], root), "trace_avg_launch_ms": k["trace_avg_launch_ms"],
+            "rel_diff_trace_vs_instances_hip_events": k["rel_diff_trace_vs_instances"],
+            "rel_diff_trace_vs_that_rounds_bench_line": k["rel_diff_trace_vs_reference_bench"]}
+
+
 def band_problem_flops(n, p, fwd):
     """2·64³ block-product flops of one problem's fused sweep (gpx_api.hip band_fused_flops)."""
     U = 2.0 * 64 ** 3
@@ -872,6 +891,7 @@ def main():
             # MFMA fraction is reported as the contract's roofline, `occupancy` beside it
             "bound": "latency" if b16 else "mfma", "achieved": k["achieved"], "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": k["frac"], "traffic": k["traffic"], "traffic_source": k["traffic_source"],
+            "trace_check": trace_check(kname),
             "occupancy": (tm["band16_wave_ms"] / (WAVE_SLOTS * elapsed * 1e3)) if b16 else None,
             "occupancy_note": (f"sum over band16 launches of problems x HIP-event launch ms, over {WAVE_SLOTS} wave "
                                "slots (256 CUs x 4 SIMDs x 2 sweeps per SIMD) x the timed wall ms") if b16 else None,

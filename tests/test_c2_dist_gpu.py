@@ -5,7 +5,8 @@ configuration fitted through the bench's own path against the oracle's whole fit
 Protocol: GPR/model_trainer.py:15-20 — GPflow defaults (σ² = ℓ = 1), σn² = 1e-5 fixed,
 Scipy().minimize(maxiter=100), predict_f at the training inputs; inputs the C2 generator
 (X = day offsets 0..4095). The path under test is bench.py's: band-storage slots, the band16
-sweeps, Scipy.minimize_stream over a ModelStream in two device groups.
+sweeps or block cyclic reduction (both routes, the `route` fixture), Scipy.minimize_stream over a
+ModelStream in two device groups.
 
 Asserted per seed: loss* within 1e-5 relative of the oracle's fit (SURVEY §8c's bar), θ* within
 1e-4, and the GPU's loss and gradient at its own θ* equal to the CPU restatement's there (loss
@@ -37,7 +38,21 @@ K = gpx.kernels
 NOISE = 1e-5
 
 
-def test_c2_fits_in_distribution(golden_dir):
+@pytest.fixture(params=["bcr", "sweeps"], autouse=True)
+def route(request, monkeypatch):
+    """Both banded routes of a call: block cyclic reduction for every call
+    (GPX_BCR_MAX far above the problems per call) and the band16 sweeps (GPX_BCR_MAX=0). By default
+    the library sends a call to BCR when it holds at most 32 band16 problems."""
+    monkeypatch.setenv("GPX_BCR_MAX", "1000000" if request.param == "bcr" else "0")
+    return request.param
+
+
+def _check_route(engines, route):
+    bcr = sum(e.last_timing().bcr_evals for e in engines)
+    assert (bcr > 0) == (route == "bcr"), (route, bcr)
+
+
+def test_c2_fits_in_distribution(golden_dir, route):
     from oracle import band_oracle as BO
     from oracle import gp_oracle as O
     fx = np.load(os.path.join(golden_dir, "c2_dist_n4096.npz"))
@@ -62,6 +77,7 @@ def test_c2_fits_in_distribution(golden_dir):
                                                     predict_train=True, options=dict(maxiter=100))
     evals = sum(e.last_timing().evals for e in engines)
     assert sum(e.last_timing().band_evals for e in engines) == evals > 0
+    _check_route(engines, route)
     nf_gpu, nf_ora = [], []
     worst = dict(loss=0.0, theta=0.0, at_loss=0.0, at_grad=0.0)
     for i, (s, r) in enumerate(zip(seeds, res)):
@@ -101,12 +117,15 @@ def _fit_on_device(data, n):
     models = gpx.optimizers.ModelStream(len(data), model, input_dim=1, max_points=n)
     spec = compile_spec(K.SquaredExponential(), 1)
     engines = [Engine([data[g][0]], [data[g][1]], [spec], band_storage=True) for g in range(2)]
+    for e in engines:
+        e.ctx.set_profiling(True)
+        e.reset_timing()
     res, _ = gpx.optimizers.Scipy().minimize_stream(models, width=len(data), engine=engines, groups=2,
                                                     predict_train=True, options=dict(maxiter=100))
-    return models, res
+    return models, res, engines
 
 
-def test_c2_nfev_population_vs_band_oracle(golden_dir):
+def test_c2_nfev_population_vs_band_oracle(golden_dir, route):
     """512 C2 seeds through the bench's path against the band oracle's fits of the same seeds:
     every fitted loss within 1e-5 and θ* within 1e-4, and the mean evaluations per fit within
     ±10 % (VERDICT r03 item 5's bar; the population's standard error is ~0.4 evaluations, ~2 %)."""
@@ -115,7 +134,8 @@ def test_c2_nfev_population_vs_band_oracle(golden_dir):
     n = int(fx["n"][0])
     seeds = [int(s) for s in fx["seeds"]]
     data = [O.synthetic_series(n, s) for s in seeds]
-    models, res = _fit_on_device(data, n)
+    models, res, engines = _fit_on_device(data, n)
+    _check_route(engines, route)
     nf = np.array([r.nfev for r in res], dtype=np.float64)
     worst_l = worst_t = 0.0
     for i, (s, r) in enumerate(zip(seeds, res)):

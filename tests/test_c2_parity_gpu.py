@@ -4,7 +4,8 @@ through the bench's own path, against oracle fixtures committed by tests/golden/
 C2 = synthetic 1-D series, N = 4096, X = day offsets 0..4095, SquaredExponential at GPflow's
 defaults, σn² = 1e-5 fixed, Scipy().minimize(maxiter=100), predict_f at the training inputs
 (GPR/model_trainer.py:15-20). The path under test is bench.py's: band-storage slots
-(gpx_batch_create_banded), the fused banded sweeps, the stepped L-BFGS-B driver
+(gpx_batch_create_banded), the band16 sweeps or block cyclic reduction (both routes, the
+`route` fixture), the stepped L-BFGS-B driver
 (Scipy.minimize_stream over a ModelStream) and predict at the training inputs from the banded
 factor. The fixtures use GPflow's square_distance form of r² (oracle R2_FORM "gpflow"), as
 the device does.
@@ -28,6 +29,20 @@ N_C2 = 4096
 NOISE = 1e-5
 
 
+@pytest.fixture(params=["bcr", "sweeps"], autouse=True)
+def route(request, monkeypatch):
+    """Both banded routes of a call: block cyclic reduction for every call
+    (GPX_BCR_MAX far above the problems per call) and the band16 sweeps (GPX_BCR_MAX=0). By default
+    the library sends a call to BCR when it holds at most 32 band16 problems."""
+    monkeypatch.setenv("GPX_BCR_MAX", "1000000" if request.param == "bcr" else "0")
+    return request.param
+
+
+def _check_route(engines, route):
+    bcr = sum(e.last_timing().bcr_evals for e in engines)
+    assert (bcr > 0) == (route == "bcr"), (route, bcr)
+
+
 @pytest.fixture(scope="module")
 def c2(golden_dir):
     return np.load(os.path.join(golden_dir, "c2_n4096.npz"))
@@ -46,7 +61,7 @@ def _model(y, ell=None):
 
 
 @pytest.mark.parametrize("band_storage", [True, False])
-def test_c2_fixed_theta_logml_and_gradient(c2, band_storage):
+def test_c2_fixed_theta_logml_and_gradient(c2, band_storage, route):
     """logML and ∂loss/∂u at ℓ ∈ {1, 1.18, 1.72} (σ² = 1) for seeds 0 and 1: six problems in
     one batched call, every one through the banded path (band storage = the bench's slots;
     and the dense-layout batch the general API uses)."""
@@ -65,6 +80,8 @@ def test_c2_fixed_theta_logml_and_gradient(c2, band_storage):
     t = eng.last_timing()
     assert not info.any()
     assert t.band_evals == len(models) and t.band_fallbacks == 0 and t.shadow_evals == 0
+    if band_storage:
+        _check_route([eng], route)
     worst_l, worst_g = 0.0, 0.0
     for b, (m, r) in enumerate(zip(models, refs)):
         loss, g = m.loss_and_grad_unconstrained(lml=lml[b], grad_theta=grad[b])
@@ -79,7 +96,7 @@ def test_c2_fixed_theta_logml_and_gradient(c2, band_storage):
     print(f"C2 fixed-θ parity (band_storage={band_storage}): logML rel {worst_l:.2e}, grad rel {worst_g:.2e}")
 
 
-def test_c2_loss_along_the_oracle_trajectory(c2):
+def test_c2_loss_along_the_oracle_trajectory(c2, route):
     """The GPU's loss at every point the oracle's L-BFGS-B requested (fit|hist_u) equals the
     oracle's (rel 1e-9): the fit sees the same function all along its path, not only at θ*."""
     for s in (0, 1):
@@ -90,14 +107,17 @@ def test_c2_loss_along_the_oracle_trajectory(c2):
                 v.assign(ui)
         eng = Engine([m.data[0] for m in models], [m.data[1] for m in models],
                      [compile_spec(m.kernel, 1) for m in models], band_storage=True)
+        eng.ctx.set_profiling(True)
+        eng.reset_timing()
         th = np.stack([m.theta_row() for m in models])
         lml, _, info = eng.lml_grad(list(range(len(models))), th)
         assert not info.any()
+        _check_route([eng], route)
         rel = np.abs(-lml - hf) / np.abs(hf)
         assert rel.max() <= 1e-9, (s, rel.max(), int(rel.argmax()))
 
 
-def test_c2_full_fit_and_predict_through_bench_path(c2):
+def test_c2_full_fit_and_predict_through_bench_path(c2, route):
     """Two C2 fits exactly as bench.py runs them: a ModelStream of fresh GPR models (GPflow
     defaults, σn² = 1e-5 frozen), minimize_stream over band-storage slots in two device
     groups, predict_f at the training inputs. Against the oracle's fit: loss* rel 1e-5,
@@ -118,6 +138,7 @@ def test_c2_full_fit_and_predict_through_bench_path(c2):
     evals = sum(e.last_timing().evals for e in engines)
     band = sum(e.last_timing().band_evals for e in engines)
     assert band == evals > 0          # every evaluation took the banded path, as in the bench
+    _check_route(engines, route)
     for s, (r, (mu, var)) in enumerate(zip(res, preds)):
         p = f"s{s}|"
         assert r.fun == pytest.approx(float(c2[p + "fit|loss"][0]), rel=1e-5)
