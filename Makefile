@@ -6,8 +6,16 @@ LIB := portfoliooptgp_amd/libgpx.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 
 CSMOKE := tests/c/gpx_c_smoke
+# the L-BFGS-B driver loop in C++ (CPython extension calling scipy's setulb; lbfgsb.BatchStepper)
+PYINC := $(shell python3 -c "import sysconfig; print(sysconfig.get_paths()['include'])")
+PYEXT := $(shell python3 -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
+LOOPMOD := portfoliooptgp_amd/_gpx_lbfgsb$(PYEXT)
 
-all: $(LIB) $(CSMOKE)
+all: $(LIB) $(CSMOKE) $(LOOPMOD)
+
+$(LOOPMOD): $(CSRC)/gpx_lbfgsb_host.cpp
+	g++ -O2 -std=c++17 -fPIC -shared -Wall -Wextra -Wno-missing-field-initializers -Wno-cast-function-type \
+	  -I$(PYINC) $< -o $@
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/gpx_internal.h $(CSRC)/gpx_host.h $(CSRC)/gpx_kfun.h $(CSRC)/gpx_leaf.h $(CSRC)/gpx_b16core.h include/gpx.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

@@ -246,6 +246,16 @@ int gpx_batch_predict_train(gpx_batch* batch, int n_active, const int32_t* activ
                             int32_t* info, void* stream);
 
 /*
+ * gpx_batch_predict_train with the outputs packed by position: mean, var : device fp64
+ * [n_active, N_max], row i for problem active[i] (rows < n[active[i]] written). A caller that
+ * keeps each fit's prediction (the stepped drivers: a few dozen finished fits per round of a
+ * 1024-slot batch) allocates only those rows. Same values as gpx_batch_predict_train.
+ */
+int gpx_batch_predict_train_rows(gpx_batch* batch, int n_active, const int32_t* active,
+                                 const double* theta, int add_noise, double* mean, double* var,
+                                 int32_t* info, void* stream);
+
+/*
  * Posterior mean and FULL covariance at Xnew: GPflow GPR.predict_f(Xnew, full_cov=True)
  * (GPflow returns the covariance as [1, M, M]; predict_y has no full_cov form in GPflow).
  *   Xnew : device fp64 [B, M, D];  mean : device fp64 [B, M];  cov : device fp64 [B, M, M].

@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "gpx_batch_rebind_device", "gpx_batch_rebind_device_boxed", "gpx_batch_slot_boxes",
     "gpx_batch_destroy", "gpx_batch_lml_grad", "gpx_batch_lml_grad_submit", "gpx_batch_lml_grad_complete",
     "gpx_batch_lml_grad_query", "gpx_batch_band_width",
-    "gpx_batch_predict", "gpx_batch_predict_full_cov", "gpx_batch_predict_train",
+    "gpx_batch_predict", "gpx_batch_predict_full_cov", "gpx_batch_predict_train", "gpx_batch_predict_train_rows",
     "gpx_batch_last_timing",
     "gpx_set_profiling", "gpx_batch_reset_timing", "gpx_batch_rebind",
     "gpx_batch_wave_trace", "gpx_batch_wave_trace_read", "gpx_batch_band_class",
@@ -154,6 +154,9 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_predict_train.restype = c_int
         lib.gpx_batch_predict_train.argtypes = [c_void_p, c_int, c_int_p, c_double_p, c_int, c_void_p,
                                                 c_void_p, c_int_p, c_void_p]
+        lib.gpx_batch_predict_train_rows.restype = c_int
+        lib.gpx_batch_predict_train_rows.argtypes = [c_void_p, c_int, c_int_p, c_double_p, c_int, c_void_p,
+                                                     c_void_p, c_int_p, c_void_p]
         lib.gpx_batch_last_timing.restype = c_int
         lib.gpx_batch_last_timing.argtypes = [c_void_p, ctypes.POINTER(GpxTiming)]
         lib.gpx_batch_rebind.restype = c_int

@@ -1115,6 +1115,7 @@ static int batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, 
       hipMalloc(&bt->ldiag, vec) != hipSuccess ||
       hipMalloc(&bt->partial, (size_t)B * bt->partial_stride * sizeof(double)) != hipSuccess ||
       hipMalloc(&bt->d_n, sizeof(int) * B) != hipSuccess ||
+      hipMalloc(&bt->d_orow, sizeof(int) * B) != hipSuccess ||
       hipMalloc(&bt->d_specs, sizeof(DevSpec) * B) != hipSuccess)
     return cleanup("out of device memory for batch vectors");
   {
@@ -1239,7 +1240,7 @@ int gpx_batch_destroy(gpx_batch* bt) {
   for (void* p : {(void*)bt->shX, (void*)bt->shY, (void*)bt->d_wtrace, (void*)bt->d_wtrace_n})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
-                  (void*)bt->ldiag, (void*)bt->partial, (void*)bt->d_io, (void*)bt->d_n,
+                  (void*)bt->ldiag, (void*)bt->partial, (void*)bt->d_io, (void*)bt->d_n, (void*)bt->d_orow,
                   (void*)bt->d_specs, (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw,
                   (void*)bt->bres, (void*)bt->bcr_ws})
     if (p) (void)hipFree(p);
@@ -2307,7 +2308,7 @@ int gpx_batch_lml_grad(gpx_batch* bt, int n_active, const int32_t* active, const
 // (cov != nullptr).
 static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
                         const double* Xnew, int M, int add_noise, double* mean, double* var,
-                        double* cov, int32_t* info, void* stream, bool train = false) {
+                        double* cov, int32_t* info, void* stream, bool train = false, bool rows = false) {
   if (!bt) return GPX_BAD_ARG;
   gpx_ctx* ctx = bt->ctx;
   if ((!train && (!Xnew || M <= 0)) || !mean || !(var || cov) || !info)
@@ -2329,6 +2330,17 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   // this θ stays here; every other problem is predicted on the dense fallback slots, one by one
   std::vector<int32_t> keep;
   int shadow_status = GPX_OK;
+  // rows (train only): outputs [n_active, Nmax], row i for active[i]; orow[b] = i
+  std::vector<int32_t> orow;
+  if (rows) {
+    if (!train || n_active <= 0 || n_active > bt->B || !active) return fail(ctx, GPX_BAD_ARG, "bad active set");
+    orow.assign(bt->B, 0);
+    for (int i = 0; i < n_active; ++i) {
+      if (active[i] < 0 || active[i] >= bt->B) return fail(ctx, GPX_BAD_ARG, "active index out of range");
+      orow[active[i]] = i;
+    }
+  }
+  auto out_row = [&](int b) -> size_t { return rows ? (size_t)orow[b] : (size_t)b; };
   if (bt->compact) {
     if (n_active <= 0 || n_active > bt->B || !active || !theta)
       return fail(ctx, GPX_BAD_ARG, "bad active set / theta");
@@ -2354,8 +2366,8 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
       std::memcpy(th.data(), theta + (size_t)b * GPX_THETA_STRIDE, sizeof(double) * GPX_THETA_STRIDE);
       inf[0] = 0;
       if (train)
-        rc = predict_impl(sh, 1, &act0, th.data(), nullptr, 0, add_noise, mean + (size_t)b * bt->Nmax,
-                          var + (size_t)b * bt->Nmax, nullptr, inf.data(), s, true);
+        rc = predict_impl(sh, 1, &act0, th.data(), nullptr, 0, add_noise, mean + out_row(b) * bt->Nmax,
+                          var + out_row(b) * bt->Nmax, nullptr, inf.data(), s, true);
       else
         rc = predict_impl(sh, 1, &act0, th.data(), Xnew + (size_t)b * M * bt->D, M, add_noise,
                           mean + (size_t)b * M, var ? var + (size_t)b * M : nullptr,
@@ -2420,6 +2432,10 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
     ta.alpha = bt->alpha; ta.sVec = Np; ta.Y = bt->Y; ta.sY = bt->Nmax; ta.nvalid = bt->d_n;
     ta.specs = bt->d_specs; ta.theta = bt->d_theta; ta.add_noise = add_noise;
     ta.mean = mean; ta.var = var; ta.sOut = bt->Nmax;
+    if (rows) {
+      HIPX(ctx, hipMemcpyAsync(bt->d_orow, orow.data(), sizeof(int) * bt->B, hipMemcpyHostToDevice, s));
+      ta.orow = bt->d_orow;
+    }
     if (n_dense > 0) launch_train_pred(ta, n_dense, Np, s);
     if (n_dense < n_active) {
       // banded: diag(K⁻¹) from the selected inverse in K's diagonal blocks
@@ -2564,6 +2580,12 @@ int gpx_batch_predict_train(gpx_batch* bt, int n_active, const int32_t* active, 
                             int add_noise, double* mean, double* var, int32_t* info, void* stream) {
   return predict_impl(bt, n_active, active, theta, nullptr, 0, add_noise, mean, var, nullptr, info,
                       stream, true);
+}
+
+int gpx_batch_predict_train_rows(gpx_batch* bt, int n_active, const int32_t* active, const double* theta,
+                                 int add_noise, double* mean, double* var, int32_t* info, void* stream) {
+  return predict_impl(bt, n_active, active, theta, nullptr, 0, add_noise, mean, var, nullptr, info,
+                      stream, true, true);
 }
 
 int gpx_batch_predict_full_cov(gpx_batch* bt, int n_active, const int32_t* active,

@@ -286,10 +286,11 @@ __global__ __launch_bounds__(256) void band_train_pred_kernel(TrainPredArgs a) {
   if (j >= n) return;
   const double s2 = a.theta[b * GPX_THETA_STRIDE + a.specs[b].n_params];
   const double zjj = a.W[(long long)b * a.sW + (long long)j * a.ld + j];
-  a.mean[(long long)b * a.sOut + j] = fma(-s2, a.alpha[(long long)b * a.sVec + j], a.Y[(long long)b * a.sY + j]);
+  const long long ro = (a.orow ? a.orow[b] : b) * a.sOut;
+    a.mean[ro + j] = fma(-s2, a.alpha[(long long)b * a.sVec + j], a.Y[(long long)b * a.sY + j]);
   double v = fma(-s2 * s2, zjj, s2);
   if (a.add_noise) v += s2;
-  a.var[(long long)b * a.sOut + j] = v;
+  a.var[ro + j] = v;
 }
 
 void launch_band_train_pred(const TrainPredArgs& a, int n_active, int Np, hipStream_t s) {

@@ -262,7 +262,7 @@ __global__ __launch_bounds__(64 * Q) void bcr_fwd_kernel(BcrArgs a) {
   const BcrLayout Lw(bs, a.nbm);
   double* ws = a.ws + (long long)p * a.sWs;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
-  const int I = X - (1 << l), K = X + (1 << l);
+  const int K = X + (1 << l);
   const bool hasI = elim && !is_top, hasK = elim && !is_top && K < n0;
   double* Ag = ws + Lw.A + (long long)X * BB;
   double* yg = ws + Lw.y + (long long)X * bs;

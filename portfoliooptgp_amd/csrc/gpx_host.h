@@ -33,6 +33,7 @@ struct gpx_batch {
   gpx::DevSpec* d_specs = nullptr;
   double* d_theta = nullptr;
   int* d_active = nullptr;
+  int* d_orow = nullptr;  // gpx_batch_predict_train_rows: output row of each slot
   int* d_info = nullptr;
   double *K = nullptr, *L = nullptr, *W = nullptr;     // [B][Np][Np] (band storage: see below)
   // band storage (gpx_batch_create_banded): K, L, W keep only the 64-block band of width

@@ -92,6 +92,7 @@ struct TrainPredArgs {
   const DevSpec* specs; const double* theta;
   int add_noise;
   double* mean; double* var; long long sOut;
+  const int* orow;  // output row of slot b (null: row b) — gpx_batch_predict_train_rows
   int n_active;                    // set by the launcher (1-D grid: blocks x problems)
 };
 

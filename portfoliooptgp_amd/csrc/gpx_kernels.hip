@@ -927,10 +927,11 @@ __global__ __launch_bounds__(256) void train_pred_kernel(TrainPredArgs a) {
   if (wave == 0 && j < n) {
     const double kinv = (sred[0][lane] + sred[1][lane]) + (sred[2][lane] + sred[3][lane]);
     const double s2 = a.theta[b * GPX_THETA_STRIDE + a.specs[b].n_params];
-    a.mean[(long long)b * a.sOut + j] = fma(-s2, a.alpha[(long long)b * a.sVec + j], a.Y[(long long)b * a.sY + j]);
+    const long long ro = (a.orow ? a.orow[b] : b) * a.sOut;
+    a.mean[ro + j] = fma(-s2, a.alpha[(long long)b * a.sVec + j], a.Y[(long long)b * a.sY + j]);
     double v = fma(-s2 * s2, kinv, s2);
     if (a.add_noise) v += s2;
-    a.var[(long long)b * a.sOut + j] = v;
+    a.var[ro + j] = v;
   }
 }
 

@@ -388,15 +388,19 @@ class Engine:
         (gpx_batch_predict_train). ``column``: each output as an [n, 1] view (GPflow's
         predict_f shape) made by one indexing op per problem."""
         dev = f"cuda:{self.device}"
-        mean = torch.empty(self.B, self.Nmax, dtype=torch.float64, device=dev)
-        var = torch.empty(self.B, self.Nmax, dtype=torch.float64, device=dev)
+        act = np.ascontiguousarray(act, dtype=np.int32)
+        # the predicted rows only, packed by position (gpx_batch_predict_train_rows): a long run
+        # keeps every fit's prediction, so views into [B, Nmax] buffers would keep whole batches'
+        # buffers alive (64 MiB per call at B = 1024)
+        mean = torch.empty(len(act), self.Nmax, dtype=torch.float64, device=dev)
+        var = torch.empty(len(act), self.Nmax, dtype=torch.float64, device=dev)
         info = np.zeros(self.B, dtype=np.int32)
         dp = ctypes.POINTER(ctypes.c_double)
         ip = ctypes.POINTER(ctypes.c_int32)
-        rc = self.lib.gpx_batch_predict_train(self.handle, len(act), act.ctypes.data_as(ip),
-                                              theta.ctypes.data_as(dp), 1 if add_noise else 0,
-                                              ctypes.c_void_p(mean.data_ptr()), ctypes.c_void_p(var.data_ptr()),
-                                              info.ctypes.data_as(ip), self._stream())
+        rc = self.lib.gpx_batch_predict_train_rows(self.handle, len(act), act.ctypes.data_as(ip),
+                                                   theta.ctypes.data_as(dp), 1 if add_noise else 0,
+                                                   ctypes.c_void_p(mean.data_ptr()), ctypes.c_void_p(var.data_ptr()),
+                                                   info.ctypes.data_as(ip), self._stream())
         self._harvest_boxes()
         if rc == N.GPX_NOT_PD:
             bad = [int(b) for b in act if info[b] != 0]
@@ -405,19 +409,14 @@ class Engine:
                 "positive definite", info)
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_predict_train failed ({rc}): {self.ctx.last_error()}")
-        # the predicted rows only, in a compact copy (same stream): views into the [B, Nmax]
-        # buffers would keep the whole batch's buffers alive as long as any one fit's prediction
-        # is referenced (a long run holds every fit's prediction: 64 MiB per call at B = 1024)
-        if len(act) < self.B:
-            idx = torch.as_tensor(np.asarray(act, dtype=np.int64), device=dev)
-            mean, var = mean.index_select(0, idx), var.index_select(0, idx)
-            rows = range(len(act))
-        else:
-            rows = act
         if column:
             mean, var = mean.unsqueeze(-1), var.unsqueeze(-1)
-        return ([mean[k, : self.n[b]] for k, b in zip(rows, act)], [var[k, : self.n[b]] for k, b in zip(rows, act)],
-                info)
+        # one view per problem: unbind makes them in one call, a slice only where n < Nmax
+        ms, vs = mean.unbind(0), var.unbind(0)
+        nb = self.n
+        full = self.Nmax
+        return ([m if nb[b] == full else m[: nb[b]] for m, b in zip(ms, act)],
+                [v if nb[b] == full else v[: nb[b]] for v, b in zip(vs, act)], info)
 
     def rebind(self, b: int, X, Y, spec: N.GpxKernelSpec) -> None:
         """Load a new problem into slot b (continuous batching). Host inputs are staged in

@@ -28,6 +28,10 @@ try:  # scipy ≥ 1.15: the C port of L-BFGS-B (task codes as int32 pairs)
     AVAILABLE = hasattr(_lbfgsb, "setulb") and isinstance(status_messages, dict)
 except Exception:  # pragma: no cover - older scipy: callers use the threaded driver
     AVAILABLE = False
+try:  # the same loop in C++ over a batch of fits (csrc/gpx_lbfgsb_host.cpp), when built
+    from . import _gpx_lbfgsb as _native_loop
+except ImportError:  # pragma: no cover - the Python stepper serves
+    _native_loop = None
 if not AVAILABLE:  # pragma: no cover - said once, at import: the fits still run, more slowly
     import warnings
     warnings.warn("scipy's L-BFGS-B routine setulb (scipy >= 1.15 layout) is not available: batched fits use the "
@@ -87,11 +91,7 @@ class LbfgsbStepper:
     def __init__(self, x0, options: Optional[dict] = None):
         opts = dict(_DEFAULTS)
         opts.update({k: v for k, v in (options or {}).items() if k in _DEFAULTS})
-        x0 = np.atleast_1d(np.asarray(x0))
-        if x0.ndim != 1:
-            raise ValueError("'x0' must only have one dimension.")
-        if x0.dtype.kind in np.typecodes["AllInteger"]:
-            x0 = np.asarray(x0, dtype=float)
+        x0 = _x0(x0)
         if not opts["maxls"] > 0:
             raise ValueError("maxls must be positive.")
         self.nfev = 0
@@ -183,10 +183,110 @@ class LbfgsbStepper:
             warnflag = 1
         else:
             warnflag = 2
-        s = wa[0: m * n].reshape(m, n)
-        y = wa[m * n: 2 * m * n].reshape(m, n)
-        n_corrs = min(isave[30], m)
-        msg = status_messages[task[0]] + ": " + task_messages[task[1]]
-        self._res = _Result(fun=f, jac=g, nfev=self.nfev, njev=self.nfev, nit=n_iterations,
-                            status=warnflag, message=msg, x=x, success=(warnflag == 0),
-                            _sy=(s[:n_corrs], y[:n_corrs]))
+        self._res = _result(x, f, g, wa, task, isave, m, n, self.nfev, n_iterations, warnflag)
+
+
+def _result(x, f, g, wa, task, isave, m, n, nfev, nit, warnflag, copy=False):
+    """scipy's OptimizeResult of a finished run from its work arrays (_minimize_lbfgsb's tail);
+    copy=True when the arrays belong to a reused batch slot."""
+    s = wa[0: m * n].reshape(m, n)
+    y = wa[m * n: 2 * m * n].reshape(m, n)
+    n_corrs = min(isave[30], m)
+    msg = status_messages[task[0]] + ": " + task_messages[task[1]]
+    if copy:
+        x, g, s, y = x.copy(), g.copy(), s[:n_corrs].copy(), y[:n_corrs].copy()
+    else:
+        s, y = s[:n_corrs], y[:n_corrs]
+    return _Result(fun=f, jac=g, nfev=nfev, njev=nfev, nit=nit, status=warnflag, message=msg, x=x,
+                   success=(warnflag == 0), _sy=(s, y))
+
+
+def _x0(x0):
+    x0 = np.atleast_1d(np.asarray(x0))
+    if x0.ndim != 1:
+        raise ValueError("'x0' must only have one dimension.")
+    if x0.dtype.kind in np.typecodes["AllInteger"]:
+        x0 = np.asarray(x0, dtype=float)
+    return x0
+
+
+class BatchStepper:
+    """``cap`` L-BFGS-B runs of dimension ``n`` with common options, advanced by the C++ loop of
+    csrc/gpx_lbfgsb_host.cpp (``_gpx_lbfgsb``): the same loop as LbfgsbStepper around scipy's own
+    ``setulb``, for a whole round of fits in one call (``tell``), so the per-evaluation host cost
+    is the setulb calls themselves. Slot ``i`` holds one run at a time (``start``); ``gather``
+    reads the rows' requested points, ``tell`` hands back their (f, g) and flags the finished
+    ones; ``stepper(i)`` is the LbfgsbStepper-shaped view of one slot."""
+
+    NATIVE = _native_loop is not None
+
+    def __init__(self, cap: int, n: int, options: Optional[dict] = None):
+        if _native_loop is None:
+            raise RuntimeError("the native L-BFGS-B loop (portfoliooptgp_amd/_gpx_lbfgsb*.so) is not built")
+        o = dict(_DEFAULTS)
+        o.update({k: v for k, v in (options or {}).items() if k in _DEFAULTS})
+        if not o["maxls"] > 0:
+            raise ValueError("maxls must be positive.")
+        self.o, self.n, self.m = o, n, o["maxcor"]
+        m = self.m
+        # _minimize_lbfgsb's work arrays (dtypes and sizes), per slot; the bounds stay zero (none)
+        self.arrays = [(np.zeros(n), np.zeros(n), np.zeros(n), np.zeros(n, np.int32), np.zeros(n),
+                        np.zeros(2 * m * n + 5 * n + 11 * m * m + 8 * m), np.zeros(3 * n, np.int32),
+                        np.zeros(2, np.int32), np.zeros(4, np.int32), np.zeros(44, np.int32), np.zeros(29),
+                        np.zeros(2, np.int32)) for _ in range(cap)]
+        factr = o["ftol"] / np.finfo(float).eps
+        self._b = _native_loop.Batch(_lbfgsb.setulb, cap, n, m, float(factr), float(o["gtol"]), int(o["maxls"]),
+                                     int(o["maxiter"]), int(o["maxfun"]), self.arrays)
+        self.gather = self._b.gather  # gather(rows int32[k], out float64[k, n])
+        self.tell = self._b.tell      # tell(rows int32[k], f float64[k], g float64[k, n], done uint8[k])
+
+    def start(self, slot: int, x0) -> "_SlotStepper":
+        x0 = _x0(x0).ravel()
+        if x0.shape[0] != self.n:
+            raise ValueError(f"x0 has {x0.shape[0]} elements, the batch {self.n}")
+        self._b.start(slot, np.ascontiguousarray(x0, dtype=np.float64))
+        return _SlotStepper(self, slot)
+
+    def request(self, slot: int) -> np.ndarray:
+        return np.frombuffer(self._b.request(slot), dtype=np.float64)
+
+    def result(self, slot: int) -> OptimizeResult:
+        state, nfev, nit, f = self._b.state(slot)
+        x, _, _, _, g, wa, _, task, _, isave, _, _ = self.arrays[slot]
+        o = self.o
+        if task[0] == 4:
+            warnflag = 0
+        elif nfev > o["maxfun"] or nit >= o["maxiter"]:
+            warnflag = 1
+        else:
+            warnflag = 2
+        return _result(x, f, g, wa, task, isave, self.m, self.n, nfev, nit, warnflag, copy=True)
+
+
+class _SlotStepper:
+    """LbfgsbStepper's interface over one BatchStepper slot."""
+    __slots__ = ("b", "slot", "_res")
+
+    def __init__(self, b: BatchStepper, slot: int):
+        self.b, self.slot, self._res = b, slot, None
+
+    @property
+    def x(self):
+        return None if self.done else self.b.request(self.slot)
+
+    @property
+    def done(self) -> bool:
+        return self.b._b.state(self.slot)[0] == 3
+
+    @property
+    def nfev(self) -> int:
+        return self.b._b.state(self.slot)[1]
+
+    def tell(self, f, g) -> None:
+        self.b._b.tell_one(self.slot, float(LbfgsbStepper._scalar(f)),
+                           np.ascontiguousarray(np.atleast_1d(g), dtype=np.float64))
+
+    def result(self) -> OptimizeResult:
+        if self._res is None and self.done:
+            self._res = self.b.result(self.slot)
+        return self._res

@@ -765,6 +765,11 @@ class _SteppedDriver:
                      and all(hasattr(e, "band_width") or hasattr(e, "band_class") for e, _, _, _ in self.groups))
         self.moves = 0
         self._narrow_q = int(os.environ.get("GPX_NARROW_Q", "3"))
+        # the fits' L-BFGS-B loops advanced a round at a time by the C++ loop around scipy's
+        # setulb (lbfgsb.BatchStepper; GPX_NATIVE_LBFGSB=0: the Python stepper per fit). Not with
+        # wide-group routing, which moves a fit's loop state between batches
+        self.native = (lbfgsb.BatchStepper.NATIVE and not self.wide
+                       and os.environ.get("GPX_NATIVE_LBFGSB", "1") != "0")
 
     def _next(self) -> Optional[int]:
         with self.qlock:
@@ -843,12 +848,15 @@ class _SteppedDriver:
         finally:
             torch.cuda.set_stream(prev)
 
-    def _bind(self, i: int, eng, row: int, lock):
+    def _bind(self, i: int, eng, row: int, lock, gs=None):
         m = self.models[i]
         if not self.fixed:
             t0 = time.perf_counter()
+            # (the model compiled its kernel's spec for its own input width at construction)
+            spec = m._spec if (getattr(m, "_spec", None) is not None and m.data[0].shape[-1] == self.D) \
+                else compile_spec(m.kernel, self.D)
             with lock:
-                eng.rebind(row, m.data[0], m.data[1], compile_spec(m.kernel, self.D))
+                eng.rebind(row, m.data[0], m.data[1], spec)
             if self.stats is not None:
                 self.stats["bind_rebind"] = self.stats.get("bind_rebind", 0.0) + (time.perf_counter() - t0)
             m._attach(eng, row)
@@ -858,7 +866,10 @@ class _SteppedDriver:
         cols, lower = m.theta_layout(variables)
         # the slot's θ row: fixed parameters now, the trainable columns rewritten every round
         self._theta_of(eng)[row] = m.theta_row()
-        return {"i": i, "m": m, "v": variables, "st": lbfgsb.LbfgsbStepper(_pack(variables), self.options),
+        x0 = _pack(variables)
+        native = gs is not None and self.native
+        st = gs.batch(self, len(x0)).start(row, x0) if native else lbfgsb.LbfgsbStepper(x0, self.options)
+        return {"i": i, "m": m, "v": variables, "st": st, "native": native,
                 "cols": cols, "lower": lower, "key": (len(cols), cols.tobytes(), lower.tobytes())}
 
     def _theta_of(self, eng) -> np.ndarray:
@@ -874,11 +885,13 @@ class _SteppedDriver:
             self.g, self.eng, self.lock, self.stream = g, eng, lock, stream
             self.free = list(rows) if not drv.fixed else []
             self.active = {}
+            self.batches = {}   # P -> lbfgsb.BatchStepper over the engine's rows (drv.native)
+            self.reeval = set()  # rows held for one more evaluation at their result's x (_finish)
             if drv.fixed:
                 for r in rows:
                     if r < len(drv.models):
                         try:
-                            self.active[r] = drv._bind(r, eng, r, lock)
+                            self.active[r] = drv._bind(r, eng, r, lock, self)
                         except BaseException as e:
                             drv.errors[r] = e
             self.theta = drv._theta_of(eng)
@@ -890,6 +903,12 @@ class _SteppedDriver:
             self.n_calls = 0
             self.act = self.packs = None
             self.t_call = 0.0
+
+        def batch(self, drv, P: int):
+            b = self.batches.get(P)
+            if b is None:
+                b = self.batches[P] = lbfgsb.BatchStepper(self.eng.B, P, drv.options)
+            return b
 
     def _tick(self, key, t0):
         if self.stats is not None:
@@ -906,7 +925,7 @@ class _SteppedDriver:
                 break
             r = gs.free.pop(0)
             try:
-                gs.active[r] = self._bind(i, gs.eng, r, gs.lock)
+                gs.active[r] = self._bind(i, gs.eng, r, gs.lock, gs)
             except BaseException as e:
                 self.errors[i] = e
                 self.models[i]._engine = None
@@ -928,10 +947,16 @@ class _SteppedDriver:
             for key, rs in layouts.items():
                 s0 = active[rs[0]]
                 P = key[0]
-                # a finished fit held for one more evaluation at its result's x (see _finish)
-                U = np.array([active[r]["st"].x if active[r].get("reeval") is None else active[r]["reeval"]
-                              for r in rs], dtype=np.float64).reshape(len(rs), P)
                 R = np.asarray(rs, dtype=np.int32)
+                if s0["native"]:
+                    U = np.empty((len(rs), P))
+                    gs.batches[P].gather(R, U)
+                    for k in ([k for k, r in enumerate(rs) if r in gs.reeval] if gs.reeval else ()):
+                        U[k] = active[rs[k]]["reeval"]
+                else:
+                    # a finished fit held for one more evaluation at its result's x (see _finish)
+                    U = np.array([active[r]["st"].x if active[r].get("reeval") is None else active[r]["reeval"]
+                                  for r in rs], dtype=np.float64).reshape(len(rs), P)
                 if not moved:
                     lib.gpx_host_theta_rows(len(rs), P, U.ctypes.data, R.ctypes.data, s0["cols"].ctypes.data,
                                             s0["lower"].ctypes.data, gs.theta.ctypes.data)
@@ -1002,7 +1027,11 @@ class _SteppedDriver:
             gu = np.empty((len(rs), P))
             lib.gpx_host_loss_grad_u(len(rs), P, U.ctypes.data, R.ctypes.data, cols.ctypes.data,
                                      lml.ctypes.data, grad.ctypes.data, loss.ctypes.data, gu.ctypes.data)
-            for k, r in enumerate(rs):
+            rest = range(len(rs))
+            if active[rs[0]]["native"]:
+                rest = self._tell_native(gs, P, R, U, loss, gu, info, done)
+            for k in rest:
+                r = rs[k]
                 if info[r] == N.INFO_DEFERRED:
                     gs.pending[r] = (P, U[k].copy(), cols)
                     continue
@@ -1020,7 +1049,7 @@ class _SteppedDriver:
                 self._take(gs, r, P, u, loss[0], gu[0], info[r], done)
         self._tick("steps", t0)
         t_steps = clk()
-        held = self._finish(eng, gs.lock, active, done)
+        held = self._finish(eng, gs.lock, active, done, gs)
         self._tick("finish", t_steps)
         if self.trace is not None:  # GPX_TRACE_ROUNDS: (group, call start, call end, steps end, finish end, n)
             self.trace.append((gs.g, gs.t_call, t_call_end, t_steps, clk(), len(gs.act)))
@@ -1030,9 +1059,43 @@ class _SteppedDriver:
         for r, _ in done:
             if r in held:
                 continue
+            gs.reeval.discard(r)
             del active[r]
             if not self.fixed:
                 gs.free.append(r)
+
+    def _tell_native(self, gs, P, R, U, loss, gu, info, done):
+        """The pack's ordinary rows (a result, no deferral, no pending re-evaluation) through one
+        BatchStepper.tell; returns the pack positions left for _take."""
+        normal = info[R] == 0
+        if gs.reeval:
+            normal &= ~np.isin(R, np.fromiter(gs.reeval, dtype=np.int32))
+        idx = np.flatnonzero(normal)
+        if len(idx) == 0:
+            return range(len(R))
+        whole = len(idx) == len(R)
+        Rn = R if whole else np.ascontiguousarray(R[idx])
+        d = np.zeros(len(idx), np.uint8)
+        err = None
+        try:
+            gs.batches[P].tell(Rn, loss if whole else np.ascontiguousarray(loss[idx]),
+                               gu if whole else np.ascontiguousarray(gu[idx]), d)
+        except BaseException as e:  # a Python error inside setulb at the row flagged 2
+            err = e
+        active = gs.active
+        for j in np.flatnonzero(d == 1):
+            r = int(Rn[j])
+            active[r]["last_u"] = U[idx[j]]
+            done.append((r, True))
+        rest = list(np.flatnonzero(~normal))
+        if err is not None:
+            bad = np.flatnonzero(d == 2)
+            j0 = int(bad[0]) if len(bad) else len(idx)
+            for j in bad:
+                self.errors[active[int(Rn[j])]["i"]] = err
+                done.append((int(Rn[j]), False))
+            rest += [int(idx[j]) for j in range(j0 + 1, len(idx))]  # untouched by the failed call
+        return rest
 
     def _take(self, gs, r, P, u, loss, gu, inf, done):
         """One fit's (loss, grad) at its requested point u: the L-BFGS-B step, or its failure;
@@ -1202,14 +1265,14 @@ class _SteppedDriver:
                 submit_idle()
             drain_idle()
 
-    def _finish(self, eng, lock, active, done):
+    def _finish(self, eng, lock, active, done, gs=None):
         """Results of the finished fits and their predictions. Returns the rows held back for
         one more evaluation: predict at the training inputs reuses the factor of the fit's last
         evaluated point, which is the result's x unless L-BFGS-B returned an earlier point (its
         line search backed off); such a fit is evaluated once more at its result's x in the
         next batched round (banded and asynchronous, like any other evaluation) instead of being
         re-factorised alone by the predict call."""
-        pred_rows, xs, held = [], [], set()
+        pred_rows, xs, held, refit = [], [], set(), []
         for r, ok in done:
             s = active[r]
             if ok:
@@ -1219,6 +1282,8 @@ class _SteppedDriver:
                     s["res"] = res
                     s["reeval"] = np.array(res.x, dtype=np.float64)
                     held.add(r)
+                    if gs is not None:
+                        gs.reeval.add(r)
                     continue
                 _unpack(s["v"], res.x)
                 self.results[s["i"]] = res
@@ -1231,13 +1296,22 @@ class _SteppedDriver:
                 _unpack(s["v"], res.x)
                 self.results[s["i"]] = res
                 pred_rows.append(r)
+                refit.append(r)
                 xs.append(s["m"].data[0])
             elif not self.fixed:
                 s["m"]._engine = None
         if pred_rows:
-            theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
-            for r in pred_rows:
-                theta[r] = active[r]["m"].theta_row()
+            if gs is not None:
+                # the group's θ rows hold each finished fit's last evaluated point, which is its
+                # result's x (else it was held for one more evaluation above): the native θ rows
+                # are Parameter.value's bits, and exactly what the cached factor was computed at
+                theta = gs.theta
+                for r in refit:
+                    theta[r] = active[r]["m"].theta_row()
+            else:
+                theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
+                for r in pred_rows:
+                    theta[r] = active[r]["m"].theta_row()
             try:
                 with lock:
                     if self.predict_inputs is None and hasattr(eng, "_predict_train"):

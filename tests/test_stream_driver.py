@@ -11,6 +11,17 @@ import portfoliooptgp_amd as gpx
 from portfoliooptgp_amd import _native as N
 
 
+@pytest.fixture(params=["native", "python"], autouse=True)
+def lbfgsb_loop(request, monkeypatch):
+    """Every driver test with both L-BFGS-B loops: the C++ loop over a batch of fits
+    (lbfgsb.BatchStepper, the default) and the Python stepper per fit (GPX_NATIVE_LBFGSB=0)."""
+    from portfoliooptgp_amd.lbfgsb import BatchStepper
+    if request.param == "native" and not BatchStepper.NATIVE:
+        pytest.skip("portfoliooptgp_amd/_gpx_lbfgsb*.so is not built")
+    monkeypatch.setenv("GPX_NATIVE_LBFGSB", "1" if request.param == "native" else "0")
+    return request.param
+
+
 class FakeEngine:
     """lml(θ) = −Σ_p (log θ_p − log t_p)² with per-problem targets t from the bound data."""
 
@@ -174,6 +185,75 @@ def test_lbfgsb_stepper_is_scipy():
         np.testing.assert_array_equal(r1.jac, r0.jac)
         assert (r1.fun, r1.nfev, r1.njev, r1.nit, r1.status, r1.message) == \
                (r0.fun, r0.nfev, r0.njev, r0.nit, r0.status, r0.message)
+
+
+def test_batch_stepper_is_scipy(lbfgsb_loop):
+    """The C++ loop (lbfgsb.BatchStepper: scipy's setulb called from gpx_lbfgsb_host.cpp, a whole
+    round of fits per call) against scipy.optimize.minimize, atol = 0: the cases of
+    test_lbfgsb_stepper_is_scipy, each one run in several slots of one batch stepped together,
+    a slot reused for a second fit, and the L-BFGS memory (hess_inv) as well."""
+    if lbfgsb_loop != "native":
+        pytest.skip("the native loop's own test")
+    from portfoliooptgp_amd.lbfgsb import BatchStepper
+
+    def rosen(x):
+        return scipy.optimize.rosen(x), scipy.optimize.rosen_der(x)
+
+    def walled(x):
+        if x[0] > 2.0:
+            return float("inf"), np.zeros_like(x)
+        return float(-x[0] + (x[1] - 1.0) ** 2), np.array([-1.0, 2.0 * (x[1] - 1.0)])
+
+    cases = [(rosen, [-1.2, 1.0, 0.3, 2.0], {}), (rosen, [0.0] * 7, dict(maxiter=15)),
+             (rosen, [3.0, -2.0], dict(maxfun=20)), (walled, [0.0, 0.0], dict(maxiter=100)),
+             (rosen, [0.5413248546129181] * 2, dict(maxiter=100, ftol=1e-12, gtol=1e-9, maxcor=5, maxls=10))]
+    for fn, x0, opts in cases:
+        n = len(x0)
+        starts = [np.array(x0) + 0.25 * k for k in range(3)]
+        refs = [scipy.optimize.minimize(fn, s0, jac=True, method="L-BFGS-B", options=opts) for s0 in starts]
+        b = BatchStepper(3, n, opts)
+        # slot 2 first runs another fit to its end, then the case's third start: a reused slot
+        b.start(2, np.array(x0) - 0.5)
+        for phase in (0, 1):
+            rows = [2] if phase == 0 else [0, 1, 2]
+            if phase == 1:
+                for k in rows:
+                    b.start(k, starts[k])
+            act = np.array(rows, dtype=np.int32)
+            while len(act):
+                U = np.empty((len(act), n))
+                b.gather(act, U)
+                F, G = np.empty(len(act)), np.empty((len(act), n))
+                for j in range(len(act)):
+                    F[j], G[j] = fn(U[j].copy())
+                d = np.zeros(len(act), np.uint8)
+                b.tell(act, F, G, d)
+                act = act[d == 0]
+        for k, r0 in enumerate(refs):
+            r1 = b.result(k)
+            np.testing.assert_array_equal(r1.x, r0.x)
+            np.testing.assert_array_equal(r1.jac, r0.jac)
+            assert (r1.fun, r1.nfev, r1.njev, r1.nit, r1.status, r1.message) == \
+                   (r0.fun, r0.nfev, r0.njev, r0.nit, r0.status, r0.message)
+            np.testing.assert_array_equal(r1.hess_inv.sk, r0.hess_inv.sk)
+            np.testing.assert_array_equal(r1.hess_inv.yk, r0.hess_inv.yk)
+
+
+def test_stream_driver_uses_the_native_loop(lbfgsb_loop, monkeypatch):
+    """By default the stepped driver advances its fits through BatchStepper.tell (one call per
+    pack of a round), and GPX_NATIVE_LBFGSB=0 keeps it on the per-fit Python stepper."""
+    from portfoliooptgp_amd import lbfgsb
+    calls = []
+    real = lbfgsb.BatchStepper.__init__
+
+    def init(self, *a, **k):
+        real(self, *a, **k)
+        t = self.tell
+        self.tell = lambda *x: (calls.append(len(x[0])), t(*x))[1]
+    monkeypatch.setattr(lbfgsb.BatchStepper, "__init__", init)
+    res, _ = gpx.optimizers.Scipy().minimize_stream(_models(6), width=3, engine=FakeEngine(3))
+    assert all(r.success for r in res)
+    assert (sum(calls) > 0) == (lbfgsb_loop == "native")
 
 
 def test_batch_equals_solo():
