@@ -18,8 +18,9 @@ through the slots (no drain between steps), bracketed by one barrier + synchroni
 side. For N > 1 GPUs the timed region ends with an RCCL all_gather of every fit's (θ*, loss*,
 nfev, last predicted mean/var) — the per-asset hand-off to the portfolio step.
 
-Host processes per GPU (``--procs``, default 2): scipy's L-BFGS-B steps hold the GIL, so one
-host thread stepping ~1500 fits becomes the limit before the GPU does. The rank process starts
+Host processes per GPU (``--procs``, default 8, each with one device batch of --width / procs
+slots): a process's host work (model construction, L-BFGS-B steps, predictions) and its device
+calls alternate, so several processes keep the GPU's queues full. The rank process starts
 ``procs - 1`` helper processes (multiprocessing "spawn", BEFORE any GPU call in the rank) that
 share the GPU; each fits its own slice of the step's series through its own slots and device
 batches. All of them finish their warmup and report ready; the rank starts its clock, signals
@@ -307,6 +308,29 @@ def share(total, parts, i):
     return total // parts + (1 if i < total % parts else 0)
 
 
+def last_points(ts):
+    """t[-1, 0] of every [n, 1] prediction tensor in ts (the horizon point of each fit's
+    predict_f), by one gather per device buffer the predictions are views of (a call's finished
+    fits share one) instead of an indexing op per fit."""
+    import torch
+    if not ts:
+        return torch.empty(0, dtype=torch.float64)
+    dev = ts[0].device
+    out = torch.empty(len(ts), dtype=torch.float64, device=dev)
+    groups = {}
+    for i, t in enumerate(ts):
+        b = t._base if t._base is not None else t
+        g = groups.get(id(b))
+        if g is None:
+            g = groups[id(b)] = (b, [], [])
+        g[1].append(i)
+        g[2].append(t.storage_offset() - b.storage_offset() + (t.shape[0] - 1) * t.stride(0))
+    for b, idx, offs in groups.values():
+        flat = b.reshape(-1) if b.is_contiguous() else b.contiguous().reshape(-1)
+        out[torch.as_tensor(idx, device=dev)] = flat[torch.as_tensor(offs, device=dev)]
+    return out
+
+
 class FitWorker:
     """One host process's part of a step on one GPU: its slice of the step's series (fits
     f0 .. f0 + F_w − 1 of the rank's F), its slots (width / procs) in `groups` device batches,
@@ -393,8 +417,8 @@ class FitWorker:
             self.driver_stats.append(dict(self.opt.last_stats))
         host = np.array([[m.kernel.lengthscales.value, m.kernel.variance.value, float(r.fun), float(r.nfev)]
                          for m, r in zip(models, res)], dtype=np.float64)
-        mu = torch.cat([p[0][-1:, 0] for p in preds]).cpu().numpy()
-        var = torch.cat([p[1][-1:, 0] for p in preds]).cpu().numpy()
+        mu = last_points([p[0] for p in preds]).cpu().numpy()
+        var = last_points([p[1] for p in preds]).cpu().numpy()
         return [r.nfev for r in res], np.concatenate([host, mu[:, None], var[:, None]], axis=1)
 
     def reset_timing(self):

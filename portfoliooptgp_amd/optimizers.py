@@ -35,6 +35,7 @@ from . import _native as N
 from . import lbfgsb
 from .engine import Engine
 from .kernels import compile_spec
+from .parameter import UnconstrainedVariable
 
 
 # GPX_THREADED_DRIVER=1: one host thread per fit/slot around scipy.optimize.minimize (the
@@ -131,11 +132,17 @@ def _guarded(fn, as_inf: bool):
 
 
 def _pack(variables) -> np.ndarray:
+    if all(type(v) is UnconstrainedVariable for v in variables):  # scalar parameters: their u as stored
+        return np.array([v._param._u for v in variables], dtype=np.float64)
     return np.concatenate([np.atleast_1d(v.numpy()).ravel() for v in variables]).astype(np.float64)
 
 
 def _unpack(variables, x) -> None:
     x = np.asarray(x, dtype=np.float64)
+    if all(type(v) is UnconstrainedVariable for v in variables) and x.shape == (len(variables),):
+        for v, u in zip(variables, x.tolist()):  # (UnconstrainedVariable.assign: the same float)
+            v._param._u = u
+        return
     o = 0
     for v in variables:
         shape = tuple(v.shape)
@@ -359,7 +366,10 @@ class Scipy:
                                  predict_train=predict_train or predict_inputs is not None,
                                  predict_inputs=predict_inputs, width=width, wide_group=wide_group,
                                  admission=admission)
+            t_run = time.perf_counter()
             drv.run()
+            if drv.stats is not None:  # the whole run, phases or not (the gaps are the loop itself)
+                drv.stats["run_total"] = time.perf_counter() - t_run
             self.last_trace = drv.trace
             self.last_stats = drv.stats
             for e in drv.errors:
@@ -1037,16 +1047,27 @@ class _SteppedDriver:
                     continue
                 self._take(gs, r, P, U[k], loss[k], gu[k], info[r], done)
         if gs.pending:
-            # deferred rows of earlier calls that this complete (or drain) delivered
+            # deferred rows of earlier calls that this complete (or drain) delivered: per variable
+            # layout one native chain rule and one batched step, as for the call's own rows
             got = [r for r in gs.pending if info[r] != N.INFO_UNSET and info[r] != N.INFO_DEFERRED]
+            lays = {}
             for r in got:
                 P, u, cols = gs.pending.pop(r)
-                loss = np.empty(1)
-                gu = np.empty((1, P))
-                R = np.array([r], dtype=np.int32)
-                lib.gpx_host_loss_grad_u(1, P, u.ctypes.data, R.ctypes.data, cols.ctypes.data, lml.ctypes.data,
+                ent = lays.setdefault((P, cols.tobytes()), (P, cols, [], []))
+                ent[2].append(r)
+                ent[3].append(u)
+            for P, cols, rows, us in lays.values():
+                R = np.asarray(rows, dtype=np.int32)
+                U = np.array(us, dtype=np.float64).reshape(len(rows), P)
+                loss = np.empty(len(rows))
+                gu = np.empty((len(rows), P))
+                lib.gpx_host_loss_grad_u(len(rows), P, U.ctypes.data, R.ctypes.data, cols.ctypes.data, lml.ctypes.data,
                                          grad.ctypes.data, loss.ctypes.data, gu.ctypes.data)
-                self._take(gs, r, P, u, loss[0], gu[0], info[r], done)
+                rest = range(len(rows))
+                if active[rows[0]]["native"]:
+                    rest = self._tell_native(gs, P, R, U, loss, gu, info, done)
+                for k in rest:
+                    self._take(gs, rows[k], P, U[k], loss[k], gu[k], info[rows[k]], done)
         self._tick("steps", t0)
         t_steps = clk()
         held = self._finish(eng, gs.lock, active, done, gs)

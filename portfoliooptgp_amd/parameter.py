@@ -79,7 +79,7 @@ class Parameter:
     """A scalar positive parameter (θ = lower + softplus(u))."""
 
     def __init__(self, value: float, lower: float = 0.0, trainable: bool = True, name: str = "parameter"):
-        value = float(np.asarray(value, dtype=np.float64).reshape(()))
+        value = value if type(value) is float else float(np.asarray(value, dtype=np.float64).reshape(()))
         if not value > lower:
             raise ValueError(f"{name}: value {value} must be > {lower} (positive transform)")
         self.lower = float(lower)
@@ -97,7 +97,7 @@ class Parameter:
         return np.float64(self.value)
 
     def assign(self, value) -> None:
-        value = float(np.asarray(value, dtype=np.float64).reshape(()))
+        value = value if type(value) is float else float(np.asarray(value, dtype=np.float64).reshape(()))
         if not value > self.lower:
             raise ValueError(f"{self.name}: value {value} must be > {self.lower}")
         self._u = softplus_inverse(value - self.lower)
