@@ -470,6 +470,10 @@ RouteLimits route_limits(const gpx_batch* bt) {
   const char* ef = getenv("GPX_BAND_FUSED");  // 0: p <= 2 problems take the per-block launches too
   L.fused_on = !(ef && atoi(ef) == 0);
   L.q16lim = L.fused_on ? band16_limit(bt) : -1;
+  // the widest SE1 band16 class (GPX_BAND16_QMAX, default kBand16MaxQ): only with both sweeps
+  // computing K's tiles inline
+  const char* eq = getenv("GPX_BAND16_QMAX");
+  L.q16wide = b16_inline_k() == 3 ? std::min(kBand16MaxQ, eq ? atoi(eq) : kBand16MaxQ) : kBand16MaxQAny;
   return L;
 }
 
@@ -479,7 +483,10 @@ RouteKind route_one(const gpx_batch* bt, int b, const double* thb, const RouteLi
   w = p;
   if (p >= 0 && p <= L.plim) {
     // p <= 2 problems whose band is at most kBand16MaxQ 16-blocks: the band16 sweeps
-    const int q16 = (p <= 2 && L.q16lim > 0) ? band_width16(bt, b, thb) : -1;
+    int q16 = (p <= 2 && L.q16lim > 0) ? band_width16(bt, b, thb) : -1;
+    // Q = 6..8 (a one-wave sweep whose window fills the register file): SE1 problems whose K
+    // tiles both sweeps compute inline (their LDS holds no K tiles), up to GPX_BAND16_QMAX
+    if (q16 > kBand16MaxQAny && !(q16 <= L.q16wide && se1_spec(bt->specs[b]))) q16 = -1;
     if (q16 >= 0 && q16 <= L.q16lim) {
       w = std::max(q16, 1);
       return kRouteBand16;
@@ -580,6 +587,41 @@ double band16_flops(int Np, int Q, bool fwd) {
   return f;
 }
 
+// which SE1 band16 sweeps compute their K tiles from X (bit 0: forward, bit 1: backward;
+// GPX_B16_INLINE_K, read once): a sweep that does not reads K's band. Same bits every way.
+// the same for the wide launch of a deferred part (GPX_B16_INLINE_K_WIDE, default: as above)
+int b16_inline_k_wide() {
+  static const int kin = [] {
+    const char* e = getenv("GPX_B16_INLINE_K_WIDE");
+    return e ? (atoi(e) & 3) : b16_inline_k();
+  }();
+  return kin;
+}
+
+// the widest band16 class a deferred part's wide launch takes: 5, or 8 (GPX_WIDE_QMAX, default
+// 8) for SE1 parts whose sweeps compute K inline
+int wide_qmax(bool se1) {
+  static const int wq = [] {
+    const char* e = getenv("GPX_WIDE_QMAX");
+    return e ? std::max(5, std::min(8, atoi(e))) : 8;
+  }();
+  return (se1 && b16_inline_k_wide() == 3) ? wq : 5;
+}
+
+int b16_inline_k() {
+  static const int kin = [] {
+    const char* e = getenv("GPX_B16_INLINE_K");
+    return e ? (atoi(e) & 3) : 3;  // default: both (round 4: +4-7 % on the C2 bench, K's band never in HBM)
+  }();
+  return kin;
+}
+
+// the reference's kernel: one SquaredExponential term on one input column (the band16 sweeps'
+// straight-line contraction, and the only family of the Q > kBand16MaxQAny classes)
+bool se1_spec(const gpx_kernel_spec& sp) {
+  return sp.n_terms == 1 && sp.terms[0].kind == GPX_SE && sp.terms[0].dim_count == 1;
+}
+
 // the most band16 problems a call may hold for them to take the block-cyclic-reduction path
 // (gpx_bcr.hip) instead of the one-wavefront sweeps (GPX_BCR_MAX; 0 turns it off)
 static int bcr_max_problems() {
@@ -627,6 +669,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   // d <= Q; kband16 — 2, or 3 when the class holds p = 2 problems — still tells the sweeps which
   // entries are exact zeros by the 64-row bound), the 64-row p <= 1 class (two 64-block
   // diagonals), the 64-row p = 2 class (three).
+  const int wq = wide_qmax(se1);  // the widest class a deferred part's wide launch takes
   struct Lane { int kind, g, n, off, g_end; };
   Lane lanes[kBand16MaxQ + 2];
   int nl = 0;
@@ -634,17 +677,18 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     int off = 0;
     // (r.bcr_q: each band16 width group as a block-cyclic-reduction chain of its own width,
     // gpx_bcr.hip: a problem's arithmetic depends on its own width only, not on the call's mix)
-    for (int g = 0; g < n_g16 && r.bcr_q > 0; ++g) {
+    int g = 0;
+    for (; g < n_g16 && r.bcr_q > 0 && g16_q[g] <= kBcrMaxQ; ++g) {
       lanes[nl++] = Lane{4, g, g16_n[g], off, g + 1};
       off += g16_n[g];
     }
-    for (int g = 0; g < n_g16 && r.bcr_q == 0; ++g) {
+    for (; g < n_g16; ++g) {
       // (r.wide_from: the SE1 groups of width 4 and 5 as one lane, one band16_wide_kernel launch)
-      if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= 5 && nl > 0 &&
+      if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= wq && nl > 0 &&
           lanes[nl - 1].kind == 3) {
         lanes[nl - 1].n += g16_n[g];
         lanes[nl - 1].g_end = g + 1;
-      } else if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= 5) {
+      } else if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= wq) {
         lanes[nl++] = Lane{3, g, g16_n[g], off, g + 1};
       } else {
         lanes[nl++] = Lane{0, g, g16_n[g], off, g + 1};
@@ -671,17 +715,11 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   // GPX_B16_INLINE_K): a sweep that does not reads K's band — written by band16_build_kernel
   // when the forward reads it too, by the forward itself when only the backward reads it (1:
   // each K tile's exp once, the band through HBM once each way). Same bits every way.
-  static const int kin = [] {
-    const char* e = getenv("GPX_B16_INLINE_K");
-    return e ? (atoi(e) & 3) : 3;  // default: both (round 4: +4-7 % on the C2 bench, K's band never in HBM)
-  }();
+  static const int kin = b16_inline_k();
   // the same for the wide launch (the Q = 4, 5 classes of a deferred part, one wavefront per SIMD:
   // there the exp on each sweep's chain costs more than a build launch; GPX_B16_INLINE_K_WIDE,
   // default: as GPX_B16_INLINE_K)
-  static const int kin_wide = [] {
-    const char* e = getenv("GPX_B16_INLINE_K_WIDE");
-    return e ? (atoi(e) & 3) : kin;
-  }();
+  static const int kin_wide = b16_inline_k_wide();
   // GPX_BAND_LANE_STREAMS: streams the lanes are spread over (the bulk lane alone on the call's
   // stream, the others round-robin on the rest). A process gets GPU_MAX_HW_QUEUES hardware
   // queues (the bench: 2, so that 8 processes stay within the 16 the GPU maps without
@@ -714,7 +752,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       f16.kband = kband16;
       f16.active = r.d_act + l.off;
       f16.kstore = se1 && (kin & 1) && !(kin & 2);
-      launch_band16(f16, g16_q[l.g], max_terms, se1, kin, l.n, ls, ev16 ? ev16[l.g] : nullptr);
+      launch_band16(f16, g16_q[l.g], max_terms, se1, kin, l.n, ls, ev16 ? ev16[l.g - r.ev16_g0] : nullptr);
     } else if (l.kind == 3) {
       // the wide SE1 groups: their K bands (unless computed in the sweeps), then one launch
       int goff = l.off;
@@ -731,17 +769,17 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       f16.active = r.d_act + l.off;
       f16.kstore = (kin_wide & 1) && !(kin_wide & 2);
       if (ev16)
-        for (int g = l.g + 1; g < l.g_end; ++g) (void)hipEventRecord(ev16[g][0], ls);
-      launch_band16_wide(f16, kin_wide, l.n, ls, ev16 ? ev16[l.g] : nullptr);
+        for (int g = l.g + 1; g < l.g_end; ++g) (void)hipEventRecord(ev16[g - r.ev16_g0][0], ls);
+      launch_band16_wide(f16, kin_wide, l.n, ls, ev16 ? ev16[l.g - r.ev16_g0] : nullptr, g16_q[l.g_end - 1]);
       if (ev16)
         for (int g = l.g + 1; g < l.g_end; ++g)
-          for (int e = 1; e < 4; ++e) (void)hipEventRecord(ev16[g][e], ls);
+          for (int e = 1; e < 4; ++e) (void)hipEventRecord(ev16[g - r.ev16_g0][e], ls);
     } else if (l.kind == 4) {
       BcrArgs ca{};
       ca.active = r.d_act + l.off; ca.specs = bt->d_specs; ca.theta = fa.theta; ca.nvalid = bt->d_n;
       ca.X = bt->X; ca.sX = (long long)bt->Nmax * bt->D; ca.D = bt->D; ca.Y = bt->Y; ca.sY = bt->Nmax;
       // (workspace: every problem of the call at its position, in slots of the widest layout)
-      ca.sWs = bcr_ws_doubles(kBand16MaxQ, bt->Nmax);
+      ca.sWs = bcr_ws_doubles(kBcrMaxQ, bt->Nmax);
       ca.ws = bt->bcr_ws + (size_t)l.off * (size_t)ca.sWs; ca.info = fa.info;
       ca.z = bt->z; ca.ldiag = bt->ldiag; ca.alpha = bt->alpha; ca.sVec = Np; ca.Np = Np;
       ca.Kd = bt->K; ca.sMat = st; ca.ld = mat_ld(bt);
@@ -1713,7 +1751,7 @@ static int deliver_slow(gpx_batch* bt, gpx_batch::SlowRec& rec, double* lml, dou
       (void)hipEventElapsedTime(&f1, rec.fq16[g][2], rec.fq16[g][3]);
       const int n = rec.g16_n[g], q = rec.g16_q[g];
       const double fl = n * (band16_flops(bt->Np, q, true) + band16_flops(bt->Np, q, false));
-      if (rec.se1 && q >= 4 && q <= 5) {
+      if (rec.se1 && q >= 4 && q <= wide_qmax(true) && (q <= 5 || b16_inline_k_wide() == 3)) {
         // the wide launch (band_fused_eval's kind-3 lane): every one of its groups' events spans
         // the one kernel, so it is counted once, apart from the per-class launches
         if (!wide_seen) {
@@ -1836,6 +1874,10 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   // a call with few band16 problems takes them by block cyclic reduction (gpx_bcr.hip): the
   // one-wavefront sweeps' N/16-step chain would be the whole call's latency
   const int bcr_q = (n16 > 0 && n16 <= bcr_max_problems()) ? 1 : 0;
+  // (the width groups of Q <= kBcrMaxQ: the reduction; wider ones keep their sweeps, so a
+  // problem's arithmetic depends on its own width and the call's size only)
+  int g_bcr = 0, n16_bcr = 0;
+  while (bcr_q > 0 && g_bcr < n_g16 && g16_q[g_bcr] <= kBcrMaxQ) n16_bcr += g16_n[g_bcr++];
   // the problems launched by this call (band storage: without the shadowed ones)
   n_active = n_dense + n_band + n_fused;
   // band storage: a few fallback problems go out at once on the fallback stream (more than the
@@ -1870,8 +1912,8 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     const int e = ensure(ctx, bt->bres, bt->bres_cap, (size_t)bt->B * bt->Np);
     if (e != GPX_OK) return drop_shadow(e);
   }
-  if (bcr_q > 0) {
-    const int e = ensure(ctx, bt->bcr_ws, bt->bcr_ws_cap, (size_t)n16 * (size_t)bcr_ws_doubles(kBand16MaxQ, bt->Nmax));
+  if (n16_bcr > 0) {
+    const int e = ensure(ctx, bt->bcr_ws, bt->bcr_ws_cap, (size_t)n16_bcr * (size_t)bcr_ws_doubles(kBcrMaxQ, bt->Nmax));
     if (e != GPX_OK) return drop_shadow(e);
     if (ctx->profiling && !bt->bcr_ev[0])
       for (auto& e2 : bt->bcr_ev) HIPX(ctx, hipEventCreate(&e2));
@@ -2009,7 +2051,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     for (int i = off; i < n_active; ++i) max_terms = std::max(max_terms, (int)bt->specs[order[i]].n_terms);
     for (int i = off; i < off + (n16 - n16_run); ++i) {
       const gpx_kernel_spec& sp = bt->specs[order[i]];
-      se1s = se1s && sp.n_terms == 1 && sp.terms[0].kind == GPX_SE && sp.terms[0].dim_count == 1;
+      se1s = se1s && se1_spec(sp);
     }
     if (defer_own_stream()) {
       const int rcs = submit_slow(bt, s, order.data() + off, off, n_slow, n_g16 - n_g16_run, g16_q + n_g16_run,
@@ -2028,11 +2070,12 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (ctx->profiling && old_fused)
       for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&fqe[e]));
     pe->n_band16 = n16;
-    pe->n_g16 = bcr_q > 0 ? 0 : n_g16;
-    pe->n_bcr = bcr_q > 0 ? n16 : 0;
+    // (timing: the swept groups g_bcr.. only; the reduction's chain has its own events)
+    pe->n_g16 = n_g16 - g_bcr;
+    pe->n_bcr = n16_bcr;
     for (int g = 0; g < pe->n_g16; ++g) {
-      pe->g16_q[g] = g16_q[g];
-      pe->g16_n[g] = g16_n[g];
+      pe->g16_q[g] = g16_q[g_bcr + g];
+      pe->g16_n[g] = g16_n[g_bcr + g];
       if (ctx->profiling)
         for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&pe->fq16[g][e]));
     }
@@ -2041,10 +2084,11 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     bool se1 = true;
     for (int i = n_dense + n_band; i < n_dense + n_band + n16; ++i) {
       const gpx_kernel_spec& sp = bt->specs[order[i]];
-      se1 = se1 && sp.n_terms == 1 && sp.terms[0].kind == GPX_SE && sp.terms[0].dim_count == 1;
+      se1 = se1 && se1_spec(sp);
     }
     Run rf{bt, bt->d_active + n_dense + n_band, n_fused, s};
     rf.bcr_q = bcr_q;
+    rf.ev16_g0 = g_bcr;
     band_fused_eval(rf, n16, n_g16, g16_q, g16_n, se1,
                     b16_p2 ? 3 : 2, n_fused1,
                     max_terms, (ctx->profiling && old_fused) ? fqe : nullptr, ctx->profiling ? pe->fq16 : nullptr);

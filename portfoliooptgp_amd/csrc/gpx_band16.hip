@@ -7,7 +7,8 @@
 // every ∂K/∂θ vanish exactly (exp underflow) outside the band. What changes is the granularity:
 //
 //   * blocks are 16 rows, one v_mfma_f64_16x16x4_f64 tile, and the band is Q 16-blocks wide
-//     (Q = 1..5: at the reference's day-offset inputs and ℓ ∈ [1, 1.68], the band of exact
+//     (Q = 1..5 for every band kernel family, 6..8 for SE1 problems with K's tiles computed in the
+//     sweeps (ℓ up to ≈ 3.3 at unit spacing); at the reference's day-offset inputs and ℓ ∈ [1, 1.68], the band of exact
 //     nonzeros is 39-65 entries: Q = 3-4 instead of the 64-row kernels' 128-wide two-block band,
 //     so a step multiplies ~(56/96)² of the 64-row kernels' block entries and none of the
 //     exactly-zero triangles of the 64-row blocks);
@@ -449,7 +450,7 @@ struct Bwd16 {  // the backward sweep's LDS, in doubles
 };
 template <int Q, int NT, bool SE1, bool KIN>
 __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __restrict__ lds, double* __restrict__ sx) {
-  static_assert(!SE1 || Q <= 5, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 5");
+  static_assert(!SE1 || KIN || Q <= 5, "the SE1 sweep double-buffers its K tiles in LDS: Q <= 5");
   static_assert(!KIN || SE1, "inline K tiles: SE1 sweeps only");
   using Ly = Bwd16<Q, NT, SE1, KIN>;
   // sx: X ring [Q+1][16·D] (block m in slot m % (Q+1); not SE1)
@@ -999,22 +1000,33 @@ __device__ __forceinline__ void fused_sweeps(const BandFusedArgs& a, double* __r
   wsync();
   bwd_sweep<Q, 1, true, KB>(a, lds, nullptr);
 }
-template <bool KF, bool KB>
+template <int Q, bool KF, bool KB>
+constexpr int fused_lds() {
+  return Fwd16<Q, KF>::size > Bwd16<Q, 1, true, KB>::size ? Fwd16<Q, KF>::size : Bwd16<Q, 1, true, KB>::size;
+}
+// WQ = 8 (K inline in both sweeps only): the Q = 6..8 classes in the same launch
+template <bool KF, bool KB, int WQ>
 __global__ __launch_bounds__(64, 1) void band16_wide_kernel(BandFusedArgs a) {
-  constexpr int f4 = Fwd16<4, KF>::size, b4 = Bwd16<4, 1, true, KB>::size;
-  constexpr int f5 = Fwd16<5, KF>::size, b5 = Bwd16<5, 1, true, KB>::size;
-  constexpr int n4 = f4 > b4 ? f4 : b4, n5 = f5 > b5 ? f5 : b5;
-  __shared__ __attribute__((aligned(16))) double lds[n4 > n5 ? n4 : n5];
+  constexpr int n4 = fused_lds<4, KF, KB>(), n5 = fused_lds<5, KF, KB>();
+  constexpr int n8 = WQ > 5 ? fused_lds<8, KF, KB>() : 0;
+  constexpr int n45 = n4 > n5 ? n4 : n5;
+  __shared__ __attribute__((aligned(16))) double lds[n45 > n8 ? n45 : n8];
   const int Q = a.bandp[a.active[blockIdx.x]];
+  if constexpr (WQ > 5) {
+    if (Q == 8) return fused_sweeps<8, KF, KB>(a, lds);
+    if (Q == 7) return fused_sweeps<7, KF, KB>(a, lds);
+    if (Q == 6) return fused_sweeps<6, KF, KB>(a, lds);
+  }
   if (Q == 5)
     fused_sweeps<5, KF, KB>(a, lds);
   else
     fused_sweeps<4, KF, KB>(a, lds);
 }
 
-void launch_band16_wide(const BandFusedArgs& a, int kin, int n_active, hipStream_t s, hipEvent_t* ev) {
-  auto k = (kin & 1) ? ((kin & 2) ? band16_wide_kernel<true, true> : band16_wide_kernel<true, false>)
-                     : ((kin & 2) ? band16_wide_kernel<false, true> : band16_wide_kernel<false, false>);
+void launch_band16_wide(const BandFusedArgs& a, int kin, int n_active, hipStream_t s, hipEvent_t* ev, int wq) {
+  auto k = (kin & 1) ? ((kin & 2) ? (wq > 5 ? band16_wide_kernel<true, true, 8> : band16_wide_kernel<true, true, 5>)
+                                  : band16_wide_kernel<true, false, 5>)
+                     : ((kin & 2) ? band16_wide_kernel<false, true, 5> : band16_wide_kernel<false, false, 5>);
   if (ev) {
     hipExtLaunchKernelGGL(k, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
     (void)hipEventRecord(ev[2], s);
@@ -1060,6 +1072,23 @@ static void launch16_q(const BandFusedArgs& a, int max_terms, bool se1, int kin,
   hipLaunchKernelGGL(bwd, dim3(n_active), dim3(64), xs, s, a);
 }
 
+// Q = 6..8 (the routing sends only SE1 problems with both sweeps computing K inline): one
+// wavefront per SIMD whose window tiles fill VGPRs and AGPRs — 28 / 36 / 45 forward window
+// tiles; Q = 6 fits (241 + 256 registers, no scratch), Q = 7 and 8 spill (240-920 B per lane),
+// still one launch pair per class instead of the 64-row p = 2 sweeps' 73 KiB workgroups
+template <int Q>
+static void launch16_wide_q(const BandFusedArgs& a, int n_active, hipStream_t s, hipEvent_t* ev) {
+  auto fwd = band16_fwd_kernel<Q, true>;
+  auto bwd = band16_bwd_kernel<Q, 1, true, true>;
+  if (ev) {
+    hipExtLaunchKernelGGL(fwd, dim3(n_active), dim3(64), 0, s, ev[0], ev[1], 0, a);
+    hipExtLaunchKernelGGL(bwd, dim3(n_active), dim3(64), 0, s, ev[2], ev[3], 0, a);
+    return;
+  }
+  hipLaunchKernelGGL(fwd, dim3(n_active), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(bwd, dim3(n_active), dim3(64), 0, s, a);
+}
+
 void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int kin, int n_active, hipStream_t s,
                    hipEvent_t* ev) {
   switch (Q) {
@@ -1067,7 +1096,10 @@ void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int k
     case 2: launch16_q<2>(a, max_terms, se1, kin, n_active, s, ev); break;
     case 3: launch16_q<3>(a, max_terms, se1, kin, n_active, s, ev); break;
     case 4: launch16_q<4>(a, max_terms, se1, kin, n_active, s, ev); break;
-    default: launch16_q<5>(a, max_terms, se1, kin, n_active, s, ev); break;
+    case 5: launch16_q<5>(a, max_terms, se1, kin, n_active, s, ev); break;
+    case 6: launch16_wide_q<6>(a, n_active, s, ev); break;
+    case 7: launch16_wide_q<7>(a, n_active, s, ev); break;
+    default: launch16_wide_q<8>(a, n_active, s, ev); break;
   }
 }
 

@@ -197,7 +197,9 @@ inline long long mat_stride(const gpx_batch* bt) { return bt->smat ? bt->smat : 
 inline int mat_ld(const gpx_batch* bt) { return bt->ldm ? bt->ldm : bt->Np; }
 constexpr int kBandStoreP = 2;     // band width (64-blocks) held by band storage
 constexpr int kBox = 16;           // rows per bounding box of the band tables (16: the band16 path's block)
-constexpr int kBand16MaxQ = 5;     // widest band (16-blocks) of the band16 kernels (gpx_band16.hip)
+constexpr int kBand16MaxQ = 8;     // widest band (16-blocks) of the band16 kernels (gpx_band16.hip)
+constexpr int kBand16MaxQAny = 5;  // ... for any kernel family; Q = 6..8 only for SE1 problems with K inline
+constexpr int kBcrMaxQ = 5;        // widest band (16-blocks) of the block-cyclic-reduction path (gpx_bcr.hip)
 constexpr int kBand16MaxD = 8;     // input columns the band16 backward sweep stages per block
 constexpr int kBand16MaxNp = 8192;
 constexpr int kShadowSlots = 4;    // dense fallback slots of a band-storage batch
@@ -217,7 +219,9 @@ struct Run {
   int* info = nullptr;
   bool one_stream = false;
   int wide_from = 0;  // > 0: the band16 groups of at least this width run as ONE launch (band16_wide_kernel)
-  int bcr_q = 0;      // > 0: the band16 width groups run as block cyclic reduction (gpx_bcr.hip), each at its width
+  int bcr_q = 0;      // > 0: the band16 width groups of Q <= kBcrMaxQ run as block cyclic reduction
+                      // (gpx_bcr.hip), each at its width; wider groups keep their sweeps
+  int ev16_g0 = 0;    // the band16 group the ev16 timing events start at (the first swept group)
 };
 
 struct PhaseTimer {
@@ -280,7 +284,11 @@ struct Route {
 void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double* theta, Route& rt);
 // the per-call limits of the routing, and one problem's path under them (w: its band width, in
 // 16-blocks for kRouteBand16, in 64-blocks otherwise, -1 when not banded)
-struct RouteLimits { int plim = -1, q16lim = -1; bool fused_on = true; };
+struct RouteLimits { int plim = -1, q16lim = -1, q16wide = -1; bool fused_on = true; };
+int b16_inline_k();                            // GPX_B16_INLINE_K (bit 0 forward, bit 1 backward)
+int b16_inline_k_wide();                       // ... for the wide launch (GPX_B16_INLINE_K_WIDE)
+int wide_qmax(bool se1);                       // widest class of the wide launch (5, or 8: GPX_WIDE_QMAX)
+bool se1_spec(const gpx_kernel_spec& sp);     // one SquaredExponential term on one column
 enum RouteKind { kRouteDense, kRouteShadow, kRouteBand, kRouteFused, kRouteBand16 };
 RouteLimits route_limits(const gpx_batch* bt);
 RouteKind route_one(const gpx_batch* bt, int b, const double* theta_row, const RouteLimits& L, int& w);

@@ -195,7 +195,7 @@ void launch_band_fused1(const BandFusedArgs& a, int max_terms, int n_active, hip
 void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s);
 void launch_wave_marker(unsigned long long* wt, unsigned int* wn, unsigned int cap, int kind, hipStream_t s);
 // SE1 band16 problems of widths Q = 4 and 5 (bandp) in one launch, both sweeps per wavefront
-void launch_band16_wide(const BandFusedArgs& a, int kin, int n_active, hipStream_t s, hipEvent_t* ev);
+void launch_band16_wide(const BandFusedArgs& a, int kin, int n_active, hipStream_t s, hipEvent_t* ev, int wq = 5);
 void launch_slow_gather(const int* act, int n, const double* res, int stride, double* out, const int* info,
                         int* info_out, hipStream_t s);
 void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int kin, int n_active, hipStream_t s,

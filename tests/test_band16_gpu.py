@@ -217,3 +217,83 @@ def test_band16_wide_class_p64_2():
     with _Dense():
         ld, gd, _ = eng.lml_grad(act, th)
     _close(lb, gb, ld, gd, 3, "band16 vs dense (p = 2)")
+
+
+def _band_oracle_loss_grad(x, y, ell, var):
+    """The band oracle (oracle/band_oracle.py: block-tridiagonal Cholesky + Takahashi on the
+    exact-zero band, numpy/LAPACK, pinned against the dense oracle in tests/test_band_oracle.py)
+    at (ℓ, σ²): loss and ∂loss/∂u for the two kernel parameters (σn² fixed)."""
+    from oracle import band_oracle as BO
+    bm = BO.OBandGPR(x, y, 1e-5)
+    bm.ell, bm.var = float(ell), float(var)
+    return bm.loss_and_grad_u()
+
+
+def test_band16_se1_q6_to_q8_n4096():
+    """ℓ ∈ {2, 2.3, 2.5, 2.8, 3} at the C2 inputs: bands of Q = 5..8 16-blocks (p64 = 2). SE1
+    problems with K's tiles inline take the band16 sweeps (one wavefront per SIMD, window in VGPRs
+    and AGPRs) — no 64-row sweep launch — and agree with the 64-row p = 2 sweeps
+    (GPX_BAND16_QMAX=5 sends them there), the dense path, and the band oracle at ℓ ∈ {2, 2.5, 3}
+    (logML 1e-9, ∂loss/∂u 1e-6·max(1, |g|): VERDICT r04 item 2)."""
+    n = 4096
+    ells = [2.0, 2.3, 2.5, 2.8, 3.0]
+    data = [O.synthetic_series(n, seed=40 + s) for s in range(len(ells))]
+    eng = _engine([d[0] for d in data], [d[1] for d in data], K.SquaredExponential())
+    th = _theta(eng, [(e, 0.9, 1e-5) for e in ells])
+    act = list(range(len(ells)))
+    cls = eng.band_class(act, th)
+    assert list(cls) == [5, 6, 6, 7, 8], cls  # (ℓ = 2: Q = 5, the widest class of any kernel family)
+    eng.reset_timing()
+    lb, gb, ib = eng.lml_grad(act, th)
+    t = eng.last_timing()
+    assert not ib.any() and t.band16_evals == len(ells) and t.band_fallbacks == 0, (t.band16_evals, t.band_fallbacks)
+    assert t.band16_q_sum == int(sum(cls)) and t.band_fused_launches == 0, (t.band16_q_sum, t.band_fused_launches)
+    m16, v16, _ = eng._predict_train(np.arange(len(ells), dtype=np.int32), th, False)
+    with _Env("GPX_BAND16_QMAX", "5"):
+        eng.reset_timing()
+        l64, g64, i64 = eng.lml_grad(act, th)
+        t = eng.last_timing()
+        assert not i64.any() and t.band16_evals == 1 and t.band_fused_launches > 0  # (ℓ = 2 stays at Q = 5)
+        m64, v64, _ = eng._predict_train(np.arange(len(ells), dtype=np.int32), th, False)
+    _close(lb, gb, l64, g64, 3, "band16 Q 6-8 vs band64 p = 2")
+    for b in range(len(ells)):
+        np.testing.assert_allclose(m16[b].cpu().numpy(), m64[b].cpu().numpy(), rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(v16[b].cpu().numpy(), v64[b].cpu().numpy(), rtol=1e-7, atol=1e-13)
+    with _Dense():
+        ld, gd, idn = eng.lml_grad(act, th)
+        assert not idn.any()
+    _close(lb, gb, ld, gd, 3, "band16 Q 6-8 vs dense")
+    for b, e in enumerate(ells):
+        if e not in (2.0, 2.5, 3.0):
+            continue
+        m = gpx.models.GPR(data[b], kernel=K.SquaredExponential(lengthscales=e, variance=0.9), noise_variance=1e-5)
+        gpx.set_trainable(m.likelihood.variance, False)
+        loss, g = m.loss_and_grad_unconstrained(lml=lb[b], grad_theta=gb[b])
+        lo, go = _band_oracle_loss_grad(*data[b], e, 0.9)
+        assert abs(loss - lo) <= 1e-9 * abs(lo), (e, loss, lo)
+        assert np.abs(g - go).max() <= 1e-6 * max(1.0, np.abs(go).max()), (e, g, go)
+
+
+def test_mixed_ell_c2_call_band_storage_no_64row_sweeps():
+    """A C2 call through band storage (the bench's slots) with ℓ from 1 to 3 (Q = 3..8): every
+    evaluation on the band16 sweeps — no 64-row sweep launch, nothing on the fallback slots —
+    and each problem's logML and gradient the same as in a call of its own (composition)."""
+    from portfoliooptgp_amd.engine import Engine
+    from portfoliooptgp_amd.kernels import compile_spec
+    n = 4096
+    ells = [1.0, 1.18, 1.5, 1.8, 2.0, 2.2, 2.5, 2.7, 3.0, 1.3, 2.9, 1.1]
+    data = [O.synthetic_series(n, seed=60 + s) for s in range(len(ells))]
+    spec = compile_spec(K.SquaredExponential(), 1)
+    eng = Engine([d[0] for d in data], [d[1] for d in data], [spec] * len(ells), band_storage=True)
+    eng.ctx.set_profiling(True)
+    th = _theta(eng, [(e, 1.0, 1e-5) for e in ells])
+    act = list(range(len(ells)))
+    eng.reset_timing()
+    l, g, info = eng.lml_grad(act, th)
+    t = eng.last_timing()
+    assert not info.any()
+    assert t.band16_evals == len(ells) and t.shadow_evals == 0 and t.band_fused_launches == 0, \
+        (t.band16_evals, t.shadow_evals, t.band_fused_launches)
+    for b in (0, 4, 8, 10):
+        l1, g1, _ = eng.lml_grad([b], th)
+        assert l1[b] == l[b] and np.array_equal(g1[b, :3], g[b, :3]), b

@@ -75,12 +75,25 @@ def test_two_wave_sweeps_fit_256_registers(kernels, q):
 
 
 def test_bench_sweeps_do_not_spill(kernels):
-    """Every sweep a C2 (SE1) evaluation can launch: band16 fwd/bwd for Q = 1..5 with K's tiles
-    computed in the sweeps (the default) or read from the K band, the fused sweeps, the wide
-    (Q = 4/5, deferred) kernel, and the build."""
-    pats = [r"band16_fwd_kernelILi[1-5]ELb[01]E", r"band16_bwd_kernelILi[1-5]ELi1ELb1ELb[01]E",
+    """Every sweep a C2 (SE1) evaluation can launch up to ℓ ≈ 2.4: band16 fwd/bwd for Q = 1..6
+    with K's tiles computed in the sweeps (the default) or read from the K band, the fused sweeps,
+    the wide (Q = 4/5, deferred) kernel, and the build."""
+    pats = [r"band16_fwd_kernelILi[1-6]ELb[01]E", r"band16_bwd_kernelILi[1-6]ELi1ELb1ELb[01]E",
             r"band16_fused_kernelILi[1-5]ELb0ELb0E", r"band16_fused_kernelILi[1-5]ELb1ELb1E",
-            r"band16_wide_kernel", r"band16_build_kernel"]
+            r"band16_wide_kernelILb[01]ELb[01]ELi5E", r"band16_build_kernel"]
     for p in pats:
         for name, (v, a, scratch) in _find(kernels, p).items():
             assert scratch == 0, (name, v, a, scratch)
+
+
+def test_widest_band16_classes_spill_within_budget(kernels):
+    """Q = 7, 8 (ℓ ≈ 2.5-3.3 at the C2 inputs, SE1 with K inline): the window no longer fits the
+    512 VGPRs + AGPRs of one wave; their spills stay under 1 KiB per lane (2 KiB for the wide
+    launch that holds every class from 4 to 8), and nothing wider than Q = 8 is built."""
+    for q in (7, 8):
+        for name, (v, a, scratch) in _find(kernels, rf"band16_(fwd|bwd)_kernelILi{q}E").items():
+            assert scratch <= 1024, (name, v, a, scratch)
+    # the wide launch that also takes Q = 6..8 (one kernel: the widest branch sets its scratch)
+    for name, (v, a, scratch) in _find(kernels, r"band16_wide_kernelILb1ELb1ELi8E").items():
+        assert scratch <= 2048, (name, v, a, scratch)
+    assert not [k for k in kernels if re.search(r"band16_(fwd|bwd)_kernelILi(9|1[0-9])E", k)]
