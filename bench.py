@@ -906,7 +906,7 @@ def main():
         k = sweeps[kname]
         b16 = kname.startswith("band16")
         roofline = {
-            "kernel": ("band16_wide_kernel (the deferred Q = 4, 5 classes: one wavefront walks a problem's 256 block "
+            "kernel": ("band16_wide_kernel (the deferred Q = 4..8 classes: one wavefront walks a problem's 256 block "
                        "steps forward, then back)" if kname == "band16_wide_kernel" else
                        f"{kname}<Q> (16-row blocks, one wavefront walks a problem's 256 block steps; mean Q {q_mean:.2f})"
                        if b16 else f"{kname} (p<=1 class: one workgroup walks a problem's 64 block steps)"),

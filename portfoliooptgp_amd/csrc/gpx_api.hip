@@ -498,14 +498,16 @@ RouteKind route_one(const gpx_batch* bt, int b, const double* thb, const RouteLi
   return bt->compact ? kRouteShadow : kRouteDense;   // (band storage: dense on the fallback slots)
 }
 
-void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double* theta, Route& rt) {
+void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double* theta, Route& rt,
+                int q16wide_cap) {
   std::vector<int32_t>& order = rt.order;
   order.clear();
   order.reserve(n_active);
   rt.shadow_ids.clear();
   std::vector<int32_t> band_ids, fused_ids;
   int pband = 0;
-  const RouteLimits L = route_limits(bt);
+  RouteLimits L = route_limits(bt);
+  L.q16wide = std::min(L.q16wide, q16wide_cap);
   std::vector<int32_t> b16_ids[kBand16MaxQ + 1];  // band16 class by width Q (16-blocks)
   bool b16_p2 = false;                             // ... holding p = 2 problems (K band of 3 diagonals)
   for (int i = 0; i < n_active; ++i) {
@@ -1864,6 +1866,12 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   // band16 sweeps by width, the 64-row fused sweeps, or the fallback slots of band storage)
   Route rt;
   route_call(bt, n_active, active, theta, rt);
+  // a call with few band16 problems takes them by block cyclic reduction (gpx_bcr.hip, Q <= 5):
+  // there its p64 = 2 problems go back to the 64-row sweeps (a Q = 6..8 one-wave sweep is the
+  // throughput choice, but its N/16-step chain is 2-3x the 64-row sweeps' latency)
+  const int bcr_max = bcr_max_problems();
+  if (rt.n16 > 0 && rt.n16 <= bcr_max && rt.n_g16 > 0 && rt.g16_q[rt.n_g16 - 1] > kBcrMaxQ)
+    route_call(bt, n_active, active, theta, rt, kBcrMaxQ);
   std::vector<int32_t>& order = rt.order;
   std::vector<int32_t>& shadow_ids = rt.shadow_ids;
   const int n_dense = rt.n_dense, n_band = rt.n_band, n_fused = rt.n_fused, n16 = rt.n16;
@@ -1873,7 +1881,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   const bool b16_p2 = rt.b16_p2;
   // a call with few band16 problems takes them by block cyclic reduction (gpx_bcr.hip): the
   // one-wavefront sweeps' N/16-step chain would be the whole call's latency
-  const int bcr_q = (n16 > 0 && n16 <= bcr_max_problems()) ? 1 : 0;
+  const int bcr_q = (n16 > 0 && n16 <= bcr_max) ? 1 : 0;
   // (the width groups of Q <= kBcrMaxQ: the reduction; wider ones keep their sweeps, so a
   // problem's arithmetic depends on its own width and the call's size only)
   int g_bcr = 0, n16_bcr = 0;

@@ -281,7 +281,10 @@ struct Route {
   int n_g16 = 0, g16_q[kBand16MaxQ] = {}, g16_n[kBand16MaxQ] = {};
   bool b16_p2 = false;
 };
-void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double* theta, Route& rt);
+// q16wide_cap: the widest SE1 band16 class this call may use (a latency-bound call of few problems
+// keeps its p64 = 2 problems on the 64-row sweeps: one wavefront walking N/16 steps is slower there)
+void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double* theta, Route& rt,
+                int q16wide_cap = kBand16MaxQ);
 // the per-call limits of the routing, and one problem's path under them (w: its band width, in
 // 16-blocks for kRouteBand16, in 64-blocks otherwise, -1 when not banded)
 struct RouteLimits { int plim = -1, q16lim = -1, q16wide = -1; bool fused_on = true; };
