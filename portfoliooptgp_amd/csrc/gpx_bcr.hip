@@ -41,6 +41,11 @@
 // wave w owns tile column w of every right-hand side and of every product it forms, so no tile
 // is computed twice and the results of a phase meet in LDS behind one barrier.
 #include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+
 #include "gpx_internal.h"
 #include "gpx_b16core.h"
 
@@ -898,7 +903,7 @@ static void launch_bcr_q(BcrArgs a, int max_terms, int np, int Nmax, hipStream_t
   hipLaunchKernelGGL(bcr_finish_kernel, dim3(np), dim3(256), 0, s, a);
 }
 
-void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStream_t s) {
+static void launch_bcr_direct(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStream_t s) {
   switch (Q) {
     case 1: launch_bcr_q<1>(a, max_terms, np, Nmax, s); break;
     case 2: launch_bcr_q<2>(a, max_terms, np, Nmax, s); break;
@@ -906,6 +911,72 @@ void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStr
     case 4: launch_bcr_q<4>(a, max_terms, np, Nmax, s); break;
     default: launch_bcr_q<5>(a, max_terms, np, Nmax, s); break;
   }
+}
+
+// The chain as a HIP graph. A call of few problems is launch-bound on the host: ~20 dependent
+// launches (build, ⌈log2 n0⌉ + 1 forward and as many backward levels, contraction, finish) cost
+// ~0.1 ms of submit time per call, a quarter of the device chain. The chain's launches are a pure
+// function of (Q, terms, problems, N_max) and the argument block (device pointers into the
+// batch's buffers, which stay put between calls), so it is captured once per distinct key and
+// replayed: the same kernels with the same arguments, one launch. GPX_BCR_GRAPH=0: direct launches.
+namespace {
+struct BcrGraphKey {
+  int Q, max_terms, np, Nmax, D, Np, ld;
+  long long sX, sY, sWs, sVec, sMat, sPartial;
+  const void* p[14];
+  bool operator==(const BcrGraphKey& o) const { return std::memcmp(this, &o, sizeof(*this)) == 0; }
+};
+struct BcrGraphHash {
+  size_t operator()(const BcrGraphKey& k) const {
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(&k);
+    size_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(k); ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+  }
+};
+std::mutex g_bcr_graph_mu;
+std::unordered_map<BcrGraphKey, hipGraphExec_t, BcrGraphHash> g_bcr_graphs;
+constexpr size_t kBcrGraphCap = 1024;  // distinct chains kept (beyond: direct launches)
+}  // namespace
+
+void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStream_t s) {
+  static const bool graphs = [] {
+    const char* e = getenv("GPX_BCR_GRAPH");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!graphs) return launch_bcr_direct(a, Q, max_terms, np, Nmax, s);
+  BcrGraphKey k;
+  std::memset(&k, 0, sizeof(k));  // (padding included: the key is compared and hashed bytewise)
+  k.Q = Q; k.max_terms = max_terms; k.np = np; k.Nmax = Nmax; k.D = a.D; k.Np = a.Np; k.ld = a.ld;
+  k.sX = a.sX; k.sY = a.sY; k.sWs = a.sWs; k.sVec = a.sVec; k.sMat = a.sMat; k.sPartial = a.sPartial;
+  const void* ptrs[14] = {a.active, a.specs, a.theta, a.nvalid, a.X, a.Y, a.ws, a.info,
+                          a.z, a.ldiag, a.alpha, a.Kd, a.partial, a.results};
+  std::memcpy(k.p, ptrs, sizeof(ptrs));
+  hipGraphExec_t exec = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_bcr_graph_mu);
+    auto it = g_bcr_graphs.find(k);
+    if (it != g_bcr_graphs.end()) exec = it->second;
+    else if (g_bcr_graphs.size() >= kBcrGraphCap) return launch_bcr_direct(a, Q, max_terms, np, Nmax, s);
+  }
+  if (!exec) {
+    hipGraph_t g = nullptr;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) != hipSuccess)
+      return launch_bcr_direct(a, Q, max_terms, np, Nmax, s);
+    BcrArgs c = a;
+    c.level = 0;
+    launch_bcr_direct(c, Q, max_terms, np, Nmax, s);
+    if (hipStreamEndCapture(s, &g) != hipSuccess || !g ||
+        hipGraphInstantiate(&exec, g, nullptr, nullptr, 0) != hipSuccess) {
+      if (g) (void)hipGraphDestroy(g);
+      (void)hipGetLastError();
+      return launch_bcr_direct(a, Q, max_terms, np, Nmax, s);
+    }
+    (void)hipGraphDestroy(g);
+    std::lock_guard<std::mutex> lk(g_bcr_graph_mu);
+    g_bcr_graphs.emplace(k, exec);
+  }
+  (void)hipGraphLaunch(exec, s);
 }
 
 }  // namespace gpx

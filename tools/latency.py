@@ -50,7 +50,7 @@ def solo(n, seed, reps, evals):
             "fit_ms_all": [round(1e3 * w, 3) for w in walls], "nfev": nfev, "loss": fun}
 
 
-def c3(reps):
+def c3(reps, groups=1):
     from portfoliooptgp_amd.engine import Engine
     from portfoliooptgp_amd.kernels import compile_spec
     out = {"case": "c3"}
@@ -62,7 +62,9 @@ def c3(reps):
             data = [B.synthetic_series(2048, s) for s in range(k)]
             data = [(torch.as_tensor(a, device=dev), torch.as_tensor(b, device=dev)) for a, b in data]
             spec = compile_spec(gpx.kernels.SquaredExponential(), 1)
-            eng = Engine([d[0] for d in data], [d[1] for d in data], [spec] * k, device=0, band_storage=True)
+            G = max(1, min(groups, k))
+            eng = [Engine([d[0] for d in data[g::G]], [d[1] for d in data[g::G]], [spec] * len(data[g::G]), device=0,
+                          band_storage=True) for g in range(G)]
             ms = []
             for i in range(k):
                 m = gpx.models.GPR(data=data[i], kernel=gpx.kernels.SquaredExponential(), device=0)
@@ -70,13 +72,21 @@ def c3(reps):
                 gpx.set_trainable(m.likelihood.variance, False)
                 ms.append(m)
             torch.cuda.synchronize()
+            os.environ["GPX_DRIVER_STATS"] = "1"
+            opt = gpx.optimizers.Scipy()
             t0 = time.perf_counter()
-            gpx.optimizers.Scipy().minimize_stream(ms, width=k, engine=eng, predict_train=True,
-                                                   options=dict(maxiter=100))
+            opt.minimize_stream(ms, width=k, engine=eng if G > 1 else eng[0], groups=G, predict_train=True,
+                                options=dict(maxiter=100))
             torch.cuda.synchronize()
             t.append(time.perf_counter() - t0)
+            os.environ.pop("GPX_DRIVER_STATS", None)
+            st = dict(opt.last_stats or {})
         t = sorted(t[1:])
         out[f"wall_ms_{k}"] = 1e3 * t[len(t) // 2]
+        if k == 20 and st.get("rounds"):  # the host loop's phases per round (the last run)
+            out["per_round_ms_20"] = {kk: round(1e3 * v / st["rounds"], 4) for kk, v in st.items()
+                                      if isinstance(v, float)}
+            out["rounds_20"] = st["rounds"]
     return out
 
 
@@ -84,6 +94,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--solo-reps", type=int, default=5)
     ap.add_argument("--c3-reps", type=int, default=3)
+    ap.add_argument("--c3-groups", type=int, default=1, help="device batches the C3 fits are split over")
+    ap.add_argument("--c3-only", action="store_true")
     ap.add_argument("--evals", type=int, default=50)
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--chain-only", action="store_true", help="only the per-evaluation device chain lines")
@@ -94,13 +106,16 @@ def main():
             os.environ.pop("GPX_BCR_MAX", None)
         else:
             os.environ["GPX_BCR_MAX"] = cap
-        for seed in (0, 1):
+        for seed in (() if a.c3_only else (0, 1)):
             r = solo(a.n, seed, a.solo_reps, a.evals)
             r["mode"] = mode
             print(json.dumps(r), flush=True)
-        r = c3(a.c3_reps)
+        r = c3(a.c3_reps, a.c3_groups)
         r["mode"] = mode
+        r["groups"] = a.c3_groups
         print(json.dumps(r), flush=True)
+    if a.c3_only:
+        return
     # device time of one reduction chain (profiling on: HIP events around the chain)
     os.environ.pop("GPX_BCR_MAX", None)
     N.Context.get(0).set_profiling(True)
