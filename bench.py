@@ -530,12 +530,14 @@ def c4_kernel(gpx, kind):
     return K.Exponential(active_dims=slice(0, 4)) * K.Exponential(active_dims=slice(4, 5))
 
 
-def secondary_c4(gpu, fits=32, kind="m52"):
+def secondary_c4(gpu, fits=32, kind="m52", groups=1):
     """Config C4 (BASELINE.json configs[3]) on the dense path: D = 5 (4 z-scored random-walk
     features + z-scored time), Matern52 (or `kind` "expxexp": the reference's Exponential ×
     Exponential product), N = 4096, fp64 (the reference's precision), σn² = 1e-3 fixed, scipy
-    defaults + maxiter 100, predict_f at the training inputs; `fits` series in two device
-    batches. Also the fused K⁻¹ + gradient contraction's rate over those launches."""
+    defaults + maxiter 100, predict_f at the training inputs; `fits` series in `groups` device
+    batches (one: the 32-problem calls keep the GEMMs' tiles fuller than two concurrent batches of
+    16 — 36.1 vs 33.7 fits/s on one box, 4 batches 30.8, tools/c4_layouts.py). Also the fused
+    K⁻¹ + gradient contraction's rate over those launches."""
     import torch
     import portfoliooptgp_amd as gpx
     n = 4096
@@ -558,17 +560,18 @@ def secondary_c4(gpu, fits=32, kind="m52"):
     from portfoliooptgp_amd.engine import Engine
     from portfoliooptgp_amd.kernels import compile_spec
     spec = compile_spec(c4_kernel(gpx, kind), 5)
-    engines = [Engine([d[0] for d in data[g::2]], [d[1] for d in data[g::2]], [spec] * len(data[g::2]), device=gpu)
-               for g in range(2)]
+    engines = [Engine([d[0] for d in data[g::groups]], [d[1] for d in data[g::groups]], [spec] * len(data[g::groups]),
+                      device=gpu) for g in range(groups)]
     engines[0].ctx.set_profiling(True)
     opt = gpx.optimizers.Scipy()
-    opt.minimize_stream(models(2), width=2, engine=engines, groups=2, predict_train=True,
+    eng_arg = engines if groups > 1 else engines[0]
+    opt.minimize_stream(models(groups), width=groups, engine=eng_arg, groups=groups, predict_train=True,
                         options=dict(maxiter=MAXITER))  # warm-up
     for e in engines:
         e.reset_timing()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res, _ = opt.minimize_stream(models(fits), width=fits, engine=engines, groups=2, predict_train=True,
+    res, _ = opt.minimize_stream(models(fits), width=fits, engine=eng_arg, groups=groups, predict_train=True,
                                  options=dict(maxiter=MAXITER))
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -582,7 +585,7 @@ def secondary_c4(gpu, fits=32, kind="m52"):
     kname = "Matern52" if kind == "m52" else "Exponential(dims 0-3) x Exponential(dim 4)"
     epi = "EPI_CONTRACT1" if kind == "m52" else "EPI_CONTRACT2"
     return {"config": "C4", "workload": f"Multi-Input shape: D=5, {kname}, N=4096, fp64, sigma_n^2=1e-3 fixed, "
-            f"{fits} fits, L-BFGS-B maxiter=100 + predict_f(X_train), dense path, 2 device batches",
+            f"{fits} fits, L-BFGS-B maxiter=100 + predict_f(X_train), dense path, {groups} device batch(es)",
             "fits_per_s": fits / dt, "fits": fits, "seconds": dt, "nfev_mean": float(np.mean([r.nfev for r in res])),
             "evals_per_s": evals / dt, "dense_evals": evals - sum(t.band_evals for t in tms),
             "eval_alg_tflops": evals * (n ** 3 + 2 * (P + 1) * n ** 2) / dt / 1e12,
