@@ -896,6 +896,14 @@ def main():
         ppl = k["alg_flops_per_launch"] / band_problem_flops(n, pw, fwd)
         tkey = ("band_fwd1_kernel" if fwd else "band_bwd1_kernel")  # (the committed traffic passes: the p <= 1 pair)
         k["traffic"], k["traffic_source"] = band_traffic(tkey, ppl) if (ppl > 0 and pw == 1) else (None, None)
+    # wave-time of each band16 kernel: problems per launch x launch ms, summed (one wavefront per
+    # problem): the SIMD time it holds, which is what bounds the fits/s when thousands of problems
+    # are in flight (the wide launch has the most device time — its few waves take ~10 ms each —
+    # but holds a small share of the wave slots)
+    for key in ("band16_fwd_kernel", "band16_bwd_kernel", "band16_wide_kernel"):
+        k = sweeps[key]
+        ev = tm["band16_wide_evals"] if key == "band16_wide_kernel" else e16 - tm["band16_wide_evals"]
+        k["wave_s"] = ev * k["avg_launch_ms"] * 1e-3 if k["launches"] > 0 else 0.0
     from_p = tm["band_p_sum"] / max(tm["band_evals"], 1.0)
     # the whole chip over the timed region: the MFMA flops of every banded evaluation (band16
     # tile products + the 64-row sweeps' block products) / wall time
@@ -925,10 +933,17 @@ def main():
             "traffic_unit": "bytes/launch", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
             "alg_flops_per_launch": k["alg_flops_per_launch"], "mean_p_blocks": from_p,
             "band16_share_of_band_evals": e16 / max(tm["band_evals"], 1.0), "band16_mean_q": q_mean,
-            "sweeps": {kk: {f: v[f] for f in ("achieved", "frac", "avg_launch_ms", "launches", "traffic")}
+            "sweeps": {kk: {f: v.get(f) for f in ("achieved", "frac", "avg_launch_ms", "launches", "traffic", "wave_s")}
                        for kk, v in sweeps.items() if v["launches"] > 0},
+            "by_wave_time": (lambda kw: {"kernel": kw, "frac": sweeps[kw]["frac"], "achieved": sweeps[kw]["achieved"],
+                                         "wave_s_share": sweeps[kw]["wave_s"] / max(sum(sweeps[x].get("wave_s", 0.0)
+                                                                                       for x in sweeps), 1e-30)})(
+                max(("band16_fwd_kernel", "band16_bwd_kernel", "band16_wide_kernel"),
+                    key=lambda x: sweeps[x].get("wave_s", 0.0))) if b16 else None,
             "chip_achieved": chip_ach, "chip_frac": chip_ach / FP64_PEAK_TFLOPS,
-            "note": ("banded path (DESIGN.md §3c/§3d): achieved = the MFMA flops a launch's problems issue (band16: "
+            "note": ("banded path (DESIGN.md §3c/§3d): the roofline kernel is the one with the most device time; "
+                     "by_wave_time names the one holding the most wave-slot time (problems x launch ms), which bounds "
+                     "the throughput; achieved = the MFMA flops a launch's problems issue (band16: "
                      "2*16^3 per 16x16x16 tile product, the 16x16 leaves' VALU work not counted; 64-row sweeps: "
                      "2*64^3 per block product, leaf 2/3 of one) / the launch's HIP-event duration; launches of "
                      "several device batches and host processes overlap on the GPU; traffic: the kernel's "
