@@ -601,13 +601,21 @@ class OFitResult:
     history: list = field(default_factory=list)
 
 
-def scipy_minimize(model: OGPR, maxiter: Optional[int] = 100) -> OFitResult:
+def scipy_minimize(model: OGPR, maxiter: Optional[int] = 100, on_not_pd: str = "raise") -> OFitResult:
     """gpflow.optimizers.Scipy().minimize(model.training_loss, model.trainable_variables,
-    options=dict(maxiter=...)) — scipy L-BFGS-B with jac=True, scipy defaults otherwise."""
+    options=dict(maxiter=...)) — scipy L-BFGS-B with jac=True, scipy defaults otherwise.
+    on_not_pd: "raise" (GPflow: a failed Cholesky escapes the fit) or "inf" (the product's
+    documented opt-in, optimizers.Scipy(on_not_pd="inf"): an infinite loss and a zero gradient
+    at that point, so the line search backs off)."""
     x0 = model.get_u()
 
     def func(u):
         model.set_u(u)
+        if on_not_pd == "inf":
+            try:
+                return model.loss_and_grad_u()
+            except np.linalg.LinAlgError:
+                return float("inf"), np.zeros_like(np.asarray(u, dtype=np.float64))
         return model.loss_and_grad_u()
 
     options = {} if maxiter is None else dict(maxiter=maxiter)
