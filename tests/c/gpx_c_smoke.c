@@ -62,6 +62,14 @@ int main(int argc, char** argv) {
   CHECK(gpx_batch_predict_train(bt, 1, act, theta, 1, dMean, dVar, info, NULL));
   double ytrain_var0;
   hipMemcpy(&ytrain_var0, dVar, sizeof(double), hipMemcpyDeviceToHost);
+  /* the same prediction packed by position: problem 1's row lands in row 0 */
+  const int32_t act1[1] = {1};
+  CHECK(gpx_batch_predict_train(bt, 1, act1, theta, 1, dMean, dVar, info, NULL));
+  double v1_full[2], v1_rows[2];
+  hipMemcpy(v1_full, dVar + N, sizeof(v1_full), hipMemcpyDeviceToHost);
+  CHECK(gpx_batch_predict_train_rows(bt, 1, act1, theta, 1, dMean, dVar, info, NULL));
+  hipMemcpy(v1_rows, dVar, sizeof(v1_rows), hipMemcpyDeviceToHost);
+  const int rows_match = v1_full[0] == v1_rows[0] && v1_full[1] == v1_rows[1];
   /* a bad argument comes back as a status code, never as a C++ exception */
   const int bad = gpx_batch_lml_grad(bt, 0, act, theta, lml, grad, info, NULL);
 
@@ -72,7 +80,8 @@ int main(int argc, char** argv) {
   for (int i = 0; i < 2 * M; ++i) printf("%s%.17g", i ? ", " : "", mean[i]);
   printf("], \"var\": [");
   for (int i = 0; i < 2 * M; ++i) printf("%s%.17g", i ? ", " : "", var[i]);
-  printf("], \"ytrain_var0\": %.17g, \"bad_arg_status\": %d}\n", ytrain_var0, bad);
+  printf("], \"ytrain_var0\": %.17g, \"train_rows_match\": %d, \"bad_arg_status\": %d}\n", ytrain_var0,
+         rows_match, bad);
   gpx_batch_destroy(bt);
   gpx_destroy(ctx);
   hipFree(dX); hipFree(dY); hipFree(dXn); hipFree(dMean); hipFree(dVar);

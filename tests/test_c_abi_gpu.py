@@ -54,3 +54,4 @@ def test_c_consumer_matches_oracle():
     _, v0 = cases[0][4].predict_f(x0)
     assert abs(out["ytrain_var0"] - (float(v0.ravel()[0]) + 1e-2)) <= 1e-8
     assert out["bad_arg_status"] == 2  # GPX_BAD_ARG, no exception across the ABI
+    assert out["train_rows_match"] == 1  # gpx_batch_predict_train_rows: the same bits, packed by position
