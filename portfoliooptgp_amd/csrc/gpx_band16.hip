@@ -367,11 +367,21 @@ __device__ __forceinline__ void fwd_sweep(const BandFusedArgs& a, double* __rest
 #pragma unroll
           for (int r = 0; r < 4; ++r) xe[r] = -0.5 * sqdist1_b(ac[r], m2ar, ar2);
           E.exp4(xe, ev);
+          if (bn * 16 + 16 <= n) {
+            // (uniform) every row of block bn holds data, so every entry of its tiles does: only
+            // the diagonal tile's diagonal takes σn² — the general form below without its selects
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int gj = c * 16 + 4 * r + l4;
-            const double v = kvar * ev[r];
-            t[r] = !(gi < n && gj < n) ? (gi == gj ? 1.0 : 0.0) : (gi == gj ? v + knoise : v);
+            for (int r = 0; r < 4; ++r) {
+              const double v = kvar * ev[r];
+              t[r] = (j == Q && 4 * r + l4 == l15) ? v + knoise : v;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int gj = c * 16 + 4 * r + l4;
+              const double v = kvar * ev[r];
+              t[r] = !(gi < n && gj < n) ? (gi == gj ? 1.0 : 0.0) : (gi == gj ? v + knoise : v);
+            }
           }
           if (kst) ktile_store(K, ld, bn, c, t, l15, l4);
         }

@@ -14,7 +14,7 @@ import portfoliooptgp_amd as gpx
 from portfoliooptgp_amd.engine import Engine
 from portfoliooptgp_amd.kernels import compile_spec
 import bench
-n = 4096
+n = int(os.environ["BITS_N"])
 ells = np.linspace(0.4, 3.2, 64)
 data = [bench.synthetic_series(n, s) for s in range(64)]
 eng = Engine([d[0] for d in data], [d[1] for d in data], [compile_spec(gpx.kernels.SquaredExponential(), 1)] * 64,
@@ -26,17 +26,18 @@ print(json.dumps({"lml": [float(v).hex() for v in l], "g": [float(v).hex() for v
 '''
 
 
-def run(lib):
-    env = dict(os.environ, REPO=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+def run(lib, n):
+    env = dict(os.environ, REPO=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), BITS_N=str(n))
     if lib:
         env["GPX_LIB"] = lib
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, check=True).stdout
     return json.loads(out.strip().splitlines()[-1])
 
 
-a = run(None)
-b = run(os.environ["GPX_LIB_ALT"])
-same_l = sum(x == y for x, y in zip(a["lml"], b["lml"]))
-same_g = sum(x == y for x, y in zip(a["g"], b["g"]))
-print(json.dumps({"lml_identical": same_l, "of": len(a["lml"]), "grad_identical": same_g, "of_g": len(a["g"]),
-                  "info_equal": a["info"] == b["info"]}))
+for n in (4096, 4001):  # (a whole number of 16-row blocks, and a ragged last block)
+    a = run(None, n)
+    b = run(os.environ["GPX_LIB_ALT"], n)
+    same_l = sum(x == y for x, y in zip(a["lml"], b["lml"]))
+    same_g = sum(x == y for x, y in zip(a["g"], b["g"]))
+    print(json.dumps({"n": n, "lml_identical": same_l, "of": len(a["lml"]), "grad_identical": same_g,
+                      "of_g": len(a["g"]), "info_equal": a["info"] == b["info"]}))
