@@ -587,6 +587,7 @@ def secondary_c4(gpu, fits=32, kind="m52", groups=1):
     return {"config": "C4", "workload": f"Multi-Input shape: D=5, {kname}, N=4096, fp64, sigma_n^2=1e-3 fixed, "
             f"{fits} fits, L-BFGS-B maxiter=100 + predict_f(X_train), dense path, {groups} device batch(es)",
             "fits_per_s": fits / dt, "fits": fits, "seconds": dt, "nfev_mean": float(np.mean([r.nfev for r in res])),
+            "nfev_max": int(max(r.nfev for r in res)),
             "evals_per_s": evals / dt, "dense_evals": evals - sum(t.band_evals for t in tms),
             "eval_alg_tflops": evals * (n ** 3 + 2 * (P + 1) * n ** 2) / dt / 1e12,
             "contraction_roofline": {

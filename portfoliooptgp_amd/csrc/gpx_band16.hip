@@ -682,12 +682,14 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
           const bool dg = i == 0 && il == l15;
           double kraw;
           if constexpr (KIN) {
-            // (rows past n: the ring holds 0 there and `ok` masks them; off the diagonal tile the
-            // rows past n are exact zeros of K for any finite r², as the built band holds)
+            // (a zero tile's kexp stays 0: kraw is 0.0 there, as the built band holds. Rows past
+            // n: on the diagonal tile `ok` masks them; off it their α (the ring holds 0) and Z
+            // entries are exact zeros, so each of their terms below adds ±0 to a sum that starts
+            // at +0 and only meets finite values — the sums' bits are those of the masked form)
             kraw = 0.0;
             if (!zero) {
               const double kv = fvar * kexp[r];  // (stationary_value<GPX_SE>'s operations)
-              kraw = dg ? kv + noise : (i > 0 && gi >= n ? 0.0 : kv);
+              kraw = dg ? kv + noise : kv;
             }
           } else {
             const bool up = i == 0 && il < l15;
@@ -697,7 +699,7 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
           // rows or columns past n: off the diagonal tile the built band holds exact zeros there
           // (the padding is the identity), so only the diagonal tile needs the mask
           const bool ok = i > 0 || (jok && gi < n);
-          const double kij = (zero || !ok) ? 0.0 : kraw;
+          const double kij = KIN ? (ok ? kraw : 0.0) : ((zero || !ok) ? 0.0 : kraw);
           const double kg = i > 0 ? kij : (ok ? (dg ? fvar : kij) : 0.0);  // σ²·g (the noise is not part of ∂K/∂θ)
           sums[0][0] = fma(v, kg * r2, sums[0][0]);  // (× 1/ℓ once, at the end)
           sums[0][1] = fma(v, kg, sums[0][1]);

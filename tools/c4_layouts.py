@@ -12,4 +12,4 @@ for g in [int(v) for v in sys.argv[1:]] or [1, 2, 4]:
     for kind in ("m52",):
         r = bench.secondary_c4(0, kind=kind, groups=g)
         print(json.dumps({"groups": g, "kind": kind, "fits_per_s": r["fits_per_s"], "eval_alg_tflops": r["eval_alg_tflops"],
-                          "nfev_mean": r["nfev_mean"], "contraction_frac": r["contraction_roofline"]["frac"]}), flush=True)
+                          "nfev_mean": r["nfev_mean"], "nfev_max": r["nfev_max"], "seconds": r["seconds"], "contraction_frac": r["contraction_roofline"]["frac"]}), flush=True)
