@@ -516,6 +516,11 @@ def wave_trace_summary(recs, wall_s, clock_hz=1e8):
             "fwd_wave_ms_mean": float(dur[fwd].mean()) if fwd.any() else None,
             "bwd_wave_ms_mean": float(dur[bwd].mean()) if bwd.any() else None,
             "q_hist": {int(q): int((kind % 16 == q).sum() // 2) for q in np.unique(kind % 16)},
+            # per width class: waves, mean forward / backward wave ms, share of all wave time
+            "q_wave": {int(q): [int((kind == q).sum()), float(dur[kind == q].mean()) if (kind == q).any() else None,
+                                float(dur[kind == 16 + q].mean()) if (kind == 16 + q).any() else None,
+                                float(dur[kind % 16 == q].sum() / max(dur.sum(), 1e-30))]
+                       for q in np.unique(kind % 16)},
             "note": "band16 wavefronts only (s_memrealtime at each wave's start and end); span = first "
                     "start to last end over all host processes of this GPU"}
 

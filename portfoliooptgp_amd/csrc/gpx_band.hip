@@ -279,9 +279,10 @@ void launch_band_contract(const BandContractArgs& a, int max_terms, int n_active
 // predict_f / predict_y at the training inputs from a banded factorisation:
 //   mean_j = y_j − σn² α_j,  var_j = σn² − σn⁴ Z_jj  (+σn²)   (as train_pred_kernel, with the
 // diagonal of K⁻¹ read from the selected inverse instead of Σ_i W_ij²)
-__global__ __launch_bounds__(256) void band_train_pred_kernel(TrainPredArgs a) {
+// (one-wave workgroups, as the reduce kernel: they fit any free wave slot)
+__global__ __launch_bounds__(64) void band_train_pred_kernel(TrainPredArgs a) {
   const int b = a.active[blockIdx.y];
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int j = blockIdx.x * 64 + threadIdx.x;
   const int n = a.nvalid[b];
   if (j >= n) return;
   const double s2 = a.theta[b * GPX_THETA_STRIDE + a.specs[b].n_params];
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(256) void band_train_pred_kernel(TrainPredArgs a) {
 }
 
 void launch_band_train_pred(const TrainPredArgs& a, int n_active, int Np, hipStream_t s) {
-  hipLaunchKernelGGL(band_train_pred_kernel, dim3((Np + 255) / 256, n_active), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(band_train_pred_kernel, dim3((Np + 63) / 64, n_active), dim3(64), 0, s, a);
 }
 
 // =======================================================================================
@@ -1412,15 +1413,16 @@ void launch_band_fused1(const BandFusedArgs& a, int max_terms, int n_active, hip
 
 namespace gpx {
 // flush_rebinds' gather: one workgroup per rebound slot
-__global__ __launch_bounds__(256) void rebind_gather_kernel(const RebindDesc* desc, int Nmax, int D, double* box) {
+// (one-wave workgroups: they fit any free wave slot beside the other processes' sweeps)
+__global__ __launch_bounds__(64) void rebind_gather_kernel(const RebindDesc* desc, int Nmax, int D, double* box) {
   const RebindDesc d = desc[blockIdx.x];
   const int tid = threadIdx.x, n = d.n, nx = Nmax * D, nv = n * D;
-  for (int e = tid; e < nx; e += 256) d.dx[e] = e < nv ? d.x[e] : 0.0;
-  for (int e = tid; e < Nmax; e += 256) d.dy[e] = e < n ? d.y[e] : 0.0;
+  for (int e = tid; e < nx; e += 64) d.dx[e] = e < nv ? d.x[e] : 0.0;
+  for (int e = tid; e < Nmax; e += 64) d.dy[e] = e < n ? d.y[e] : 0.0;
   if (d.box < 0) return;
   const int nb = (Nmax + 15) / 16;  // 16-row boxes (kBox)
   double* out = box + (size_t)d.box * nb * D * 2;
-  for (int t = tid; t < nb * D; t += 256) {
+  for (int t = tid; t < nb * D; t += 64) {
     const int k = t / D, q = t - k * D;
     double lo = INFINITY, hi = -INFINITY;
     for (int r = k * 16; r < min(n, k * 16 + 16); ++r) {
@@ -1434,7 +1436,7 @@ __global__ __launch_bounds__(256) void rebind_gather_kernel(const RebindDesc* de
 }
 
 void launch_rebind_gather(const RebindDesc* desc, int m, int Nmax, int D, double* box, hipStream_t s) {
-  hipLaunchKernelGGL(rebind_gather_kernel, dim3(m), dim3(256), 0, s, desc, Nmax, D, box);
+  hipLaunchKernelGGL(rebind_gather_kernel, dim3(m), dim3(64), 0, s, desc, Nmax, D, box);
 }
 }  // namespace gpx
 

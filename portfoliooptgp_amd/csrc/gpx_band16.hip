@@ -965,11 +965,11 @@ __global__ __launch_bounds__(256) void band16_build_kernel(BuildArgs a, int Q) {
 
 // a deferred slow part's results, gathered for one download: rows act[i] of the batch's result
 // block and info into compact [n][stride] / [n] buffers
-__global__ __launch_bounds__(256) void slow_gather_kernel(const int* __restrict__ act, int n,
+__global__ __launch_bounds__(64) void slow_gather_kernel(const int* __restrict__ act, int n,
                                                           const double* __restrict__ res, int stride,
                                                           double* __restrict__ out, const int* __restrict__ info,
                                                           int* __restrict__ info_out) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int t = blockIdx.x * 64 + threadIdx.x;
   if (t >= n * stride) return;
   const int i = t / stride, c = t - i * stride, b = act[i];
   out[t] = res[(long long)b * stride + c];
@@ -979,7 +979,7 @@ __global__ __launch_bounds__(256) void slow_gather_kernel(const int* __restrict_
 void launch_slow_gather(const int* act, int n, const double* res, int stride, double* out, const int* info,
                         int* info_out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(slow_gather_kernel, dim3((n * stride + 255) / 256), dim3(256), 0, s, act, n, res, stride, out,
+  hipLaunchKernelGGL(slow_gather_kernel, dim3((n * stride + 63) / 64), dim3(64), 0, s, act, n, res, stride, out,
                      info, info_out);
 }
 

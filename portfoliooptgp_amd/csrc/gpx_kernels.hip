@@ -950,49 +950,57 @@ void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s) {
 // ======================================================================================
 // logML and gradient from the per-tile partials: one WG per problem, fixed order.
 // ======================================================================================
-__global__ __launch_bounds__(256) void reduce_kernel(ReduceArgs a) {
+// One wave per problem: the four 256-thread partial sums (virtual thread v·64 + lane, wave v)
+// are formed one after another, each with the same loop and the same butterfly, and combined in
+// the same order — the bits of a 256-thread workgroup. A one-wave workgroup fits any free wave
+// slot: on a chip full of one-wave sweeps a four-wave one waits until four slots of one CU are
+// free at once, which the sweeps' dispatches rarely leave (≈ 1 ms per call, call timeline).
+__global__ __launch_bounds__(64) void reduce_kernel(ReduceArgs a) {
   const int b = a.active[blockIdx.x];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lane = threadIdx.x;
   __shared__ double sred[4][GPX_THETA_STRIDE + 2];
-  double ps[GPX_THETA_STRIDE];
-#pragma unroll
-  for (int p = 0; p < GPX_THETA_STRIDE; ++p) ps[p] = 0.0;
   const double* part = a.partial + (long long)b * a.sPartial;
-  for (int t = tid; t < a.ntiles; t += 256) {
-#pragma unroll
-    for (int p = 0; p < GPX_THETA_STRIDE; ++p) ps[p] += part[(long long)t * GPX_THETA_STRIDE + p];
-  }
-  double zz = 0.0, sl = 0.0;
   const double* z = a.z + (long long)b * a.sVec;
   const double* ld = a.ldiag + (long long)b * a.sVec;
-  for (int i = tid; i < a.Np; i += 256) {
-    zz = fma(z[i], z[i], zz);
-    sl += ld[i];
-  }
+#pragma unroll 1
+  for (int wave = 0; wave < 4; ++wave) {
+    const int tid = wave * 64 + lane;
+    double ps[GPX_THETA_STRIDE];
 #pragma unroll
-  for (int p = 0; p < GPX_THETA_STRIDE; ++p) ps[p] = wave_sum(ps[p]);
-  zz = wave_sum(zz);
-  sl = wave_sum(sl);
-  if (lane == 0) {
+    for (int p = 0; p < GPX_THETA_STRIDE; ++p) ps[p] = 0.0;
+    for (int t = tid; t < a.ntiles; t += 256) {
 #pragma unroll
-    for (int p = 0; p < GPX_THETA_STRIDE; ++p) sred[wave][p] = ps[p];
-    sred[wave][GPX_THETA_STRIDE] = zz;
-    sred[wave][GPX_THETA_STRIDE + 1] = sl;
+      for (int p = 0; p < GPX_THETA_STRIDE; ++p) ps[p] += part[(long long)t * GPX_THETA_STRIDE + p];
+    }
+    double zz = 0.0, sl = 0.0;
+    for (int i = tid; i < a.Np; i += 256) {
+      zz = fma(z[i], z[i], zz);
+      sl += ld[i];
+    }
+#pragma unroll
+    for (int p = 0; p < GPX_THETA_STRIDE; ++p) ps[p] = wave_sum(ps[p]);
+    zz = wave_sum(zz);
+    sl = wave_sum(sl);
+    if (lane == 0) {
+#pragma unroll
+      for (int p = 0; p < GPX_THETA_STRIDE; ++p) sred[wave][p] = ps[p];
+      sred[wave][GPX_THETA_STRIDE] = zz;
+      sred[wave][GPX_THETA_STRIDE + 1] = sl;
+    }
   }
   __syncthreads();
-  if (tid < GPX_THETA_STRIDE + 2) {
-    const double v = sred[0][tid] + sred[1][tid] + sred[2][tid] + sred[3][tid];
+  if (lane < GPX_THETA_STRIDE + 2) {
+    const double v = sred[0][lane] + sred[1][lane] + sred[2][lane] + sred[3][lane];
     double* res = a.results + (long long)b * kResStride;
-    if (tid < GPX_THETA_STRIDE) {
-      res[1 + tid] = 0.5 * v;
-    } else if (tid == GPX_THETA_STRIDE) {
+    if (lane < GPX_THETA_STRIDE) {
+      res[1 + lane] = 0.5 * v;
+    } else if (lane == GPX_THETA_STRIDE) {
       res[17] = v;
     } else {
       res[18] = v;
     }
   }
-  __syncthreads();
-  if (tid == 0) {
+  if (lane == 0) {
     double* res = a.results + (long long)b * kResStride;
     const double zz2 = sred[0][GPX_THETA_STRIDE] + sred[1][GPX_THETA_STRIDE] +
                        sred[2][GPX_THETA_STRIDE] + sred[3][GPX_THETA_STRIDE];
@@ -1004,7 +1012,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(ReduceArgs a) {
 }
 
 void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_kernel, dim3(n_active), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(reduce_kernel, dim3(n_active), dim3(64), 0, s, a);
 }
 
 // var_j = k(x*_j, x*_j) − Σ_rowtiles colsum partials (+ σn² for predict_y)
