@@ -1646,11 +1646,12 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
   if (own) {
     HIPX(ctx, hipEventRecord(bt->slow_up, s));
     HIPX(ctx, hipStreamWaitEvent(ss, bt->slow_up, 0));
-    HIPX(ctx, hipMemcpyAsync(bt->d_slow_act, bt->d_active + off, sizeof(int) * n, hipMemcpyDeviceToDevice, ss));
-    HIPX(ctx, hipMemcpyAsync(bt->d_slow_theta, bt->d_theta, sizeof(double) * bt->B * GPX_THETA_STRIDE,
-                             hipMemcpyDeviceToDevice, ss));
-    HIPX(ctx, hipMemcpyAsync(bt->d_slow_bandp, bt->d_bandp, sizeof(int) * bt->B, hipMemcpyDeviceToDevice, ss));
-    HIPX(ctx, hipMemsetAsync(bt->d_slow_info, 0, sizeof(int) * bt->B, ss));
+    // one launch of one-wave workgroups, not the runtime's three copies and a fill: its blit
+    // kernels' multi-wave workgroups wait for free CU space behind the other processes' sweeps
+    // (+2.8 % on the bench, profiles/r05_ab.md)
+    launch_slow_inputs(bt->d_active + off, n, bt->d_slow_act, bt->d_theta, bt->d_slow_theta, bt->d_bandp,
+                       bt->d_slow_bandp, bt->d_slow_info, bt->B, ss);
+    HIPX(ctx, hipGetLastError());
     HIPX(ctx, hipEventRecord(bt->slow_in, ss));
     bt->slow_in_armed = true;
   }

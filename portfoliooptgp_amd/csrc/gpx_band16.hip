@@ -976,6 +976,26 @@ __global__ __launch_bounds__(64) void slow_gather_kernel(const int* __restrict__
   if (c == 0) info_out[i] = info[b];
 }
 
+__global__ __launch_bounds__(64) void slow_inputs_kernel(const int* __restrict__ act, int n, int* __restrict__ act_out,
+                                                         const double* __restrict__ theta, double* __restrict__ theta_out,
+                                                         const int* __restrict__ bandp, int* __restrict__ bandp_out,
+                                                         int* __restrict__ info_out, int B) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t < B * GPX_THETA_STRIDE) theta_out[t] = theta[t];
+  if (t < n) act_out[t] = act[t];
+  if (t < B) {
+    bandp_out[t] = bandp[t];
+    info_out[t] = 0;
+  }
+}
+
+void launch_slow_inputs(const int* act, int n, int* act_out, const double* theta, double* theta_out, const int* bandp,
+                        int* bandp_out, int* info_out, int B, hipStream_t s) {
+  const int m = std::max(B * GPX_THETA_STRIDE, n);
+  hipLaunchKernelGGL(slow_inputs_kernel, dim3((m + 63) / 64), dim3(64), 0, s, act, n, act_out, theta, theta_out, bandp,
+                     bandp_out, info_out, B);
+}
+
 void launch_slow_gather(const int* act, int n, const double* res, int stride, double* out, const int* info,
                         int* info_out, hipStream_t s) {
   if (n <= 0) return;

@@ -196,6 +196,10 @@ void launch_band16_build(const BuildArgs& a, int Q, int n_active, hipStream_t s)
 void launch_wave_marker(unsigned long long* wt, unsigned int* wn, unsigned int cap, int kind, hipStream_t s);
 // SE1 band16 problems of widths Q = 4 and 5 (bandp) in one launch, both sweeps per wavefront
 void launch_band16_wide(const BandFusedArgs& a, int kin, int n_active, hipStream_t s, hipEvent_t* ev, int wq = 5);
+// the deferred part's private copies of the call's active rows, θ and widths, and its zeroed
+// info block, in one launch of one-wave workgroups
+void launch_slow_inputs(const int* act, int n, int* act_out, const double* theta, double* theta_out, const int* bandp,
+                        int* bandp_out, int* info_out, int B, hipStream_t s);
 void launch_slow_gather(const int* act, int n, const double* res, int stride, double* out, const int* info,
                         int* info_out, hipStream_t s);
 void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int kin, int n_active, hipStream_t s,
