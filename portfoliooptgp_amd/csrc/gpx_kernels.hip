@@ -950,20 +950,22 @@ void launch_trmv_t(const TrmvArgs& a, int n_active, hipStream_t s) {
 // ======================================================================================
 // logML and gradient from the per-tile partials: one WG per problem, fixed order.
 // ======================================================================================
-// One wave per problem: the four 256-thread partial sums (virtual thread v·64 + lane, wave v)
-// are formed one after another, each with the same loop and the same butterfly, and combined in
-// the same order — the bits of a 256-thread workgroup. A one-wave workgroup fits any free wave
-// slot: on a chip full of one-wave sweeps a four-wave one waits until four slots of one CU are
-// free at once, which the sweeps' dispatches rarely leave (≈ 1 ms per call, call timeline).
-__global__ __launch_bounds__(64) void reduce_kernel(ReduceArgs a) {
+// The four 64-lane partial sums of a problem (virtual thread v·64 + lane, v = 0..3: the same
+// loops, butterflies and combine order either way, so the same bits) formed by four waves at
+// once (NW = 4), or by one wave one after another (NW = 1): a one-wave workgroup fits any free
+// wave slot, while on a chip full of one-wave sweeps a four-wave one waits until four slots of
+// one CU are free at once (≈ 1 ms per call in the call timeline). Calls with few problems (an
+// idle chip) keep the four-wave form.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void reduce_kernel(ReduceArgs a) {
   const int b = a.active[blockIdx.x];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   __shared__ double sred[4][GPX_THETA_STRIDE + 2];
   const double* part = a.partial + (long long)b * a.sPartial;
   const double* z = a.z + (long long)b * a.sVec;
   const double* ld = a.ldiag + (long long)b * a.sVec;
 #pragma unroll 1
-  for (int wave = 0; wave < 4; ++wave) {
+  for (int wave = (int)threadIdx.x >> 6; wave < 4; wave += NW) {
     const int tid = wave * 64 + lane;
     double ps[GPX_THETA_STRIDE];
 #pragma unroll
@@ -989,18 +991,19 @@ __global__ __launch_bounds__(64) void reduce_kernel(ReduceArgs a) {
     }
   }
   __syncthreads();
-  if (lane < GPX_THETA_STRIDE + 2) {
-    const double v = sred[0][lane] + sred[1][lane] + sred[2][lane] + sred[3][lane];
+  const int tid = threadIdx.x;
+  if (tid < GPX_THETA_STRIDE + 2) {
+    const double v = sred[0][tid] + sred[1][tid] + sred[2][tid] + sred[3][tid];
     double* res = a.results + (long long)b * kResStride;
-    if (lane < GPX_THETA_STRIDE) {
-      res[1 + lane] = 0.5 * v;
-    } else if (lane == GPX_THETA_STRIDE) {
+    if (tid < GPX_THETA_STRIDE) {
+      res[1 + tid] = 0.5 * v;
+    } else if (tid == GPX_THETA_STRIDE) {
       res[17] = v;
     } else {
       res[18] = v;
     }
   }
-  if (lane == 0) {
+  if (tid == 0) {
     double* res = a.results + (long long)b * kResStride;
     const double zz2 = sred[0][GPX_THETA_STRIDE] + sred[1][GPX_THETA_STRIDE] +
                        sred[2][GPX_THETA_STRIDE] + sred[3][GPX_THETA_STRIDE];
@@ -1012,7 +1015,10 @@ __global__ __launch_bounds__(64) void reduce_kernel(ReduceArgs a) {
 }
 
 void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_kernel, dim3(n_active), dim3(64), 0, s, a);
+  if (n_active <= 64)
+    hipLaunchKernelGGL(reduce_kernel<4>, dim3(n_active), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(reduce_kernel<1>, dim3(n_active), dim3(64), 0, s, a);
 }
 
 // var_j = k(x*_j, x*_j) − Σ_rowtiles colsum partials (+ σn² for predict_y)
