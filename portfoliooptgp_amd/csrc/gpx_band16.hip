@@ -458,7 +458,11 @@ struct Bwd16 {  // the backward sweep's LDS, in doubles
   static constexpr int kCs = kXT + (SE1 ? (Q + 1) * 16 : 0);   // band check: column sums ring
   static constexpr int kTh = kCs + (Q + 1) * 16;                // θ (not SE1: the term interpreter reads it in the loop)
   static constexpr int kRed = kTh + (SE1 ? 0 : 16);
-  static constexpr int size = kRed + (SE1 ? 0 : 16);
+  // LP (the Q = 4 inline-K sweep): the next step's W_kk and P_iᵀ staged in LDS by glds instead
+  // of registers — 40 VGPRs fewer, so the sweep fits two waves per SIMD without spilling
+  static constexpr bool LP = SE1 && KIN && Q == 4;
+  static constexpr int kPf = kRed + (SE1 ? 0 : 16);
+  static constexpr int size = kPf + (LP ? (Q + 1) * 256 : 0);
 };
 template <int Q, int NT, bool SE1, bool KIN>
 __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __restrict__ lds, double* __restrict__ sx) {
@@ -505,12 +509,29 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
   // W_kk and P_iᵀ (the forward sweep's tiles, frag_store layout) straight into registers: two
   // 16-byte loads per lane and tile, issued once this step's P/G registers are dead (after Z_kk),
   // so the prefetch needs no LDS and no extra registers
+  constexpr bool LP = Ly::LP;
+  double* spf = lds + Ly::kPf;  // LP: tile i (W_kk, P_iᵀ) as two 1 KiB halves (a lane's 16-byte pieces)
   auto fetch_f = [&](int kk, t4& Wn, t4 (&Pn)[Q + 1]) {
     const int q1 = min(Q, nb - 1 - kk);
     const double* Lk = L + (long long)kk * ((Q + 1) * 256) + 4 * lane;
-    Wn = *reinterpret_cast<const t4*>(Lk);
+    if constexpr (LP) {
 #pragma unroll
-    for (int i = 1; i <= Q; ++i) Pn[i] = (i <= q1) ? *reinterpret_cast<const t4*>(Lk + i * 256) : tzero();
+      for (int i = 0; i <= Q; ++i)
+        if (i <= q1) {
+          __builtin_amdgcn_global_load_lds(Lk + i * 256, spf + i * 256, 16, 0, 0);
+          __builtin_amdgcn_global_load_lds(Lk + i * 256 + 2, spf + i * 256 + 128, 16, 0, 0);
+        }
+    } else {
+      Wn = *reinterpret_cast<const t4*>(Lk);
+#pragma unroll
+      for (int i = 1; i <= Q; ++i) Pn[i] = (i <= q1) ? *reinterpret_cast<const t4*>(Lk + i * 256) : tzero();
+    }
+  };
+  // LP: tile i back from the staging buffer (lane's 4 doubles as they lie in the frag layout)
+  auto lds_tile = [&](int i) {
+    const double2 a0 = *reinterpret_cast<const double2*>(spf + i * 256 + 2 * lane);
+    const double2 a1 = *reinterpret_cast<const double2*>(spf + i * 256 + 128 + 2 * lane);
+    return (t4){a0.x, a0.y, a1.x, a1.y};
   };
   double zr[4], xr[2];
   t4 Wn, Pn[Q + 1];
@@ -561,10 +582,18 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
   for (int k = nb - 1; k >= 0; --k) {
     const int qk = min(Q, nb - 1 - k), k16 = k * 16, cs = k % (Q + 1);
     // this step's W_kk and P_iᵀ (loaded during the previous step)
-    const t4 Wf = Wn;
-    t4 P[Q + 1];  // P_iᵀ, then G_i
+    t4 Wf, P[Q + 1];  // P_iᵀ, then G_i
+    if constexpr (LP) {
+      vm_drain();  // (the staged tiles have landed; this step's reads precede the next fetch_f)
+      wsync();
+      Wf = lds_tile(0);
 #pragma unroll
-    for (int i = 1; i <= Q; ++i) P[i] = Pn[i];
+      for (int i = 1; i <= Q; ++i) P[i] = (i <= qk) ? lds_tile(i) : tzero();
+    } else {
+      Wf = Wn;
+#pragma unroll
+      for (int i = 1; i <= Q; ++i) P[i] = Pn[i];
+    }
     // X rows of block k -> ring slot cs (scaled by 1/ℓ as GPflow's Stationary.scale when fast)
     if constexpr (!SE1) {
 #pragma unroll
@@ -592,9 +621,17 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
     // reaches past the matrix stay 0 — and adding their zero products leaves every value as is)
     double t[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int i = 1; i <= Q; ++i)
+    for (int i = 1; i <= Q; ++i) {
+      // (LP: α_{k+i}[l15] from the ring the contraction reads — the value al[i] holds, without
+      // its registers and shifts)
+      double ai;
+      if constexpr (LP)
+        ai = salT[(k + i) % (Q + 1)][(l15 & 3) * 4 + (l15 >> 2)];
+      else
+        ai = al[i];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) t[r] = fma(P[i][r], al[i], t[r]);
+      for (int r = 0; r < 4; ++r) t[r] = fma(P[i][r], ai, t[r]);
+    }
     double ap = 0.0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) ap = fma(Wf[r], zc[r] - sum16(t[r]), ap);
@@ -818,7 +855,7 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
     S[wid(0, 0)] = Zk;
 #pragma unroll
     for (int i = Q; i >= 1; --i) {
-      al[i] = al[i - 1];
+      if constexpr (!LP) al[i] = al[i - 1];
       R[i] = R[i - 1];
     }
     R[1] = tzero();
@@ -868,7 +905,8 @@ __device__ __forceinline__ void bwd_sweep(const BandFusedArgs& a, double* __rest
 }
 
 template <int Q, int NT, bool SE1, bool KIN>
-__global__ __launch_bounds__(64, (Q <= GPX_B16_BWD_2W_QMAX && SE1) ? 2 : 1) void band16_bwd_kernel(BandFusedArgs a) {
+__global__ __launch_bounds__(64, ((Q <= GPX_B16_BWD_2W_QMAX && SE1) || Bwd16<Q, NT, SE1, KIN>::LP) ? 2 : 1)
+void band16_bwd_kernel(BandFusedArgs a) {
   extern __shared__ double sx[];
   __shared__ __attribute__((aligned(16))) double lds[Bwd16<Q, NT, SE1, KIN>::size];
   bwd_sweep<Q, NT, SE1, KIN>(a, lds, sx);

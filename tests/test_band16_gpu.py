@@ -297,3 +297,27 @@ def test_mixed_ell_c2_call_band_storage_no_64row_sweeps():
     for b in (0, 4, 8, 10):
         l1, g1, _ = eng.lml_grad([b], th)
         assert l1[b] == l[b] and np.array_equal(g1[b, :3], g[b, :3]), b
+
+
+def test_reduce_forms_bit_identical():
+    """The reduce kernel forms a problem's four 64-lane partial sums with four waves at once in
+    calls of at most 64 problems and with one wave, one after another, in larger calls
+    (gpx_kernels.hip reduce_kernel<NW>): the same loops, butterflies and combine order, so a
+    problem's logML and gradient carry the same bits in a call of 40 and in one of 80 (band16
+    sweeps both times: each problem's arithmetic is its own wavefront's)."""
+    n = 1024
+    data = [O.synthetic_series(n, seed=s) for s in range(80)]
+    eng = _engine([d[0] for d in data], [d[1] for d in data], K.SquaredExponential())
+    ells = np.linspace(0.8, 1.6, 80)
+    th = _theta(eng, [(l, 0.9, 1e-5) for l in ells])
+    eng.reset_timing()
+    l80, g80, i80 = eng.lml_grad(list(range(80)), th)
+    assert eng.last_timing().band16_evals == 80
+    for half in (range(0, 40), range(40, 80)):
+        act = list(half)
+        eng.reset_timing()
+        l40, g40, i40 = eng.lml_grad(act, th)
+        assert eng.last_timing().band16_evals == 40
+        assert np.array_equal(l40[act], l80[act])
+        assert np.array_equal(g40[act, :3], g80[act, :3])
+        assert np.array_equal(i40[act], i80[act])

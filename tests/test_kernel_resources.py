@@ -83,7 +83,16 @@ def test_bench_sweeps_do_not_spill(kernels):
             r"band16_wide_kernelILb[01]ELb[01]ELi5E", r"band16_build_kernel"]
     for p in pats:
         for name, (v, a, scratch) in _find(kernels, p).items():
-            assert scratch == 0, (name, v, a, scratch)
+            # the two-wave Q = 4 inline-K backward (its W/P prefetch staged in LDS, Bwd16::LP)
+            # keeps one 8-byte value in scratch across the step loop, reloaded after it
+            budget = 16 if re.search(r"band16_bwd_kernelILi4ELi1ELb1ELb1E", name) else 0
+            assert scratch <= budget, (name, v, a, scratch)
+
+
+def test_two_wave_q4_backward(kernels):
+    """The Q = 4 inline-K backward sweep runs two wavefronts per SIMD (<= 256 VGPRs + AGPRs)."""
+    for name, (v, a, scratch) in _find(kernels, r"band16_bwd_kernelILi4ELi1ELb1ELb1E").items():
+        assert v + a <= 256 and scratch <= 16, (name, v, a, scratch)
 
 
 def test_widest_band16_classes_spill_within_budget(kernels):
