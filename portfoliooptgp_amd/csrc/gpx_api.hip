@@ -55,7 +55,14 @@ double gemm_issued_flops(const GemmArgs& a, int na) {
 
 void gemm(const Run& r, GemmArgs a, int epi, bool ta, bool tb) {
   a.active = r.d_act;
-  a.small_tiles = r.bt->small_tiles;
+  // store GEMMs (the recursion's panels, trailing updates and inverses) pick 128-tiles only when
+  // the launch still has a workgroup per CU (64-tiles otherwise: 4x the workgroups for the
+  // recursion's lower levels in calls of few problems). An entry's sum runs over the same k in
+  // the same 4-wide MFMA chunks either way — a wider tile's k-range only adds products with the
+  // triangular operand's exact zeros, each ±0 onto a sum that is +0 until its first nonzero —
+  // so a problem's arithmetic still does not depend on its call (tests/test_gpu_parity.py).
+  // The contraction's per-tile partials do depend on the tile: it keeps the shape-only rule.
+  a.small_tiles = r.bt->small_tiles || epi == EPI_STORE;
   launch_gemm(a, epi, ta, tb, r.na, r.s);
   if (r.bt->ctx->profiling) r.bt->flops_acc += gemm_issued_flops(a, r.na);
 }

@@ -36,14 +36,19 @@ for _ in range(reps):
 for b1 in (1, 4):
     eng.lml_grad(act[:b1], th)
 torch.cuda.synchronize()
-t1 = {}
+t1, small = {}, []
 for b1 in (1, 4):
     t = time.perf_counter()
     for _ in range(reps):
-        eng.lml_grad(act[:b1], th)
+        ls, gs_, _ = eng.lml_grad(act[:b1], th)
     torch.cuda.synchronize()
     t1[b1] = (time.perf_counter() - t) / reps * 1e3
-print(json.dumps({"lml": [float(v).hex() for v in l], "g": [float(v).hex() for v in g[:, :3].ravel()],
+    small += [float(v).hex() for v in ls[:b1]] + [float(v).hex() for v in gs_[:b1, :3].ravel()]
+# (the small calls' bits against the same problems' in the B-problem call)
+same_small = small == ([float(v).hex() for v in l[:1]] + [float(v).hex() for v in g[:1, :3].ravel()]
+                       + [float(v).hex() for v in l[:4]] + [float(v).hex() for v in g[:4, :3].ravel()])
+print(json.dumps({"small_calls_match_full": same_small, "small": small,
+                  "lml": [float(v).hex() for v in l], "g": [float(v).hex() for v in g[:, :3].ravel()],
                   "info": info.tolist(), "ms_median": float(np.median(ts)) * 1e3, "ms_min": min(ts) * 1e3,
                   "ms_b1": t1[1], "ms_b4": t1[4]}))
 '''
@@ -68,12 +73,14 @@ def main():
             sys.exit(1)
         d = json.loads(out.stdout.strip().splitlines()[-1])
         first = first or d
+        same_s = first["small"] == d["small"]
         same_l = sum(x == y for x, y in zip(first["lml"], d["lml"]))
         same_g = sum(x == y for x, y in zip(first["g"], d["g"]))
         print(json.dumps({"setting": kv, "b": args.b, "ms_median": round(d["ms_median"], 2), "ms_min": round(d["ms_min"], 2),
                           "ms_b1": round(d["ms_b1"], 2), "ms_b4": round(d["ms_b4"], 2),
                           "lml_identical_to_first": f"{same_l}/{len(d['lml'])}",
-                          "grad_identical_to_first": f"{same_g}/{len(d['g'])}", "info_equal": d["info"] == first["info"]}),
+                          "grad_identical_to_first": f"{same_g}/{len(d['g'])}", "info_equal": d["info"] == first["info"],
+                          "b1_b4_bits_as_first": same_s, "b1_b4_bits_as_in_full_call": d["small_calls_match_full"]}),
               flush=True)
 
 
