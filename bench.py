@@ -151,10 +151,11 @@ def cpu_baseline(n: int, nfev_per_fit: float, evals: int = 3):
         "unit": "fits/s",
         "cores": int(cores),
         "kind": "port",
-        "sample": (f"oracle/gp_oracle.py (numpy {np.__version__} + OpenBLAS, fp64) on this host, "
-                   f"BLAS on {cores} threads: {evals} loss+grad evals ({t_eval:.3f} s each) + 1 predict_f "
-                   f"({t_pred:.3f} s) at N={n}; fit time = mean GPU nfev/fit ({nfev_per_fit:.1f}) x eval + "
-                   "predict"),
+        "extrapolated": True,
+        "sample": (f"EXTRAPOLATED from a timed sample: oracle/gp_oracle.py (numpy {np.__version__} + OpenBLAS, fp64) "
+                   f"on this host, BLAS on {cores} threads: {evals} loss+grad evals ({t_eval:.3f} s each) + 1 "
+                   f"predict_f ({t_pred:.3f} s) at N={n}; fit time = mean GPU nfev/fit ({nfev_per_fit:.1f}) x eval "
+                   "+ predict (a whole fit is minutes on the CPU)"),
         "eval_s": t_eval,
         "predict_s": t_pred,
         "value_1core": 1.0 / t_fit1,
@@ -625,8 +626,9 @@ def secondary_c3(gpu, n=2048, series=20, share=3, reps=3):
         gpx.set_trainable(m.likelihood.variance, False)
         return m
 
-    def run(k):
-        eng = Engine([d[0] for d in data[:k]], [d[1] for d in data[:k]], [spec] * k, device=gpu, band_storage=True)
+    def run(k, route="bcr"):
+        eng = Engine([d[0] for d in data[:k]], [d[1] for d in data[:k]], [spec] * k, device=gpu, band_storage=True,
+                     band_route=route)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         res, _ = gpx.optimizers.Scipy().minimize_stream([model(i) for i in range(k)], width=k, engine=eng,
@@ -636,6 +638,8 @@ def secondary_c3(gpu, n=2048, series=20, share=3, reps=3):
 
     run(share)  # warm-up
     w_all = sorted(run(series)[0] for _ in range(reps))[reps // 2]
+    run(share, "sweeps")
+    w_all_sweeps = sorted(run(series, "sweeps")[0] for _ in range(reps))[reps // 2]
     t_share, res_share = [], None
     for _ in range(reps):
         t, res_share = run(share)
@@ -647,8 +651,11 @@ def secondary_c3(gpu, n=2048, series=20, share=3, reps=3):
             "wall_s_per_gpu_share_at_8gpus": w_share, "share_series": share,
             "nfev_of_share": [int(r.nfev) for r in res_share],
             "ratio_wall_all_over_share": w_all / w_share,
-            "note": "calls of at most GPX_BCR_MAX (32) problems take the block-cyclic-reduction path (DESIGN.md "
-                    "§3f); wall(20) / wall(share) is an upper bound on the 8-GPU speed-up of this batch (the ranks' "
+            "band_route": "bcr",
+            "wall_s_all_series_1gpu_sweeps_route": w_all_sweeps,
+            "note": "the engine takes the latency route, block cyclic reduction (Engine(band_route='bcr'), "
+                    "DESIGN.md §3f; the default route, the one-wavefront sweeps, is timed beside it); "
+                    "wall(20) / wall(share) is an upper bound on the 8-GPU speed-up of this batch (the ranks' "
                     "shares run concurrently): each fit is a chain of ~20 dependent evaluations"}
 
 
@@ -656,8 +663,8 @@ def secondary_solo(gpu, n=N_POINTS, seeds=(0, 1, 2), reps=3):
     """The reference's own call pattern: ONE exact GPR fit at a time, as GPR/model_trainer.py:15-20
     runs it inside its kernel loop — models.GPR from GPflow's defaults, Scipy().minimize
     (maxiter=100), predict_f at the training inputs — on the C2 series (N = 4096, SE, sigma_n^2 =
-    1e-5 fixed). A call of one problem takes the block-cyclic-reduction path; the
-    one-wavefront band16 sweeps (GPX_BCR_MAX=0) are timed beside it on the same fits. Median wall
+    1e-5 fixed), on each banded route: the latency route (block cyclic reduction, DESIGN.md §3f;
+    gpx.set_default_band_route("bcr")) and the default, the one-wavefront band16 sweeps. Median wall
     time of `reps` fits per seed (after a warm-up fit), and the device time of one evaluation's
     reduction chain (HIP events, profiling on, a separate pass)."""
     import torch
@@ -678,14 +685,14 @@ def secondary_solo(gpu, n=N_POINTS, seeds=(0, 1, 2), reps=3):
 
     out = {"config": "C2, one fit at a time", "workload": f"synthetic 1-D series, N={n}, SE, fp64, sigma_n^2=1e-5 "
            "fixed, models.GPR + Scipy().minimize(maxiter=100) + predict_f(X_train), one GPR per call (the "
-           "reference's GPR/model_trainer.py:15-20 loop)", "seeds": list(seeds)}
-    prev = os.environ.get("GPX_BCR_MAX")
+           "reference's GPR/model_trainer.py:15-20 loop)", "seeds": list(seeds),
+           "note": "band16_sweeps = the default route (the headline's; a fit's bits equal its bits in any batch); "
+                   "bcr = gpx.set_default_band_route('bcr'), the latency route (DESIGN.md §3f)"}
+    prev = os.environ.pop("GPX_BCR_MAX", None)
+    prev_route = gpx.set_default_band_route("sweeps")
     try:
-        for mode, cap in (("bcr", prev), ("band16_sweeps", "0")):
-            if cap is None:
-                os.environ.pop("GPX_BCR_MAX", None)
-            else:
-                os.environ["GPX_BCR_MAX"] = cap
+        for mode, route in (("bcr", "bcr"), ("band16_sweeps", "sweeps")):
+            gpx.set_default_band_route(route)
             walls, nfevs, funs = [], [], []
             for s in seeds:
                 x, y = synthetic_series(n, s)
@@ -699,11 +706,8 @@ def secondary_solo(gpu, n=N_POINTS, seeds=(0, 1, 2), reps=3):
                 funs.append(fun)
             out[mode] = {"fit_ms_per_seed": [1e3 * v for v in walls], "fit_ms_median": 1e3 * sorted(walls)[len(walls) // 2],
                          "nfev": nfevs, "loss": funs}
-        if prev is None:
-            os.environ.pop("GPX_BCR_MAX", None)
-        else:
-            os.environ["GPX_BCR_MAX"] = prev
         # one evaluation's device chain on the reduction path (profiling on: HIP events around it)
+        gpx.set_default_band_route("bcr")
         x, y = synthetic_series(n, seeds[0])
         _, _, _, m = fit(x, y)
         ctx = N.Context.get(gpu)
@@ -718,9 +722,8 @@ def secondary_solo(gpu, n=N_POINTS, seeds=(0, 1, 2), reps=3):
         out["bcr_chain_ms_per_eval"] = t.bcr_ms_total / max(t.bcr_calls, 1.0)
         out["device_ms_per_eval"] = t.eval_ms_total / max(t.evals, 1.0)
     finally:
-        if prev is None:
-            os.environ.pop("GPX_BCR_MAX", None)
-        else:
+        gpx.set_default_band_route(prev_route)
+        if prev is not None:
             os.environ["GPX_BCR_MAX"] = prev
     out["speedup_vs_band16_sweeps"] = out["band16_sweeps"]["fit_ms_median"] / out["bcr"]["fit_ms_median"]
     return out
@@ -933,9 +936,13 @@ def main():
             "bound": "latency" if b16 else "mfma", "achieved": k["achieved"], "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": k["frac"], "traffic": k["traffic"], "traffic_source": k["traffic_source"],
             "trace_check": trace_check(kname),
-            "occupancy": (tm["band16_wave_ms"] / (WAVE_SLOTS * elapsed * 1e3)) if b16 else None,
-            "occupancy_note": (f"sum over band16 launches of problems x HIP-event launch ms, over {WAVE_SLOTS} wave "
-                               "slots (256 CUs x 4 SIMDs x 2 sweeps per SIMD) x the timed wall ms") if b16 else None,
+            # NOT an occupancy: launch spans include the time a problem's wave is queued behind other
+            # processes' work, so this can exceed 1. The measured residency is the wave trace's
+            # (GPX_WAVE_TRACE=1: wave_trace.occupancy_2048; 0.67 of 2048 slots in round 5)
+            "slot_demand": (tm["band16_wave_ms"] / (WAVE_SLOTS * elapsed * 1e3)) if b16 else None,
+            "slot_demand_note": (f"sum over band16 launches of problems x HIP-event launch ms (queued time "
+                                 f"included), over {WAVE_SLOTS} wave slots (256 CUs x 4 SIMDs x 2 sweeps per SIMD) "
+                                 "x the timed wall ms; not a residency (see wave_trace.occupancy_2048)") if b16 else None,
             "traffic_unit": "bytes/launch", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
             "alg_flops_per_launch": k["alg_flops_per_launch"], "mean_p_blocks": from_p,
             "band16_share_of_band_evals": e16 / max(tm["band_evals"], 1.0), "band16_mean_q": q_mean,
@@ -996,6 +1003,7 @@ def main():
                    "admission_places": args.admission, "wide_slots_per_process": args.wide_slots,
                    "deferred_above_q": args.defer_q,
                    "slot_storage": args.storage, "kernel": "SquaredExponential",
+                   "band_route": wk.engines[0].band_route,
                    "parallelism": f"independent fits, {world} rank(s) x 1 GPU x {P} host processes, "
                                   "RCCL all_gather of the per-fit results"},
         "nfev_mean": nfev_mean,

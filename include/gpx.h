@@ -219,6 +219,24 @@ int gpx_batch_band_class(gpx_batch* batch, int n_rows, const int32_t* rows, cons
  * call's other problems never wait for the slow classes, whose sweeps (one wavefront per SIMD,
  * or 73 KiB of LDS per workgroup) start late under a full band16 load. Same results, bit for
  * bit, as without deferral. q < 0 turns it off (the default). */
+/* Which banded route the batch's band16 problems take (GPX_BAND_ROUTE_*), a property of the batch,
+ * never of a call: a problem's arithmetic then depends on its own data, θ and this setting only —
+ * not on how many problems share its call — so a fit reproduces bit for bit whichever fits run
+ * beside it (the solo GPR of GPR/model_trainer.py:15-19 and the same series inside a batch of
+ * thousands give the same trajectory).
+ *   SWEEPS (0, the default): the one-wavefront band16 sweeps (throughput: thousands of problems
+ *     in flight fill the chip);
+ *   BCR (1): block cyclic reduction for the widths it covers (Q <= 5; log-depth latency for calls
+ *     of a few problems, ~4x the sweeps' work), wider problems on the 64-row sweeps;
+ *   AUTO (2): BCR for calls of at most GPX_BCR_MAX (default 32) band16 problems, else the sweeps —
+ *     the round-5 rule, whose results depend on the call's size (the two routes agree to ~1e-9
+ *     relative, not bit for bit).
+ * The environment variable GPX_BCR_MAX, when set, overrides the setting for every batch of the
+ * process (0: sweeps, a large value: BCR; the A/B knob of the tests and tools). */
+#define GPX_BAND_ROUTE_SWEEPS 0
+#define GPX_BAND_ROUTE_BCR 1
+#define GPX_BAND_ROUTE_AUTO 2
+int gpx_batch_set_band_route(gpx_batch* batch, int route);
 int gpx_batch_set_deferred(gpx_batch* batch, int q);
 int gpx_batch_deferred_wait(gpx_batch* batch, double* lml, double* grad, int32_t* info);
 /* rows with a deferred evaluation in flight: writes up to cap slot indices, returns the count */

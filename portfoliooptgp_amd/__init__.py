@@ -13,10 +13,11 @@ gfx950 in ``libgpx.so`` behind the C ABI of ``include/gpx.h``.
 """
 from . import _native, data, inducing_variables, kernels, likelihoods, models, optimizers, utilities
 from ._native import GPXError, InvalidParameterError, NotPositiveDefiniteError
+from .engine import set_default_band_route
 from .parameter import Parameter
 from .utilities import print_summary, set_trainable
 
 __all__ = ["inducing_variables", "kernels", "likelihoods", "models", "optimizers", "utilities", "Parameter",
            "set_trainable", "print_summary", "GPXError", "InvalidParameterError",
-           "NotPositiveDefiniteError"]
+           "NotPositiveDefiniteError", "set_default_band_route"]
 __version__ = "0.1.0"

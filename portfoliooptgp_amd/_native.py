@@ -19,6 +19,8 @@ GPX_MAX_DIM = 16
 (GPX_SE, GPX_MATERN12, GPX_MATERN32, GPX_MATERN52, GPX_EXPONENTIAL, GPX_RQ, GPX_PERIODIC_SE,
  GPX_LINEAR) = range(1, 9)
 GPX_SUM, GPX_PRODUCT = 0, 1
+# gpx_batch_set_band_route (include/gpx.h)
+BAND_ROUTES = {"sweeps": 0, "bcr": 1, "auto": 2}
 
 # GPX_LIB: an alternative build of the library (A/B experiments); default the in-tree one
 LIB_PATH = os.environ.get("GPX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgpx.so")
@@ -35,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "gpx_set_profiling", "gpx_batch_reset_timing", "gpx_batch_rebind",
     "gpx_batch_wave_trace", "gpx_batch_wave_trace_read", "gpx_batch_band_class",
     "gpx_batch_set_deferred", "gpx_batch_deferred_wait", "gpx_batch_deferred_rows",
+    "gpx_batch_set_band_route",
     "gpx_svgp_create", "gpx_svgp_destroy", "gpx_svgp_partials", "gpx_svgp_bind_partials",
     "gpx_svgp_eval_local", "gpx_svgp_eval_finish", "gpx_svgp_elbo_grad", "gpx_svgp_predict",
     "gpx_host_theta_rows", "gpx_host_loss_grad_u",
@@ -176,6 +179,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.gpx_batch_reset_timing.argtypes = [c_void_p]
         lib.gpx_batch_set_deferred.restype = c_int
         lib.gpx_batch_set_deferred.argtypes = [c_void_p, c_int]
+        lib.gpx_batch_set_band_route.restype = c_int
+        lib.gpx_batch_set_band_route.argtypes = [c_void_p, c_int]
         lib.gpx_batch_deferred_wait.restype = c_int
         lib.gpx_batch_deferred_wait.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p]
         lib.gpx_batch_deferred_rows.restype = c_int

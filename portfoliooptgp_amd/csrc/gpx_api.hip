@@ -632,10 +632,17 @@ bool se1_spec(const gpx_kernel_spec& sp) {
 }
 
 // the most band16 problems a call may hold for them to take the block-cyclic-reduction path
-// (gpx_bcr.hip) instead of the one-wavefront sweeps (GPX_BCR_MAX; 0 turns it off)
-static int bcr_max_problems() {
-  const char* e = getenv("GPX_BCR_MAX");  // (read per call: a process can compare the paths)
-  return e ? atoi(e) : 32;
+// (gpx_bcr.hip) instead of the one-wavefront sweeps: the batch's route (gpx_batch_set_band_route:
+// sweeps 0, BCR every call, AUTO GPX_BCR_MAX or 32), unless GPX_BCR_MAX is set, which overrides
+// it for the whole process (read per call: a process can compare the paths)
+static int bcr_max_problems(const gpx_batch* bt) {
+  const char* e = getenv("GPX_BCR_MAX");
+  if (e) return atoi(e);
+  switch (bt->band_route) {
+    case GPX_BAND_ROUTE_BCR: return 1 << 30;
+    case GPX_BAND_ROUTE_AUTO: return 32;
+    default: return 0;
+  }
 }
 
 // stream-order markers in the wave trace (diagnostic; no-op unless gpx_batch_wave_trace is on):
@@ -750,8 +757,10 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     hipStream_t ls = lane_stream(i);
     if (l.kind == 0) {
       // SE1 classes compute their K tiles inside the sweeps (band16 KIN): no build launch (a
-      // forward computing them while the backward reads the band writes the band itself)
-      if (!(se1 && (kin & 1))) {
+      // forward computing them while the backward reads the band writes the band itself). The
+      // Q > kBand16MaxQAny classes hold SE1 problems only and always compute K inline, whatever
+      // the rest of the call holds (se1 is the whole call's), so they never need the build.
+      if (!(se1 && (kin & 1)) && g16_q[l.g] <= kBand16MaxQAny) {
         BuildArgs bg = ba;
         bg.active = r.d_act + l.off;
         launch_band16_build(bg, g16_q[l.g], l.n, ls);
@@ -793,7 +802,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       ca.z = bt->z; ca.ldiag = bt->ldiag; ca.alpha = bt->alpha; ca.sVec = Np; ca.Np = Np;
       ca.Kd = bt->K; ca.sMat = st; ca.ld = mat_ld(bt);
       ca.partial = bt->partial; ca.sPartial = bt->partial_stride; ca.results = bt->results;
-      launch_bcr(ca, g16_q[l.g], max_terms, l.n, bt->Nmax, ls);
+      launch_bcr(ca, g16_q[l.g], max_terms, l.n, bt->Nmax, ls, &bt->bcr_graphs);
     } else if (l.kind == 1) {
       BuildArgs b1 = ba;
       b1.active = r.d_act + l.off;
@@ -1293,6 +1302,8 @@ int gpx_batch_destroy(gpx_batch* bt) {
     if (p) (void)hipFree(p);
   for (hipEvent_t e : bt->bcr_ev)
     if (e) (void)hipEventDestroy(e);
+  bcr_graph_cache_free(bt->bcr_graphs);  // (every stream of the batch has drained above)
+  bt->bcr_graphs = nullptr;
   if (bt->h_io) (void)hipHostFree(bt->h_io);
   if (bt->h_io_pred) (void)hipHostFree(bt->h_io_pred);
   if (bt->h_stage) (void)hipHostFree(bt->h_stage);
@@ -1877,7 +1888,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   // a call with few band16 problems takes them by block cyclic reduction (gpx_bcr.hip, Q <= 5):
   // there its p64 = 2 problems go back to the 64-row sweeps (a Q = 6..8 one-wave sweep is the
   // throughput choice, but its N/16-step chain is 2-3x the 64-row sweeps' latency)
-  const int bcr_max = bcr_max_problems();
+  const int bcr_max = bcr_max_problems(bt);
   if (rt.n16 > 0 && rt.n16 <= bcr_max && rt.n_g16 > 0 && rt.g16_q[rt.n_g16 - 1] > kBcrMaxQ)
     route_call(bt, n_active, active, theta, rt, kBcrMaxQ);
   std::vector<int32_t>& order = rt.order;
@@ -2394,11 +2405,15 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
   std::vector<int32_t> orow;
   if (rows) {
     if (!train || n_active <= 0 || n_active > bt->B || !active) return fail(ctx, GPX_BAD_ARG, "bad active set");
-    orow.assign(bt->B, 0);
+    orow.assign(bt->B, -1);
     for (int i = 0; i < n_active; ++i) {
       if (active[i] < 0 || active[i] >= bt->B) return fail(ctx, GPX_BAD_ARG, "active index out of range");
+      // a slot listed twice would leave an earlier output row unwritten (uninitialised memory
+      // returned as a prediction)
+      if (orow[active[i]] >= 0) return fail(ctx, GPX_BAD_ARG, "a slot appears twice in the active set");
       orow[active[i]] = i;
     }
+    for (int& o : orow) o = std::max(o, 0);  // (rows not in the call are never read)
   }
   auto out_row = [&](int b) -> size_t { return rows ? (size_t)orow[b] : (size_t)b; };
   if (bt->compact) {
@@ -2675,6 +2690,15 @@ int gpx_batch_set_deferred(gpx_batch* bt, int q) {
     return fail(bt->ctx, GPX_BAD_ARG, "deferred evaluations in flight (gpx_batch_deferred_wait first)");
   bt->defer_q = q < 0 ? -1 : q;
   if (bt->deferred.size() != (size_t)bt->B) bt->deferred.assign(bt->B, 0);
+  return GPX_OK;
+}
+
+int gpx_batch_set_band_route(gpx_batch* bt, int route) {
+  if (!bt) return GPX_BAD_ARG;
+  if (route != GPX_BAND_ROUTE_SWEEPS && route != GPX_BAND_ROUTE_BCR && route != GPX_BAND_ROUTE_AUTO)
+    return fail(bt->ctx, GPX_BAD_ARG, "unknown band route");
+  if (bt->pending_eval) return fail(bt->ctx, GPX_BAD_ARG, "an evaluation is submitted on this batch");
+  bt->band_route = route;
   return GPX_OK;
 }
 

@@ -919,9 +919,11 @@ static void launch_bcr_direct(const BcrArgs& a, int Q, int max_terms, int np, in
 // function of (Q, terms, problems, N_max) and the argument block (device pointers into the
 // batch's buffers, which stay put between calls), so it is captured once per distinct key and
 // replayed: the same kernels with the same arguments, one launch. GPX_BCR_GRAPH=0: direct launches.
+// The graphs belong to the batch whose buffers they point into (gpx_batch::bcr_graphs): created on
+// its first reduction call, destroyed with it (gpx_batch_destroy → bcr_graph_cache_free).
 namespace {
 struct BcrGraphKey {
-  int Q, max_terms, np, Nmax, D, Np, ld;
+  int device, Q, max_terms, np, Nmax, D, Np, ld;
   long long sX, sY, sWs, sVec, sMat, sPartial;
   const void* p[14];
   bool operator==(const BcrGraphKey& o) const { return std::memcmp(this, &o, sizeof(*this)) == 0; }
@@ -934,19 +936,33 @@ struct BcrGraphHash {
     return h;
   }
 };
-std::mutex g_bcr_graph_mu;
-std::unordered_map<BcrGraphKey, hipGraphExec_t, BcrGraphHash> g_bcr_graphs;
-constexpr size_t kBcrGraphCap = 1024;  // distinct chains kept (beyond: direct launches)
+struct BcrGraphCache {
+  std::mutex mu;
+  std::unordered_map<BcrGraphKey, hipGraphExec_t, BcrGraphHash> m;
+};
+// distinct chains kept per batch (keys shift with the call's width mix and the offset of each width
+// group in the call's active list; beyond the cap: direct launches)
+constexpr size_t kBcrGraphCap = 1024;
 }  // namespace
 
-void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStream_t s) {
+void bcr_graph_cache_free(void* cache) {
+  BcrGraphCache* c = static_cast<BcrGraphCache*>(cache);
+  if (!c) return;
+  for (auto& kv : c->m) (void)hipGraphExecDestroy(kv.second);
+  delete c;
+}
+
+void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStream_t s, void** cache) {
   static const bool graphs = [] {
     const char* e = getenv("GPX_BCR_GRAPH");
     return !(e && atoi(e) == 0);
   }();
-  if (!graphs) return launch_bcr_direct(a, Q, max_terms, np, Nmax, s);
+  if (!graphs || !cache) return launch_bcr_direct(a, Q, max_terms, np, Nmax, s);
+  if (!*cache) *cache = new BcrGraphCache();
+  BcrGraphCache& gc = *static_cast<BcrGraphCache*>(*cache);
   BcrGraphKey k;
   std::memset(&k, 0, sizeof(k));  // (padding included: the key is compared and hashed bytewise)
+  (void)hipGetDevice(&k.device);
   k.Q = Q; k.max_terms = max_terms; k.np = np; k.Nmax = Nmax; k.D = a.D; k.Np = a.Np; k.ld = a.ld;
   k.sX = a.sX; k.sY = a.sY; k.sWs = a.sWs; k.sVec = a.sVec; k.sMat = a.sMat; k.sPartial = a.sPartial;
   const void* ptrs[14] = {a.active, a.specs, a.theta, a.nvalid, a.X, a.Y, a.ws, a.info,
@@ -954,10 +970,10 @@ void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStr
   std::memcpy(k.p, ptrs, sizeof(ptrs));
   hipGraphExec_t exec = nullptr;
   {
-    std::lock_guard<std::mutex> lk(g_bcr_graph_mu);
-    auto it = g_bcr_graphs.find(k);
-    if (it != g_bcr_graphs.end()) exec = it->second;
-    else if (g_bcr_graphs.size() >= kBcrGraphCap) return launch_bcr_direct(a, Q, max_terms, np, Nmax, s);
+    std::lock_guard<std::mutex> lk(gc.mu);
+    auto it = gc.m.find(k);
+    if (it != gc.m.end()) exec = it->second;
+    else if (gc.m.size() >= kBcrGraphCap) return launch_bcr_direct(a, Q, max_terms, np, Nmax, s);
   }
   if (!exec) {
     hipGraph_t g = nullptr;
@@ -973,8 +989,8 @@ void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStr
       return launch_bcr_direct(a, Q, max_terms, np, Nmax, s);
     }
     (void)hipGraphDestroy(g);
-    std::lock_guard<std::mutex> lk(g_bcr_graph_mu);
-    g_bcr_graphs.emplace(k, exec);
+    std::lock_guard<std::mutex> lk(gc.mu);
+    gc.m.emplace(k, exec);
   }
   (void)hipGraphLaunch(exec, s);
 }

@@ -77,6 +77,7 @@ struct gpx_batch {
   // block-cyclic-reduction workspace (gpx_bcr.hip: calls with few band16 problems), grow-only
   double* bcr_ws = nullptr; size_t bcr_ws_cap = 0;
   hipEvent_t bcr_ev[2] = {};       // profiling: the last call's reduction chain, start / end
+  void* bcr_graphs = nullptr;      // the reduction chains captured as HIP graphs (gpx_bcr.hip), freed with the batch
   int force_dense = 0;         // re-evaluation of problems whose band check failed
   // pinned staging for gpx_batch_rebind_host, one region per slot ([Nmax*D] X, [Nmax] Y, n and
   // the spec): a slot's previous copies have completed before it is rebound (every evaluation
@@ -139,6 +140,7 @@ struct gpx_batch {
   // the call's active list / θ / widths (d_slow_*), and their results come back with a later
   // _complete (or gpx_batch_deferred_wait); the call itself completes with the rest
   int defer_q = -1;
+  int band_route = GPX_BAND_ROUTE_SWEEPS;  // gpx_batch_set_band_route
   hipStream_t slow_s = nullptr;
   hipEvent_t slow_in = nullptr;       // the latest slow part's copies are done (the next upload waits)
   hipEvent_t slow_up = nullptr;       // the call's upload (and rebind gather) are in: the slow part may start

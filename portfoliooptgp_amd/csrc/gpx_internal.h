@@ -234,7 +234,9 @@ struct BcrArgs {
 long long bcr_ws_doubles(int Q, int Nmax);
 // the whole evaluation of np problems of band width <= Q 16-blocks (Q <= 5): forward levels,
 // backward levels, contraction, per-problem finish; the reduce kernel follows (launch_reduce)
-void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStream_t s);
+// cache: the batch's captured chains (gpx_batch::bcr_graphs; created on first use), or nullptr
+void launch_bcr(const BcrArgs& a, int Q, int max_terms, int np, int Nmax, hipStream_t s, void** cache);
+void bcr_graph_cache_free(void* cache);
 
 void launch_band_solve(const BandSolveArgs& a, int n_active, hipStream_t s);
 void launch_band_transpose(const BandTransposeArgs& a, int q, int n_active, hipStream_t s);

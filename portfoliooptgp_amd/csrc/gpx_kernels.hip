@@ -728,9 +728,13 @@ void gemm_kernel(GemmArgs a) {
 }
 
 // 128x128 tiles for operands of at least 512x512, else 64x64 tiles (small recursion levels are
-// latency-bound on a single CU per tile otherwise). The choice depends on the shape only, not
-// on how many problems share the launch, so a problem's arithmetic — and therefore its fit —
-// is bit-identical whichever other problems are batched with it (same padded size Np).
+// latency-bound on a single CU per tile otherwise). For the contraction (its per-tile partials
+// depend on the tile) the choice depends on the shape only. For store GEMMs (small_tiles: the
+// recursion's panels, trailing updates and inverses, and the SVGP chain) it also depends on how
+// many problems share the launch — 128-tiles only when they still put a workgroup on every CU —
+// which leaves every stored entry's bits unchanged: an entry's sum runs over the same k in the
+// same 4-wide MFMA chunks either way (gemm() in gpx_api.hip), so a problem's arithmetic — and
+// therefore its fit — is bit-identical whichever other problems are batched with it.
 int gemm_tile(const GemmArgs& a, int n_active) {
   if (a.M % 128 != 0 || a.N % 128 != 0) return 64;
   if (a.small_tiles) {

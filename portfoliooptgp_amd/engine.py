@@ -111,13 +111,32 @@ def _immutable_entry(x: torch.Tensor):
     return ent
 
 
+# The banded route every new engine takes (include/gpx.h gpx_batch_set_band_route): "sweeps"
+# (default), "bcr" or "auto". A property of the engine, never of a call, so a fit's bits do not
+# depend on which other fits share its calls; GPX_BAND_ROUTE sets the process default.
+_DEFAULT_BAND_ROUTE = os.environ.get("GPX_BAND_ROUTE", "sweeps")
+
+
+def set_default_band_route(route: str) -> str:
+    """Set the banded route of engines created from now on ("sweeps": the one-wavefront band16
+    sweeps, throughput; "bcr": block cyclic reduction, latency for calls of a few problems;
+    "auto": BCR for calls of at most 32 band16 problems — call-size dependent bits). Returns the
+    previous default. Engines already created keep theirs (Engine.set_band_route)."""
+    global _DEFAULT_BAND_ROUTE
+    if route not in N.BAND_ROUTES:
+        raise ValueError(f"band route must be one of {sorted(N.BAND_ROUTES)}")
+    prev, _DEFAULT_BAND_ROUTE = _DEFAULT_BAND_ROUTE, route
+    return prev
+
+
 class Engine:
     def __init__(self, Xs: Sequence, Ys: Sequence, specs: Sequence[N.GpxKernelSpec],
-                 device: Optional[int] = None, band_storage: bool = False):
+                 device: Optional[int] = None, band_storage: bool = False, band_route: Optional[str] = None):
         """B problem slots (gpx_batch). ``band_storage``: the workspace keeps only the 64-block
         band of width 2 (gpx_batch_create_banded: 25 MiB per slot at N = 4096 instead of
         384 MiB), for many resident slots of banded fits; anything else runs on the batch's
-        dense fallback slots. Same results either way."""
+        dense fallback slots. Same results either way. ``band_route``: see
+        set_default_band_route (default: the process default, "sweeps")."""
         self.device = require_gpu(device)
         self.ctx = N.Context.get(self.device)
         self.lib = self.ctx.lib
@@ -155,6 +174,8 @@ class Engine:
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_create failed ({rc}): {self.ctx.last_error()}")
         self.handle = h
+        self.band_route = "sweeps"
+        self.set_band_route(_DEFAULT_BAND_ROUTE if band_route is None else band_route)
         self.n_params = np.asarray([s.n_params for s in specs], dtype=np.int64)
         self.eval_count = 0
         self._rebound = {}  # slot -> device tensors of its last rebind (kept alive for the gather)
@@ -281,6 +302,15 @@ class Engine:
         if rc != N.GPX_OK:
             raise N.GPXError(f"gpx_batch_band_width failed ({rc}): {self.ctx.last_error()}")
         return out
+
+    def set_band_route(self, route: str) -> None:
+        """This engine's banded route (include/gpx.h gpx_batch_set_band_route)."""
+        if route not in N.BAND_ROUTES:
+            raise ValueError(f"band route must be one of {sorted(N.BAND_ROUTES)}")
+        rc = self.lib.gpx_batch_set_band_route(self.handle, N.BAND_ROUTES[route])
+        if rc != N.GPX_OK:
+            raise N.GPXError(f"gpx_batch_set_band_route failed ({rc}): {self.ctx.last_error()}")
+        self.band_route = route
 
     deferral = -1
 
@@ -438,7 +468,9 @@ class Engine:
         c = self._rb_cache.get((id(X), id(Y)))
         if (c is not None and c[0]() is X and c[1]() is Y and X.data_ptr() == c[2] and Y.data_ptr() == c[3]
                 and _immutable_entry(X) is c[4]):
-            return self._rebind_dev(b, c[5], c[6], c[7], spec, c[4])
+            # (views made afresh: the cache holds no tensor, so it never keeps a dropped series'
+            # device storage alive)
+            return self._rebind_dev(b, X.detach(), Y.detach().reshape(-1), c[5], spec, c[4])
         ok_dev = (isinstance(X, torch.Tensor) and isinstance(Y, torch.Tensor) and X.is_cuda and Y.is_cuda
                   and X.device.index == self.device and Y.device.index == self.device
                   and X.dtype == torch.float64 and Y.dtype == torch.float64)
@@ -461,10 +493,13 @@ class Engine:
         if D != self.D or n > self.Nmax or ny != n:
             raise ValueError(f"problem does not fit slot shape (N <= {self.Nmax}, D = {self.D})")
         if ok_dev and ent is not None:
-            if len(self._rb_cache) > 65536:
-                self._rb_cache.clear()
-            self._rb_cache[(id(X), id(Y))] = (weakref.ref(X), weakref.ref(Y), X.data_ptr(), Y.data_ptr(), ent, x, y,
-                                              n)
+            # only contiguous pairs are cached (x, y are then views of X, Y, re-derived on a hit):
+            # the entry keeps weak references and scalars, never device storage, and a copy of a
+            # strided Y would miss later in-place writes to it
+            if X.is_contiguous() and Y.is_contiguous():
+                if len(self._rb_cache) >= max(4 * self.B, 1024):
+                    self._rb_cache.clear()
+                self._rb_cache[(id(X), id(Y))] = (weakref.ref(X), weakref.ref(Y), X.data_ptr(), Y.data_ptr(), ent, n)
             return self._rebind_dev(b, x, y, n, spec, ent)
         self.specs[b] = spec
         self.n_params[b] = spec.n_params
@@ -672,7 +707,7 @@ def solo_engine(model) -> Engine:
         _SOLO_POOL = OrderedDict()
     X, Y = model.data
     n, D = int(X.shape[0]), int(X.shape[1])
-    key = (int(model.device), (n + 63) // 64 * 64, D)
+    key = (int(model.device), (n + 63) // 64 * 64, D, _DEFAULT_BAND_ROUTE)  # (the route: set_default_band_route)
     eng = _SOLO_POOL.get(key)
     if eng is None:
         npad = key[1]

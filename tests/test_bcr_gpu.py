@@ -1,6 +1,6 @@
-"""GPU parity of the block-cyclic-reduction path (csrc/gpx_bcr.hip): calls with at most
-GPX_BCR_MAX band16 problems evaluate them by block cyclic reduction over the block-tridiagonal
-band (log-depth levels instead of the one-wavefront sweeps' N/16 steps).
+"""GPU parity of the block-cyclic-reduction path (csrc/gpx_bcr.hip): engines on the "bcr" route
+(gpx_batch_set_band_route) evaluate their band16 problems by block cyclic reduction over the
+block-tridiagonal band (log-depth levels instead of the one-wavefront sweeps' N/16 steps).
 
 Against the band16 sweeps of the same build (GPX_BCR_MAX=0), the dense path and the oracle.
 Both banded paths are exact restatements of the dense factorisation that differ
@@ -22,6 +22,16 @@ K = gpx.kernels
 
 def _sweeps():
     return _Env("GPX_BCR_MAX", "0")
+
+
+@pytest.fixture(autouse=True)
+def _bcr_route(monkeypatch):
+    """The engines of these tests take the BCR route (gpx_batch_set_band_route; the default is the
+    sweeps); _sweeps() switches a block to the sweeps by the process-wide override."""
+    monkeypatch.delenv("GPX_BCR_MAX", raising=False)
+    prev = gpx.set_default_band_route("bcr")
+    yield
+    gpx.set_default_band_route(prev)
 
 
 def _close(la, ga, lb, gb, P, what, rows=None):
