@@ -299,9 +299,27 @@ def parse_args(argv=None):
                          "dense N x N layout (384 MiB per slot)")
     ap.add_argument("--points", "--n", dest="n", type=int, default=N_POINTS,
                     help="points per series (use --points under torch.distributed.run, whose parser takes --n)")
+    # strong scaling: a FIXED batch of --total-fits fits per step over all
+    # ranks (the reference's per-asset loop is fixed-size: Multi-Input_GPR/main.py:535-552), split by
+    # distributed.shard_lpt; the timed region ends with the last rank's all_gather of the result
+    # table. The default stays weak scaling (--fits per GPU, the headline metric).
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=os.environ.get("GPX_BENCH_SCALING", "weak"))
+    ap.add_argument("--total-fits", type=int, default=int(os.environ.get("GPX_BENCH_TOTAL_FITS", 8 * 6144)),
+                    help="strong scaling: fits per step over all ranks")
+    ap.add_argument("--total-series", type=int, default=int(os.environ.get("GPX_BENCH_TOTAL_SERIES", 8 * 512)),
+                    help="strong scaling: distinct series of the batch (fit i fits series i mod this)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C4 / C5 secondary lines")
     return ap.parse_args(argv)
+
+
+def strong_fit_ids(args, world, procs):
+    """distributed.strong_plan of the fixed batch: plan[rank][proc] = global fit indices. Every
+    fit of the C2 batch has the same cost (the same N, the same day-offset inputs, GPflow's default
+    start), so LPT deals them out evenly."""
+    from portfoliooptgp_amd import distributed as D
+    cost = D.series_cost(np.arange(args.n, dtype=np.float64)[:, None])
+    return D.strong_plan([cost] * args.total_fits, world, procs)
 
 
 def share(total, parts, i):
@@ -345,16 +363,29 @@ class FitWorker:
         self.torch, self.gpx = torch, gpx
         self.args, self.w, self.gpu = args, w, gpu
         self.admission = admission
-        F = args.fits
-        self.F = share(F, P, w)
-        # distinct series of this process (fits cycle over them: fit f of a step is series
-        # f mod S_w), seeds rank·S + s0 + s
-        S = max(1, min(args.series, F))
-        self.S = share(S, P, w)
-        s0 = sum(share(S, P, i) for i in range(w))
         n = self.n = args.n
         dev = torch.device(f"cuda:{gpu}")
-        data = [synthetic_series(n, rank * S + s0 + s) for s in range(self.S)]
+        self.fit_ids = None
+        if args.scaling == "strong":
+            # this process's share of the fixed batch (strong_plan: the same plan on every process);
+            # global fit i fits series i mod total_series (seed = that series index)
+            world = int(os.environ.get("WORLD_SIZE", "1"))
+            self.fit_ids = strong_fit_ids(args, world, P)[rank][w]
+            seeds = sorted({i % args.total_series for i in self.fit_ids})
+            self.F, self.S = len(self.fit_ids), len(seeds)
+            pos = {sd: k for k, sd in enumerate(seeds)}
+            self.series_of = [pos[i % args.total_series] for i in self.fit_ids]
+            data = [synthetic_series(n, sd) for sd in seeds]
+        else:
+            F = args.fits
+            self.F = share(F, P, w)
+            # distinct series of this process (fits cycle over them: fit f of a step is series
+            # f mod S_w), seeds rank·S + s0 + s
+            S = max(1, min(args.series, F))
+            self.S = share(S, P, w)
+            s0 = sum(share(S, P, i) for i in range(w))
+            self.series_of = [f % self.S for f in range(self.F)]
+            data = [synthetic_series(n, rank * S + s0 + s) for s in range(self.S)]
         self.Xd = [torch.as_tensor(x, device=dev) for x, _ in data]  # resident in HBM before timing
         self.Yd = [torch.as_tensor(y, device=dev) for _, y in data]
         # read-only series: their band-table boxes are computed at the first rebind and reused
@@ -394,7 +425,8 @@ class FitWorker:
     def make_model(self, f):
         # GPflow defaults (σ²=1, ℓ=1), σn² = 1e-5 frozen — GPR/model_trainer.py:15-17
         gpx = self.gpx
-        m = gpx.models.GPR(data=(self.Xd[f % self.S], self.Yd[f % self.S]), kernel=gpx.kernels.SquaredExponential(),
+        sr = self.series_of[f]
+        m = gpx.models.GPR(data=(self.Xd[sr], self.Yd[sr]), kernel=gpx.kernels.SquaredExponential(),
                            device=self.gpu)
         m.likelihood.variance.assign(NOISE)
         gpx.set_trainable(m.likelihood.variance, False)
@@ -420,7 +452,12 @@ class FitWorker:
                          for m, r in zip(models, res)], dtype=np.float64)
         mu = last_points([p[0] for p in preds]).cpu().numpy()
         var = last_points([p[1] for p in preds]).cpu().numpy()
-        return [r.nfev for r in res], np.concatenate([host, mu[:, None], var[:, None]], axis=1)
+        table = np.concatenate([host, mu[:, None], var[:, None]], axis=1)
+        if self.fit_ids is not None:  # strong scaling: each row keyed by its global fit index
+            ids = np.asarray(self.fit_ids, dtype=np.float64)
+            gidx = np.concatenate([ids + st * self.args.total_fits for st in range(k)])
+            table = np.concatenate([gidx[:, None], table], axis=1)
+        return [r.nfev for r in res], table
 
     def reset_timing(self):
         for e in self.engines:
@@ -729,6 +766,141 @@ def secondary_solo(gpu, n=N_POINTS, seeds=(0, 1, 2), reps=3):
     return out
 
 
+def _c1_series():
+    """The reference's own C1 data (BASELINE configs[0]): AAPL daily / weekly / monthly returns as
+    GPR/data_handler.py:26-65 prepares them (N = 89 / 19 / 5, unnormalised day offsets), from the
+    committed fixture tests/golden/kernel_cases.npz (generated from the reference's CSVs by
+    tests/golden/make_golden.py)."""
+    d = np.load(os.path.join(REPO, "tests", "golden", "kernel_cases.npz"))
+    return [(tf, d[f"data|aapl_{tf}|x"], d[f"data|aapl_{tf}|y"]) for tf in ("d", "w", "m")]
+
+
+def c1_cpu_baseline(reps=5):
+    """The CPU leg of secondary_c1_solo (the oracle, never part of the GPU figures): the same
+    sweep with oracle/gp_oracle.py's restatement of GPflow (numpy/scipy, fp64, one host thread of
+    BLAS), and its per-evaluation time at each N."""
+    import threadpoolctl
+    from oracle import gp_oracle as O
+    out = {"kind": "port", "cores": 1, "eval_us": {}}
+    with threadpoolctl.threadpool_limits(limits=1, user_api="blas"):
+        for tf, x, y in _c1_series():
+            m = O.OGPR(x, y, O.OSquaredExponential(), noise_variance=1e-5)
+            m.noise.trainable = False
+            m.loss_and_grad_u()
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                for _ in range(50):
+                    m.loss_and_grad_u()
+                ts.append((time.perf_counter() - t0) / 50)
+            out["eval_us"][str(len(x))] = sorted(ts)[reps // 2] * 1e6
+        walls, nfev = [], 0
+        for _ in range(3):
+            ks = O.reference_kernel_list()  # (shared across d -> w -> m, as GPR/main.py:105-114)
+            t0 = time.perf_counter()
+            nfev = 0
+            for tf, x, y in _c1_series():
+                for k in ks:
+                    m = O.OGPR(x, y, k, noise_variance=1e-5)
+                    m.noise.trainable = False
+                    try:
+                        r = O.scipy_minimize(m, 100)
+                        nfev += r.nfev
+                        m.predict_f(x)
+                    except np.linalg.LinAlgError:
+                        pass
+            walls.append(time.perf_counter() - t0)
+        out["sweep_ms"] = 1e3 * sorted(walls)[1]
+        out["sweep_nfev"] = nfev
+    out["sample"] = ("oracle/gp_oracle.py on one host thread: the AAPL d/w/m 8-kernel sweep (median of 3) and 50 "
+                     "SE evaluations per N (median of 5 x 50)")
+    return out
+
+
+def secondary_c1_solo(gpu, reps=5):
+    """The drop-in pattern at the reference's real sizes: GPR/main.py's AAPL
+    d -> w -> m sweep with the 8 shared kernel objects of GPR/main.py:105-114, each fit exactly as
+    GPR/model_trainer.py:14-20 runs it — ONE GPR at a time (models.GPR, noise 1e-5 frozen,
+    Scipy().minimize(maxiter=100), predict_f at the training inputs, the training MSE) — through the
+    INTEGRATION.md §1 import swap. Reports the sweep's wall time, ms per evaluation inside the fits
+    (scipy's own loop included), and µs per bare loss+gradient evaluation at N = 89 / 19 / 5, next
+    to the CPU oracle's (c1_cpu_baseline)."""
+    import torch
+    import portfoliooptgp_amd as gpx
+    K = gpx.kernels
+    series = _c1_series()
+
+    def kernels():
+        return [K.SquaredExponential(), K.Matern12(), K.RationalQuadratic(), K.Exponential(),
+                K.SquaredExponential() + K.Matern12(),
+                K.Exponential() + K.Periodic(K.SquaredExponential()) + K.Linear(),
+                K.Exponential() + K.Periodic(K.SquaredExponential()),
+                K.SquaredExponential() * K.Matern12()]
+
+    def sweep():
+        ks = kernels()
+        nfev, raised, best = 0, 0, {}
+        for tf, x, y in series:
+            best_mse = None
+            for k in ks:
+                m = gpx.models.GPR(data=(x, y), kernel=k, device=gpu)
+                m.likelihood.variance.assign(1e-5)
+                gpx.set_trainable(m.likelihood.variance, False)
+                try:
+                    r = gpx.optimizers.Scipy().minimize(m.training_loss, m.trainable_variables,
+                                                        options=dict(maxiter=MAXITER))
+                except (gpx.NotPositiveDefiniteError, gpx.InvalidParameterError):
+                    raised += 1
+                    continue
+                nfev += int(r.nfev)
+                mean, _ = m.predict_f(x)
+                mse = float(np.mean((y.reshape(-1) - mean.numpy().reshape(-1)) ** 2))
+                best_mse = mse if best_mse is None else min(best_mse, mse)
+            best[tf] = best_mse
+        return nfev, raised, best
+
+    sweep()  # warm-up (engines for the three padded sizes, code objects)
+    walls = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        nfev, raised, best = sweep()
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+    wall = sorted(walls)[reps // 2]
+    ev = {}
+    for tf, x, y in series:
+        m = gpx.models.GPR(data=(x, y), kernel=K.SquaredExponential(), device=gpu)
+        m.likelihood.variance.assign(1e-5)
+        gpx.set_trainable(m.likelihood.variance, False)
+        m.loss_and_grad_unconstrained()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            for _ in range(200):
+                m.loss_and_grad_unconstrained()
+            ts.append((time.perf_counter() - t0) / 200)
+        ev[str(len(x))] = sorted(ts)[reps // 2] * 1e6
+    out = {"config": "C1 (BASELINE configs[0]): the reference's plumbing at its real sizes",
+           "workload": "AAPL d/w/m (N = 89 / 19 / 5), the 8 kernels of GPR/main.py:105-114 shared across timeframes, "
+                       "one GPR at a time as GPR/model_trainer.py:14-20 (Scipy maxiter 100 + predict_f + MSE)",
+           "sweep_ms": wall * 1e3, "sweep_fits": 24 - raised, "sweep_raised": raised, "sweep_nfev": nfev,
+           "ms_per_fit_evaluation": wall * 1e3 / max(nfev, 1),
+           "eval_us_gpu": ev, "best_train_mse": best,
+           "note": "eval_us_gpu: one bare loss+gradient (m.loss_and_grad_unconstrained, SE) per call, median of "
+                   f"{reps} x 200; ms_per_fit_evaluation: the sweep's wall / its evaluations (scipy's loop, "
+                   "model construction and predict_f included). N <= 64 takes the one-launch small-problem "
+                   "kernel (DESIGN.md §3h)"}
+    try:
+        out["cpu_baseline"] = c1_cpu_baseline()
+        cb = out["cpu_baseline"]
+        out["gpu_over_cpu_eval_time"] = {n: ev[n] / cb["eval_us"][n] for n in ev if n in cb["eval_us"]}
+        out["sweep_speedup_vs_cpu"] = cb["sweep_ms"] / out["sweep_ms"]
+    except Exception as e:  # reported, never fatal
+        out["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
+    return out
+
+
 def secondary_c5(gpu, reps=20):
     """Config C5 (BASELINE.json configs[4]): SVGP ELBO + gradients at N = 65536, M = 1024, D = 1,
     SE, whitened full q_sqrt, fp64; ms per evaluation (one GPU)."""
@@ -832,7 +1004,12 @@ def main():
     parts += collect(q, helpers, "done", 1800)  # each sent after synchronising its device work
     parts.sort(key=lambda p: p[0])
     table = np.concatenate([p[2] for p in parts])
-    if world > 1:  # the per-asset hand-off: one all_gather of every fit's summary row
+    if args.scaling == "strong":
+        # the fixed batch's hand-off: one all_gather of every rank's rows (device tensors over
+        # RCCL, distributed.all_gather_results), the table sorted by global fit index
+        from portfoliooptgp_amd import distributed as D
+        table = D.gather_table(table)
+    elif world > 1:  # the per-asset hand-off: one all_gather of every fit's summary row
         t = torch.as_tensor(table, device=cdev)
         gathered = [torch.empty_like(t) for _ in range(world)]
         dist.all_gather(gathered, t)
@@ -860,7 +1037,11 @@ def main():
     else:
         nfev_mean = float(np.mean(nfev_all))
         evals_all = tm["evals"]
-    total_fits = args.fits * args.steps * world
+    if args.scaling == "strong":
+        total_fits = args.total_fits * args.steps
+        assert table.shape[0] == total_fits and np.array_equal(table[:, 0], np.arange(total_fits)), table.shape
+    else:
+        total_fits = args.fits * args.steps * world
     assert table.shape[0] == total_fits, (table.shape, total_fits)
     value = total_fits / elapsed
     n = args.n
@@ -992,7 +1173,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (C2 generator, seeded per rank/series)",
@@ -1021,6 +1202,26 @@ def main():
                               "profiles/r05_ab.md)", "fresh_series_fits_per_s_same_box": 13431.2,
                       "cached_fits_per_s_same_box": 14191.8},
     }
+    if args.scaling == "strong":
+        out["config"]["fits_per_gpu_per_step"] = None
+        out["config"]["total_fits_per_step"] = args.total_fits
+        out["config"]["total_series"] = args.total_series
+        out["data"] = "synthetic (C2 generator; one fixed batch of series split over the ranks)"
+        hosts = [host]
+        if world > 1:
+            hosts = [None] * world
+            dist.all_gather_object(hosts, host)
+        plan = strong_fit_ids(args, world, P)
+        out["strong"] = {
+            "fits_per_rank_per_step": [sum(len(p) for p in pr) for pr in plan],
+            "rank_host_share": [[h.get("host_share") for h in hr] for hr in hosts],
+            "rank_busy_s_max": [max(h.get("busy_s") or 0.0 for h in hr) for hr in hosts],
+            "note": ("a fixed batch of total_fits_per_step fits per step (the reference's per-asset loop is "
+                     "fixed-size, Multi-Input_GPR/main.py:535-552) split by distributed.shard_lpt; the timed "
+                     "region ends after the all_gather of the result table on every rank (max over ranks). "
+                     "C3's own 20-series batch is bounded by secondary_c3_batch.ratio_wall_all_over_share: each "
+                     "fit is a chain of ~20 dependent evaluations, so a batch of few fits cannot speed up past "
+                     "that ratio; this batch holds thousands of fits per rank")}
     if parts[0][6] is not None:
         out["wave_trace"] = wave_trace_summary([p[6] for p in parts], elapsed)
         if os.environ.get("GPX_WAVE_TRACE_OUT"):  # raw records per host process (tools/wave_overlap.py)
@@ -1028,7 +1229,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, nfev_mean)
     if rank == 0 and world == 1 and not args.no_secondary:
-        for name, fn in (("secondary_solo", lambda: secondary_solo(gpu)),
+        for name, fn in (("secondary_c1_solo", lambda: secondary_c1_solo(gpu)),
+                         ("secondary_solo", lambda: secondary_solo(gpu)),
                          ("secondary_c3_batch", lambda: secondary_c3(gpu)),
                          ("secondary_c4_dense", lambda: secondary_c4(gpu)),
                          ("secondary_c4_expxexp", lambda: secondary_c4(gpu, kind="expxexp")),

@@ -340,6 +340,9 @@ typedef struct {
   /* of band_fused_launches: the timed 64-row launch pairs that were the p = 2 class's
    * (band_fwd_kernel / band_bwd_kernel) rather than the p <= 1 class's (band_fwd1_kernel / band_bwd1_kernel) */
   double band_fused_p2_launches;
+  /* band16 problem-evaluations of widths Q = 6..8 taken by the block-cyclic-reduction chain of block
+   * size 128 (whatever the batch's route; they no longer run as one-wavefront sweeps) */
+  double bcr_wide_evals;
 } gpx_timing;
 int gpx_batch_last_timing(const gpx_batch* batch, gpx_timing* out);
 int gpx_batch_reset_timing(gpx_batch* batch);

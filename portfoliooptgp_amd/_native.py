@@ -75,7 +75,7 @@ class GpxTiming(ctypes.Structure):
                 ("band16_wide_launches", ctypes.c_double), ("band16_wide_flops", ctypes.c_double),
                 ("band16_wide_evals", ctypes.c_double), ("bcr_ms_total", ctypes.c_double),
                 ("bcr_calls", ctypes.c_double), ("bcr_evals", ctypes.c_double),
-                ("band_fused_p2_launches", ctypes.c_double)]
+                ("band_fused_p2_launches", ctypes.c_double), ("bcr_wide_evals", ctypes.c_double)]
 
 
 class GPXError(RuntimeError):

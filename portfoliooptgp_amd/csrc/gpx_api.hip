@@ -193,6 +193,30 @@ void reduce(const Run& r) {
 }
 
 
+// Np = 64 batches: every dense evaluation is one fused launch (small64_kernel; GPX_SMALL64=0:
+// the six-launch chain, for A/B). Which path runs depends on Np only, never on the call.
+bool small64_on(const gpx_batch* bt) {
+  static const bool on = [] {
+    const char* e = getenv("GPX_SMALL64");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && bt->Np == kLeaf;
+}
+
+// the fused small-problem evaluation (grad: the gradient and logML too) for the problems of r
+void small64_eval(const Run& r, bool grad) {
+  gpx_batch* bt = r.bt;
+  Small64Args a{};
+  a.active = r.d_act; a.specs = bt->d_specs; a.theta = bt->d_theta; a.nvalid = bt->d_n;
+  a.X = bt->X; a.sX = (long long)bt->Nmax * bt->D; a.D = bt->D; a.Y = bt->Y; a.sY = bt->Nmax;
+  a.W = bt->W; a.sMat = mat_stride(bt); a.ld = bt->Np;
+  a.z = bt->z; a.alpha = bt->alpha; a.ldiag = bt->ldiag; a.sVec = bt->Np;
+  a.info = bt->d_info; a.results = bt->results; a.grad = grad ? 1 : 0;
+  int max_terms = 1;
+  for (int b = 0; b < bt->B; ++b) max_terms = std::max(max_terms, (int)bt->specs[b].n_terms);
+  launch_small64(a, max_terms, r.na, r.s);
+}
+
 // ---------------------------------------------------------------------------------------
 // Block-banded path (kernels in gpx_band.hip)
 // ---------------------------------------------------------------------------------------
@@ -617,6 +641,27 @@ int wide_qmax(bool se1) {
   return (se1 && b16_inline_k_wide() == 3) ? wq : 5;
 }
 
+// band16 widths Q > kBcrMaxQ (6..8) by the block-cyclic-reduction chain of block size 128
+// (gpx_bcr.hip bcrw_*) instead of one-wavefront sweeps (GPX_WIDE_BCR=0: the sweeps, round 5):
+// a problem's path still depends on its own width only, whatever the batch's route or call
+bool wide_bcr_on() {
+  static const bool on = [] {
+    const char* e = getenv("GPX_WIDE_BCR");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// the widest class a deferred part's wide launch (band16_wide_kernel) takes
+static int wide_launch_qmax(bool se1) { return wide_bcr_on() ? std::min(wide_qmax(se1), kBcrMaxQ) : wide_qmax(se1); }
+
+// reduction workspace of band16 groups g0 .. g1-1 (each problem in slots of its group's layout)
+long long bcr_ws_need(const int* q, const int* cnt, int g0, int g1, int Nmax) {
+  long long t = 0;
+  for (int g = g0; g < g1; ++g) t += (long long)cnt[g] * bcr_ws_doubles(q[g], Nmax);
+  return t;
+}
+
 int b16_inline_k() {
   static const int kin = [] {
     const char* e = getenv("GPX_B16_INLINE_K");
@@ -686,33 +731,45 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   // entries are exact zeros by the 64-row bound), the 64-row p <= 1 class (two 64-block
   // diagonals), the 64-row p = 2 class (three).
   const int wq = wide_qmax(se1);  // the widest class a deferred part's wide launch takes
-  struct Lane { int kind, g, n, off, g_end; };
+  struct Lane { int kind, g, n, off, g_end; long long wso; };
   Lane lanes[kBand16MaxQ + 2];
   int nl = 0;
   {
     int off = 0;
+    long long wso = 0;  // (the reduction lanes' workspace offsets, in group order)
     // (r.bcr_q: each band16 width group as a block-cyclic-reduction chain of its own width,
     // gpx_bcr.hip: a problem's arithmetic depends on its own width only, not on the call's mix)
     int g = 0;
     for (; g < n_g16 && r.bcr_q > 0 && g16_q[g] <= kBcrMaxQ; ++g) {
-      lanes[nl++] = Lane{4, g, g16_n[g], off, g + 1};
+      lanes[nl++] = Lane{4, g, g16_n[g], off, g + 1, wso};
       off += g16_n[g];
+      wso += (long long)g16_n[g] * bcr_ws_doubles(g16_q[g], bt->Nmax);
     }
     for (; g < n_g16; ++g) {
-      // (r.wide_from: the SE1 groups of width 4 and 5 as one lane, one band16_wide_kernel launch)
-      if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= wq && nl > 0 &&
+      if (wide_bcr_on() && g16_q[g] > kBcrMaxQ) {
+        // the widths 6..8 (always the tail of the groups) as ONE reduction chain of block size 128
+        if (nl > 0 && lanes[nl - 1].kind == 5) {
+          lanes[nl - 1].n += g16_n[g];
+          lanes[nl - 1].g_end = g + 1;
+        } else {
+          lanes[nl++] = Lane{5, g, g16_n[g], off, g + 1, wso};
+        }
+        wso += (long long)g16_n[g] * bcr_ws_doubles(g16_q[g], bt->Nmax);
+        if (bt->ctx->profiling) bt->timing.bcr_wide_evals += g16_n[g];
+      } else if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= wq && nl > 0 &&
           lanes[nl - 1].kind == 3) {
+        // (r.wide_from: the SE1 groups of width 4 and 5 as one lane, one band16_wide_kernel launch)
         lanes[nl - 1].n += g16_n[g];
         lanes[nl - 1].g_end = g + 1;
       } else if (r.wide_from > 0 && se1 && g16_q[g] >= std::max(r.wide_from, 4) && g16_q[g] <= wq) {
-        lanes[nl++] = Lane{3, g, g16_n[g], off, g + 1};
+        lanes[nl++] = Lane{3, g, g16_n[g], off, g + 1, 0};
       } else {
-        lanes[nl++] = Lane{0, g, g16_n[g], off, g + 1};
+        lanes[nl++] = Lane{0, g, g16_n[g], off, g + 1, 0};
       }
       off += g16_n[g];
     }
-    if (n1 > 0) lanes[nl++] = Lane{1, 0, n1, n16, 0};
-    if (nlo < r.na) lanes[nl++] = Lane{2, 0, r.na - nlo, nlo, 0};
+    if (n1 > 0) lanes[nl++] = Lane{1, 0, n1, n16, 0, 0};
+    if (nlo < r.na) lanes[nl++] = Lane{2, 0, r.na - nlo, nlo, 0, 0};
   }
   // GPX_LANE_ORDER=1: the small (slow-class) lanes are enqueued first, ahead of the bulk lane,
   // so their wavefronts reach the dispatcher before the bulk lane's fill the chip
@@ -792,17 +849,19 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       if (ev16)
         for (int g = l.g + 1; g < l.g_end; ++g)
           for (int e = 1; e < 4; ++e) (void)hipEventRecord(ev16[g - r.ev16_g0][e], ls);
-    } else if (l.kind == 4) {
+    } else if (l.kind == 4 || l.kind == 5) {
+      // a reduction chain: the group's width (kind 4), or the widths 6..8 at block size 128 (kind 5)
+      const int qc = l.kind == 5 ? kBcrWideQ : g16_q[l.g];
       BcrArgs ca{};
       ca.active = r.d_act + l.off; ca.specs = bt->d_specs; ca.theta = fa.theta; ca.nvalid = bt->d_n;
       ca.X = bt->X; ca.sX = (long long)bt->Nmax * bt->D; ca.D = bt->D; ca.Y = bt->Y; ca.sY = bt->Nmax;
-      // (workspace: every problem of the call at its position, in slots of the widest layout)
-      ca.sWs = bcr_ws_doubles(kBcrMaxQ, bt->Nmax);
-      ca.ws = bt->bcr_ws + (size_t)l.off * (size_t)ca.sWs; ca.info = fa.info;
+      // (workspace: the lane's problems in slots of its layout, at the lane's offset)
+      ca.sWs = bcr_ws_doubles(qc, bt->Nmax);
+      ca.ws = r.bcr_ws + l.wso; ca.info = fa.info;
       ca.z = bt->z; ca.ldiag = bt->ldiag; ca.alpha = bt->alpha; ca.sVec = Np; ca.Np = Np;
       ca.Kd = bt->K; ca.sMat = st; ca.ld = mat_ld(bt);
       ca.partial = bt->partial; ca.sPartial = bt->partial_stride; ca.results = bt->results;
-      launch_bcr(ca, g16_q[l.g], max_terms, l.n, bt->Nmax, ls, &bt->bcr_graphs);
+      launch_bcr(ca, qc, max_terms, l.n, bt->Nmax, ls, &bt->bcr_graphs);
     } else if (l.kind == 1) {
       BuildArgs b1 = ba;
       b1.active = r.d_act + l.off;
@@ -1298,7 +1357,7 @@ int gpx_batch_destroy(gpx_batch* bt) {
   for (void* p : {(void*)bt->K, (void*)bt->L, (void*)bt->W, (void*)bt->z, (void*)bt->alpha,
                   (void*)bt->ldiag, (void*)bt->partial, (void*)bt->d_io, (void*)bt->d_n, (void*)bt->d_orow,
                   (void*)bt->d_specs, (void*)bt->kxs, (void*)bt->pvp, (void*)bt->abuf, (void*)bt->covw,
-                  (void*)bt->bres, (void*)bt->bcr_ws})
+                  (void*)bt->bres, (void*)bt->bcr_ws, (void*)bt->bcr_ws_slow})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : bt->bcr_ev)
     if (e) (void)hipEventDestroy(e);
@@ -1650,9 +1709,42 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
     HIPX(ctx, hipHostMalloc(&rec->h_info, sizeof(int) * bt->B));
   }
   rec->ids.assign(ids, ids + n);
+  // The wide launch's waves in reverse order, widest first (GPX_WIDE_REVERSE=0: ascending): its
+  // workgroups are dispatched in index order as wave slots free up under the other processes'
+  // sweeps, and a Q = 6..8 wave — 2-3x a Q = 4 / 5 wave's time — dispatched last used to end the
+  // launch alone. Each wave's arithmetic is its own problem's, so the bits are unchanged; the
+  // part's active copy and its result gather (rec->ids) take the same order.
+  static const bool wide_rev = [] {
+    const char* e = getenv("GPX_WIDE_REVERSE");
+    return !(e && atoi(e) == 0);
+  }();
+  int r0 = 0, r1 = 0;
+  {
+    static const bool wide_on = [] {
+      const char* e = getenv("GPX_DEFER_WIDE");
+      return !(e && atoi(e) == 0);
+    }();
+    const int wq = wide_launch_qmax(se1);
+    if (wide_rev && wide_on && se1 && defer_own_stream()) {
+      int o = 0;
+      r0 = r1 = -1;
+      for (int g = 0; g < n_g16; ++g) {
+        if (q[g] >= 4 && q[g] <= wq) {
+          if (r0 < 0) r0 = o;
+          r1 = o + cnt[g];
+        }
+        o += cnt[g];
+      }
+      if (r0 < 0) r0 = r1 = 0;
+      std::reverse(rec->ids.begin() + r0, rec->ids.begin() + r1);
+    }
+  }
   rec->theta.assign(theta, theta + (size_t)bt->B * GPX_THETA_STRIDE);
   rec->clear_events();
-  rec->n_g16 = n_g16;
+  // (the swept groups: the wide ones, Q > kBcrMaxQ, run as a reduction chain without band16 events)
+  int g_sw = n_g16;
+  while (wide_bcr_on() && g_sw > 0 && q[g_sw - 1] > kBcrMaxQ) --g_sw;
+  rec->n_g16 = g_sw;
   rec->se1 = se1;
   for (int g = 0; g < n_g16; ++g) {
     rec->g16_q[g] = q[g];
@@ -1668,14 +1760,18 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
     // kernels' multi-wave workgroups wait for free CU space behind the other processes' sweeps
     // (+2.8 % on the bench, profiles/r05_ab.md)
     launch_slow_inputs(bt->d_active + off, n, bt->d_slow_act, bt->d_theta, bt->d_slow_theta, bt->d_bandp,
-                       bt->d_slow_bandp, bt->d_slow_info, bt->B, ss);
+                       bt->d_slow_bandp, bt->d_slow_info, bt->B, ss, r0, r1);
     HIPX(ctx, hipGetLastError());
     HIPX(ctx, hipEventRecord(bt->slow_in, ss));
     bt->slow_in_armed = true;
   }
   const bool fused64 = n > n16;
+  if (g_sw < n_g16) {
+    const int e = ensure(ctx, bt->bcr_ws_slow, bt->bcr_ws_slow_cap, (size_t)bcr_ws_need(q, cnt, g_sw, n_g16, bt->Nmax));
+    if (e != GPX_OK) return e;
+  }
   if (ctx->profiling) {
-    for (int g = 0; g < n_g16; ++g)
+    for (int g = 0; g < g_sw; ++g)
       for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&rec->fq16[g][e]));
     if (fused64) {
       for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&rec->fq[e]));
@@ -1687,6 +1783,7 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
   // (on the call's stream, after its download: the next call's upload follows this part in the
   // stream's order, so the part reads the call's own active list, θ and widths in place)
   Run r{bt, own ? bt->d_slow_act : bt->d_active + off, n, ss};
+  r.bcr_ws = bt->bcr_ws_slow;
   if (own) {
     r.theta = bt->d_slow_theta;
     r.bandp = bt->d_slow_bandp;
@@ -1889,7 +1986,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   // there its p64 = 2 problems go back to the 64-row sweeps (a Q = 6..8 one-wave sweep is the
   // throughput choice, but its N/16-step chain is 2-3x the 64-row sweeps' latency)
   const int bcr_max = bcr_max_problems(bt);
-  if (rt.n16 > 0 && rt.n16 <= bcr_max && rt.n_g16 > 0 && rt.g16_q[rt.n_g16 - 1] > kBcrMaxQ)
+  if (!wide_bcr_on() && rt.n16 > 0 && rt.n16 <= bcr_max && rt.n_g16 > 0 && rt.g16_q[rt.n_g16 - 1] > kBcrMaxQ)
     route_call(bt, n_active, active, theta, rt, kBcrMaxQ);
   std::vector<int32_t>& order = rt.order;
   std::vector<int32_t>& shadow_ids = rt.shadow_ids;
@@ -1939,8 +2036,12 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     const int e = ensure(ctx, bt->bres, bt->bres_cap, (size_t)bt->B * bt->Np);
     if (e != GPX_OK) return drop_shadow(e);
   }
-  if (n16_bcr > 0) {
-    const int e = ensure(ctx, bt->bcr_ws, bt->bcr_ws_cap, (size_t)n16_bcr * (size_t)bcr_ws_doubles(kBcrMaxQ, bt->Nmax));
+  // the wide groups (Q > kBcrMaxQ, a suffix of the groups) on the bs = 128 reduction
+  int g_wide = n_g16;
+  while (wide_bcr_on() && g_wide > 0 && g16_q[g_wide - 1] > kBcrMaxQ) --g_wide;
+  if (n16_bcr > 0 || g_wide < n_g16) {
+    const long long need = bcr_ws_need(g16_q, g16_n, 0, g_bcr, bt->Nmax) + bcr_ws_need(g16_q, g16_n, g_wide, n_g16, bt->Nmax);
+    const int e = ensure(ctx, bt->bcr_ws, bt->bcr_ws_cap, (size_t)need);
     if (e != GPX_OK) return drop_shadow(e);
     if (ctx->profiling && !bt->bcr_ev[0])
       for (auto& e2 : bt->bcr_ev) HIPX(ctx, hipEventCreate(&e2));
@@ -1964,7 +2065,10 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   std::vector<PhaseTimer>& pts = pe->pts;
   pe->ct.reset(new PhaseTimer(ctx->profiling != 0 && n_dense > 0, s));
   PhaseTimer& ct = *pe->ct;
-  if (n_dense > 0) {
+  if (n_dense > 0 && small64_on(bt)) {
+    // Np = 64: the whole evaluation of every dense problem in one launch
+    small64_eval(Run{bt, bt->d_active, n_dense, s}, true);
+  } else if (n_dense > 0) {
     // Split the dense problems into up to kGroups ranges, each running the whole pipeline on
     // its own stream: one group's latency-bound phases (64x64 leaves, small recursion levels)
     // overlap another group's large MFMA GEMMs.
@@ -2097,8 +2201,8 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     if (ctx->profiling && old_fused)
       for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&fqe[e]));
     pe->n_band16 = n16;
-    // (timing: the swept groups g_bcr.. only; the reduction's chain has its own events)
-    pe->n_g16 = n_g16 - g_bcr;
+    // (timing: the swept groups g_bcr .. g_wide only; the reductions' chains have their own events)
+    pe->n_g16 = std::min(n_g16, g_wide) - g_bcr;
     pe->n_bcr = n16_bcr;
     for (int g = 0; g < pe->n_g16; ++g) {
       pe->g16_q[g] = g16_q[g_bcr + g];
@@ -2115,6 +2219,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     }
     Run rf{bt, bt->d_active + n_dense + n_band, n_fused, s};
     rf.bcr_q = bcr_q;
+    rf.bcr_ws = bt->bcr_ws;
     rf.ev16_g0 = g_bcr;
     band_fused_eval(rf, n16, n_g16, g16_q, g16_n, se1,
                     b16_p2 ? 3 : 2, n_fused1,
@@ -2494,8 +2599,12 @@ static int predict_impl(gpx_batch* bt, int n_active, const int32_t* active, cons
     HIPX(ctx, hipMemcpyAsync(bt->d_active, refac.data(), sizeof(int) * refac.size(),
                              hipMemcpyHostToDevice, s));
     const Run rr{bt, bt->d_active, (int)refac.size(), s};
-    factor(rr);
-    alpha_solve(rr);
+    if (small64_on(bt)) {
+      small64_eval(rr, false);
+    } else {
+      factor(rr);
+      alpha_solve(rr);
+    }
   }
   if (!refac.empty() || n_dense < n_active)
     HIPX(ctx, hipMemcpyAsync(bt->d_active, order.data(), sizeof(int) * n_active, hipMemcpyHostToDevice, s));

@@ -1017,10 +1017,10 @@ __global__ __launch_bounds__(64) void slow_gather_kernel(const int* __restrict__
 __global__ __launch_bounds__(64) void slow_inputs_kernel(const int* __restrict__ act, int n, int* __restrict__ act_out,
                                                          const double* __restrict__ theta, double* __restrict__ theta_out,
                                                          const int* __restrict__ bandp, int* __restrict__ bandp_out,
-                                                         int* __restrict__ info_out, int B) {
+                                                         int* __restrict__ info_out, int B, int r0, int r1) {
   const int t = blockIdx.x * 64 + threadIdx.x;
   if (t < B * GPX_THETA_STRIDE) theta_out[t] = theta[t];
-  if (t < n) act_out[t] = act[t];
+  if (t < n) act_out[t] = (t >= r0 && t < r1) ? act[r0 + r1 - 1 - t] : act[t];
   if (t < B) {
     bandp_out[t] = bandp[t];
     info_out[t] = 0;
@@ -1028,10 +1028,10 @@ __global__ __launch_bounds__(64) void slow_inputs_kernel(const int* __restrict__
 }
 
 void launch_slow_inputs(const int* act, int n, int* act_out, const double* theta, double* theta_out, const int* bandp,
-                        int* bandp_out, int* info_out, int B, hipStream_t s) {
+                        int* bandp_out, int* info_out, int B, hipStream_t s, int r0, int r1) {
   const int m = std::max(B * GPX_THETA_STRIDE, n);
   hipLaunchKernelGGL(slow_inputs_kernel, dim3((m + 63) / 64), dim3(64), 0, s, act, n, act_out, theta, theta_out, bandp,
-                     bandp_out, info_out, B);
+                     bandp_out, info_out, B, r0, r1);
 }
 
 void launch_slow_gather(const int* act, int n, const double* res, int stride, double* out, const int* info,

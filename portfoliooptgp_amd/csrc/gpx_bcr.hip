@@ -48,6 +48,7 @@
 
 #include "gpx_internal.h"
 #include "gpx_b16core.h"
+#include "gpx_host.h"
 
 namespace gpx {
 
@@ -659,7 +660,9 @@ __global__ __launch_bounds__(64 * Q) void bcr_bwd_kernel(BcrArgs a) {
 // gradient row and its check maximum go to the workspace for bcr_finish_kernel; diag(Z_JJ) onto
 // K's diagonal and α into the batch's α vector.
 // ---------------------------------------------------------------------------------------
-template <int Q, int NTm>
+// GZ (the bs = 128 reduction of the wide classes): Z_JJ, Z_{J+1,J} and Z_{J,J−1} are read from the
+// workspace where they lie instead of being staged in LDS (2 x 128 KB) and registers
+template <int Q, int NTm, bool GZ = false>
 __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
   constexpr int bs = Bcr<Q>::bs, BB = Bcr<Q>::BB, G = 256 / bs;
   constexpr int NV = GPX_MAX_TERMS * 3 + 1;
@@ -667,9 +670,10 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
   __shared__ double sred[4][NV];
   __shared__ double smax[4];
   __shared__ double sx[3 * bs * kXs];  // single-term stationary kernels: x/ℓ of blocks J−1, J, J+1
-  __shared__ double sZD[BB], sZ1[BB];  // Z_JJ, Z_{J+1,J}
+  __shared__ double sZs[GZ ? 1 : 2 * BB];  // Z_JJ, Z_{J+1,J}
   __shared__ double sal[2 * bs];       // α of blocks J, J+1
-  constexpr int VM = (bs + G - 1) / G;  // entries of Z_{J,J−1} per thread (its check part)
+  constexpr int VM = (bs + G - 1) / G;  // entries per thread of each block's column (and of Z_{J,J−1}'s check part)
+  constexpr int VMC = GZ ? 1 : VM;      // (GZ: Z_{J,J−1} read in place, not held in registers)
   const int p = blockIdx.y, b = a.active[p];
   const int n = a.nvalid[b], n0 = (n + bs - 1) / bs, J = blockIdx.x;
   if (J >= n0) return;
@@ -690,8 +694,14 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
   const double* ZCJ1 = ws + Lw.C + (long long)(J + 1) * BB;  // Z_{J+1,J} (J + 1 < n0)
   // the block's Z tiles and α rows into LDS, its share of Z_{J,J−1} into registers: every load
   // issued before the first use
-  double zc[VM];
-  {
+  double zc[VMC];
+  const double* sZD = GZ ? ZD : sZs;
+  const double* sZ1 = GZ ? ZCJ1 : sZs + BB;
+  if constexpr (GZ) {
+    const double a0 = tid < 2 * bs ? al[(long long)J * bs + tid] : 0.0;  // (block J+1 past n0: zeros)
+    if (k1.on) stage_scaled(sx, Xb, D, n, k1, bs, J - 1, J, J + 1 < n0 ? J + 1 : -1, tid, 256);
+    if (tid < 2 * bs) sal[tid] = a0;
+  } else {
     constexpr int PERC = BB / 256;
     double v0[PERC], v1[PERC];
 #pragma unroll
@@ -706,10 +716,11 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
     }
     const double a0 = tid < 2 * bs ? al[(long long)J * bs + tid] : 0.0;  // (block J+1 past n0: zeros)
     if (k1.on) stage_scaled(sx, Xb, D, n, k1, bs, J - 1, J, J + 1 < n0 ? J + 1 : -1, tid, 256);
+    double* sw = sZs;
 #pragma unroll
     for (int k = 0; k < PERC; ++k) {
-      sZD[tid + k * 256] = v0[k];
-      sZ1[tid + k * 256] = v1[k];
+      sw[tid + k * 256] = v0[k];
+      sw[BB + tid + k * 256] = v1[k];
     }
     if (tid < 2 * bs) sal[tid] = a0;
   }
@@ -761,7 +772,7 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
       if (J + 1 < n0) {  // (J+1, J)
         const int i = (J + 1) * bs + v;
         if (i < n) {
-          const double z = sZ1[v * bs + u];
+          const double z = sZ1[v * bs + u];  // (GZ: read only when block J+1 exists)
           const double kv = kgrad(2, i, 1, ju, dk);
           const double vv = 2.0 * fma(sal[bs + v], aj, -z);
 #pragma unroll
@@ -774,9 +785,11 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
     }
     // (J, J−1): the check only (its gradient share is block J−1's)
     if (J >= 1) {
-      if (k1.on) {
+      if (k1.on && GZ) {
+        for (int v = g; v < bs; v += G) cs = fma(k1.val(sqdist_scaled(sx + (bs + u) * kXs, sx + v * kXs, k1.dn)), ZCJ[u * bs + v], cs);
+      } else if (!GZ && k1.on) {
 #pragma unroll
-        for (int k = 0; k < VM; ++k) {
+        for (int k = 0; k < VMC; ++k) {
           const int v = g + k * G;
           if (v < bs) cs = fma(k1.val(sqdist_scaled(sx + (bs + u) * kXs, sx + v * kXs, k1.dn)), zc[k], cs);
         }
@@ -839,6 +852,397 @@ __global__ __launch_bounds__(256) void bcr_contract_kernel(BcrArgs a) {
   BP_END(2, 0);
 }
 
+// ---------------------------------------------------------------------------------------
+// The wide classes (band16 widths Q = 6..8) as ONE reduction of block size
+// bs = 128 (kBcrWideQ = 8: a band of at most 8 16-blocks is block tridiagonal in 128-row blocks,
+// whatever its own width). The Q <= 5 kernels above keep every block of a node in LDS and every
+// right-hand side in registers; at bs = 128 one block is 128 x 146 doubles (150 KB of the 160 KB
+// LDS) and the four right-hand sides 256 VGPRs per wave, so these kernels split the work:
+//   bcrw_fwd_factor  A_X in LDS; the Cholesky sweep with the couplings' solves (P_Iᵀ, P_Kᵀ) in
+//                    registers, then a second substitution pass for W_X and z from the L left in
+//                    LDS (read-only there: no barriers)
+//   bcrw_fwd_delta   the neighbours' Δ updates and the new coupling from P_Iᵀ / P_Kᵀ as the
+//                    factor launch left them in the workspace (C fragments read from L2)
+//   bcrw_bwd         α, G, the Z panels and Z_XX with every block operand read from the workspace;
+//                    Z_IX / Z_KX meet the other waves through the workspace behind a barrier
+//   bcrw_contract    bcr_contract_kernel with Z read from the workspace instead of LDS
+// Same mathematics as the Q <= 5 kernels (block cyclic reduction + Takahashi's selected inverse);
+// a problem's arithmetic depends on its own data only (every Q = 6..8 problem takes bs = 128).
+// ---------------------------------------------------------------------------------------
+template <int Q>
+__global__ __launch_bounds__(64 * Q) void bcrw_fwd_factor_kernel(BcrArgs a) {
+  constexpr int bs = Bcr<Q>::bs, rs = Bcr<Q>::rs, BB = Bcr<Q>::BB, NT = 64 * Q;
+  __shared__ __attribute__((aligned(16))) double lds[Bcr<Q>::mat + bs + 16 * kSC];
+  double* sA = lds;                  // A_X -> L (W_tt on the diagonal tiles)
+  double* sz = lds + Bcr<Q>::mat;    // y_X
+  double* sc = sz + bs;              // leaf16m's scratch
+  const int p = blockIdx.y, b = a.active[p];
+  const int n = a.nvalid[b], n0 = (n + bs - 1) / bs, l = a.level;
+  const int m = lvl_m(n0, l), top = lvl_top(n0);
+  const int j = blockIdx.x;
+  if (l > top || j >= m) return;
+  const bool is_top = l == top;
+  const bool elim = is_top || (j & 1);
+  if (l == 0 && !elim) return;
+  const int X = j << l, h = l > 0 ? 1 << (l - 1) : 0;
+  const bool pl = l > 0 && X > 0, pr = l > 0 && X + h < n0;
+  const BcrLayout Lw(bs, a.nbm);
+  double* ws = a.ws + (long long)p * a.sWs;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
+  const int K = X + (1 << l);
+  const bool hasI = elim && !is_top, hasK = elim && !is_top && K < n0;
+  double* Ag = ws + Lw.A + (long long)X * BB;
+  double* yg = ws + Lw.y + (long long)X * bs;
+  const double* CX = ws + Lw.C + (long long)X * BB;
+  const double* CK = ws + Lw.C + (long long)K * BB;
+  {  // A_X − (ΔR of X − h + ΔL of X + h), eight loads of each in flight per thread
+    const double* dR = ws + Lw.DR + (long long)(X - h) * BB;
+    const double* dL = ws + Lw.DL + (long long)(X + h) * BB;
+    constexpr int CH = 8;
+#pragma unroll 1
+    for (int e0 = tid; e0 < BB; e0 += CH * NT) {
+      double va[CH], vr[CH], vl[CH];
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int e = e0 + k * NT;
+        va[k] = Ag[e];
+        vr[k] = pl ? dR[e] : 0.0;
+        vl[k] = pr ? dL[e] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int e = e0 + k * NT, r = e / bs, c = e - r * bs;
+        const double v = va[k] - (vr[k] + vl[k]);
+        if (elim)
+          sA[r * rs + c] = v;
+        else
+          Ag[e] = v;
+      }
+    }
+    if (tid < bs) {
+      const double yr = pl ? ws[Lw.dyR + (long long)(X - h) * bs + tid] : 0.0;
+      const double yl = pr ? ws[Lw.dyL + (long long)(X + h) * bs + tid] : 0.0;
+      const double vy = yg[tid] - (yr + yl);
+      if (elim)
+        sz[tid] = vy;
+      else
+        yg[tid] = vy;
+    }
+  }
+  if (!elim) return;
+  // the couplings' right-hand sides, tile column w: R1 = E_XI, R2 = E_KXᵀ
+  t4 R1[Q], R2[Q];
+#pragma unroll
+  for (int t = 0; t < Q; ++t) {
+    R1[t] = hasI ? fr(CX, bs, t, w, l15, l4) : tzero();
+    R2[t] = hasK ? frT(CK, bs, w, t, l15, l4) : tzero();
+  }
+  __syncthreads();
+  // pass 1: right-looking Cholesky of A_X over its tile columns, with R1, R2
+#pragma unroll
+  for (int t = 0; t < Q; ++t) {
+    if (w == t) {
+      t4 Ad, V, Wr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = l15, cc = 4 * r + l4;
+        Ad[r] = rr >= cc ? sA[(16 * t + rr) * rs + 16 * t + cc] : sA[(16 * t + cc) * rs + 16 * t + rr];
+      }
+      double lii;
+      int fl;
+      leaf16m(Ad, V, Wr, lii, fl, sc, l15, l4);
+      fst(sA, rs, t, t, Wr, l15, l4);  // W_tt
+      const int g = X * bs + 16 * t + l15;
+      if (l4 == 0 && g < a.Np) a.ldiag[(long long)b * a.sVec + g] = log(lii);
+      if (fl >= 0 && lane == 0) atomicCAS(a.info + b, 0, X * bs + 16 * t + fl + 1);
+    }
+    __syncthreads();
+    const t4 WtT = frT(sA, rs, t, t, l15, l4);
+    if (w > t) {  // panel L(w, t) = A(w, t) W_ttᵀ
+      t4 c = tzero();
+      mma(c, frT(sA, rs, w, t, l15, l4), WtT);
+      fst(sA, rs, w, t, c, l15, l4);
+    }
+    {
+      t4 c1 = tzero(), c2 = tzero();
+      if (hasI) mma(c1, WtT, R1[t]);
+      if (hasK) mma(c2, WtT, R2[t]);
+      R1[t] = c1;
+      R2[t] = c2;
+    }
+    __syncthreads();
+    {
+      int idx = 0;
+#pragma unroll
+      for (int s2 = t + 1; s2 < Q; ++s2)
+#pragma unroll
+        for (int r = t + 1; r <= s2; ++r, ++idx)
+          if (idx % Q == w) {
+            t4 c = fr(sA, rs, s2, r, l15, l4);
+            mms(c, frT(sA, rs, s2, t, l15, l4), frT(sA, rs, r, t, l15, l4));
+            fst(sA, rs, s2, r, c, l15, l4);
+          }
+    }
+#pragma unroll
+    for (int s2 = t + 1; s2 < Q; ++s2) {
+      const t4 Ls = frT(sA, rs, s2, t, l15, l4);
+      if (hasI) mms(R1[s2], Ls, R1[t]);
+      if (hasK) mms(R2[s2], Ls, R2[t]);
+    }
+    __syncthreads();
+  }
+  double* PIg = ws + Lw.PI + (long long)X * BB;
+  double* PKg = ws + Lw.PK + (long long)X * BB;
+#pragma unroll
+  for (int t = 0; t < Q; ++t) {
+    if (hasI) fst(PIg, bs, t, w, R1[t], l15, l4);
+    if (hasK) fst(PKg, bs, t, w, R2[t], l15, l4);
+  }
+  // pass 2: W_X = L⁻¹ (tile column w) and z_X = L⁻¹ y_X (wave Q−1) by substitution with the L in
+  // LDS (read-only from here on)
+  t4 R3[Q], RY[Q];
+#pragma unroll
+  for (int t = 0; t < Q; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      R3[t][r] = (t == w && 4 * r + l4 == l15) ? 1.0 : 0.0;
+      RY[t][r] = (w == Q - 1 && l15 == 0) ? sz[16 * t + 4 * r + l4] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < Q; ++t) {
+    const t4 WtT = frT(sA, rs, t, t, l15, l4);
+    t4 c3 = tzero(), cy = tzero();
+    if (t >= w) mma(c3, WtT, R3[t]);
+    if (w == Q - 1) mma(cy, WtT, RY[t]);
+    R3[t] = c3;
+    RY[t] = cy;
+#pragma unroll
+    for (int s2 = t + 1; s2 < Q; ++s2) {
+      const t4 Ls = frT(sA, rs, s2, t, l15, l4);
+      if (t >= w) mms(R3[s2], Ls, R3[t]);
+      if (w == Q - 1) mms(RY[s2], Ls, RY[t]);
+    }
+  }
+  double* Wg = ws + Lw.Wm + (long long)X * BB;
+#pragma unroll
+  for (int t = 0; t < Q; ++t)
+    if (t >= w) fst(Wg, bs, t, w, R3[t], l15, l4);
+  if (w == Q - 1 && l15 == 0) {
+#pragma unroll
+    for (int t = 0; t < Q; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * t + 4 * r + l4, g = X * bs + i;
+        ws[Lw.z + g] = RY[t][r];
+        if (g < a.Np) a.z[(long long)b * a.sVec + g] = RY[t][r];
+      }
+  }
+}
+
+// the eliminated node's updates of its neighbours from the P_Iᵀ, P_Kᵀ, z_X the factor launch wrote
+template <int Q>
+__global__ __launch_bounds__(64 * Q) void bcrw_fwd_delta_kernel(BcrArgs a) {
+  constexpr int bs = Bcr<Q>::bs, BB = Bcr<Q>::BB;
+  const int p = blockIdx.y, b = a.active[p];
+  const int n = a.nvalid[b], n0 = (n + bs - 1) / bs, l = a.level;
+  const int m = lvl_m(n0, l), top = lvl_top(n0);
+  const int j = blockIdx.x;
+  if (l >= top || j >= m || !(j & 1)) return;  // (eliminated nodes below the top)
+  const int X = j << l, K = X + (1 << l);
+  const bool hasK = K < n0;
+  const BcrLayout Lw(bs, a.nbm);
+  double* ws = a.ws + (long long)p * a.sWs;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
+  const double* PIg = ws + Lw.PI + (long long)X * BB;
+  const double* PKg = ws + Lw.PK + (long long)X * BB;
+  __shared__ double sz[bs];
+  if (tid < bs) sz[tid] = ws[Lw.z + (long long)X * bs + tid];
+  t4 R1[Q], R2[Q];
+#pragma unroll
+  for (int k = 0; k < Q; ++k) {
+    R1[k] = fr(PIg, bs, k, w, l15, l4);
+    R2[k] = hasK ? fr(PKg, bs, k, w, l15, l4) : tzero();
+  }
+  __syncthreads();
+  {  // ΔA_I = P_I P_Iᵀ (lower tiles, column w) and y_I −= P_I z_X
+    double* dLo = ws + Lw.DL + (long long)X * BB;
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+      if (i < w) continue;
+      t4 c = tzero();
+#pragma unroll
+      for (int k = 0; k < Q; ++k) mma(c, fr(PIg, bs, k, i, l15, l4), R1[k]);
+      fst(dLo, bs, i, w, c, l15, l4);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s = fma(R1[k][r], sz[16 * k + 4 * r + l4], s);
+    s = sum4(s);
+    if (l4 == 0) ws[Lw.dyL + (long long)X * bs + 16 * w + l15] = s;
+  }
+  if (hasK) {  // ΔA_K = P_K P_Kᵀ, the new coupling E_KI = −P_K P_Iᵀ (-> C[K]), y_K −= P_K z_X
+    double* dRo = ws + Lw.DR + (long long)X * BB;
+    double* CKo = ws + Lw.C + (long long)K * BB;
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+      t4 e = tzero();
+#pragma unroll
+      for (int k = 0; k < Q; ++k) mms(e, fr(PKg, bs, k, i, l15, l4), R1[k]);
+      fst(CKo, bs, i, w, e, l15, l4);
+      if (i < w) continue;
+      t4 c = tzero();
+#pragma unroll
+      for (int k = 0; k < Q; ++k) mma(c, fr(PKg, bs, k, i, l15, l4), R2[k]);
+      fst(dRo, bs, i, w, c, l15, l4);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s = fma(R2[k][r], sz[16 * k + 4 * r + l4], s);
+    s = sum4(s);
+    if (l4 == 0) ws[Lw.dyR + (long long)X * bs + 16 * w + l15] = s;
+  }
+}
+
+// backward level l for bs = 128 (see bcr_bwd_kernel for the recurrences)
+template <int Q>
+__global__ __launch_bounds__(64 * Q) void bcrw_bwd_kernel(BcrArgs a) {
+  constexpr int bs = Bcr<Q>::bs, BB = Bcr<Q>::BB;
+  __shared__ double sz[bs], saI[bs], saK[bs], st[bs];
+  const int p = blockIdx.y, b = a.active[p];
+  const int n = a.nvalid[b], n0 = (n + bs - 1) / bs, l = a.level;
+  const int m = lvl_m(n0, l), top = lvl_top(n0);
+  if (l > top) return;
+  const bool is_top = l == top;
+  int X = 0;
+  if (is_top) {
+    if (blockIdx.x != 0) return;
+  } else {
+    const int j = 2 * blockIdx.x + 1;
+    if (j >= m) return;
+    X = j << l;
+  }
+  const int I = X - (1 << l), K = X + (1 << l);
+  const bool hasI = !is_top, hasK = !is_top && K < n0;
+  const BcrLayout Lw(bs, a.nbm);
+  double* ws = a.ws + (long long)p * a.sWs;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
+  const double* Wg = ws + Lw.Wm + (long long)X * BB;
+  const double* PIg = ws + Lw.PI + (long long)X * BB;
+  const double* PKg = ws + Lw.PK + (long long)X * BB;
+  double* al = ws + Lw.al;
+  if (tid < bs) {
+    sz[tid] = ws[Lw.z + (long long)X * bs + tid];
+    saI[tid] = hasI ? al[(long long)I * bs + tid] : 0.0;
+    saK[tid] = hasK ? al[(long long)K * bs + tid] : 0.0;
+  }
+  __syncthreads();
+  // α_X = W_Xᵀ (z_X − P_Iᵀ α_I − P_Kᵀ α_K): four threads per row (NT = 4·bs)
+  {
+    const int i = tid >> 2, q = tid & 3;
+    double t = 0.0;
+    if (hasI)
+      for (int c = q; c < bs; c += 4) t = fma(PIg[i * bs + c], saI[c], t);
+    if (hasK)
+      for (int c = q; c < bs; c += 4) t = fma(PKg[i * bs + c], saK[c], t);
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    if (q == 0) st[i] = sz[i] - t;
+  }
+  __syncthreads();
+  {
+    const int i = tid >> 2, q = tid & 3;
+    double v = 0.0;
+    for (int r = i + q; r < bs; r += 4) v = fma(Wg[r * bs + i], st[r], v);
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    if (q == 0) al[(long long)X * bs + i] = v;
+  }
+  // G_I = P_I W_X, G_K = P_K W_X (column w)
+  t4 GI[Q], GK[Q];
+#pragma unroll
+  for (int k = 0; k < Q; ++k) {
+    GI[k] = tzero();
+    GK[k] = tzero();
+  }
+  if (hasI) {
+#pragma unroll
+    for (int mm = 0; mm < Q; ++mm) {
+      if (mm < w) continue;
+      const t4 Wm = fr(Wg, bs, mm, w, l15, l4);
+#pragma unroll
+      for (int k = 0; k < Q; ++k) {
+        mma(GI[k], fr(PIg, bs, mm, k, l15, l4), Wm);
+        if (hasK) mma(GK[k], fr(PKg, bs, mm, k, l15, l4), Wm);
+      }
+    }
+  }
+  double* ZC = ws + Lw.C;
+  double* ZCX = ZC + (long long)X * BB;
+  double* ZCK = ZC + (long long)K * BB;
+  if (!is_top) {
+    const double* ZI = ws + Lw.A + (long long)I * BB;
+    const double* ZK = ws + Lw.A + (long long)K * BB;
+    const double* ZKI = ZC + (long long)K * BB;
+    t4 Z1[Q];
+    // Z_IX = −(Z_II G_I + Z_KIᵀ G_K) -> C[X] as Z_{X,I} = Z_IXᵀ
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+      Z1[i] = tzero();
+#pragma unroll
+      for (int k = 0; k < Q; ++k) {
+        mms(Z1[i], frT(ZI, bs, i, k, l15, l4), GI[k]);
+        if (hasK) mms(Z1[i], fr(ZKI, bs, k, i, l15, l4), GK[k]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < Q; ++i) fstT(ZCX, bs, i, w, Z1[i], l15, l4);
+    // Z_KX = −(Z_KI G_I + Z_KK G_K) -> C[K], once every wave has read Z_KI out of it
+    if (hasK) {
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        Z1[i] = tzero();
+#pragma unroll
+        for (int k = 0; k < Q; ++k) {
+          mms(Z1[i], frT(ZKI, bs, i, k, l15, l4), GI[k]);
+          mms(Z1[i], frT(ZK, bs, i, k, l15, l4), GK[k]);
+        }
+      }
+    }
+    __syncthreads();
+    if (hasK) {
+#pragma unroll
+      for (int i = 0; i < Q; ++i) fst(ZCK, bs, i, w, Z1[i], l15, l4);
+    }
+    __syncthreads();
+  }
+  // Z_XX row w = W_Xᵀ W_X − G_Iᵀ Z_IX − G_Kᵀ Z_KX
+  t4 Zr[Q];
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    Zr[i] = tzero();
+#pragma unroll
+    for (int mm = 0; mm < Q; ++mm) {
+      if (mm < w || mm < i) continue;
+      mma(Zr[i], fr(Wg, bs, mm, w, l15, l4), fr(Wg, bs, mm, i, l15, l4));
+    }
+    if (!is_top) {
+#pragma unroll
+      for (int k = 0; k < Q; ++k) {
+        mms(Zr[i], GI[k], frT(ZCX, bs, i, k, l15, l4));
+        if (hasK) mms(Zr[i], GK[k], fr(ZCK, bs, k, i, l15, l4));
+      }
+    }
+  }
+  double* ZX = ws + Lw.A + (long long)X * BB;
+#pragma unroll
+  for (int i = 0; i < Q; ++i) fst(ZX, bs, w, i, Zr[i], l15, l4);
+}
+
 // per problem: the [16] gradient row (Σ over blocks, in a fixed order) for the reduce kernel, the
 // band check's maximum, and zeros in z / log L_ii / α past the last block (rows < Np). 256
 // threads: thread t sums blocks t, t + 16, ... of parameter t % 16 (all loads in flight at once).
@@ -875,7 +1279,7 @@ __global__ __launch_bounds__(256) void bcr_finish_kernel(BcrArgs a) {
 }
 
 long long bcr_ws_doubles(int Q, int Nmax) {
-  const int bs = 16 * Q;
+  const int bs = 16 * (Q > kBcrMaxQ ? kBcrWideQ : Q);  // (the wide classes share bs = 128)
   return BcrLayout(bs, (Nmax + bs - 1) / bs).total;
 }
 
@@ -888,17 +1292,27 @@ static void launch_bcr_q(BcrArgs a, int max_terms, int np, int Nmax, hipStream_t
   int top = 0;
   while (((nbm + (1 << top) - 1) >> top) > 1) ++top;
   hipLaunchKernelGGL(bcr_build_kernel<Q>, dim3(nbm, 2, np), dim3(256), 0, s, a);
+  constexpr bool wide = Q > kBcrMaxQ;
   for (int l = 0; l <= top; ++l) {
     a.level = l;
-    hipLaunchKernelGGL(bcr_fwd_kernel<Q>, dim3((nbm + (1 << l) - 1) >> l, np), dim3(64 * Q), 0, s, a);
+    const dim3 grid((nbm + (1 << l) - 1) >> l, np);
+    if constexpr (wide) {
+      hipLaunchKernelGGL(bcrw_fwd_factor_kernel<Q>, grid, dim3(64 * Q), 0, s, a);
+      if (l < top) hipLaunchKernelGGL(bcrw_fwd_delta_kernel<Q>, grid, dim3(64 * Q), 0, s, a);
+    } else {
+      hipLaunchKernelGGL(bcr_fwd_kernel<Q>, grid, dim3(64 * Q), 0, s, a);
+    }
   }
   for (int l = top; l >= 0; --l) {
     a.level = l;
     const int m = (nbm + (1 << l) - 1) >> l;
-    hipLaunchKernelGGL(bcr_bwd_kernel<Q>, dim3(std::max(1, m / 2), np), dim3(64 * Q), 0, s, a);
+    if constexpr (wide)
+      hipLaunchKernelGGL(bcrw_bwd_kernel<Q>, dim3(std::max(1, m / 2), np), dim3(64 * Q), 0, s, a);
+    else
+      hipLaunchKernelGGL(bcr_bwd_kernel<Q>, dim3(std::max(1, m / 2), np), dim3(64 * Q), 0, s, a);
   }
-  auto ck = max_terms <= 1 ? bcr_contract_kernel<Q, 1>
-                           : (max_terms == 2 ? bcr_contract_kernel<Q, 2> : bcr_contract_kernel<Q, GPX_MAX_TERMS>);
+  auto ck = max_terms <= 1 ? bcr_contract_kernel<Q, 1, wide>
+                           : (max_terms == 2 ? bcr_contract_kernel<Q, 2, wide> : bcr_contract_kernel<Q, GPX_MAX_TERMS, wide>);
   hipLaunchKernelGGL(ck, dim3(nbm, np), dim3(256), 0, s, a);
   hipLaunchKernelGGL(bcr_finish_kernel, dim3(np), dim3(256), 0, s, a);
 }
@@ -909,7 +1323,8 @@ static void launch_bcr_direct(const BcrArgs& a, int Q, int max_terms, int np, in
     case 2: launch_bcr_q<2>(a, max_terms, np, Nmax, s); break;
     case 3: launch_bcr_q<3>(a, max_terms, np, Nmax, s); break;
     case 4: launch_bcr_q<4>(a, max_terms, np, Nmax, s); break;
-    default: launch_bcr_q<5>(a, max_terms, np, Nmax, s); break;
+    case 5: launch_bcr_q<5>(a, max_terms, np, Nmax, s); break;
+    default: launch_bcr_q<kBcrWideQ>(a, max_terms, np, Nmax, s); break;  // (Q = 6..8: bs = 128)
   }
 }
 

@@ -76,6 +76,7 @@ struct gpx_batch {
   double* bres = nullptr; size_t bres_cap = 0;  // [B][Np] band-check column sums (per-block path)
   // block-cyclic-reduction workspace (gpx_bcr.hip: calls with few band16 problems), grow-only
   double* bcr_ws = nullptr; size_t bcr_ws_cap = 0;
+  double* bcr_ws_slow = nullptr; size_t bcr_ws_slow_cap = 0;  // the deferred parts' wide reductions (slow_s)
   hipEvent_t bcr_ev[2] = {};       // profiling: the last call's reduction chain, start / end
   void* bcr_graphs = nullptr;      // the reduction chains captured as HIP graphs (gpx_bcr.hip), freed with the batch
   int force_dense = 0;         // re-evaluation of problems whose band check failed
@@ -201,7 +202,8 @@ constexpr int kBandStoreP = 2;     // band width (64-blocks) held by band storag
 constexpr int kBox = 16;           // rows per bounding box of the band tables (16: the band16 path's block)
 constexpr int kBand16MaxQ = 8;     // widest band (16-blocks) of the band16 kernels (gpx_band16.hip)
 constexpr int kBand16MaxQAny = 5;  // ... for any kernel family; Q = 6..8 only for SE1 problems with K inline
-constexpr int kBcrMaxQ = 5;        // widest band (16-blocks) of the block-cyclic-reduction path (gpx_bcr.hip)
+constexpr int kBcrMaxQ = 5;        // widest band (16-blocks) of the block-cyclic-reduction kernels that keep a node in LDS
+constexpr int kBcrWideQ = 8;       // the wide classes Q = 6..8: one reduction of block size 16·8 = 128 (gpx_bcr.hip bcrw_*)
 constexpr int kBand16MaxD = 8;     // input columns the band16 backward sweep stages per block
 constexpr int kBand16MaxNp = 8192;
 constexpr int kShadowSlots = 4;    // dense fallback slots of a band-storage batch
@@ -224,6 +226,7 @@ struct Run {
   int bcr_q = 0;      // > 0: the band16 width groups of Q <= kBcrMaxQ run as block cyclic reduction
                       // (gpx_bcr.hip), each at its width; wider groups keep their sweeps
   int ev16_g0 = 0;    // the band16 group the ev16 timing events start at (the first swept group)
+  double* bcr_ws = nullptr;  // the reduction chains' workspace for this range (the call's, or the slow part's)
 };
 
 struct PhaseTimer {
@@ -292,6 +295,8 @@ void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double
 struct RouteLimits { int plim = -1, q16lim = -1, q16wide = -1; bool fused_on = true; };
 int b16_inline_k();                            // GPX_B16_INLINE_K (bit 0 forward, bit 1 backward)
 int b16_inline_k_wide();                       // ... for the wide launch (GPX_B16_INLINE_K_WIDE)
+bool wide_bcr_on();                             // band16 widths Q > kBcrMaxQ by the bs = 128 reduction (GPX_WIDE_BCR)
+long long bcr_ws_need(const int* q, const int* cnt, int g0, int g1, int Nmax);  // workspace of groups g0..g1-1
 int wide_qmax(bool se1);                       // widest class of the wide launch (5, or 8: GPX_WIDE_QMAX)
 bool se1_spec(const gpx_kernel_spec& sp);     // one SquaredExponential term on one column
 enum RouteKind { kRouteDense, kRouteShadow, kRouteBand, kRouteFused, kRouteBand16 };

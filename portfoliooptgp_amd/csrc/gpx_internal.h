@@ -107,6 +107,20 @@ struct ReduceArgs {
   int Np;
 };
 
+// ---- small problems (Np = 64): one fused launch per evaluation (small64_kernel) ----------
+struct Small64Args {
+  const int* active;
+  const DevSpec* specs; const double* theta; const int* nvalid;
+  const double* X; long long sX; int D;
+  const double* Y; long long sY;
+  double* W; long long sMat; int ld;          // the factor W = L⁻¹ (64x64 block at the origin)
+  double* z; double* alpha; double* ldiag; long long sVec;
+  int* info;
+  double* results;                            // [B][kResStride]
+  int grad;                                   // 0: factor, z, α only (predict's re-factorisation)
+};
+void launch_small64(const Small64Args& a, int max_terms, int n_active, hipStream_t s);
+
 struct PredVarArgs {
   const int* active;
   const double* partial; long long sPartial; int nrowtiles; int ldp;
@@ -199,7 +213,8 @@ void launch_band16_wide(const BandFusedArgs& a, int kin, int n_active, hipStream
 // the deferred part's private copies of the call's active rows, θ and widths, and its zeroed
 // info block, in one launch of one-wave workgroups
 void launch_slow_inputs(const int* act, int n, int* act_out, const double* theta, double* theta_out, const int* bandp,
-                        int* bandp_out, int* info_out, int B, hipStream_t s);
+                        int* bandp_out, int* info_out, int B, hipStream_t s,
+                        int r0 = 0, int r1 = 0);
 void launch_slow_gather(const int* act, int n, const double* res, int stride, double* out, const int* info,
                         int* info_out, hipStream_t s);
 void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int kin, int n_active, hipStream_t s,

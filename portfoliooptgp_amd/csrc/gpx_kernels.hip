@@ -1025,6 +1025,175 @@ void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s) {
     hipLaunchKernelGGL(reduce_kernel<1>, dim3(n_active), dim3(64), 0, s, a);
 }
 
+// ======================================================================================
+// Small problems (Np = 64: N <= 64, the reference's weekly and monthly series, N = 19 / 5, and
+// every N <= 64 fit): the whole evaluation in ONE launch, one 4-wave workgroup per problem, K in
+// LDS — instead of the six-launch chain (build, leaf, two trmv, contraction GEMM, reduce) whose
+// launch gaps were most of a solo evaluation's device time at these sizes (VERDICT r05 item 6;
+// the reference evaluates one such model at a time, GPR/model_trainer.py:14-19):
+//   K = k(X,X) + σn²I (lower, identity padding) → leaf64_lds (Cholesky + W = L⁻¹, log L_ii)
+//   z = W y, α = Wᵀ z, logML = −½‖z‖² − Σ log L_ii − n/2 log 2π
+//   K⁻¹ = WᵀW (lower tiles on f64 MFMA) and ½ Σ (ααᵀ − K⁻¹) ∘ ∂K/∂θ (weight 2 off the diagonal)
+// Writes what the chain writes: W (the 64x64 block, zeros above the diagonal), z, α, log L_ii,
+// results [lml, grad, yᵀK⁻¹y, Σ log L_ii], info. A problem's arithmetic depends on its own
+// data and Np only (the route is taken for every Np = 64 problem, whatever the call holds).
+// grad = 0 (predict's re-factorisation): the factor, z and α only.
+// ======================================================================================
+template <int NT>
+__global__ __launch_bounds__(256) void small64_kernel(Small64Args a) {
+  constexpr int S = kLeafS;
+  __shared__ __attribute__((aligned(16))) double sA[64 * S];  // K, then L (diag), then K⁻¹ (lower tiles)
+  __shared__ __attribute__((aligned(16))) double sW[64 * S];  // W = L⁻¹
+  __shared__ double sx[64 * GPX_MAX_DIM];
+  __shared__ double sth[GPX_THETA_STRIDE];
+  __shared__ double sy[64], sz[64], sal[64], sld[64];
+  __shared__ double sred[4][GPX_MAX_TERMS * 3 + 3];
+  __shared__ int sfail;
+  const int b = a.active[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int n = a.nvalid[b], D = a.D;
+  const DevSpec spec = a.specs[b];
+  const double* X = a.X + (long long)b * a.sX;
+  for (int e = tid; e < 64 * D; e += 256) {
+    const int r = e / D;
+    sx[e] = r < n ? X[(long long)e] : 0.0;
+  }
+  if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
+  if (tid < 64) sy[tid] = tid < n ? a.Y[(long long)b * a.sY + tid] : 0.0;
+  if (tid == 0) sfail = -1;
+  __syncthreads();
+  const double noise = sth[spec.n_params];
+  // K's lower triangle (the identity in the padding); W's block zero
+#pragma unroll 1
+  for (int e = tid; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    double v = 0.0;
+    if (c <= r) {
+      if (r < n) {
+        v = eval_k(spec, sth, sx + r * D, sx + c * D);
+        if (r == c) v += noise;
+      } else {
+        v = (r == c) ? 1.0 : 0.0;
+      }
+    }
+    sA[r * S + c] = v;
+    sW[r * S + c] = 0.0;
+  }
+  __syncthreads();
+  leaf64_lds(sA, sW, sld, &sfail);  // (ends with a barrier; log L_ii in sld)
+  // z = W y (wave 0, row per lane), then α = Wᵀ z (column per lane): sequential sums over k
+  if (wave == 0) {
+    double t = 0.0;
+    for (int k = 0; k <= lane; ++k) t = fma(sW[lane * S + k], sy[k], t);
+    sz[lane] = t;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    double t = 0.0;
+    for (int i = 63; i >= lane; --i) t = fma(sW[i * S + lane], sz[i], t);
+    sal[lane] = t;
+  }
+  // the factor for predict (W's block, z, α, log L_ii)
+  double* W = a.W + (long long)b * a.sMat;
+  for (int e = tid; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    W[(long long)r * a.ld + c] = sW[r * S + c];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    a.z[(long long)b * a.sVec + tid] = sz[tid];
+    a.alpha[(long long)b * a.sVec + tid] = sal[tid];
+    a.ldiag[(long long)b * a.sVec + tid] = sld[tid];
+  }
+  if (tid == 0 && sfail >= 0 && a.info[b] == 0) a.info[b] = sfail + 1;
+  if (!a.grad) return;
+  // K⁻¹ = WᵀW on the lower 16x16 tiles (I >= J), k over rows max(I, J)·16 .. 63 (W is lower):
+  // D[m][n] = Σ_k W[k][16I + m] W[k][16J + n]; the 10 tiles dealt over the 4 waves
+  for (int t = wave; t < 10; t += 4) {
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 16 * I; k0 < 64; k0 += 4) {
+      const double av = sW[(k0 + l4) * S + 16 * I + l15];
+      const double bv = sW[(k0 + l4) * S + 16 * J + l15];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sA[(16 * I + l4 + 4 * q) * S + 16 * J + l15] = acc[q];
+  }
+  __syncthreads();
+  // ½ Σ_{i,j} (α_i α_j − K⁻¹_ij) ∂K_ij/∂θ over the lower triangle (weight 2 off the diagonal)
+  double sums[NT][3];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
+  double snoise = 0.0, szz = 0.0, sl = 0.0;
+#pragma unroll 1
+  for (int e = tid; e < 4096; e += 256) {
+    const int i = e >> 6, j = e & 63;
+    if (j > i || i >= n) continue;
+    const double w = (i == j) ? 1.0 : 2.0;
+    const double v = w * fma(sal[i], sal[j], -sA[i * S + j]);
+    double dk[NT][3];
+    eval_k_grad<NT>(spec, sth, sx + i * D, sx + j * D, dk);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      sums[t][0] = fma(v, dk[t][0], sums[t][0]);
+      sums[t][1] = fma(v, dk[t][1], sums[t][1]);
+      sums[t][2] = fma(v, dk[t][2], sums[t][2]);
+    }
+    if (i == j) snoise += v;
+  }
+  if (tid < 64) {
+    szz = sz[tid] * sz[tid];
+    sl = sld[tid];
+  }
+  // fixed-order reduction: wave sums, then the four waves in turn
+  constexpr int NV = GPX_MAX_TERMS * 3 + 3;
+  double vals[NV];
+#pragma unroll
+  for (int t = 0; t < GPX_MAX_TERMS; ++t)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wave_sum(sums[t][q]) : 0.0;
+  vals[NV - 3] = wave_sum(snoise);
+  vals[NV - 2] = wave_sum(szz);
+  vals[NV - 1] = wave_sum(sl);
+  if (lane == 0) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) sred[wave][v] = vals[v];
+  }
+  __syncthreads();
+  double* res = a.results + (long long)b * kResStride;
+  if (tid < GPX_THETA_STRIDE) {
+    int slot = -1;
+    if (tid == spec.n_params) {
+      slot = NV - 3;
+    } else {
+      const DevSpec* gs = a.specs + b;
+      for (int t = 0; t < gs->n_terms; ++t) {
+        const int o = gs->terms[t].param_offset, kind = gs->terms[t].kind;
+        const int np = (kind == GPX_RQ || kind == GPX_PERIODIC_SE) ? 3 : (kind == GPX_LINEAR ? 1 : 2);
+        if (tid >= o && tid < o + np) slot = t * 3 + (tid - o);
+      }
+    }
+    const double sv = slot >= 0 ? ((sred[0][slot] + sred[1][slot]) + sred[2][slot]) + sred[3][slot] : 0.0;
+    res[1 + tid] = 0.5 * sv;
+  }
+  if (tid == 0) {
+    const double zz = ((sred[0][NV - 2] + sred[1][NV - 2]) + sred[2][NV - 2]) + sred[3][NV - 2];
+    const double l = ((sred[0][NV - 1] + sred[1][NV - 1]) + sred[2][NV - 1]) + sred[3][NV - 1];
+    res[0] = -0.5 * zz - l - 0.5 * (double)n * 1.8378770664093453;  // log(2π)
+    res[17] = zz;
+    res[18] = l;
+  }
+}
+
+void launch_small64(const Small64Args& a, int max_terms, int n_active, hipStream_t s) {
+  auto k = max_terms <= 1 ? small64_kernel<1> : (max_terms == 2 ? small64_kernel<2> : small64_kernel<GPX_MAX_TERMS>);
+  hipLaunchKernelGGL(k, dim3(n_active), dim3(256), 0, s, a);
+}
+
 // var_j = k(x*_j, x*_j) − Σ_rowtiles colsum partials (+ σn² for predict_y)
 __global__ __launch_bounds__(256) void predvar_kernel(PredVarArgs a) {
   const int b = a.active[blockIdx.y];

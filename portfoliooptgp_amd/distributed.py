@@ -174,6 +174,31 @@ def all_gather_results(local: torch.Tensor, n_items: int, group=None) -> torch.T
     return torch.cat(bufs).cpu()
 
 
+def strong_plan(costs: Sequence[float], world: int, procs: int = 1) -> List[List[List[int]]]:
+    """A FIXED batch of fits (strong scaling: the same total work whatever the world size) split
+    over `world` ranks by shard_lpt on their costs, then each rank's fits over its `procs` host
+    processes in contiguous runs: plan[rank][proc] = the global fit indices that process fits.
+    Deterministic, so every rank and helper process derives the same plan on its own."""
+    plan = []
+    for mine in shard_lpt(costs, world):
+        k = len(mine)
+        cut = [k * p // procs for p in range(procs + 1)]
+        plan.append([mine[cut[p]:cut[p + 1]] for p in range(procs)])
+    return plan
+
+
+def gather_table(local, group=None) -> np.ndarray:
+    """Rows keyed by a global index in column 0 (fp64), from every rank: one all_gather
+    (all_gather_results: device tensors on the nccl backend, host tensors on gloo), padding rows
+    dropped, sorted by the index — the same table whatever the world size."""
+    t = torch.as_tensor(np.ascontiguousarray(local, dtype=np.float64))
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        t = all_gather_results(t, len(t), group=group)
+    a = t.cpu().numpy()
+    a = a[np.isfinite(a[:, 0])]
+    return a[np.argsort(a[:, 0], kind="stable")]
+
+
 def portfolio_inputs(gathered: Dict[int, dict], order: Sequence[int]) -> Tuple[list, list]:
     """Per-asset lists of per-day [1]-arrays, the shape Portfolio(...) indexes as
     returns[i][day][0] (Multi-Input_GPR/Portfolio/portfolio.py:111-124)."""
@@ -322,7 +347,7 @@ def fit_assets(series: Sequence[Tuple[np.ndarray, np.ndarray]], horizons: Sequen
     table = pack_results(mine, local, H, n_theta)
     if checkpoint:
         _save_checkpoint(path, table, [fps[i] for i in mine], H, n_theta, cfg)
-    if world > 1:
+    if dist.is_available() and dist.is_initialized():  # (world 1 too: a torchrun of one rank takes the same path)
         table = all_gather_results(table, len(series), group)
     return unpack_results(table, H, n_theta)
 

@@ -250,6 +250,41 @@ class Engine:
             lml[got], grad[got], info[got] = l2[got], g2[got], i2[got]
         return lml, grad, info
 
+    def lml_grad_row(self, b: int, row: np.ndarray):
+        """lml_grad for ONE problem, the drop-in pattern's call (GPR/model_trainer.py:14-19 fits
+        one model at a time, so every loss+gradient is a call of one problem): the same library
+        call with buffers and argument pointers prepared once per engine, the θ check on the
+        problem's own parameters only. Returns (logML, ∂logML/∂θ [16] (a copy), info)."""
+        fp = getattr(self, "_row_fast", None)
+        if fp is None:
+            th = np.ones((self.B, N.GPX_THETA_STRIDE))
+            lml = np.zeros(self.B)
+            grad = np.zeros((self.B, N.GPX_THETA_STRIDE))
+            info = np.zeros(self.B, dtype=np.int32)
+            act = np.zeros(1, dtype=np.int32)
+            vp = ctypes.c_void_p
+            fn = ctypes.CFUNCTYPE(ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, vp, vp, vp)(("gpx_batch_lml_grad", self.lib))
+            fp = self._row_fast = (th, lml, grad, info, act, fn, act.ctypes.data, th.ctypes.data, lml.ctypes.data,
+                                   grad.ctypes.data, info.ctypes.data)
+        th, lml, grad, info, act, fn, pa, pt, pl, pg, pi = fp
+        np_b = int(self.n_params[b])
+        for v in row[:np_b + 1].tolist():
+            if not (0.0 < v < float("inf")):
+                info[b] = N.INFO_BAD_THETA
+                return float("nan"), np.full(N.GPX_THETA_STRIDE, np.nan), N.INFO_BAD_THETA
+        th[b] = row
+        act[0] = b
+        if self.deferral >= 0:  # (deferral: the general path, which waits for deferred rows)
+            l, g, i = self.lml_grad([b], th)
+            return float(l[b]), g[b].copy(), int(i[b])
+        rc = fn(self.handle.value, 1, pa, pt, pl, pg, pi, self._stream().value)
+        if self._box_want:
+            self._harvest_boxes()
+        if rc not in (N.GPX_OK, N.GPX_NOT_PD):
+            raise N.GPXError(f"gpx_batch_lml_grad failed ({rc}): {self.ctx.last_error()}")
+        self.eval_count += 1
+        return float(lml[b]), grad[b].copy(), int(info[b])
+
     @staticmethod
     def _count_reported(info: np.ndarray) -> int:
         """Problem-evaluations a deferral-mode complete reported: the call's own rows that were not
@@ -701,6 +736,11 @@ def solo_engine(model) -> Engine:
     bound. The model's data is rebound into the slot when another model used it last (the
     cached factor is dropped then, so results never mix)."""
     global _SOLO_POOL
+    c = getattr(model, "_solo_cache", None)
+    if c is not None and c[1] == _DEFAULT_BAND_ROUTE:  # (this model was the slot's last user)
+        eng = c[0]()
+        if eng is not None and eng._owner is not None and eng._owner() is model and _SOLO_POOL.get(c[2]) is eng:
+            return eng
     import weakref
     from collections import OrderedDict
     if _SOLO_POOL is None:
@@ -722,4 +762,5 @@ def solo_engine(model) -> Engine:
     if owner is not model:
         eng.rebind(0, X, Y, model._spec)
         eng._owner = weakref.ref(model)
+    model._solo_cache = (weakref.ref(eng), _DEFAULT_BAND_ROUTE, key)
     return eng

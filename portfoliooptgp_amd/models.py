@@ -115,16 +115,15 @@ class GPR:
     # ---------------------------------------------------------------- objective -------
     def _lml_and_grad_theta(self):
         eng, b = self.engine()
-        theta = np.ones((eng.B, N.GPX_THETA_STRIDE))
-        theta[b] = self.theta_row()
-        lml, grad, info = eng.lml_grad([b], theta)
-        if info[b] == N.INFO_BAD_THETA:
-            raise N.InvalidParameterError(f"hyperparameters out of (0, inf): {theta[b, :eng.n_params[b] + 1]}")
-        if info[b] != 0:
+        row = self.theta_row()
+        lml, grad, info = eng.lml_grad_row(b, row)
+        if info == N.INFO_BAD_THETA:
+            raise N.InvalidParameterError(f"hyperparameters out of (0, inf): {row[:eng.n_params[b] + 1]}")
+        if info != 0:
             raise N.NotPositiveDefiniteError(
-                f"Cholesky decomposition was not successful: pivot {int(info[b])} of K + noise I "
-                "is not positive", info[b])
-        return float(lml[b]), grad[b]
+                f"Cholesky decomposition was not successful: pivot {int(info)} of K + noise I "
+                "is not positive", info)
+        return lml, grad
 
     def log_marginal_likelihood(self) -> torch.Tensor:
         return torch.tensor(self._lml_and_grad_theta()[0], dtype=torch.float64)

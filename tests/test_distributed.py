@@ -375,3 +375,54 @@ def test_config_fingerprint_is_stable_across_processes():
         pass
     with pytest.raises(ValueError, match="stable representation"):
         D.config_fingerprint(_stand_in_fit, {"k": Opaque()})
+
+
+def _strong_rows(ids, steps, total):
+    """A deterministic stand-in for the bench's per-fit summary rows (global index first)."""
+    ids = np.asarray(ids, dtype=np.float64)
+    g = np.concatenate([ids + s * total for s in range(steps)])
+    return np.stack([g, np.sin(g), g % 7.0, np.sqrt(g + 1.0)], axis=1)
+
+
+def _strong_worker(rank, world, port, q, total, procs, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        plan = D.strong_plan([1.0] * total, world, procs)
+        local = np.concatenate([_strong_rows(ids, steps, total) for ids in plan[rank]])
+        q.put((rank, D.gather_table(local).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_strong_scaling_plan_and_table_world2_equals_world1():
+    """bench.py --scaling strong: the fixed batch is split over the ranks and
+    their host processes by strong_plan, and the all_gathered table (gather_table) is the same
+    fits in the same order at world 2 as at world 1."""
+    import bench
+    total, procs, steps = 203, 3, 2
+    for world in (1, 2, 8):
+        plan = D.strong_plan([1.0] * total, world, procs)
+        flat = sorted(i for pr in plan for p in pr for i in p)
+        assert flat == list(range(total))
+        sizes = [sum(len(p) for p in pr) for pr in plan]
+        assert max(sizes) - min(sizes) <= 1
+    one = D.gather_table(np.concatenate([_strong_rows(ids, steps, total)
+                                         for ids in D.strong_plan([1.0] * total, 1, procs)[0]]))
+    assert np.array_equal(one[:, 0], np.arange(total * steps))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_strong_worker, args=(r, 2, port, q, total, procs, steps)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, tab in outs:
+        np.testing.assert_array_equal(np.asarray(tab), one)
+    # the bench's own plan: every fit of the batch exactly once over ranks x host processes
+    args = bench.parse_args(["--scaling", "strong", "--total-fits", "1000", "--procs", "8"])
+    ids = bench.strong_fit_ids(args, 2, 8)
+    assert sorted(i for pr in ids for p in pr for i in p) == list(range(1000))
