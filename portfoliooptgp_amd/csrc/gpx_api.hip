@@ -203,8 +203,10 @@ bool small64_on(const gpx_batch* bt) {
   return on && bt->Np == kLeaf;
 }
 
-// the fused small-problem evaluation (grad: the gradient and logML too) for the problems of r
-void small64_eval(const Run& r, bool grad) {
+// the fused small-problem evaluation (grad: the gradient and logML too) for the problems of r;
+// sio: the call's I/O block in coherent pinned memory (active list, θ, info, results read and
+// written there by the kernel), else the device I/O block
+void small64_eval(const Run& r, bool grad, char* sio = nullptr) {
   gpx_batch* bt = r.bt;
   Small64Args a{};
   a.active = r.d_act; a.specs = bt->d_specs; a.theta = bt->d_theta; a.nvalid = bt->d_n;
@@ -212,6 +214,12 @@ void small64_eval(const Run& r, bool grad) {
   a.W = bt->W; a.sMat = mat_stride(bt); a.ld = bt->Np;
   a.z = bt->z; a.alpha = bt->alpha; a.ldiag = bt->ldiag; a.sVec = bt->Np;
   a.info = bt->d_info; a.results = bt->results; a.grad = grad ? 1 : 0;
+  if (sio) {
+    a.active = reinterpret_cast<const int*>(sio);
+    a.info = reinterpret_cast<int*>(sio + bt->io_info_off);
+    a.theta = reinterpret_cast<const double*>(sio + bt->io_theta_off);
+    a.results = reinterpret_cast<double*>(sio + bt->io_res_off);
+  }
   int max_terms = 1;
   for (int b = 0; b < bt->B; ++b) max_terms = std::max(max_terms, (int)bt->specs[b].n_terms);
   launch_small64(a, max_terms, r.na, r.s);
@@ -1364,6 +1372,7 @@ int gpx_batch_destroy(gpx_batch* bt) {
   bcr_graph_cache_free(bt->bcr_graphs);  // (every stream of the batch has drained above)
   bt->bcr_graphs = nullptr;
   if (bt->h_io) (void)hipHostFree(bt->h_io);
+  if (bt->h_sio) (void)hipHostFree(bt->h_sio);
   if (bt->h_io_pred) (void)hipHostFree(bt->h_io_pred);
   if (bt->h_stage) (void)hipHostFree(bt->h_stage);
   if (bt->h_rdesc) (void)hipHostFree(bt->h_rdesc);
@@ -2047,6 +2056,41 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
       for (auto& e2 : bt->bcr_ev) HIPX(ctx, hipEventCreate(&e2));
   }
   sc.lap(1);
+  // a small-problem call (Np = 64, every problem on the one fused kernel): its I/O straight through
+  // coherent pinned memory — no upload or download DMA, the kernel launch and the synchronise
+  // are the call's whole device round trip (the drop-in pattern's solo calls, VERDICT r05 item 6;
+  // GPX_SMALL_DIRECT=0: the DMA'd I/O block)
+  static const bool small_direct = [] {
+    const char* e = getenv("GPX_SMALL_DIRECT");
+    return !(e && atoi(e) == 0);
+  }();
+  if (small_direct && small64_on(bt) && n_dense == n_active && !shadow_async && shadow_ids.empty()) {
+    if (!bt->h_sio) HIPX(ctx, hipHostMalloc(&bt->h_sio, bt->io_bytes, hipHostMallocCoherent));
+    {
+      const int e = fence_io(bt, s);
+      if (e != GPX_OK) return e;
+    }
+    std::memcpy(bt->h_sio, order.data(), sizeof(int) * n_active);
+    std::memset(bt->h_sio + bt->io_info_off, 0, sizeof(int) * bt->B);
+    std::memcpy(bt->h_sio + bt->io_theta_off, theta, sizeof(double) * GPX_THETA_STRIDE * bt->B);
+    std::unique_ptr<gpx_batch::PendingEval> pd(new gpx_batch::PendingEval());
+    pd->s = s;
+    pd->n_active = n_active;
+    pd->n_dense = n_active;
+    pd->direct = true;
+    pd->theta.assign(theta, theta + (size_t)bt->B * GPX_THETA_STRIDE);
+    pd->total.reset(new PhaseTimer(ctx->profiling != 0, s));
+    pd->ct.reset(new PhaseTimer(false, s));
+    pd->bp.reset(new PhaseTimer(false, s));
+    pd->total->mark();
+    small64_eval(Run{bt, reinterpret_cast<const int*>(bt->h_sio), n_active, s}, true, bt->h_sio);
+    pd->total->mark();
+    HIPX(ctx, hipGetLastError());
+    pd->order = std::move(order);
+    bt->pending_eval = std::move(pd);
+    sc.lap(4);
+    return GPX_OK;
+  }
   int rc = upload_common(bt, n_active, order.data(), theta, s);
   if (rc != GPX_OK) return drop_shadow(rc);
   sc.lap(2);
@@ -2273,6 +2317,15 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
     HIPX(ctx, hipEventSynchronize(pe->bulk_done));
   else
     HIPX(ctx, hipStreamSynchronize(s));
+  if (pe->direct) {  // (the kernel wrote info and results into the coherent block)
+    for (int i = 0; i < pe->n_active; ++i) {
+      const int b = pe->order[i];
+      bt->h_info[b] = reinterpret_cast<const int*>(bt->h_sio + bt->io_info_off)[b];
+      std::memcpy(bt->h_results + (size_t)b * kResStride,
+                  reinterpret_cast<const double*>(bt->h_sio + bt->io_res_off) + (size_t)b * kResStride,
+                  sizeof(double) * kResStride);
+    }
+  }
   sc.lap(5);
   const int n_active = pe->n_active, n_dense = pe->n_dense, n_band = pe->n_band, n_fused = pe->n_fused;
   const int n_fused1 = pe->n_fused1, ng = pe->ng;
@@ -2290,8 +2343,9 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
       bt->timing.factor_ms += pts[g].ms(0, 1) / ng;
       bt->timing.alpha_ms += pts[g].ms(1, 2) / ng;
     }
-    bt->timing.grad_ms = n_dense > 0 ? ct.ms(0, 2) : 0.0;
-    if (n_dense > 0) {
+    // (the small-problem kernel of Np = 64 batches has no separate contraction launch to time)
+    bt->timing.grad_ms = (n_dense > 0 && ct.ev.size() >= 3) ? ct.ms(0, 2) : 0.0;
+    if (n_dense > 0 && kev[0]) {
       float kms = 0.f;
       (void)hipEventElapsedTime(&kms, kev[0], kev[1]);
       bt->timing.contract_ms_total += kms;

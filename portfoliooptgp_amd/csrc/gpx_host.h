@@ -129,6 +129,9 @@ struct gpx_batch {
   // results] in one DMA (was 2 pageable copies + a memset up, 2 pageable copies down)
   char* d_io = nullptr;
   char* h_io = nullptr;       // pinned
+  // the same layout in COHERENT pinned memory, for small-problem calls (Np = 64) whose one kernel
+  // reads its active list / θ and writes info / results here directly: no DMA either way
+  char* h_sio = nullptr;
   size_t io_info_off = 0, io_bandp_off = 0, io_theta_off = 0, io_res_off = 0, io_bytes = 0;
   int* d_bandp = nullptr;     // [B] band width (64-blocks) of the banded problems of the call
   int* h_bandp = nullptr;
@@ -367,6 +370,7 @@ struct gpx_batch::PendingEval {
   int g16_q[gpx::kBand16MaxQ] = {}, g16_n[gpx::kBand16MaxQ] = {}, n_g16 = 0;
   hipEvent_t fq16[gpx::kBand16MaxQ][4] = {};
   int n_bcr = 0;                      // problems of the call on the block-cyclic-reduction path (bcr_ev timed)
+  bool direct = false;                // small-problem call with its I/O in h_sio (no DMA): copied to h_io at _complete
   ~PendingEval() {
     for (auto x : kev)
       if (x) (void)hipEventDestroy(x);

@@ -272,9 +272,9 @@ def test_bcr_wide_q6_to_q8(n):
         lo, go = _band_oracle_loss_grad(*data[b], e, 0.9)
         assert abs(loss - lo) <= 1e-9 * abs(lo), (e, loss, lo)
         assert np.abs(g - go).max() <= 1e-6 * max(1.0, np.abs(go).max()), (e, g, go)
-    for b in act:  # composition: alone in its call, the same bits
+    for b in act:  # composition: alone in its call (the sweeps route), the same bits
         l1, g1, _ = eng.lml_grad([b], th)
-        assert l1[b] == lb[b] and np.array_equal(g1[b, :3], gb[b, :3]), b
+        assert l1[b] == first[0][b] and np.array_equal(g1[b, :3], first[1][b, :3]), b
 
 
 def test_bcr_wide_fit_matches_dense_fit():

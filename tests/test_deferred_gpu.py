@@ -128,10 +128,15 @@ def test_deferred_redo_path_and_wait_while_submitted():
     call at the same tolerance; deferred_wait is refused while an evaluation is submitted (the
     re-evaluation would need the batch), and works once it is completed."""
     import os
-    n = 2048
-    data = [O.synthetic_series(n, s) for s in range(len(ELLS))]
-    th = _theta(ELLS)
-    act = list(range(len(ELLS)))
+    # (a short fast problem, n = 600, whose synchronous dense redo in the complete is quick, and long
+    # slow ones: the slow part is still in flight when the first complete returns — round 6's wide
+    # classes take the short reduction chain, so at one size for all the part could finish first)
+    n = 4096
+    ells = [1.18, 1.6, 1.9, 2.3, 2.8, 1.6, 1.9]
+    data = [O.synthetic_series(n, s) for s in range(len(ells))]
+    data[0] = (data[0][0][:600], data[0][1][:600])
+    th = _theta(ells)
+    act = list(range(len(ells)))
     prev = os.environ.get("GPX_BAND_TOL")
     os.environ["GPX_BAND_TOL"] = "1e-30"
     try:
