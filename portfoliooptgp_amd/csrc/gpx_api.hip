@@ -650,18 +650,25 @@ int wide_qmax(bool se1) {
 }
 
 // band16 widths Q > kBcrMaxQ (6..8) by the block-cyclic-reduction chain of block size 128
-// (gpx_bcr.hip bcrw_*) instead of one-wavefront sweeps (GPX_WIDE_BCR=0: the sweeps, round 5):
-// a problem's path still depends on its own width only, whatever the batch's route or call
-bool wide_bcr_on() {
-  static const bool on = [] {
+// (gpx_bcr.hip bcrw_*; GPX_WIDE_BCR): 1 (default) in calls on the reduction route (the batch's
+// band route "bcr": latency — before round 6 these widths went to the 64-row sweeps there),
+// 2 in every call, 0 never. Measured in the C2 bench's layout (8 host processes, thousands of
+// problems in flight) mode 2 loses 35 % with deferral and 12 % without (profiles/r06_ab.md: the
+// chain's 8-wave, 150 KB-LDS workgroups wait for an empty CU behind the other processes' sweeps),
+// so the sweeps route keeps its one-wavefront Q = 6..8 sweeps. Either way a problem's path is a
+// function of its own width and the batch's route, never of the call.
+int wide_bcr_mode() {
+  static const int m = [] {
     const char* e = getenv("GPX_WIDE_BCR");
-    return !(e && atoi(e) == 0);
+    return e ? std::max(0, std::min(2, atoi(e))) : 1;
   }();
-  return on;
+  return m;
 }
+bool wide_bcr_on(bool bcr_route) { return wide_bcr_mode() == 2 || (wide_bcr_mode() == 1 && bcr_route); }
 
-// the widest class a deferred part's wide launch (band16_wide_kernel) takes
-static int wide_launch_qmax(bool se1) { return wide_bcr_on() ? std::min(wide_qmax(se1), kBcrMaxQ) : wide_qmax(se1); }
+// the widest class a deferred part's wide launch (band16_wide_kernel) takes (deferred parts
+// exist on the sweeps route only)
+static int wide_launch_qmax(bool se1) { return wide_bcr_on(false) ? std::min(wide_qmax(se1), kBcrMaxQ) : wide_qmax(se1); }
 
 // reduction workspace of band16 groups g0 .. g1-1 (each problem in slots of its group's layout)
 long long bcr_ws_need(const int* q, const int* cnt, int g0, int g1, int Nmax) {
@@ -705,7 +712,7 @@ static void trace_mark(gpx_batch* bt, int kind, hipStream_t s) {
   if (bt->d_wtrace) launch_wave_marker(bt->d_wtrace, bt->d_wtrace_n, bt->wtrace_cap, kind, s);
 }
 
-void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int kband16,
+int band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int kband16,
                      int n1, int max_terms, hipEvent_t* ev, hipEvent_t (*ev16)[4]) {
   // r's active range is [band16 problems (n16, by width group) | p <= 1 problems (n1) | p = 2
   // problems]; the p = 2 class runs as a separate launch pair on an auxiliary stream concurrently
@@ -754,7 +761,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       wso += (long long)g16_n[g] * bcr_ws_doubles(g16_q[g], bt->Nmax);
     }
     for (; g < n_g16; ++g) {
-      if (wide_bcr_on() && g16_q[g] > kBcrMaxQ) {
+      if (wide_bcr_on(r.bcr_q > 0) && g16_q[g] > kBcrMaxQ) {
         // the widths 6..8 (always the tail of the groups) as ONE reduction chain of block size 128
         if (nl > 0 && lanes[nl - 1].kind == 5) {
           lanes[nl - 1].n += g16_n[g];
@@ -785,6 +792,17 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
     const char* e = getenv("GPX_LANE_ORDER");
     return e ? atoi(e) : 0;
   }();
+  {  // the reduction lanes' workspace (grow-only; their offsets were laid out in group order)
+    long long need = 0;
+    for (int i = 0; i < nl; ++i)
+      if (lanes[i].kind == 4 || lanes[i].kind == 5)
+        need = std::max(need, lanes[i].wso + (long long)lanes[i].n *
+                                  bcr_ws_doubles(lanes[i].kind == 5 ? kBcrWideQ : g16_q[lanes[i].g], bt->Nmax));
+    if (need > 0 && (size_t)need > *r.bcr_capp) {  // (grown with headroom: each regrowth frees, which synchronises)
+      const int e = ensure(bt->ctx, *r.bcr_wsp, *r.bcr_capp, (size_t)need * 3 / 2);
+      if (e != GPX_OK) return e;
+    }
+  }
   std::sort(lanes, lanes + nl, [](const Lane& x, const Lane& y) { return x.n > y.n; });
   if (lane_order == 1 && nl > 1) std::rotate(lanes, lanes + 1, lanes + nl);  // bulk lane last (on an aux stream)
   trace_mark(bt, 40, r.s);
@@ -865,7 +883,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
       ca.X = bt->X; ca.sX = (long long)bt->Nmax * bt->D; ca.D = bt->D; ca.Y = bt->Y; ca.sY = bt->Nmax;
       // (workspace: the lane's problems in slots of its layout, at the lane's offset)
       ca.sWs = bcr_ws_doubles(qc, bt->Nmax);
-      ca.ws = r.bcr_ws + l.wso; ca.info = fa.info;
+      ca.ws = *r.bcr_wsp + l.wso; ca.info = fa.info;
       ca.z = bt->z; ca.ldiag = bt->ldiag; ca.alpha = bt->alpha; ca.sVec = Np; ca.Np = Np;
       ca.Kd = bt->K; ca.sMat = st; ca.ld = mat_ld(bt);
       ca.partial = bt->partial; ca.sPartial = bt->partial_stride; ca.results = bt->results;
@@ -900,6 +918,7 @@ void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const i
   ra.nvalid = bt->d_n; ra.specs = bt->d_specs; ra.results = bt->results; ra.Np = Np;
   launch_reduce(ra, r.na, r.s);
   trace_mark(bt, 42, r.s);
+  return GPX_OK;
 }
 
 // The batch's auxiliary streams (the forked T products of the recursion) take the priority of
@@ -1752,7 +1771,7 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
   rec->clear_events();
   // (the swept groups: the wide ones, Q > kBcrMaxQ, run as a reduction chain without band16 events)
   int g_sw = n_g16;
-  while (wide_bcr_on() && g_sw > 0 && q[g_sw - 1] > kBcrMaxQ) --g_sw;
+  while (wide_bcr_on(false) && g_sw > 0 && q[g_sw - 1] > kBcrMaxQ) --g_sw;
   rec->n_g16 = g_sw;
   rec->se1 = se1;
   for (int g = 0; g < n_g16; ++g) {
@@ -1775,10 +1794,6 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
     bt->slow_in_armed = true;
   }
   const bool fused64 = n > n16;
-  if (g_sw < n_g16) {
-    const int e = ensure(ctx, bt->bcr_ws_slow, bt->bcr_ws_slow_cap, (size_t)bcr_ws_need(q, cnt, g_sw, n_g16, bt->Nmax));
-    if (e != GPX_OK) return e;
-  }
   if (ctx->profiling) {
     for (int g = 0; g < g_sw; ++g)
       for (int e = 0; e < 4; ++e) HIPX(ctx, hipEventCreate(&rec->fq16[g][e]));
@@ -1792,7 +1807,8 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
   // (on the call's stream, after its download: the next call's upload follows this part in the
   // stream's order, so the part reads the call's own active list, θ and widths in place)
   Run r{bt, own ? bt->d_slow_act : bt->d_active + off, n, ss};
-  r.bcr_ws = bt->bcr_ws_slow;
+  r.bcr_wsp = &bt->bcr_ws_slow;
+  r.bcr_capp = &bt->bcr_ws_slow_cap;
   if (own) {
     r.theta = bt->d_slow_theta;
     r.bandp = bt->d_slow_bandp;
@@ -1812,8 +1828,11 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
     return !(e && atoi(e) == 0);
   }();
   r.wide_from = wide ? 1 : 0;
-  band_fused_eval(r, n16, n_g16, q, cnt, se1, kband16, n1, max_terms, (ctx->profiling && fused64) ? rec->fq : nullptr,
-                  ctx->profiling ? rec->fq16 : nullptr);
+  {
+    const int e = band_fused_eval(r, n16, n_g16, q, cnt, se1, kband16, n1, max_terms,
+                                  (ctx->profiling && fused64) ? rec->fq : nullptr, ctx->profiling ? rec->fq16 : nullptr);
+    if (e != GPX_OK) return e;
+  }
   launch_slow_gather(r.d_act, n, bt->results, kResStride, bt->d_slow_res, own ? bt->d_slow_info : bt->d_info,
                      bt->d_slow_info_c, ss);
   HIPX(ctx, hipMemcpyAsync(rec->h_res, bt->d_slow_res, sizeof(double) * n * kResStride, hipMemcpyDeviceToHost, ss));
@@ -1995,7 +2014,7 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   // there its p64 = 2 problems go back to the 64-row sweeps (a Q = 6..8 one-wave sweep is the
   // throughput choice, but its N/16-step chain is 2-3x the 64-row sweeps' latency)
   const int bcr_max = bcr_max_problems(bt);
-  if (!wide_bcr_on() && rt.n16 > 0 && rt.n16 <= bcr_max && rt.n_g16 > 0 && rt.g16_q[rt.n_g16 - 1] > kBcrMaxQ)
+  if (!wide_bcr_on(true) && rt.n16 > 0 && rt.n16 <= bcr_max && rt.n_g16 > 0 && rt.g16_q[rt.n_g16 - 1] > kBcrMaxQ)
     route_call(bt, n_active, active, theta, rt, kBcrMaxQ);
   std::vector<int32_t>& order = rt.order;
   std::vector<int32_t>& shadow_ids = rt.shadow_ids;
@@ -2047,11 +2066,8 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
   }
   // the wide groups (Q > kBcrMaxQ, a suffix of the groups) on the bs = 128 reduction
   int g_wide = n_g16;
-  while (wide_bcr_on() && g_wide > 0 && g16_q[g_wide - 1] > kBcrMaxQ) --g_wide;
-  if (n16_bcr > 0 || g_wide < n_g16) {
-    const long long need = bcr_ws_need(g16_q, g16_n, 0, g_bcr, bt->Nmax) + bcr_ws_need(g16_q, g16_n, g_wide, n_g16, bt->Nmax);
-    const int e = ensure(ctx, bt->bcr_ws, bt->bcr_ws_cap, (size_t)need);
-    if (e != GPX_OK) return drop_shadow(e);
+  while (wide_bcr_on(bcr_q > 0) && g_wide > 0 && g16_q[g_wide - 1] > kBcrMaxQ) --g_wide;
+  if (n16_bcr > 0 || g_wide < n_g16) {  // (the workspace is sized by band_fused_eval for what it launches)
     if (ctx->profiling && !bt->bcr_ev[0])
       for (auto& e2 : bt->bcr_ev) HIPX(ctx, hipEventCreate(&e2));
   }
@@ -2263,11 +2279,13 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     }
     Run rf{bt, bt->d_active + n_dense + n_band, n_fused, s};
     rf.bcr_q = bcr_q;
-    rf.bcr_ws = bt->bcr_ws;
+    rf.bcr_wsp = &bt->bcr_ws;
+    rf.bcr_capp = &bt->bcr_ws_cap;
     rf.ev16_g0 = g_bcr;
-    band_fused_eval(rf, n16, n_g16, g16_q, g16_n, se1,
+    const int ebf = band_fused_eval(rf, n16, n_g16, g16_q, g16_n, se1,
                     b16_p2 ? 3 : 2, n_fused1,
                     max_terms, (ctx->profiling && old_fused) ? fqe : nullptr, ctx->profiling ? pe->fq16 : nullptr);
+    if (ebf != GPX_OK) return drop_shadow(ebf);
   }
   bp.mark();
   total.mark();

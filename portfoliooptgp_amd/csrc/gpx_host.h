@@ -229,7 +229,10 @@ struct Run {
   int bcr_q = 0;      // > 0: the band16 width groups of Q <= kBcrMaxQ run as block cyclic reduction
                       // (gpx_bcr.hip), each at its width; wider groups keep their sweeps
   int ev16_g0 = 0;    // the band16 group the ev16 timing events start at (the first swept group)
-  double* bcr_ws = nullptr;  // the reduction chains' workspace for this range (the call's, or the slow part's)
+  // the reduction chains' grow-only workspace for this range (the call's, or the slow part's),
+  // sized by band_fused_eval for the lanes it actually launches
+  double** bcr_wsp = nullptr;
+  size_t* bcr_capp = nullptr;
 };
 
 struct PhaseTimer {
@@ -298,7 +301,8 @@ void route_call(gpx_batch* bt, int n_active, const int32_t* active, const double
 struct RouteLimits { int plim = -1, q16lim = -1, q16wide = -1; bool fused_on = true; };
 int b16_inline_k();                            // GPX_B16_INLINE_K (bit 0 forward, bit 1 backward)
 int b16_inline_k_wide();                       // ... for the wide launch (GPX_B16_INLINE_K_WIDE)
-bool wide_bcr_on();                             // band16 widths Q > kBcrMaxQ by the bs = 128 reduction (GPX_WIDE_BCR)
+int wide_bcr_mode();                            // GPX_WIDE_BCR: 0 never, 1 on the reduction route (default), 2 always
+bool wide_bcr_on(bool bcr_route);               // band16 widths Q > kBcrMaxQ by the bs = 128 reduction in this call
 long long bcr_ws_need(const int* q, const int* cnt, int g0, int g1, int Nmax);  // workspace of groups g0..g1-1
 int wide_qmax(bool se1);                       // widest class of the wide launch (5, or 8: GPX_WIDE_QMAX)
 bool se1_spec(const gpx_kernel_spec& sp);     // one SquaredExponential term on one column
@@ -307,7 +311,7 @@ RouteLimits route_limits(const gpx_batch* bt);
 RouteKind route_one(const gpx_batch* bt, int b, const double* theta_row, const RouteLimits& L, int& w);
 // p <= 2: [band16 groups (sizes g16_n, widths g16_q; K band of kband16 64-block diagonals) |
 // p<=1 (n1) | p=2]
-void band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int kband16,
+int band_fused_eval(const Run& r, int n16, int n_g16, const int* g16_q, const int* g16_n, bool se1, int kband16,
                      int n1, int max_terms, hipEvent_t* ev = nullptr, hipEvent_t (*ev16)[4] = nullptr);
 double band_fused_flops(int Np, int p, bool fwd);  // block-product flops of one problem's sweep
 void factor(const Run& r);       // K build + recursive Cholesky-and-inverse (W = L⁻¹)

@@ -231,8 +231,8 @@ def _band_oracle_loss_grad(x, y, ell, var):
 
 def test_band16_se1_q6_to_q8_n4096():
     """ℓ ∈ {2, 2.3, 2.5, 2.8, 3} at the C2 inputs: bands of Q = 5..8 16-blocks (p64 = 2). SE1
-    problems take the band16 sweeps up to Q = 5 and, from round 6, the widths 6..8 the
-    block-cyclic-reduction chain of block size 128 — no 64-row sweep launch — and agree with the 64-row p = 2 sweeps
+    problems with K's tiles inline take the band16 sweeps (one wavefront per SIMD, window in VGPRs
+    and AGPRs) — no 64-row sweep launch — and agree with the 64-row p = 2 sweeps
     (GPX_BAND16_QMAX=5 sends them there), the dense path, and the band oracle at ℓ ∈ {2, 2.5, 3}
     (logML 1e-9, ∂loss/∂u 1e-6·max(1, |g|): VERDICT r04 item 2)."""
     n = 4096
@@ -246,11 +246,8 @@ def test_band16_se1_q6_to_q8_n4096():
     eng.reset_timing()
     lb, gb, ib = eng.lml_grad(act, th)
     t = eng.last_timing()
-    # (round 6: the widths 6..8 take the block-cyclic-reduction chain of block size 128, the
-    # widest sweep class is Q = 5; tests/test_bcr_gpu.py::test_bcr_wide_q6_to_q8)
-    assert not ib.any() and t.band16_evals == 1 and t.bcr_wide_evals == 4 and t.band_fallbacks == 0, \
-        (t.band16_evals, t.bcr_wide_evals, t.band_fallbacks)
-    assert t.band16_q_sum == 5 and t.band_fused_launches == 0, (t.band16_q_sum, t.band_fused_launches)
+    assert not ib.any() and t.band16_evals == len(ells) and t.band_fallbacks == 0, (t.band16_evals, t.band_fallbacks)
+    assert t.band16_q_sum == int(sum(cls)) and t.band_fused_launches == 0, (t.band16_q_sum, t.band_fused_launches)
     m16, v16, _ = eng._predict_train(np.arange(len(ells), dtype=np.int32), th, False)
     with _Env("GPX_BAND16_QMAX", "5"):
         eng.reset_timing()
@@ -295,9 +292,8 @@ def test_mixed_ell_c2_call_band_storage_no_64row_sweeps():
     l, g, info = eng.lml_grad(act, th)
     t = eng.last_timing()
     assert not info.any()
-    assert t.band16_evals + t.bcr_wide_evals == len(ells) and t.shadow_evals == 0 and t.band_fused_launches == 0, \
-        (t.band16_evals, t.bcr_wide_evals, t.shadow_evals, t.band_fused_launches)
-    assert t.bcr_wide_evals == int((eng.band_class(act, th) > 5).sum()) > 0, t.bcr_wide_evals
+    assert t.band16_evals == len(ells) and t.shadow_evals == 0 and t.band_fused_launches == 0, \
+        (t.band16_evals, t.shadow_evals, t.band_fused_launches)
     for b in (0, 4, 8, 10):
         l1, g1, _ = eng.lml_grad([b], th)
         assert l1[b] == l[b] and np.array_equal(g1[b, :3], g[b, :3]), b

@@ -222,34 +222,37 @@ def test_bcr_band_storage_matches_dense_layout():
 
 @pytest.mark.parametrize("n", [4096, 4001, 2048])
 def test_bcr_wide_q6_to_q8(n):
-    """the widths Q = 6..8 (ℓ ≥ 2.3 on unit-spaced day offsets, the shared-kernel
-    warm starts of GPR/main.py:105-114 drift there) take ONE block-cyclic-reduction chain of block
-    size 128 (gpx_bcr.hip bcrw_*) on every route — no one-wavefront Q = 6..8 sweep, no 64-row
-    sweep. Against the dense path (logML 1e-9, gradient 1e-7·(1 + max|g|)), the band oracle at
-    ℓ ∈ {2.5, 3} (SURVEY §8c bars), the 64-row p = 2 sweeps (GPX_BAND16_QMAX=5), predict at the
+    """on the reduction route the widths Q = 6..8 (ℓ ≥ 2.3 on unit-spaced day
+    offsets, where the shared-kernel warm starts of GPR/main.py:105-114 drift) take ONE
+    block-cyclic-reduction chain of block size 128 (gpx_bcr.hip bcrw_*) — before round 6 they went
+    to the 64-row sweeps there. Against the dense path (logML 1e-9, gradient 1e-7·(1 + max|g|)),
+    the one-wavefront Q = 6..8 sweeps of the default route, the 64-row p = 2 sweeps
+    (GPX_BAND16_QMAX=5), the band oracle at ℓ ∈ {2.5, 3} (SURVEY §8c bars), predict at the
     training inputs against the dense factor, and each problem alone in its call (the same bits)."""
     from tests.test_band16_gpu import _band_oracle_loss_grad
     ells = [2.0, 2.3, 2.5, 2.7, 3.0]
     data = [O.synthetic_series(n, seed=70 + s) for s in range(len(ells))]
     eng = _engine([d[0] for d in data], [d[1] for d in data], K.SquaredExponential())
+    assert eng.band_route == "bcr"
     th = _theta(eng, [(e, 0.9, 1e-5) for e in ells])
     act = list(range(len(ells)))
     cls = eng.band_class(act, th)
     assert int(cls[0]) == 5 and all(6 <= int(c) <= 8 for c in cls[1:]) and int(cls[-1]) == 8, cls
-    for route in ("sweeps", "bcr"):
-        eng.set_band_route(route)
-        eng.reset_timing()
-        lb, gb, ib = eng.lml_grad(act, th)
-        t = eng.last_timing()
-        assert not ib.any() and t.bcr_wide_evals == 4 and t.band_fallbacks == 0 and t.band_fused_launches == 0, \
-            (route, t.bcr_wide_evals, t.band_fallbacks, t.band_fused_launches)
-        if route == "sweeps":
-            first = (lb.copy(), gb.copy())
-        else:  # (the wide chain is the same on both routes: the same bits)
-            for b in range(1, len(ells)):
-                assert lb[b] == first[0][b] and np.array_equal(gb[b, :3], first[1][b, :3]), b
-    eng.set_band_route("sweeps")
+    eng.reset_timing()
+    lb, gb, ib = eng.lml_grad(act, th)
+    t = eng.last_timing()
+    assert not ib.any() and t.bcr_wide_evals == 4 and t.bcr_evals >= 1 and t.band_fallbacks == 0, \
+        (t.bcr_wide_evals, t.bcr_evals, t.band_fallbacks)
+    assert t.band_fused_launches == 0 and t.band16_evals == 0, (t.band_fused_launches, t.band16_evals)
     mb, vb, _ = eng._predict_train(np.arange(len(ells), dtype=np.int32), th, False)
+    for b in act:  # composition: alone in its call, the same bits
+        l1, g1, _ = eng.lml_grad([b], th)
+        assert l1[b] == lb[b] and np.array_equal(g1[b, :3], gb[b, :3]), b
+    with _sweeps():  # the default route's one-wavefront sweeps (Q = 5..8)
+        eng.reset_timing()
+        ls, gs, i_s = eng.lml_grad(act, th)
+        assert not i_s.any() and eng.last_timing().band16_evals == len(ells) and eng.last_timing().bcr_wide_evals == 0
+    _close(lb, gb, ls, gs, 3, "bcr wide vs the Q = 6..8 sweeps")
     with _Dense():
         ld, gd, idn = eng.lml_grad(act, th)
         assert not idn.any()
@@ -258,7 +261,7 @@ def test_bcr_wide_q6_to_q8(n):
     for b in range(len(ells)):
         np.testing.assert_allclose(mb[b].cpu().numpy(), md[b].cpu().numpy(), rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(vb[b].cpu().numpy(), vd[b].cpu().numpy(), rtol=1e-7, atol=1e-13)
-    with _Env("GPX_BAND16_QMAX", "5"):
+    with _sweeps(), _Env("GPX_BAND16_QMAX", "5"):
         eng.reset_timing()
         l64, g64, i64 = eng.lml_grad(act, th)
         assert not i64.any() and eng.last_timing().band_fused_launches > 0
@@ -272,9 +275,6 @@ def test_bcr_wide_q6_to_q8(n):
         lo, go = _band_oracle_loss_grad(*data[b], e, 0.9)
         assert abs(loss - lo) <= 1e-9 * abs(lo), (e, loss, lo)
         assert np.abs(g - go).max() <= 1e-6 * max(1.0, np.abs(go).max()), (e, g, go)
-    for b in act:  # composition: alone in its call (the sweeps route), the same bits
-        l1, g1, _ = eng.lml_grad([b], th)
-        assert l1[b] == first[0][b] and np.array_equal(g1[b, :3], first[1][b, :3]), b
 
 
 def test_bcr_wide_fit_matches_dense_fit():

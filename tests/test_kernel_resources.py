@@ -75,12 +75,10 @@ def test_two_wave_sweeps_fit_256_registers(kernels, q):
 
 
 def test_bench_sweeps_do_not_spill(kernels):
-    """Every sweep a C2 (SE1) evaluation can launch: band16 fwd/bwd for Q = 1..5 with K's tiles
-    computed in the sweeps (the default) or read from the K band, the fused sweeps, the wide
-    (Q = 4/5, deferred) kernel, and the build. (Round 6: the widths 6..8 take the block-cyclic-
-    reduction chain of block size 128, test_c2_reduction_chain_does_not_spill; their band16 sweeps
-    are built for the GPX_WIDE_BCR=0 A/B only.)"""
-    pats = [r"band16_fwd_kernelILi[1-5]ELb[01]E", r"band16_bwd_kernelILi[1-5]ELi1ELb1ELb[01]E",
+    """Every sweep a C2 (SE1) evaluation can launch up to ℓ ≈ 2.4: band16 fwd/bwd for Q = 1..6
+    with K's tiles computed in the sweeps (the default) or read from the K band, the fused sweeps,
+    the wide (Q = 4/5, deferred) kernel, and the build."""
+    pats = [r"band16_fwd_kernelILi[1-6]ELb[01]E", r"band16_bwd_kernelILi[1-6]ELi1ELb1ELb[01]E",
             r"band16_fused_kernelILi[1-5]ELb0ELb0E", r"band16_fused_kernelILi[1-5]ELb1ELb1E",
             r"band16_wide_kernelILb[01]ELb[01]ELi5E", r"band16_build_kernel"]
     for p in pats:
@@ -110,11 +108,11 @@ def test_widest_band16_classes_spill_within_budget(kernels):
     assert not [k for k in kernels if re.search(r"band16_(fwd|bwd)_kernelILi(9|1[0-9])E", k)]
 
 
-def test_c2_reduction_chain_does_not_spill(kernels):
-    """The kernels a C2 evaluation reaches besides the sweeps: the wide
-    classes' reduction chain of block size 128 (bcrw_* and the bs = 128 build / contraction /
-    finish), the per-call reduce, the deferred part's input copy and result gather, and the fused
-    small-problem kernel of the drop-in sizes (Np = 64): no scratch."""
+def test_reduction_chain_and_call_kernels_do_not_spill(kernels):
+    """The wide classes' reduction chain of block size 128 (round 6: bcrw_* and the bs = 128 build /
+    contraction / finish — the latency route's Q = 6..8), the per-call reduce,
+    the deferred part's input copy and result gather, and the fused small-problem kernel of the
+    drop-in sizes (Np = 64): no scratch."""
     pats = [r"bcrw_fwd_factor_kernelILi8E", r"bcrw_fwd_delta_kernelILi8E", r"bcrw_bwd_kernelILi8E",
             r"bcr_build_kernelILi8E", r"bcr_contract_kernelILi8ELi[124]ELb1E", r"bcr_finish_kernel",
             r"reduce_kernel", r"slow_inputs_kernel", r"slow_gather_kernel", r"small64_kernel"]
