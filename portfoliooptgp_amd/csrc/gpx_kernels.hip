@@ -1064,7 +1064,11 @@ __global__ __launch_bounds__(256) void small64_kernel(Small64Args a) {
   if (tid == 0) sfail = -1;
   __syncthreads();
   const double noise = sth[spec.n_params];
-  // K's lower triangle (the identity in the padding); W's block zero
+  // the 16-blocks that hold data: the leaf skips the identity padding past them (a function of the
+  // problem's own n)
+  const int nbv = (n + 15) >> 4;
+  // K's lower triangle (the identity in the padding); W's block zero (its identity padding blocks
+  // past nbv carry their 1s already: the leaf does not visit them)
 #pragma unroll 1
   for (int e = tid; e < 4096; e += 256) {
     const int r = e >> 6, c = e & 63;
@@ -1078,20 +1082,27 @@ __global__ __launch_bounds__(256) void small64_kernel(Small64Args a) {
       }
     }
     sA[r * S + c] = v;
-    sW[r * S + c] = 0.0;
+    sW[r * S + c] = (r == c && r >= 16 * nbv) ? 1.0 : 0.0;
   }
   __syncthreads();
-  leaf64_lds(sA, sW, sld, &sfail);  // (ends with a barrier; log L_ii in sld)
-  // z = W y (wave 0, row per lane), then α = Wᵀ z (column per lane): sequential sums over k
+  switch (nbv) {  // (ends with a barrier; log L_ii in sld)
+    case 1: leaf64_lds<true, LeafNoHook, 1>(sA, sW, sld, &sfail); break;
+    case 2: leaf64_lds<true, LeafNoHook, 2>(sA, sW, sld, &sfail); break;
+    case 3: leaf64_lds<true, LeafNoHook, 3>(sA, sW, sld, &sfail); break;
+    default: leaf64_lds<true, LeafNoHook, 4>(sA, sW, sld, &sfail); break;
+  }
+  // z = W y (wave 0, row per lane), then α = Wᵀ z (column per lane): sequential sums over the
+  // rows that hold data (the padding's y, z and W entries off the diagonal are zeros)
   if (wave == 0) {
     double t = 0.0;
-    for (int k = 0; k <= lane; ++k) t = fma(sW[lane * S + k], sy[k], t);
+    const int kend = lane < n ? lane : -1;
+    for (int k = 0; k <= kend; ++k) t = fma(sW[lane * S + k], sy[k], t);
     sz[lane] = t;
   }
   __syncthreads();
   if (wave == 0) {
     double t = 0.0;
-    for (int i = 63; i >= lane; --i) t = fma(sW[i * S + lane], sz[i], t);
+    for (int i = n - 1; i >= lane; --i) t = fma(sW[i * S + lane], sz[i], t);
     sal[lane] = t;
   }
   // the factor for predict (W's block, z, α, log L_ii)
@@ -1110,7 +1121,7 @@ __global__ __launch_bounds__(256) void small64_kernel(Small64Args a) {
   if (!a.grad) return;
   // K⁻¹ = WᵀW on the lower 16x16 tiles (I >= J), k over rows max(I, J)·16 .. 63 (W is lower):
   // D[m][n] = Σ_k W[k][16I + m] W[k][16J + n]; the 10 tiles dealt over the 4 waves
-  for (int t = wave; t < 10; t += 4) {
+  for (int t = wave; t < nbv * (nbv + 1) / 2; t += 4) {  // (tiles past the data are never read)
     int I = 0;
     while ((I + 1) * (I + 2) / 2 <= t) ++I;
     const int J = t - I * (I + 1) / 2;

@@ -82,7 +82,11 @@ struct LeafNoHook {
 // rot: the hardware wave that plays wave 0 (the serial diagonal chain) is (rot & 3); callers
 // with several workgroups per CU pass a per-workgroup rotation so co-resident workgroups'
 // diagonal chains tend to sit on different SIMDs
-template <bool kLog = true, class PreInverse = LeafNoHook>
+// NB < 4 (the small-problem kernel, gpx_kernels.hip small64_kernel): only the leading NB 16-blocks
+// hold data — the rest of the block is the identity padding, whose factor and inverse are the
+// identity (the caller puts 1s on sW's diagonal there; sA's diagonal holds them already, so their
+// logs come out 0) — and the steps on the padding blocks are skipped. NB = 4 is the full leaf.
+template <bool kLog = true, class PreInverse = LeafNoHook, int NB = 4>
 __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __restrict__ sW,
                                            double* __restrict__ ldiag, int* sfail,
                                            PreInverse pre_inverse = PreInverse(), int rot = 0) {
@@ -156,13 +160,13 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
   // tile's update itself (from the panel tile it just produced) and factors it while waves
   // 1-3 apply the rest of the trailing update, so that update is off the diagonal chain.
   if (wave == 0) diag(0);
-  for (int jb = 0; jb < 4; ++jb) {
+  for (int jb = 0; jb < NB; ++jb) {
     const int c0 = jb * 16;
     __syncthreads();
     LEAF_PH(0);
-    // panel: L_(ib,jb) = A_(ib,jb) · Dᵀ for ib = jb+1 .. 3, one wave per block (wave 0 takes
+    // panel: L_(ib,jb) = A_(ib,jb) · Dᵀ for ib = jb+1 .. NB−1, one wave per block (wave 0 takes
     // ib = jb + 1, the tile its look-ahead needs)
-    const int nblk = 3 - jb;
+    const int nblk = NB - 1 - jb;
     if (wave < nblk) {
       const int r0 = (jb + 1 + wave) * 16;
       d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -181,7 +185,7 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
     // wave 0 with the next diagonal step, the others over waves 1..3
     const int ntr = nblk * (nblk + 1) / 2;
     if (wave == 0) {
-      if (jb < 3) {
+      if (jb < NB - 1) {
         tile_update((jb + 1) * 16, (jb + 1) * 16, c0);
         diag(jb + 1);
       }
@@ -197,10 +201,11 @@ __device__ __forceinline__ void leaf64_lds(double* __restrict__ sA, double* __re
   }
   __syncthreads();
   pre_inverse();
-  // W = L⁻¹: block rows 1..3, blocks j < i in parallel (wave j); the idle wave 3 takes the
+  // W = L⁻¹: block rows 1..NB−1, blocks j < i in parallel (wave j); the idle wave 3 takes the
   // logs of L's diagonal (left on sA's diagonal by the diagonal steps)
-  for (int i = 1; i < 4; ++i) {
-    if (kLog && i == 3 && wave == 3) ldiag[lane] = log(sA[lane * S + lane]);
+  if (kLog && NB == 1 && wave == 3) ldiag[lane] = log(sA[lane * S + lane]);
+  for (int i = 1; i < NB; ++i) {
+    if (kLog && i == NB - 1 && wave == 3) ldiag[lane] = log(sA[lane * S + lane]);
     if (wave < i) {
       const int j = wave;
       d4 t = {0.0, 0.0, 0.0, 0.0};

@@ -235,6 +235,26 @@ class Scipy:
             def callback(xk, *args):
                 step_callback(len(history), variables, [np.asarray(v) for v in xk])
         x0 = _pack(variables)
+        if (step_callback is None and lbfgsb.supports(method, scipy_kwargs) and not _THREADED
+                and os.environ.get("GPX_SOLO_STEPPER", "1") != "0"):
+            # the drop-in pattern (GPR/model_trainer.py:18-19, one model at a time): scipy's own
+            # setulb driven by the C++ loop (lbfgsb.BatchStepper, one slot) instead of
+            # scipy.optimize.minimize's Python loop — the same setulb calls in the same order, so
+            # the same trajectory and OptimizeResult bit for bit (tests/test_stream_driver.py),
+            # at a few µs of host time per evaluation instead of tens
+            opts = scipy_kwargs.get("options") or {}
+            st = (lbfgsb.BatchStepper(1, len(x0), opts).start(0, x0) if lbfgsb.BatchStepper.NATIVE
+                  else lbfgsb.LbfgsbStepper(x0, opts))
+            fg = _guarded(func, as_inf)
+            with _single_thread_blas():
+                while not st.done:
+                    loss, g = fg(st.x)
+                    st.tell(loss, g)
+            res = st.result()
+            _unpack(variables, res.x)
+            if track_loss_history:
+                res.loss_history = history
+            return res
         with _single_thread_blas():
             res = scipy.optimize.minimize(_guarded(func, as_inf), x0, jac=True, method=method,
                                           callback=callback, **scipy_kwargs)

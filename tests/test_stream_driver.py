@@ -645,3 +645,48 @@ def test_admission_one_place_per_pipeline(places, engines):
         assert r.nfev == r0.nfev
         np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
     assert adm.peak == 1 and adm.held == 0
+
+
+class _Var:
+    """A variable the optimizer surface accepts (numpy / assign / shape), holding one vector."""
+
+    def __init__(self, v):
+        self.v = np.array(v, dtype=np.float64)
+        self.shape = self.v.shape
+
+    def numpy(self):
+        return self.v
+
+    def assign(self, x):
+        self.v = np.array(x, dtype=np.float64).reshape(self.shape)
+
+
+def test_solo_minimize_is_scipy(monkeypatch):
+    """Scipy().minimize on one model (the drop-in pattern, GPR/model_trainer.py:18-19) drives scipy's
+    setulb through the native loop (round 6): the OptimizeResult is scipy.optimize.minimize's, atol = 0,
+    with and without the stepper (GPX_SOLO_STEPPER=0), for a converging, a maxiter-limited and a
+    backed-off (infinite loss) run."""
+    import portfoliooptgp_amd as gpx
+
+    def rosen(x):
+        return float(scipy.optimize.rosen(x)), scipy.optimize.rosen_der(x)
+
+    def walled(x):
+        if x[0] > 2.0:
+            return float("inf"), np.zeros_like(x)
+        return float(-x[0] + (x[1] - 1.0) ** 2), np.array([-1.0, 2.0 * (x[1] - 1.0)])
+
+    for fn, x0, opts in ((rosen, [-1.2, 1.0, 0.3], dict(maxiter=100)), (rosen, [0.0] * 5, dict(maxiter=7)),
+                         (walled, [0.0, 0.0], dict(maxiter=100))):
+        ref = scipy.optimize.minimize(fn, np.array(x0), jac=True, method="L-BFGS-B", options=opts)
+        for stepper in ("1", "0"):
+            monkeypatch.setenv("GPX_SOLO_STEPPER", stepper)
+            var = _Var(x0)
+
+            def closure():
+                raise AssertionError("not called: the optimizer uses _gpx_loss_and_grad")
+            closure._gpx_loss_and_grad = lambda variables: fn(variables[0].numpy())
+            res = gpx.optimizers.Scipy().minimize(closure, [var], options=opts)
+            assert res.nfev == ref.nfev and res.nit == ref.nit and res.message == ref.message, (stepper, res, ref)
+            assert res.fun == ref.fun and np.array_equal(res.x, ref.x) and np.array_equal(res.jac, ref.jac)
+            assert np.array_equal(var.numpy(), ref.x)
