@@ -209,6 +209,34 @@ def trace_check(kernel_key):
             "rel_diff_trace_vs_that_rounds_bench_line": k["rel_diff_trace_vs_reference_bench"]}
 
 
+def fp64_profile(families):
+    """The fp64 VALU work beside the MFMAs of each band16 kernel family, from the committed PMC pass
+    (profiles/<round>_fp64_summary.csv, tools/mfma_summary.py via tools/profile_round6.sh: MFMA MOPS
+    and the fp64 VALU instruction counts of one instance's launches): per family, the VALU/MFMA
+    flop ratio and the VALU/MFMA datapath-cycle ratio, weighted over the family's Q instances by
+    MFMA flops. On gfx950 the fp64 MFMA and fp64 VALU share one datapath (profiles/r06_ab.md), so
+    these turn the live MFMA flops into the sweeps' whole fp64 load. None when absent."""
+    import csv
+    import glob
+    root = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(root, "profiles", "*_fp64_summary.csv")))
+    if not files:
+        return None
+    acc = {f: [0.0, 0.0, 0.0] for f in families}  # MFMA TFLOP, VALU TFLOP, VALU-cycles in MFMA-TFLOP units
+    for r in csv.DictReader(open(files[-1])):
+        fam = next((f for f in families if f + "<" in r["Kernel_Name"]), None)
+        if fam is None or not r.get("fp64_datapath_busy_est"):
+            continue
+        m, v = float(r["Issued_fp64_TFLOP"]), float(r["VALU_fp64_TFLOP"])
+        mb, dp = float(r["MFMA_busy_frac"]), float(r["fp64_datapath_busy_est"])
+        acc[fam][0] += m
+        acc[fam][1] += v
+        acc[fam][2] += m * (dp - mb) / mb if mb > 0 else 0.0
+    return {"source": os.path.relpath(files[-1], root),
+            "families": {f: {"valu_over_mfma_flops": a[1] / a[0], "valu_over_mfma_datapath_cycles": a[2] / a[0]}
+                         for f, a in acc.items() if a[0] > 0}}
+
+
 def band_problem_flops(n, p, fwd):
     """2·64³ block-product flops of one problem's fused sweep (gpx_api.hip band_fused_flops)."""
     U = 2.0 * 64 ** 3
@@ -218,6 +246,32 @@ def band_problem_flops(n, p, fwd):
         q = min(p, nb - 1 - k)
         f += (2.0 / 3.0 + q + q * (q + 1) / 2.0) * U if fwd else (1.0 + q + q * q + q) * U
     return f
+
+
+def fp64_datapath(sweeps, elapsed):
+    """The chip's fp64 load in the timed region, MFMA and VALU together: each band16 family's live
+    MFMA flops (ms_total x achieved) scaled by its committed VALU/MFMA ratios (fp64_profile) —
+    fp64 flops/s and the estimated share of the fp64 datapath's cycles (MFMA 64 cycles per
+    16x16x4 tile, a fp64 VALU instruction ~4) over the timed wall. None without the profile."""
+    prof = fp64_profile(("band16_fwd_kernel", "band16_bwd_kernel", "band16_wide_kernel"))
+    if not prof or not prof["families"]:
+        return None
+    fl = cyc = mf = 0.0
+    for fam, r in prof["families"].items():
+        k = sweeps.get(fam)
+        if not k or not k["launches"]:
+            continue
+        m = k["achieved"] * 1e12 * k["ms_total"] * 1e-3  # the family's MFMA flops in the timed region
+        mf += m
+        fl += m * (1.0 + r["valu_over_mfma_flops"])
+        cyc += m * (1.0 + r["valu_over_mfma_datapath_cycles"])
+    return {"mfma_tflops": mf / elapsed / 1e12, "mfma_plus_valu_tflops": fl / elapsed / 1e12,
+            "datapath_busy_est": cyc / elapsed / 1e12 / FP64_PEAK_TFLOPS, "peak": FP64_PEAK_TFLOPS,
+            "ratios": prof["families"], "source": prof["source"],
+            "note": "gfx950's fp64 MFMA and fp64 VALU share one datapath (profiles/r06_ab.md, "
+                    "tools/micro/mfma_valu_overlap.hip); the band16 sweeps' exps and 16x16 leaf chains are fp64 "
+                    "VALU work the MFMA-only frac leaves out; datapath_busy_est = (MFMA cycles + fp64 VALU "
+                    "cycles) / (1024 SIMDs x clock x wall), by the committed per-family cycle ratios"}
 
 
 def contract_traffic(n, flops_per_launch):
@@ -1135,6 +1189,7 @@ def main():
                 max(("band16_fwd_kernel", "band16_bwd_kernel", "band16_wide_kernel"),
                     key=lambda x: sweeps[x].get("wave_s", 0.0))) if b16 else None,
             "chip_achieved": chip_ach, "chip_frac": chip_ach / FP64_PEAK_TFLOPS,
+            "fp64_datapath": fp64_datapath(sweeps, elapsed) if b16 else None,
             "note": ("banded path (DESIGN.md §3c/§3d): the roofline kernel is the one with the most device time; "
                      "by_wave_time names the one holding the most wave-slot time (problems x launch ms), which bounds "
                      "the throughput; achieved = the MFMA flops a launch's problems issue (band16: "

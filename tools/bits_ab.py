@@ -30,8 +30,11 @@ def run(lib, n):
     env = dict(os.environ, REPO=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), BITS_N=str(n))
     if lib:
         env["GPX_LIB"] = lib
-    out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, check=True).stdout
-    return json.loads(out.strip().splitlines()[-1])
+    p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True)
+    if p.returncode != 0:
+        sys.stderr.write(p.stderr[-4000:])
+        raise SystemExit(f"child failed ({lib or 'in-tree'}, n={n})")
+    return json.loads(p.stdout.strip().splitlines()[-1])
 
 
 for n in (4096, 4001):  # (a whole number of 16-row blocks, and a ragged last block)
