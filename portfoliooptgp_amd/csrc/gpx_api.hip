@@ -193,14 +193,19 @@ void reduce(const Run& r) {
 }
 
 
-// Np = 64 batches: every dense evaluation is one fused launch (small64_kernel; GPX_SMALL64=0:
-// the six-launch chain, for A/B). Which path runs depends on Np only, never on the call.
+// Np = 64 and Np = 128 batches: every dense evaluation is one fused launch (small64_kernel,
+// small128_kernel; GPX_SMALL64=0 / GPX_SMALL128=0: the six-launch chain, for A/B). Which path runs
+// depends on Np only, never on the call.
 bool small64_on(const gpx_batch* bt) {
-  static const bool on = [] {
+  static const bool on64 = [] {
     const char* e = getenv("GPX_SMALL64");
     return !(e && atoi(e) == 0);
   }();
-  return on && bt->Np == kLeaf;
+  static const bool on128 = [] {
+    const char* e = getenv("GPX_SMALL128");
+    return !(e && atoi(e) == 0);
+  }();
+  return (on64 && bt->Np == kLeaf) || (on128 && bt->Np == 2 * kLeaf);
 }
 
 // the fused small-problem evaluation (grad: the gradient and logML too) for the problems of r;
@@ -222,7 +227,10 @@ void small64_eval(const Run& r, bool grad, char* sio = nullptr) {
   }
   int max_terms = 1;
   for (int b = 0; b < bt->B; ++b) max_terms = std::max(max_terms, (int)bt->specs[b].n_terms);
-  launch_small64(a, max_terms, r.na, r.s);
+  if (bt->Np == kLeaf)
+    launch_small64(a, max_terms, r.na, r.s);
+  else
+    launch_small128(a, max_terms, r.na, r.s);
 }
 
 // ---------------------------------------------------------------------------------------

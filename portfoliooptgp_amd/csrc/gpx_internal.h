@@ -107,7 +107,7 @@ struct ReduceArgs {
   int Np;
 };
 
-// ---- small problems (Np = 64): one fused launch per evaluation (small64_kernel) ----------
+// ---- small problems (Np = 64 / 128): one fused launch per evaluation (small64_kernel, small128_kernel)
 struct Small64Args {
   const int* active;
   const DevSpec* specs; const double* theta; const int* nvalid;
@@ -120,6 +120,7 @@ struct Small64Args {
   int grad;                                   // 0: factor, z, α only (predict's re-factorisation)
 };
 void launch_small64(const Small64Args& a, int max_terms, int n_active, hipStream_t s);
+void launch_small128(const Small64Args& a, int max_terms, int n_active, hipStream_t s);  // Np = 128
 
 struct PredVarArgs {
   const int* active;

@@ -225,35 +225,16 @@ constexpr int L8 = 8, LBS = 16 * 17;   // blocks per side, block stride (doubles
 __device__ __forceinline__ int lblk(int bi, int bj) { return (bi * (bi + 1) / 2 + bj) * LBS; }
 }  // namespace
 
-__global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
-  __shared__ __attribute__((aligned(16))) double sS[36 * LBS];
-  __shared__ int sfail;
-  const int b = a.active[blockIdx.x];
-  const double* K = a.K + (long long)b * a.sMat;
-  double* W = a.W + (long long)b * a.sMat;
-  const int ld = a.ld, off = a.off, tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+// The 128x128 Cholesky-and-inverse on the packed lower-block LDS array sS (A in; W = L⁻¹ out, in
+// place): the first nbv 16-row blocks only (the ones that hold data; blocks past them must hold
+// the identity on the diagonal and zeros elsewhere, which are their own W). log L_ii of those
+// rows to ldg[], the first failing pivot to *sfail (which must start at −1). 256 or 512 threads; ends
+// with a barrier. leaf128_kernel (nbv = 8) and small128_kernel.
+__device__ __forceinline__ void leaf128_lds(double* __restrict__ sS, double* __restrict__ ldg, int* sfail, int nbv) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;  // (4 or 8 waves)
   const int l15 = lane & 15, l4 = lane >> 4;
-  // lower 128x128 of A (row pieces of 128 B, coalesced); blocks above the diagonal not stored
-  // 8 independent loads in flight per thread (a load-then-store loop serialises on latency)
-#pragma unroll 1
-  for (int e0 = tid; e0 < 128 * 128; e0 += 256 * 8) {
-    double v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = e0 + 256 * u, r = e >> 7, c = e & 127;
-      v[u] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = e0 + 256 * u, r = e >> 7, c = e & 127;
-      if (c <= (r | 15)) sS[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] = v[u];
-    }
-  }
-  if (tid == 0) sfail = -1;
-  __syncthreads();
-
-  for (int jb = 0; jb < L8; ++jb) {
+  for (int jb = 0; jb < nbv; ++jb) {
     const int dj = lblk(jb, jb);
     if (wave == 0) {
       double r[16];
@@ -288,14 +269,14 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
       if (lane < 16) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sS[dj + i * 17 + lane] = w[i];
-        a.ldiag[(long long)b * a.sVec + off + jb * 16 + lane] = log(r[lane & 15]);
+        ldg[jb * 16 + lane] = log(r[lane & 15]);
       }
-      if (lane == 0 && fail >= 0 && sfail < 0) sfail = jb * 16 + fail;
+      if (lane == 0 && fail >= 0 && *sfail < 0) *sfail = jb * 16 + fail;
     }
     __syncthreads();
     // panel: L_(ib,jb) = A_(ib,jb) · D_jbᵀ, in place
-    const int nblk = L8 - 1 - jb;
-    for (int t = wave; t < nblk; t += 4) {
+    const int nblk = nbv - 1 - jb;
+    for (int t = wave; t < nblk; t += nw) {
       const int pb = lblk(jb + 1 + t, jb);
       d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -311,7 +292,7 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
     __syncthreads();
     // trailing update of the lower blocks (ib, kb), jb < kb <= ib
     const int ntr = nblk * (nblk + 1) / 2;
-    for (int t = wave; t < ntr; t += 4) {
+    for (int t = wave; t < ntr; t += nw) {
       int p = 0;
       while ((p + 1) * (p + 2) / 2 <= t) ++p;
       const int q = t - p * (p + 1) / 2;
@@ -331,13 +312,13 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
     }
     __syncthreads();
   }
-  // W = L⁻¹ block rows 1..7; blocks j < i of a row (j = wave, wave + 4) in registers first
-  for (int i = 1; i < L8; ++i) {
+  // W = L⁻¹ block rows 1..7; blocks j < i of a row (j = wave, wave + nw) in registers first
+  for (int i = 1; i < nbv; ++i) {
     d4 wv[2];
     const int di = lblk(i, i);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int j = wave + 4 * h;
+      const int j = wave + nw * h;
       wv[h] = (d4){0.0, 0.0, 0.0, 0.0};
       if (j < i) {
         d4 t = {0.0, 0.0, 0.0, 0.0};
@@ -360,7 +341,7 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
     __syncthreads();   // every wave has read row i's L blocks
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int j = wave + 4 * h;
+      const int j = wave + nw * h;
       if (j < i) {
         const int wij = lblk(i, j);
 #pragma unroll
@@ -369,6 +350,35 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
+  __shared__ __attribute__((aligned(16))) double sS[36 * LBS];
+  __shared__ int sfail;
+  const int b = a.active[blockIdx.x];
+  const double* K = a.K + (long long)b * a.sMat;
+  double* W = a.W + (long long)b * a.sMat;
+  const int ld = a.ld, off = a.off, tid = threadIdx.x;
+  // lower 128x128 of A (row pieces of 128 B, coalesced); blocks above the diagonal not stored
+  // 8 independent loads in flight per thread (a load-then-store loop serialises on latency)
+#pragma unroll 1
+  for (int e0 = tid; e0 < 128 * 128; e0 += 256 * 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 256 * u, r = e >> 7, c = e & 127;
+      v[u] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 256 * u, r = e >> 7, c = e & 127;
+      if (c <= (r | 15)) sS[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] = v[u];
+    }
+  }
+  if (tid == 0) sfail = -1;
+  __syncthreads();
+
+  leaf128_lds(sS, a.ldiag + (long long)b * a.sVec + off, &sfail, L8);
   // the whole 128x128 block of W, zeros above the diagonal
   for (int e = tid; e < 128 * 128; e += 256) {
     const int r = e >> 7, c = e & 127;
@@ -1198,6 +1208,209 @@ __global__ __launch_bounds__(256) void small64_kernel(Small64Args a) {
     res[17] = zz;
     res[18] = l;
   }
+}
+
+// Np = 128 (N = 65..128: the reference's daily series, N = 89): the same one-launch evaluation on
+// eight waves (K's entries and the gradient's are the per-element work; the leaf runs on them too),
+// K and then W = L⁻¹ in leaf128's packed lower-block LDS array (78 KiB: a second 128x128 array
+// for K⁻¹ would not fit beside it), so the K⁻¹ = WᵀW tiles stay in registers and are contracted
+// with (ααᵀ − K⁻¹) ∘ ∂K/∂θ where they are formed. Blocks past the data keep their identity
+// padding (leaf128_lds walks the nbv blocks that hold rows < n).
+constexpr int kS128Waves = 8;
+template <int NT>
+__global__ __launch_bounds__(512) void small128_kernel(Small64Args a) {
+  __shared__ __attribute__((aligned(16))) double sS[36 * LBS];  // K, then W = L⁻¹ (packed lower blocks)
+  __shared__ double sx[128 * GPX_MAX_DIM];
+  __shared__ double sxs[128 * GPX_MAX_DIM];  // the stationary terms' inputs over their ℓ (eval_k_pre)
+  __shared__ double sth[GPX_THETA_STRIDE];
+  __shared__ double sy[128], sz[128], sal[128], sld[128];
+  __shared__ double sred[kS128Waves][GPX_MAX_TERMS * 3 + 3];
+  __shared__ int sfail, soff[GPX_MAX_TERMS];
+  const int b = a.active[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int n = a.nvalid[b], D = a.D;
+  const DevSpec spec = a.specs[b];
+  const double* X = a.X + (long long)b * a.sX;
+  for (int e = tid; e < 128 * D; e += 64 * kS128Waves) {
+    const int r = e / D;
+    sx[e] = r < n ? X[(long long)e] : 0.0;
+  }
+  if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
+  if (tid < 128) {
+    sy[tid] = tid < n ? a.Y[(long long)b * a.sY + tid] : 0.0;
+    sld[tid] = 0.0;  // (log 1 for the padding rows the leaf does not visit)
+  }
+  if (tid == 0) {
+    sfail = -1;
+    // where each stationary term's scaled rows go (while they fit: GPX_MAX_DIM doubles per row)
+    int o = 0;
+    for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+      const int dn = t < spec.n_terms ? spec.terms[t].dim_count : 0;
+      const bool pre = t < spec.n_terms && term_prescaled(spec.terms[t].kind) && o + dn <= GPX_MAX_DIM;
+      soff[t] = pre ? 128 * o : -1;
+      o += pre ? dn : 0;
+    }
+  }
+  __syncthreads();
+  // a = x/ℓ of each pre-scaled term, once per row (the quotient its sqdist forms per pair; the
+  // one- and two-term instances only: the pointers cost the 3-4-term one registers past 256)
+  if constexpr (NT <= 2)
+  for (int t = 0; t < spec.n_terms; ++t) {
+    if (soff[t] < 0) continue;
+    const gpx_term& tm = spec.terms[t];
+    const double ell = sth[tm.param_offset + (tm.kind == GPX_RQ ? 1 : 0)];
+    for (int e = tid; e < 128 * tm.dim_count; e += 64 * kS128Waves) {
+      const int r = e / tm.dim_count, dd = e - r * tm.dim_count;
+      sxs[soff[t] + e] = sx[r * D + tm.dim_start + dd] / ell;
+    }
+  }
+  __syncthreads();
+  const double noise = sth[spec.n_params];
+  const int nbv = (n + 15) >> 4;
+  // K's lower blocks (the diagonal blocks whole: zeros above their diagonal), the identity in the
+  // padding — which is also W there
+#pragma unroll 1
+  for (int e = tid; e < 128 * 128; e += 64 * kS128Waves) {
+    const int r = e >> 7, c = e & 127;
+    if (c > (r | 15)) continue;
+    double v = 0.0;
+    if (c <= r) {
+      if (r < n) {
+        if constexpr (NT <= 2)
+          v = eval_k_pre(spec, sth, sx + r * D, sx + c * D, sxs, soff, r, c);
+        else
+          v = eval_k(spec, sth, sx + r * D, sx + c * D);
+        if (r == c) v += noise;
+      } else {
+        v = (r == c) ? 1.0 : 0.0;
+      }
+    }
+    sS[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] = v;
+  }
+  __syncthreads();
+  leaf128_lds(sS, sld, &sfail, nbv);
+  auto wat = [&](int i, int k) { return sS[lblk(i >> 4, k >> 4) + (i & 15) * 17 + (k & 15)]; };  // W[i][k], k <= i
+  // z = W y (row per thread), then α = Wᵀ z (column per thread), over the rows that hold data
+  if (tid < 128) {
+    double t = 0.0;
+    const int kend = tid < n ? tid : -1;
+    for (int k = 0; k <= kend; ++k) t = fma(wat(tid, k), sy[k], t);
+    sz[tid] = t;
+  }
+  __syncthreads();
+  if (tid < 128) {
+    double t = 0.0;
+    for (int i = n - 1; i >= tid; --i) t = fma(wat(i, tid), sz[i], t);
+    sal[tid] = t;
+  }
+  // the factor for predict (W's block, zeros above the diagonal; z, α, log L_ii)
+  double* W = a.W + (long long)b * a.sMat;
+  for (int e = tid; e < 128 * 128; e += 64 * kS128Waves) {
+    const int r = e >> 7, c = e & 127;
+    W[(long long)r * a.ld + c] = (c <= r) ? wat(r, c) : 0.0;
+  }
+  __syncthreads();
+  if (tid < 128) {
+    a.z[(long long)b * a.sVec + tid] = sz[tid];
+    a.alpha[(long long)b * a.sVec + tid] = sal[tid];
+    a.ldiag[(long long)b * a.sVec + tid] = sld[tid];
+  }
+  if (tid == 0 && sfail >= 0 && a.info[b] == 0) a.info[b] = sfail + 1;
+  if (!a.grad) return;
+  // K⁻¹ = WᵀW on the lower 16x16 tiles (I >= J) of the data blocks, k over rows 16I .. 16nbv − 1
+  // (W is lower; the padding rows add exact zeros): acc[q] = K⁻¹[16I + l4 + 4q][16J + l15], then
+  // ½ Σ (α_i α_j − K⁻¹_ij) ∂K_ij/∂θ over the tile's lower-triangle entries (weight 2 off the diagonal)
+  double sums[NT][3];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
+  double snoise = 0.0, szz = 0.0, sl = 0.0;
+  for (int t = wave; t < nbv * (nbv + 1) / 2; t += kS128Waves) {
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int kb = I; kb < nbv; ++kb) {
+      const int oi = lblk(kb, I), oj = lblk(kb, J);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const double av = sS[oi + (4 * kk + l4) * 17 + l15];
+        const double bv = sS[oj + (4 * kk + l4) * 17 + l15];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 16 * I + l4 + 4 * q, j = 16 * J + l15;
+      if (j > i || i >= n) continue;
+      const double w = (i == j) ? 1.0 : 2.0;
+      const double v = w * fma(sal[i], sal[j], -acc[q]);
+      double dk[NT][3];
+      if constexpr (NT <= 2)
+        eval_k_grad_pre<NT>(spec, sth, sx + i * D, sx + j * D, sxs, soff, i, j, dk);
+      else
+        eval_k_grad<NT>(spec, sth, sx + i * D, sx + j * D, dk);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        sums[u][0] = fma(v, dk[u][0], sums[u][0]);
+        sums[u][1] = fma(v, dk[u][1], sums[u][1]);
+        sums[u][2] = fma(v, dk[u][2], sums[u][2]);
+      }
+      if (i == j) snoise += v;
+    }
+  }
+  if (tid < 128) {
+    szz = sz[tid] * sz[tid];
+    sl = sld[tid];
+  }
+  // fixed-order reduction: wave sums, then the waves in turn
+  constexpr int NV = GPX_MAX_TERMS * 3 + 3;
+  double vals[NV];
+#pragma unroll
+  for (int t = 0; t < GPX_MAX_TERMS; ++t)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) vals[t * 3 + q] = t < NT ? wave_sum(sums[t][q]) : 0.0;
+  vals[NV - 3] = wave_sum(snoise);
+  vals[NV - 2] = wave_sum(szz);
+  vals[NV - 1] = wave_sum(sl);
+  if (lane == 0) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) sred[wave][v] = vals[v];
+  }
+  __syncthreads();
+  double* res = a.results + (long long)b * kResStride;
+  if (tid < GPX_THETA_STRIDE) {
+    int slot = -1;
+    if (tid == spec.n_params) {
+      slot = NV - 3;
+    } else {
+      const DevSpec* gs = a.specs + b;
+      for (int t = 0; t < gs->n_terms; ++t) {
+        const int o = gs->terms[t].param_offset, kind = gs->terms[t].kind;
+        const int np = (kind == GPX_RQ || kind == GPX_PERIODIC_SE) ? 3 : (kind == GPX_LINEAR ? 1 : 2);
+        if (tid >= o && tid < o + np) slot = t * 3 + (tid - o);
+      }
+    }
+    double sv = 0.0;
+    if (slot >= 0)
+      for (int w = 0; w < kS128Waves; ++w) sv += sred[w][slot];
+    res[1 + tid] = 0.5 * sv;
+  }
+  if (tid == 0) {
+    double zz = 0.0, l = 0.0;
+    for (int w = 0; w < kS128Waves; ++w) {
+      zz += sred[w][NV - 2];
+      l += sred[w][NV - 1];
+    }
+    res[0] = -0.5 * zz - l - 0.5 * (double)n * 1.8378770664093453;  // log(2π)
+    res[17] = zz;
+    res[18] = l;
+  }
+}
+
+void launch_small128(const Small64Args& a, int max_terms, int n_active, hipStream_t s) {
+  auto k = max_terms <= 1 ? small128_kernel<1> : (max_terms == 2 ? small128_kernel<2> : small128_kernel<GPX_MAX_TERMS>);
+  hipLaunchKernelGGL(k, dim3(n_active), dim3(64 * kS128Waves), 0, s, a);
 }
 
 void launch_small64(const Small64Args& a, int max_terms, int n_active, hipStream_t s) {

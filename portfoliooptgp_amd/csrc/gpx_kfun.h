@@ -69,10 +69,14 @@ __device__ __forceinline__ double sqdist_gpflow(const double* __restrict__ xi, c
 }
 
 // Value and derivatives (w.r.t. the term's own params, GPflow order) of one term.
+// (ai, aj: the term's inputs already divided by its ℓ — the quotients sqdist_gpflow forms per
+// pair, formed once per row by the caller — or null)
 template <bool GRAD>
 __device__ __forceinline__ double eval_term(const gpx_term& t, const double* __restrict__ th,
                                             const double* __restrict__ xi,
-                                            const double* __restrict__ xj, double* dk) {
+                                            const double* __restrict__ xj, double* dk,
+                                            const double* __restrict__ ai = nullptr,
+                                            const double* __restrict__ aj = nullptr) {
   const int d0 = t.dim_start, dn = t.dim_count;
   switch (t.kind) {
     case GPX_LINEAR: {
@@ -113,7 +117,7 @@ __device__ __forceinline__ double eval_term(const gpx_term& t, const double* __r
   const bool rq = (t.kind == GPX_RQ);
   const double ell = rq ? th[1] : th[0];
   const double var = rq ? th[2] : th[1];
-  const double r2 = sqdist_gpflow(xi + d0, xj + d0, dn, ell);
+  const double r2 = ai ? sqdist_scaled(ai, aj, dn) : sqdist_gpflow(xi + d0, xj + d0, dn, ell);
   switch (t.kind) {
     case GPX_SE: {
       const double g = exp(-0.5 * r2);
@@ -225,6 +229,59 @@ __device__ __forceinline__ double eval_k_grad(const DevSpec& s, const double* __
     vals[t] = 1.0;
     if (t < s.n_terms) {
       vals[t] = eval_term<true>(s.terms[t], th + s.terms[t].param_offset, xi, xj, dk[t]);
+      if (prod) acc *= vals[t]; else acc += vals[t];
+    }
+  }
+  if (prod) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      double others = 1.0;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) if (u != t) others *= vals[u];
+      dk[t][0] *= others; dk[t][1] *= others; dk[t][2] *= others;
+    }
+  }
+  return acc;
+}
+
+// eval_k / eval_k_grad with pre-scaled inputs: term t's rows at sxs + soff[t] (row-major, the
+// term's dim_count values per row; soff[t] < 0: that term reads X as usual). The same
+// operations as eval_k / eval_k_grad, so the same bits, without two divisions per entry.
+__device__ __forceinline__ bool term_prescaled(int kind) {
+  return kind != GPX_LINEAR && kind != GPX_PERIODIC_SE;
+}
+__device__ __forceinline__ double eval_k_pre(const DevSpec& s, const double* __restrict__ th,
+                                             const double* __restrict__ xi, const double* __restrict__ xj,
+                                             const double* __restrict__ sxs, const int* __restrict__ soff,
+                                             int i, int j) {
+  const bool prod = (s.combine == GPX_PRODUCT && s.n_terms > 1);
+  double acc = prod ? 1.0 : 0.0;
+#pragma unroll
+  for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+    if (t >= s.n_terms) break;
+    const int o = soff[t], dn = s.terms[t].dim_count;
+    const double v = eval_term<false>(s.terms[t], th + s.terms[t].param_offset, xi, xj, nullptr,
+                                      o >= 0 ? sxs + o + i * dn : nullptr, o >= 0 ? sxs + o + j * dn : nullptr);
+    if (prod) acc *= v; else acc += v;
+  }
+  return acc;
+}
+template <int NT = GPX_MAX_TERMS>
+__device__ __forceinline__ double eval_k_grad_pre(const DevSpec& s, const double* __restrict__ th,
+                                                  const double* __restrict__ xi, const double* __restrict__ xj,
+                                                  const double* __restrict__ sxs, const int* __restrict__ soff,
+                                                  int i, int j, double (&dk)[NT][3]) {
+  const bool prod = (NT > 1 && s.combine == GPX_PRODUCT && s.n_terms > 1);
+  double vals[NT];
+  double acc = prod ? 1.0 : 0.0;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    dk[t][0] = dk[t][1] = dk[t][2] = 0.0;
+    vals[t] = 1.0;
+    if (t < s.n_terms) {
+      const int o = soff[t], dn = s.terms[t].dim_count;
+      vals[t] = eval_term<true>(s.terms[t], th + s.terms[t].param_offset, xi, xj, dk[t],
+                                o >= 0 ? sxs + o + i * dn : nullptr, o >= 0 ? sxs + o + j * dn : nullptr);
       if (prod) acc *= vals[t]; else acc += vals[t];
     }
   }

@@ -115,7 +115,7 @@ def test_reduction_chain_and_call_kernels_do_not_spill(kernels):
     drop-in sizes (Np = 64): no scratch."""
     pats = [r"bcrw_fwd_factor_kernelILi8E", r"bcrw_fwd_delta_kernelILi8E", r"bcrw_bwd_kernelILi8E",
             r"bcr_build_kernelILi8E", r"bcr_contract_kernelILi8ELi[124]ELb1E", r"bcr_finish_kernel",
-            r"reduce_kernel", r"slow_inputs_kernel", r"slow_gather_kernel", r"small64_kernel"]
+            r"reduce_kernel", r"slow_inputs_kernel", r"slow_gather_kernel", r"small64_kernel", r"small128_kernel", r"leaf128_kernel"]
     for p in pats:
         for name, (v, a, scratch) in _find(kernels, p).items():
             assert scratch == 0, (name, v, a, scratch)
