@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -211,7 +212,7 @@ bool small64_on(const gpx_batch* bt) {
 // the fused small-problem evaluation (grad: the gradient and logML too) for the problems of r;
 // sio: the call's I/O block in coherent pinned memory (active list, θ, info, results read and
 // written there by the kernel), else the device I/O block
-void small64_eval(const Run& r, bool grad, char* sio = nullptr) {
+void small64_eval(const Run& r, bool grad, char* sio = nullptr, int tag = 0) {
   gpx_batch* bt = r.bt;
   Small64Args a{};
   a.active = r.d_act; a.specs = bt->d_specs; a.theta = bt->d_theta; a.nvalid = bt->d_n;
@@ -224,6 +225,10 @@ void small64_eval(const Run& r, bool grad, char* sio = nullptr) {
     a.info = reinterpret_cast<int*>(sio + bt->io_info_off);
     a.theta = reinterpret_cast<const double*>(sio + bt->io_theta_off);
     a.results = reinterpret_cast<double*>(sio + bt->io_res_off);
+    if (tag > 0) {
+      a.done = reinterpret_cast<int*>(sio + bt->io_flag_off);
+      a.tag = tag;
+    }
   }
   int max_terms = 1;
   for (int b = 0; b < bt->B; ++b) max_terms = std::max(max_terms, (int)bt->specs[b].n_terms);
@@ -1274,7 +1279,8 @@ static int batch_create(gpx_ctx* ctx, int B, int N_max, int D, const double* X, 
     bt->io_bandp_off = 2 * ints;
     bt->io_theta_off = 3 * ints;
     bt->io_res_off = bt->io_theta_off + (size_t)B * GPX_THETA_STRIDE * sizeof(double);
-    bt->io_bytes = bt->io_res_off + (size_t)B * kResStride * sizeof(double);
+    bt->io_flag_off = bt->io_res_off + (size_t)B * kResStride * sizeof(double);
+    bt->io_bytes = bt->io_flag_off + ints;
     if (hipMalloc(&bt->d_io, bt->io_bytes) != hipSuccess ||
         hipHostMalloc(&bt->h_io, bt->io_bytes, hipHostMallocNonCoherent) != hipSuccess)
       return cleanup("out of memory for the batch I/O block");
@@ -2106,8 +2112,19 @@ int gpx_batch_lml_grad_submit(gpx_batch* bt, int n_active, const int32_t* active
     pd->total.reset(new PhaseTimer(ctx->profiling != 0, s));
     pd->ct.reset(new PhaseTimer(false, s));
     pd->bp.reset(new PhaseTimer(false, s));
+    // completion by polling the workgroups' flags (GPX_SMALL_POLL, default on; not when profiling,
+    // whose events complete reads): a launch + synchronise round trip costs ≈ 12 µs, a launch and
+    // a polled flag ≈ 7 (tools/micro/launch_roundtrip.hip)
+    static const bool poll = [] {
+      const char* e = getenv("GPX_SMALL_POLL");
+      return !(e && atoi(e) == 0);
+    }();
+    if (poll && !ctx->profiling) {
+      bt->direct_tag = bt->direct_tag >= (1 << 30) ? 1 : bt->direct_tag + 1;
+      pd->poll_tag = bt->direct_tag;
+    }
     pd->total->mark();
-    small64_eval(Run{bt, reinterpret_cast<const int*>(bt->h_sio), n_active, s}, true, bt->h_sio);
+    small64_eval(Run{bt, reinterpret_cast<const int*>(bt->h_sio), n_active, s}, true, bt->h_sio, pd->poll_tag);
     pd->total->mark();
     HIPX(ctx, hipGetLastError());
     pd->order = std::move(order);
@@ -2339,10 +2356,31 @@ int gpx_batch_lml_grad_complete(gpx_batch* bt, double* lml, double* grad, int32_
   HIPX(ctx, hipSetDevice(ctx->device));
   hipStream_t s = pe->s;
   SubClock sc(bt);
-  if (pe->bulk_done)  // (a slow part follows the call on its stream)
+  if (pe->poll_tag > 0) {
+    // a small-problem call: wait for every workgroup's flag (each is written after its results, a
+    // system-scope fence between); the stream is asked now and then, so a failed launch ends the
+    // wait with its error instead of a spin
+    const volatile int* flags = reinterpret_cast<const volatile int*>(bt->h_sio + bt->io_flag_off);
+    for (int i = 0, spins = 0; i < pe->n_active;) {
+      if (flags[i] == pe->poll_tag) {
+        ++i;
+        continue;
+      }
+      if (++spins % 4096 == 0) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q != hipErrorNotReady && q != hipSuccess) HIPX(ctx, q);
+        if (q == hipSuccess && flags[i] != pe->poll_tag) {  // (finished without its flag: not expected)
+          HIPX(ctx, hipStreamSynchronize(s));
+          break;
+        }
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  } else if (pe->bulk_done) {  // (a slow part follows the call on its stream)
     HIPX(ctx, hipEventSynchronize(pe->bulk_done));
-  else
+  } else {
     HIPX(ctx, hipStreamSynchronize(s));
+  }
   if (pe->direct) {  // (the kernel wrote info and results into the coherent block)
     for (int i = 0; i < pe->n_active; ++i) {
       const int b = pe->order[i];

@@ -132,7 +132,8 @@ struct gpx_batch {
   // the same layout in COHERENT pinned memory, for small-problem calls (Np = 64) whose one kernel
   // reads its active list / θ and writes info / results here directly: no DMA either way
   char* h_sio = nullptr;
-  size_t io_info_off = 0, io_bandp_off = 0, io_theta_off = 0, io_res_off = 0, io_bytes = 0;
+  size_t io_info_off = 0, io_bandp_off = 0, io_theta_off = 0, io_res_off = 0, io_flag_off = 0, io_bytes = 0;
+  int direct_tag = 0;  // the last small-problem call's completion tag (h_sio flags, GPX_SMALL_POLL)
   int* d_bandp = nullptr;     // [B] band width (64-blocks) of the banded problems of the call
   int* h_bandp = nullptr;
   double* h_results = nullptr;  // views into h_io
@@ -375,6 +376,7 @@ struct gpx_batch::PendingEval {
   hipEvent_t fq16[gpx::kBand16MaxQ][4] = {};
   int n_bcr = 0;                      // problems of the call on the block-cyclic-reduction path (bcr_ev timed)
   bool direct = false;                // small-problem call with its I/O in h_sio (no DMA): copied to h_io at _complete
+  int poll_tag = 0;                   // > 0: its workgroups write this tag to h_sio's flags when done (polled)
   ~PendingEval() {
     for (auto x : kev)
       if (x) (void)hipEventDestroy(x);

@@ -118,6 +118,7 @@ struct Small64Args {
   int* info;
   double* results;                            // [B][kResStride]
   int grad;                                   // 0: factor, z, α only (predict's re-factorisation)
+  int* done; int tag;                         // done != null: workgroup i writes tag to done[i] last
 };
 void launch_small64(const Small64Args& a, int max_terms, int n_active, hipStream_t s);
 void launch_small128(const Small64Args& a, int max_terms, int n_active, hipStream_t s);  // Np = 128

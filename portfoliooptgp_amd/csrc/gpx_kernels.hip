@@ -1049,6 +1049,16 @@ void launch_reduce(const ReduceArgs& a, int n_active, hipStream_t s) {
 // data and Np only (the route is taken for every Np = 64 problem, whatever the call holds).
 // grad = 0 (predict's re-factorisation): the factor, z and α only.
 // ======================================================================================
+// the last act of a small-problem workgroup whose caller polls (GPX_SMALL_POLL): every thread's
+// writes to the coherent host block made visible system-wide, then one vector store of the call's
+// tag — the host reads the results once all of the call's flags carry it, with no synchronise
+__device__ __forceinline__ void small_done(const Small64Args& a) {
+  if (!a.done) return;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) *reinterpret_cast<volatile int*>(a.done + blockIdx.x) = a.tag;
+}
+
 template <int NT>
 __global__ __launch_bounds__(256) void small64_kernel(Small64Args a) {
   constexpr int S = kLeafS;
@@ -1208,6 +1218,7 @@ __global__ __launch_bounds__(256) void small64_kernel(Small64Args a) {
     res[17] = zz;
     res[18] = l;
   }
+  small_done(a);
 }
 
 // Np = 128 (N = 65..128: the reference's daily series, N = 89): the same one-launch evaluation on
@@ -1406,6 +1417,7 @@ __global__ __launch_bounds__(512) void small128_kernel(Small64Args a) {
     res[17] = zz;
     res[18] = l;
   }
+  small_done(a);
 }
 
 void launch_small128(const Small64Args& a, int max_terms, int n_active, hipStream_t s) {
