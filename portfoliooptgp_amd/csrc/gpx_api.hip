@@ -1847,6 +1847,11 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
                                   (ctx->profiling && fused64) ? rec->fq : nullptr, ctx->profiling ? rec->fq16 : nullptr);
     if (e != GPX_OK) return e;
   }
+  static const int slow_delay = [] {
+    const char* e = getenv("GPX_SLOW_DELAY_US");
+    return e ? atoi(e) : 0;
+  }();
+  if (slow_delay > 0) launch_spin_us(slow_delay, ss);
   launch_slow_gather(r.d_act, n, bt->results, kResStride, bt->d_slow_res, own ? bt->d_slow_info : bt->d_info,
                      bt->d_slow_info_c, ss);
   HIPX(ctx, hipMemcpyAsync(rec->h_res, bt->d_slow_res, sizeof(double) * n * kResStride, hipMemcpyDeviceToHost, ss));

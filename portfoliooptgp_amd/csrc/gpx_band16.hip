@@ -1041,6 +1041,15 @@ void launch_slow_gather(const int* act, int n, const double* res, int stride, do
                      info, info_out);
 }
 
+// diagnostic (GPX_SLOW_DELAY_US): a one-wave kernel that spins for us microseconds on the device's
+// 100 MHz clock — lengthens a deferred part by a known amount to measure how the line depends on it
+__global__ __launch_bounds__(64) void spin_us_kernel(int us) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * (unsigned long long)us) {
+  }
+}
+void launch_spin_us(int us, hipStream_t s) { hipLaunchKernelGGL(spin_us_kernel, dim3(1), dim3(64), 0, s, us); }
+
 // a one-wave kernel that appends a stream-order marker {t, t, kind} to the wave trace: where a
 // call's device work stands when the stream reaches it (kinds >= 32, gpx_api.hip trace_mark)
 __global__ __launch_bounds__(64) void wave_marker_kernel(BandFusedArgs a, int kind) {

@@ -217,6 +217,7 @@ void launch_band16_wide(const BandFusedArgs& a, int kin, int n_active, hipStream
 void launch_slow_inputs(const int* act, int n, int* act_out, const double* theta, double* theta_out, const int* bandp,
                         int* bandp_out, int* info_out, int B, hipStream_t s,
                         int r0 = 0, int r1 = 0);
+void launch_spin_us(int us, hipStream_t s);  // diagnostic delay (GPX_SLOW_DELAY_US)
 void launch_slow_gather(const int* act, int n, const double* res, int stride, double* out, const int* info,
                         int* info_out, hipStream_t s);
 void launch_band16(const BandFusedArgs& a, int Q, int max_terms, bool se1, int kin, int n_active, hipStream_t s,

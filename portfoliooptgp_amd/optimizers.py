@@ -795,6 +795,17 @@ class _SteppedDriver:
                      and all(hasattr(e, "band_width") or hasattr(e, "band_class") for e, _, _, _ in self.groups))
         self.moves = 0
         self._narrow_q = int(os.environ.get("GPX_NARROW_Q", "3"))
+        # GPX_HOLD_WIDE="Q:H" (or Q/H; default 6:3, 0 = off): on a batch with deferred completion,
+        # a fit whose next point takes the band16 sweeps Q or more 16-blocks wide is submitted only
+        # every H-th round of its batch (held, its point unchanged, in the others), so those rare,
+        # long sweeps (one per SIMD, 7-8 ms) lengthen the deferred part's wide launch in one round
+        # of H instead of in most rounds — the deferred parts follow each other on one stream, so
+        # their length is what deferred fits wait (+2 % on the bench, profiles/r06_ab.md).
+        # Scheduling only: each fit's evaluations, and so its trajectory, are the same bits.
+        hq = os.environ.get("GPX_HOLD_WIDE", "6:3").replace("/", ":").split(":")
+        self._hold_q = int(hq[0] or 0)
+        self._hold_every = max(1, int(hq[1])) if len(hq) > 1 else 2
+        self.held = 0
         # the fits' L-BFGS-B loops advanced a round at a time by the C++ loop around scipy's
         # setulb (lbfgsb.BatchStepper; GPX_NATIVE_LBFGSB=0: the Python stepper per fit). Not with
         # wide-group routing, which moves a fit's loop state between batches
@@ -993,8 +1004,33 @@ class _SteppedDriver:
                 gs.packs.append((rs, P, U, R, s0["cols"]))
             if moved or not self.wide or not self._migrate(gs):
                 break
+        if (self._hold_q > 0 and len(gs.act) > 1 and gs.n_calls % self._hold_every
+                and getattr(gs.eng, "deferral", -1) >= 0):
+            self._hold(gs)
         self._tick("theta", t0)
         return bool(gs.act)
+
+    def _hold(self, gs):
+        """GPX_HOLD_WIDE: leave this round's rows of band16 width >= the hold width out of the
+        call (never all of them); their θ rows and requested points stay for the next round."""
+        cls_fn = getattr(gs.eng, "band_class", None)
+        if cls_fn is None:
+            return
+        c = cls_fn(gs.act, gs.theta)
+        hold = (c >= self._hold_q) & (c < 16)
+        if not hold.any() or hold.all():
+            return
+        held = {r for r, h in zip(gs.act, hold) if h}
+        gs.act = [r for r in gs.act if r not in held]
+        packs = []
+        for rs, P, U, R, cols in gs.packs:
+            keep = np.fromiter((r not in held for r in rs), dtype=bool, count=len(rs))
+            if keep.all():
+                packs.append((rs, P, U, R, cols))
+            elif keep.any():
+                packs.append(([r for r, k in zip(rs, keep) if k], P, U[keep], R[keep], cols))
+        gs.packs = packs
+        self.held += len(held)
 
     def _wide_classes(self, gs):
         """Per active row of the group: True (wide), False (narrow) or None (not known yet).

@@ -611,6 +611,36 @@ def test_deferred_rows_keep_trajectories(engines):
     assert sum(e.deferred_total for e in eng) > 0
 
 
+class HoldFakeEngine(DeferringFakeEngine):
+    """DeferringFakeEngine answering the band-class query: band16 width 6 (a wide sweep) above
+    ℓ = 2, 3 below; records each call's classes."""
+
+    def band_class(self, rows, theta):
+        return np.array([6 if theta[r, 0] > 2.0 else 3 for r in rows], dtype=np.int32)
+
+    def lml_grad_submit(self, rows, theta):
+        self.classes = getattr(self, "classes", []) + [self.band_class(list(rows), theta)]
+        super().lml_grad_submit(rows, theta)
+
+
+def test_hold_wide_keeps_trajectories(monkeypatch):
+    """GPX_HOLD_WIDE (default 6:3): on a deferring batch, the rows whose next point is band16
+    width >= 6 are submitted only in every H-th round (never all rows held). The schedule
+    changes — fewer calls carry a wide row — and every fit's trajectory is still the solo one."""
+    ref = [_solo(m) for m in _models(17)]
+    share = {}
+    for hold in ("0", "6:3", "6/2"):
+        monkeypatch.setenv("GPX_HOLD_WIDE", hold)
+        eng = HoldFakeEngine(6)
+        res, _ = gpx.optimizers.Scipy().minimize_stream(_models(17), width=6, engine=eng, predict_train=True)
+        for r, r0 in zip(res, ref):
+            assert r.nfev == r0.nfev
+            np.testing.assert_allclose(r.x, r0.x, rtol=0, atol=0)
+        assert any((c == 6).any() for c in eng.classes)
+        share[hold] = np.mean([(c == 6).any() for c in eng.classes])
+    assert share["6:3"] < share["0"] and share["6/2"] < share["0"], share
+
+
 class _CountingAdmission:
     """DeviceAdmission's interface over a plain semaphore, counting the places held at once; a
     blocking acquire that cannot be served fails the test instead of hanging it."""
