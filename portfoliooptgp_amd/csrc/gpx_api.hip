@@ -670,6 +670,16 @@ int wide_qmax(bool se1) {
 // chain's 8-wave, 150 KB-LDS workgroups wait for an empty CU behind the other processes' sweeps),
 // so the sweeps route keeps its one-wavefront Q = 6..8 sweeps. Either way a problem's path is a
 // function of its own width and the batch's route, never of the call.
+// GPX_SLOW_DIRECT (default 0 until measured): a deferred part's results written by its gather
+// kernel into coherent pinned host buffers instead of two copy-engine downloads
+static bool slow_direct() {
+  static const bool on = [] {
+    const char* e = getenv("GPX_SLOW_DIRECT");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 int wide_bcr_mode() {
   static const int m = [] {
     const char* e = getenv("GPX_WIDE_BCR");
@@ -1747,8 +1757,9 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
   } else {
     rec.reset(new gpx_batch::SlowRec());
     HIPX(ctx, hipEventCreateWithFlags(&rec->done, hipEventDisableTiming));
-    HIPX(ctx, hipHostMalloc(&rec->h_res, sizeof(double) * bt->B * kResStride));
-    HIPX(ctx, hipHostMalloc(&rec->h_info, sizeof(int) * bt->B));
+    const unsigned fl = slow_direct() ? hipHostMallocCoherent : hipHostMallocDefault;
+    HIPX(ctx, hipHostMalloc(&rec->h_res, sizeof(double) * bt->B * kResStride, fl));
+    HIPX(ctx, hipHostMalloc(&rec->h_info, sizeof(int) * bt->B, fl));
   }
   rec->ids.assign(ids, ids + n);
   // The wide launch's waves in reverse order, widest first (GPX_WIDE_REVERSE=0: ascending): its
@@ -1852,10 +1863,18 @@ static int submit_slow(gpx_batch* bt, hipStream_t s, const int32_t* ids, int off
     return e ? atoi(e) : 0;
   }();
   if (slow_delay > 0) launch_spin_us(slow_delay, ss);
-  launch_slow_gather(r.d_act, n, bt->results, kResStride, bt->d_slow_res, own ? bt->d_slow_info : bt->d_info,
-                     bt->d_slow_info_c, ss);
-  HIPX(ctx, hipMemcpyAsync(rec->h_res, bt->d_slow_res, sizeof(double) * n * kResStride, hipMemcpyDeviceToHost, ss));
-  HIPX(ctx, hipMemcpyAsync(rec->h_info, bt->d_slow_info_c, sizeof(int) * n, hipMemcpyDeviceToHost, ss));
+  if (slow_direct()) {
+    // the gather writes the part's result rows straight into the record's coherent pinned
+    // buffers: no copy-engine download on the slow stream, whose deferred parts follow each
+    // other (their length is what deferred fits wait)
+    launch_slow_gather(r.d_act, n, bt->results, kResStride, rec->h_res, own ? bt->d_slow_info : bt->d_info,
+                       rec->h_info, ss);
+  } else {
+    launch_slow_gather(r.d_act, n, bt->results, kResStride, bt->d_slow_res, own ? bt->d_slow_info : bt->d_info,
+                       bt->d_slow_info_c, ss);
+    HIPX(ctx, hipMemcpyAsync(rec->h_res, bt->d_slow_res, sizeof(double) * n * kResStride, hipMemcpyDeviceToHost, ss));
+    HIPX(ctx, hipMemcpyAsync(rec->h_info, bt->d_slow_info_c, sizeof(int) * n, hipMemcpyDeviceToHost, ss));
+  }
   HIPX(ctx, hipEventRecord(rec->done, ss));
   if (!own) {
     // same-stream mode reads the call's active list, θ, widths and info in place: the next

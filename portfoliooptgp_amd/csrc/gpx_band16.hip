@@ -1012,6 +1012,7 @@ __global__ __launch_bounds__(64) void slow_gather_kernel(const int* __restrict__
   const int i = t / stride, c = t - i * stride, b = act[i];
   out[t] = res[(long long)b * stride + c];
   if (c == 0) info_out[i] = info[b];
+  __threadfence_system();  // (out / info_out may be coherent host memory: GPX_SLOW_DIRECT)
 }
 
 __global__ __launch_bounds__(64) void slow_inputs_kernel(const int* __restrict__ act, int n, int* __restrict__ act_out,
