@@ -352,7 +352,11 @@ __device__ __forceinline__ void leaf128_lds(double* __restrict__ sS, double* __r
   }
 }
 
-__global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
+#ifndef GPX_LEAF128_WAVES
+#define GPX_LEAF128_WAVES 8
+#endif
+constexpr int kLeaf128Waves = GPX_LEAF128_WAVES;  // (4: round 5's leaf; the same bits either way)
+__global__ __launch_bounds__(64 * kLeaf128Waves) void leaf128_kernel(LeafArgs a) {
   __shared__ __attribute__((aligned(16))) double sS[36 * LBS];
   __shared__ int sfail;
   const int b = a.active[blockIdx.x];
@@ -362,16 +366,16 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
   // lower 128x128 of A (row pieces of 128 B, coalesced); blocks above the diagonal not stored
   // 8 independent loads in flight per thread (a load-then-store loop serialises on latency)
 #pragma unroll 1
-  for (int e0 = tid; e0 < 128 * 128; e0 += 256 * 8) {
+  for (int e0 = tid; e0 < 128 * 128; e0 += 64 * kLeaf128Waves * 8) {
     double v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int e = e0 + 256 * u, r = e >> 7, c = e & 127;
+      const int e = e0 + 64 * kLeaf128Waves * u, r = e >> 7, c = e & 127;
       v[u] = (c <= r) ? K[(long long)(off + r) * ld + off + c] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int e = e0 + 256 * u, r = e >> 7, c = e & 127;
+      const int e = e0 + 64 * kLeaf128Waves * u, r = e >> 7, c = e & 127;
       if (c <= (r | 15)) sS[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] = v[u];
     }
   }
@@ -380,7 +384,7 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
 
   leaf128_lds(sS, a.ldiag + (long long)b * a.sVec + off, &sfail, L8);
   // the whole 128x128 block of W, zeros above the diagonal
-  for (int e = tid; e < 128 * 128; e += 256) {
+  for (int e = tid; e < 128 * 128; e += 64 * kLeaf128Waves) {
     const int r = e >> 7, c = e & 127;
     const double v = (c <= r) ? sS[lblk(r >> 4, c >> 4) + (r & 15) * 17 + (c & 15)] : 0.0;
     W[(long long)(off + r) * ld + off + c] = v;
@@ -389,7 +393,7 @@ __global__ __launch_bounds__(256) void leaf128_kernel(LeafArgs a) {
 }
 
 void launch_leaf128(const LeafArgs& a, int n_active, hipStream_t s) {
-  hipLaunchKernelGGL(leaf128_kernel, dim3(n_active), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(leaf128_kernel, dim3(n_active), dim3(64 * kLeaf128Waves), 0, s, a);
 }
 
 // ======================================================================================
