@@ -234,46 +234,72 @@ __device__ __forceinline__ void leaf128_lds(double* __restrict__ sS, double* __r
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;  // (4 or 8 waves)
   const int l15 = lane & 15, l4 = lane >> 4;
+  // the diagonal block jb: wave 0 factors it and inverts it in registers -> D_jb over A_jb,jb
+  auto diag = [&](const int jb) __attribute__((always_inline)) {
+    const int dj = lblk(jb, jb);
+    double r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = sS[dj + l15 * 17 + k];
+    int fail = -1;
+    double invd[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const double piv = bc16(r[j], j);
+      if (!(piv > 0.0) && fail < 0) fail = j;
+      const double inv = rsqrt_nr(piv);
+      const double ljj = piv * inv;
+      invd[j] = inv;
+      r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
+#pragma unroll
+      for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], bc16(r[j], k), r[k]);
+    }
+    double w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = (i == l15) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      w[k] *= invd[k];
+      // column k's broadcasts wait for w_k (else all 120 are hoisted: ~240 registers)
+      double rk = r[k];
+      asm volatile("" : "+v"(rk) : "v"(w[k]));
+#pragma unroll
+      for (int i = k + 1; i < 16; ++i) w[i] = fma(-bc16(rk, i), w[k], w[i]);
+    }
+    // D_j over A_jj (this wave read the whole block into registers above)
+    if (lane < 16) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sS[dj + i * 17 + lane] = w[i];
+      ldg[jb * 16 + lane] = log(r[lane & 15]);
+    }
+    if (lane == 0 && fail >= 0 && *sfail < 0) *sfail = jb * 16 + fail;
+  };
+  // trailing tile t of step jb (tiles (jb+1+p, jb+1+q), q <= p, numbered row by row)
+  auto trail = [&](const int jb, const int t) __attribute__((always_inline)) {
+    int p = 0;
+    while ((p + 1) * (p + 2) / 2 <= t) ++p;
+    const int q = t - p * (p + 1) / 2;
+    const int bi = jb + 1 + p, bk = jb + 1 + q;
+    const int ob = lblk(bi, bk), li = lblk(bi, jb), lk = lblk(bk, jb);
+    d4 acc;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = sS[ob + (l4 + 4 * u) * 17 + l15];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const double av = sS[li + l15 * 17 + 4 * kk + l4];
+      const double bv = sS[lk + l15 * 17 + 4 * kk + l4];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 1);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sS[ob + (l4 + 4 * u) * 17 + l15] = acc[u];
+  };
+  // right-looking over the block columns, the next diagonal block factored ahead: in step jb wave 0
+  // updates tile (jb+1, jb+1) first and factors it while the other waves update the rest of the
+  // trailing tiles (each tile's updates in the same order and form as one after another: the
+  // same bits, a barrier per step less on the critical path)
+  if (wave == 0) diag(0);
+  __syncthreads();
   for (int jb = 0; jb < nbv; ++jb) {
     const int dj = lblk(jb, jb);
-    if (wave == 0) {
-      double r[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) r[k] = sS[dj + l15 * 17 + k];
-      int fail = -1;
-      double invd[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const double piv = bc16(r[j], j);
-        if (!(piv > 0.0) && fail < 0) fail = j;
-        const double inv = rsqrt_nr(piv);
-        const double ljj = piv * inv;
-        invd[j] = inv;
-        r[j] = (l15 > j) ? r[j] * inv : ((l15 == j) ? ljj : 0.0);
-#pragma unroll
-        for (int k = j + 1; k < 16; ++k) r[k] = fma(-r[j], bc16(r[j], k), r[k]);
-      }
-      double w[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) w[i] = (i == l15) ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        w[k] *= invd[k];
-        // column k's broadcasts wait for w_k (else all 120 are hoisted: ~240 registers)
-        double rk = r[k];
-        asm volatile("" : "+v"(rk) : "v"(w[k]));
-#pragma unroll
-        for (int i = k + 1; i < 16; ++i) w[i] = fma(-bc16(rk, i), w[k], w[i]);
-      }
-      // D_j over A_jj (this wave read the whole block into registers above)
-      if (lane < 16) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sS[dj + i * 17 + lane] = w[i];
-        ldg[jb * 16 + lane] = log(r[lane & 15]);
-      }
-      if (lane == 0 && fail >= 0 && *sfail < 0) *sfail = jb * 16 + fail;
-    }
-    __syncthreads();
     // panel: L_(ib,jb) = A_(ib,jb) · D_jbᵀ, in place
     const int nblk = nbv - 1 - jb;
     for (int t = wave; t < nblk; t += nw) {
@@ -290,25 +316,14 @@ __device__ __forceinline__ void leaf128_lds(double* __restrict__ sS, double* __r
       for (int q = 0; q < 4; ++q) sS[pb + (l4 + 4 * q) * 17 + l15] = acc[q];
     }
     __syncthreads();
-    // trailing update of the lower blocks (ib, kb), jb < kb <= ib
+    if (nblk == 0) break;
     const int ntr = nblk * (nblk + 1) / 2;
-    for (int t = wave; t < ntr; t += nw) {
-      int p = 0;
-      while ((p + 1) * (p + 2) / 2 <= t) ++p;
-      const int q = t - p * (p + 1) / 2;
-      const int bi = jb + 1 + p, bk = jb + 1 + q;
-      const int ob = lblk(bi, bk), li = lblk(bi, jb), lk = lblk(bk, jb);
-      d4 acc;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = sS[ob + (l4 + 4 * u) * 17 + l15];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const double av = sS[li + l15 * 17 + 4 * kk + l4];
-        const double bv = sS[lk + l15 * 17 + 4 * kk + l4];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 1);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) sS[ob + (l4 + 4 * u) * 17 + l15] = acc[u];
+    if (wave == 0) {
+      trail(jb, 0);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // (its LDS writes before diag's reads)
+      diag(jb + 1);
+    } else {
+      for (int t = wave; t < ntr; t += nw - 1) trail(jb, t);
     }
     __syncthreads();
   }
