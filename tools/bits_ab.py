@@ -1,6 +1,7 @@
 """Bit identity of two library builds on the band16 sweeps (the in-tree libgpx.so and
 GPX_LIB_ALT): logML and gradient of 64 C2 problems at a spread of lengthscales (Q = 1..8), each
-build in its own process. usage: python tools/bits_ab.py (GPU box)"""
+build in its own process, on the sweeps route (BITS_ROUTE=bcr: the block-cyclic-reduction route).
+usage: python tools/bits_ab.py (GPU box)"""
 import json
 import os
 import subprocess
@@ -9,8 +10,8 @@ import sys
 CHILD = r'''
 import os, sys, json, numpy as np
 sys.path.insert(0, os.environ["REPO"])
-os.environ["GPX_BCR_MAX"] = "0"
 import portfoliooptgp_amd as gpx
+gpx.set_default_band_route(os.environ.get("BITS_ROUTE", "sweeps"))
 from portfoliooptgp_amd.engine import Engine
 from portfoliooptgp_amd.kernels import compile_spec
 import bench
