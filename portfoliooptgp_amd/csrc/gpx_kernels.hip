@@ -115,6 +115,40 @@ __global__ __launch_bounds__(256) void build_kernel(BuildArgs a) {
     sxj[e] = fast ? xj / fell : xj;
   }
   if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
+  // the general path: each stationary term's inputs over its ℓ staged once per row (the quotients
+  // sqdist_gpflow forms per pair: the same bits, eval_k_pre), term t's at soff[t] in sxp, the
+  // tile's 64 rows then its 64 columns, while they fit GPX_MAX_DIM doubles per row
+  __shared__ double sxp[128 * GPX_MAX_DIM];
+  __shared__ int soff[GPX_MAX_TERMS];
+  if (!fast) {
+    const DevSpec* gs = a.specs + b;  // (dynamic term index: read from memory, not the register copy)
+    int P = 0;
+    for (int t = 0; t < gs->n_terms; ++t) P += term_prescaled(gs->terms[t].kind) ? gs->terms[t].dim_count : 0;
+    if (P > GPX_MAX_DIM) P = 0;
+    if (tid == 0) {  // (soff[t] < 0: term t reads X as eval_k does)
+      int o = 0;
+      for (int t = 0; t < GPX_MAX_TERMS; ++t) {
+        const bool pre = P > 0 && t < gs->n_terms && term_prescaled(gs->terms[t].kind);
+        soff[t] = pre ? 128 * o : -1;
+        o += pre ? gs->terms[t].dim_count : 0;
+      }
+    }
+    if (P > 0) {
+      for (int t = 0, o = 0; t < gs->n_terms; ++t) {
+        const gpx_term& tm = gs->terms[t];
+        if (!term_prescaled(tm.kind)) continue;
+        const double ell = a.theta[b * GPX_THETA_STRIDE + term_ell_slot(tm)];
+        const int dn = tm.dim_count;
+        for (int e = tid; e < 64 * dn; e += 256) {
+          const int r = e / dn, d = tm.dim_start + (e - r * dn);
+          const int gi = ti * 64 + r, gj = tj * 64 + r;
+          sxp[128 * o + e] = (gi < n ? X[(long long)gi * D + d] : 0.0) / ell;
+          sxp[128 * o + 64 * dn + e] = (gj < ncol ? X2[(long long)gj * D + d] : 0.0) / ell;
+        }
+        o += dn;
+      }
+    }
+  }
   __syncthreads();
   const double noise = sth[spec.n_params];
   double* out = a.out + (long long)b * a.sOut;
@@ -134,15 +168,16 @@ __global__ __launch_bounds__(256) void build_kernel(BuildArgs a) {
     const int r = (tid >> 6) + 4 * q;
     const int gi = ti * 64 + r;
     double v;
+    auto kv = [&]() { return eval_k_pre(spec, sth, sxi + r * D, sxj + c * D, sxp, soff, r, 64 + c); };
     if (a.symmetric) {
       if (gi < n && gj < n) {
-        v = eval_k(spec, sth, sxi + r * D, sxj + c * D);
+        v = kv();
         if (gi == gj) v += noise;
       } else {
         v = (gi == gj) ? 1.0 : 0.0;
       }
     } else {
-      v = (gi < n && gj < ncol) ? eval_k(spec, sth, sxi + r * D, sxj + c * D) : 0.0;
+      v = (gi < n && gj < ncol) ? kv() : 0.0;
     }
     out[(long long)gi * a.ldo + gj] = v;
   }
@@ -627,18 +662,43 @@ void gemm_kernel(GemmArgs a) {
     // The accumulators go through LDS in two halves so that the kernel-derivative code runs
     // as a compact loop (keeping its registers out of the MFMA main loop's budget).
     const int D = a.D;
-    double* sacc = smem;                      // [4 waves][16][WT]
-    double* sxi = sacc + 4 * 16 * WT;         // [BM][D]
-    double* sxj = sxi + BM * D;               // [BN][D]
-    double* sai = sxj + BN * D;               // [BM]
-    double* saj = sai + BM;                   // [BN]
-    double* sth = saj + BN;                   // [16]
-    double* sred = sth + GPX_THETA_STRIDE;    // [4 waves][16]
-    __syncthreads();
     const int n = a.nvalid[b];
     const double* X = a.X + (long long)b * a.sX;
     const double* al = a.vec + (long long)b * a.sVec;
     const DevSpec spec = a.specs[b];
+    // the general (term-interpreter) derivatives of the one- and two-term instances: each
+    // stationary term's inputs divided by its ℓ once per row, as small128 does (the quotients its
+    // sqdist forms per pair: the same bits), while they fit the GPX_MAX_DIM doubles a row has here
+    // (not the fast single-term path below: it stages its inputs pre-scaled already)
+    const bool fast1 = (NT == 1) && spec.n_terms == 1 && spec.terms[0].kind >= GPX_SE &&
+                       spec.terms[0].kind <= GPX_EXPONENTIAL;
+    __shared__ int soff[NT];  // (in LDS: the element loop's registers are at the cap)
+    int P = 0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const bool pre = NT <= 2 && !fast1 && t < spec.n_terms && term_prescaled(spec.terms[t].kind);
+      P += pre ? spec.terms[t].dim_count : 0;
+    }
+    if (D + P > GPX_MAX_DIM) P = 0;
+    if (tid == 0) {
+      int o = 0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const bool pre = P > 0 && !fast1 && t < spec.n_terms && term_prescaled(spec.terms[t].kind);
+        soff[t] = pre ? (BM + BN) * o : -1;
+        o += pre ? spec.terms[t].dim_count : 0;
+      }
+    }
+    double* sacc = smem;                      // [4 waves][16][WT]
+    double* sxi = sacc + 4 * 16 * WT;         // [BM][D]
+    double* sxj = sxi + BM * D;               // [BN][D]
+    // the pre-scaled terms' x/ℓ: term t's at soff[t], [BM + BN][its dims], the tile's rows i0.. then j0..
+    double* sxp = sxj + BN * D;
+    double* sai = sxp + (BM + BN) * P;        // [BM]
+    double* saj = sai + BM;                   // [BN]
+    double* sth = saj + BN;                   // [16]
+    double* sred = sth + GPX_THETA_STRIDE;    // [4 waves][16]
+    __syncthreads();
     // single-term isotropic stationary specs (the SE / Matern / Exponential fits): the inputs
     // are staged pre-scaled by 1/ℓ and ℓ-dependent factors hoisted out of the per-element
     // derivative (no division per element)
@@ -657,6 +717,21 @@ void gemm_kernel(GemmArgs a) {
     }
     if (tid < BM) { sai[tid] = al[i0 + tid]; saj[tid] = al[j0 + tid]; }
     if (tid < GPX_THETA_STRIDE) sth[tid] = a.theta[b * GPX_THETA_STRIDE + tid];
+    if (P > 0) {
+      const double* th = a.theta + b * GPX_THETA_STRIDE;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (soff[t] < 0) continue;
+        const gpx_term& tm = spec.terms[t];
+        const double ell = th[term_ell_slot(tm)];
+        const int dn = tm.dim_count;
+        for (int e = tid; e < BM * dn; e += 256) {
+          const int r = e / dn, d = tm.dim_start + (e - r * dn);
+          sxp[soff[t] + e] = ((i0 + r < n) ? X[(long long)(i0 + r) * D + d] : 0.0) / ell;
+          sxp[soff[t] + BM * dn + e] = ((j0 + r < n) ? X[(long long)(j0 + r) * D + d] : 0.0) / ell;
+        }
+      }
+    }
     double sums[NT][3];
 #pragma unroll
     for (int t = 0; t < NT; ++t) sums[t][0] = sums[t][1] = sums[t][2] = 0.0;
@@ -689,7 +764,9 @@ void gemm_kernel(GemmArgs a) {
             if (fast) {
               stationary_grad(fkind, sqdist_scaled(sxi + il * D + fd0, sxj + jl * D + fd0, fdn), fvar,
                               finv_ell, dk[0]);
-            } else {
+            } else if constexpr (NT <= 2) {  // (soff[t] < 0: term t reads X as eval_k_grad does)
+              eval_k_grad_pre<NT>(spec, sth, sxi + il * D, sxj + jl * D, sxp, soff, il, BM + jl, dk);
+            } else {  // (the four-term instance: its registers are at the cap already)
               eval_k_grad<NT>(spec, sth, sxi + il * D, sxj + jl * D, dk);
             }
 #pragma unroll

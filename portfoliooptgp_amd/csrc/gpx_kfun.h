@@ -250,6 +250,10 @@ __device__ __forceinline__ double eval_k_grad(const DevSpec& s, const double* __
 __device__ __forceinline__ bool term_prescaled(int kind) {
   return kind != GPX_LINEAR && kind != GPX_PERIODIC_SE;
 }
+// the θ slot of a pre-scaled term's ℓ (eval_term's: RQ keeps α first)
+__device__ __forceinline__ int term_ell_slot(const gpx_term& t) {
+  return t.param_offset + (t.kind == GPX_RQ ? 1 : 0);
+}
 __device__ __forceinline__ double eval_k_pre(const DevSpec& s, const double* __restrict__ th,
                                              const double* __restrict__ xi, const double* __restrict__ xj,
                                              const double* __restrict__ sxs, const int* __restrict__ soff,
